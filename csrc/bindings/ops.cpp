@@ -1,0 +1,469 @@
+// pybind11 bindings for the tfk gfx950 kernel library. Every entry point validates device,
+// dtype, alignment and the maximum element index each kernel will touch BEFORE launching, so a
+// shape bug raises a Python exception instead of faulting the GPU. All launches go to the
+// current HIP stream (graph-capturable: no allocation or synchronisation in here).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+#include <vector>
+
+
+
+#include "../kernels/gemm_params.h"
+
+extern "C" {
+int tfk_gemm_launch(tfk::GemmParams p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits, hipStream_t s);
+int tfk_gemm_splits(int K, int splits);
+int tfk_bn_finalize(float*, int, int, float, const float*, const float*, float, float, float*, float*, float*, float*,
+                    float*, float*, hipStream_t);
+int tfk_bn_stats(const void*, long long, int, float*, int, hipStream_t);
+int tfk_bn_apply(const void*, const float*, const float*, const void*, const float*, const float*, int, void*, long long,
+                 int, hipStream_t);
+int tfk_bn_bwd_reduce(const void*, const void*, const void*, const float*, const float*, const void*, const float*,
+                      const float*, long long, int, float*, int, hipStream_t);
+int tfk_bn_bwd_finalize(float*, int, int, float, const float*, const float*, const float*, const float*, float*, float*,
+                        float*, float*, float*, float*, hipStream_t);
+int tfk_bn_bwd_apply(const void*, const void*, const void*, const float*, const float*, const float*, void*, const void*,
+                     const float*, const float*, const float*, void*, void*, long long, int, hipStream_t);
+int tfk_maxpool_fwd(const void*, void*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+int tfk_maxpool_bwd(const void*, const uint8_t*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                    hipStream_t);
+int tfk_avgpool_fwd(const void*, void*, int, int, int, hipStream_t);
+int tfk_avgpool_bwd(const void*, void*, int, int, int, hipStream_t);
+int tfk_softmax_xent(const void*, const int*, int, int, long long, float, int, float, float*, void*, float*, hipStream_t);
+int tfk_sgd(float*, void*, const float*, float*, long long, float, float, float, int, float, const float*, hipStream_t);
+int tfk_adamw(float*, void*, const float*, float*, float*, long long, float, float, float, float, float, float, float, float,
+              const float*, hipStream_t);
+int tfk_lamb(float*, void*, const float*, float*, float*, float*, const long long*, const int*, const int*, int, float*,
+             float, float, float, float, float, float, float, float, const float*, hipStream_t);
+int tfk_sumsq(const float*, long long, float*, hipStream_t);
+int tfk_clip_coef(const float*, float, float*, float*, hipStream_t);
+int tfk_splitk_reduce(const float*, int, long long, long long, float*, void*, int, float, hipStream_t);
+int tfk_transpose_arb(const void*, void*, int, int, int, hipStream_t);
+int tfk_transpose_f32(const float*, float*, int, int, hipStream_t);
+int tfk_cast_f32_bf16(const float*, void*, long long, hipStream_t);
+int tfk_cast_bf16_f32(const void*, float*, long long, hipStream_t);
+int tfk_synth_uniform(void*, long long, int, int, float, float, unsigned long long, hipStream_t);
+int tfk_synth_normal_f32(float*, long long, float, float, unsigned long long, hipStream_t);
+int tfk_synth_labels(int*, long long, int, unsigned long long, hipStream_t);
+int tfk_colsum(const void*, long long, int, long long, float*, hipStream_t);
+int tfk_act_fwd(const void*, const float*, int, void*, long long, int, hipStream_t);
+int tfk_act_bwd(const void*, const void*, void*, long long, int, hipStream_t);
+int tfk_dropout(const void*, void*, long long, float, unsigned long long, hipStream_t);
+int tfk_add(const void*, const void*, void*, long long, float, float, hipStream_t);
+int tfk_layernorm_fwd(const void*, const void*, const float*, const float*, void*, void*, float*, float*, int, int, float,
+                      hipStream_t);
+int tfk_layernorm_bwd(const void*, const void*, const float*, const float*, const float*, void*, float*, float*, int, int,
+                      hipStream_t);
+int tfk_embedding_fwd(const int*, const void*, void*, long long, int, int, hipStream_t);
+int tfk_embedding_bwd(const int*, const void*, float*, long long, int, int, hipStream_t);
+int tfk_attn_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, long long, long long,
+                 long long, long long, float, int, const int*, hipStream_t);
+int tfk_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, void*, void*, void*, float*,
+                 int, int, int, int, int, long long, long long, long long, long long, float, int, const int*, hipStream_t);
+}
+
+namespace {
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, "tfk kernel launch failed: ", what, " rc=", rc); }
+
+void need(const torch::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void need_bf16(const torch::Tensor& t, const char* n) { need(t, at::kBFloat16, n); }
+void need_f32(const torch::Tensor& t, const char* n) { need(t, at::kFloat, n); }
+void need_aligned(const torch::Tensor& t, int bytes, const char* n) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % bytes == 0, n, " must be ", bytes, "-byte aligned");
+}
+void need_numel(const torch::Tensor& t, long long n, const char* name) {
+  TORCH_CHECK(t.numel() >= n, name, " too small: numel=", t.numel(), " < required ", n);
+}
+template <typename T>
+T* opt_ptr(const c10::optional<torch::Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+enum { A_KIN = 0, A_KOUT = 1, A_CONV_FWD = 2, A_CONV_DGRAD = 3 };
+enum { B_KIN = 0, B_KOUT = 1, B_CONV_WGRAD = 2 };
+
+// conv = [Nimg, H, W, Cin, P, Q, Cout, R, S, sh, sw, ph, pw, dh, dw]
+void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
+          int amode, int bmode, int epi, int bm, int bn, double alpha, double beta, c10::optional<torch::Tensor> bias,
+          c10::optional<torch::Tensor> resid, int act, c10::optional<torch::Tensor> stats, int shards, int splits,
+          int batch, int64_t sA, int64_t sB, int64_t sC, int64_t split_stride, std::vector<int64_t> conv) {
+  need_bf16(A, "A");
+  need_bf16(B, "B");
+  TORCH_CHECK(epi == 0 || epi == 1, "epi");
+  need(C, epi == 0 ? at::kBFloat16 : at::kFloat, "C");
+  need_aligned(A, 16, "A");
+  need_aligned(B, 16, "B");
+  need_aligned(C, 16, "C");
+  TORCH_CHECK(M > 0 && N > 0 && K > 0 && batch >= 1, "bad gemm dims M=", M, " N=", N, " K=", K);
+  TORCH_CHECK(conv.size() == 15, "conv geometry must have 15 ints");
+  tfk::GemmParams p{};
+  p.A = A.data_ptr(); p.B = B.data_ptr(); p.C = C.data_ptr();
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.sA = sA; p.sB = sB; p.sC = sC;
+  p.Nimg = conv[0]; p.H = conv[1]; p.W = conv[2]; p.Cin = conv[3]; p.P = conv[4]; p.Q = conv[5]; p.Cout = conv[6];
+  p.R = conv[7]; p.S = conv[8]; p.sh = conv[9]; p.sw = conv[10]; p.ph = conv[11]; p.pw = conv[12]; p.dh = conv[13];
+  p.dw = conv[14];
+  p.alpha = (float)alpha; p.beta = (float)beta;
+  p.act = act;
+  p.stats_shards = shards;
+  p.split_stride = split_stride;
+  const long long bA = (long long)(batch - 1) * sA, bB = (long long)(batch - 1) * sB, bC = (long long)(batch - 1) * sC;
+  // ---- operand A extents
+  switch (amode) {
+    case A_KIN:
+      TORCH_CHECK(K % 8 == 0 && lda % 8 == 0 && lda >= K, "A_KIN needs K%8==0, lda%8==0, lda>=K");
+      need_numel(A, bA + (long long)(M - 1) * lda + K, "A");
+      break;
+    case A_KOUT:
+      TORCH_CHECK(M % 8 == 0 && lda % 8 == 0 && lda >= M, "A_KOUT needs M%8==0, lda%8==0, lda>=M");
+      need_numel(A, bA + (long long)(K - 1) * lda + M, "A");
+      break;
+    case A_CONV_FWD:
+      TORCH_CHECK(p.Cin % 8 == 0, "conv fwd needs Cin%8==0");
+      TORCH_CHECK((long long)M == (long long)p.Nimg * p.P * p.Q && K == p.R * p.S * p.Cin, "conv fwd M/K mismatch");
+      need_numel(A, (long long)p.Nimg * p.H * p.W * p.Cin, "X");
+      break;
+    case A_CONV_DGRAD:
+      TORCH_CHECK(p.Cout % 8 == 0, "conv dgrad needs Cout%8==0");
+      TORCH_CHECK((long long)M == (long long)p.Nimg * p.H * p.W && K == p.R * p.S * p.Cout, "conv dgrad M/K mismatch");
+      need_numel(A, (long long)p.Nimg * p.P * p.Q * p.Cout, "dY");
+      break;
+    default: TORCH_CHECK(false, "bad amode");
+  }
+  switch (bmode) {
+    case B_KIN:
+      TORCH_CHECK(K % 8 == 0 && ldb % 8 == 0 && ldb >= K, "B_KIN needs K%8==0, ldb%8==0");
+      need_numel(B, bB + (long long)(N - 1) * ldb + K, "B");
+      break;
+    case B_KOUT:
+      TORCH_CHECK(N % 8 == 0 && ldb % 8 == 0 && ldb >= N, "B_KOUT needs N%8==0, ldb%8==0");
+      need_numel(B, bB + (long long)(K - 1) * ldb + N, "B");
+      break;
+    case B_CONV_WGRAD:
+      TORCH_CHECK(p.Cin % 8 == 0, "conv wgrad needs Cin%8==0");
+      TORCH_CHECK(N == p.R * p.S * p.Cin && (long long)K == (long long)p.Nimg * p.P * p.Q, "conv wgrad N/K mismatch");
+      need_numel(B, (long long)p.Nimg * p.H * p.W * p.Cin, "X");
+      break;
+    default: TORCH_CHECK(false, "bad bmode");
+  }
+  TORCH_CHECK(ldc >= N, "ldc < N");
+  int ns = tfk_gemm_splits(K, splits);
+  if (epi == 0) {
+    TORCH_CHECK(ns == 1, "split-K requires the f32 epilogue");
+    TORCH_CHECK(ldc % 8 == 0, "bf16 C needs ldc%8==0");
+    need_numel(C, bC + (long long)(M - 1) * ldc + N, "C");
+  } else {
+    TORCH_CHECK(ldc % 4 == 0, "f32 C needs ldc%4==0");
+    TORCH_CHECK(ns == 1 || batch == 1, "split-K with batch>1 unsupported");
+    need_numel(C, bC + (long long)(ns - 1) * split_stride + (long long)(M - 1) * ldc + N, "C");
+  }
+  if (bias.has_value() && bias->defined()) { need_f32(*bias, "bias"); need_numel(*bias, N, "bias"); }
+  if (resid.has_value() && resid->defined()) {
+    need_bf16(*resid, "resid");
+    need_numel(*resid, bC + (long long)(M - 1) * ldc + N, "resid");
+  }
+  if (stats.has_value() && stats->defined()) {
+    need_f32(*stats, "stats");
+    TORCH_CHECK(shards >= 1, "shards");
+    need_numel(*stats, (long long)shards * 2 * N, "stats");
+  }
+  p.bias = opt_ptr<const float>(bias);
+  p.resid = opt_ptr<const void>(resid);
+  p.stats = opt_ptr<float>(stats);
+  TORCH_CHECK((bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64), "unsupported tile");
+  check_rc(tfk_gemm_launch(p, bm, bn, amode, bmode, epi, batch, splits, cur_stream()), "gemm");
+}
+
+int64_t gemm_splits(int K, int splits) { return tfk_gemm_splits(K, splits); }
+
+void bn_finalize(torch::Tensor stats, int shards, int C, double count, torch::Tensor gamma, torch::Tensor beta, double eps,
+                 double momentum, c10::optional<torch::Tensor> run_mean, c10::optional<torch::Tensor> run_var,
+                 torch::Tensor mean, torch::Tensor invstd, torch::Tensor scale, torch::Tensor shift) {
+  need_f32(stats, "stats"); need_numel(stats, (long long)shards * 2 * C, "stats");
+  for (auto* t : {&gamma, &beta, &mean, &invstd, &scale, &shift}) { need_f32(*t, "bn vec"); need_numel(*t, C, "bn vec"); }
+  check_rc(tfk_bn_finalize(stats.data_ptr<float>(), shards, C, (float)count, gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                           (float)eps, (float)momentum, opt_ptr<float>(run_mean), opt_ptr<float>(run_var),
+                           mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                           shift.data_ptr<float>(), cur_stream()),
+           "bn_finalize");
+}
+
+void bn_stats(torch::Tensor y, int64_t M, int C, torch::Tensor stats, int shards) {
+  need_bf16(y, "y"); need_numel(y, M * C, "y"); TORCH_CHECK(C % 8 == 0, "C%8");
+  need_f32(stats, "stats"); need_numel(stats, (long long)shards * 2 * C, "stats");
+  check_rc(tfk_bn_stats(y.data_ptr(), M, C, stats.data_ptr<float>(), shards, cur_stream()), "bn_stats");
+}
+
+void bn_apply(torch::Tensor y, torch::Tensor scale, torch::Tensor shift, c10::optional<torch::Tensor> r,
+              c10::optional<torch::Tensor> rscale, c10::optional<torch::Tensor> rshift, bool relu, torch::Tensor out,
+              int64_t M, int C) {
+  need_bf16(y, "y"); need_bf16(out, "out"); need_numel(y, M * C, "y"); need_numel(out, M * C, "out");
+  TORCH_CHECK(C % 8 == 0, "C%8");
+  need_aligned(y, 16, "y"); need_aligned(out, 16, "out");
+  need_f32(scale, "scale"); need_f32(shift, "shift"); need_numel(scale, C, "scale"); need_numel(shift, C, "shift");
+  if (r.has_value() && r->defined()) { need_bf16(*r, "r"); need_numel(*r, M * C, "r"); }
+  if (rscale.has_value() && rscale->defined()) { need_numel(*rscale, C, "rscale"); need_numel(*rshift, C, "rshift"); }
+  check_rc(tfk_bn_apply(y.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), opt_ptr<const void>(r),
+                        opt_ptr<const float>(rscale), opt_ptr<const float>(rshift), relu ? 1 : 0, out.data_ptr(), M, C,
+                        cur_stream()),
+           "bn_apply");
+}
+
+void bn_bwd_reduce(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tensor y, torch::Tensor mean,
+                   torch::Tensor invstd, c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> mean2,
+                   c10::optional<torch::Tensor> invstd2, int64_t M, int C, torch::Tensor sums, int shards) {
+  need_bf16(da, "da"); need_bf16(y, "y"); need_numel(da, M * C, "da"); need_numel(y, M * C, "y");
+  TORCH_CHECK(C % 8 == 0, "C%8");
+  if (a.has_value() && a->defined()) need_numel(*a, M * C, "a");
+  if (y2.has_value() && y2->defined()) need_numel(*y2, M * C, "y2");
+  need_f32(sums, "sums"); need_numel(sums, (long long)shards * 3 * C, "sums");
+  check_rc(tfk_bn_bwd_reduce(da.data_ptr(), opt_ptr<const void>(a), y.data_ptr(), mean.data_ptr<float>(),
+                             invstd.data_ptr<float>(), opt_ptr<const void>(y2), opt_ptr<const float>(mean2),
+                             opt_ptr<const float>(invstd2), M, C, sums.data_ptr<float>(), shards, cur_stream()),
+           "bn_bwd_reduce");
+}
+
+void bn_bwd_finalize(torch::Tensor sums, int shards, int C, double count, torch::Tensor gamma, torch::Tensor invstd,
+                     c10::optional<torch::Tensor> gamma2, c10::optional<torch::Tensor> invstd2, torch::Tensor dgamma,
+                     torch::Tensor dbeta, c10::optional<torch::Tensor> dgamma2, c10::optional<torch::Tensor> dbeta2,
+                     torch::Tensor coef, c10::optional<torch::Tensor> coef2) {
+  need_f32(sums, "sums"); need_numel(sums, (long long)shards * 3 * C, "sums");
+  need_numel(dgamma, C, "dgamma"); need_numel(dbeta, C, "dbeta"); need_numel(coef, 3 * C, "coef");
+  if (coef2.has_value() && coef2->defined()) need_numel(*coef2, 3 * C, "coef2");
+  check_rc(tfk_bn_bwd_finalize(sums.data_ptr<float>(), shards, C, (float)count, gamma.data_ptr<float>(),
+                               invstd.data_ptr<float>(), opt_ptr<const float>(gamma2), opt_ptr<const float>(invstd2),
+                               dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), opt_ptr<float>(dgamma2),
+                               opt_ptr<float>(dbeta2), coef.data_ptr<float>(), opt_ptr<float>(coef2), cur_stream()),
+           "bn_bwd_finalize");
+}
+
+void bn_bwd_apply(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tensor y, torch::Tensor mean,
+                  torch::Tensor invstd, torch::Tensor coef, torch::Tensor dy, c10::optional<torch::Tensor> y2,
+                  c10::optional<torch::Tensor> mean2, c10::optional<torch::Tensor> invstd2,
+                  c10::optional<torch::Tensor> coef2, c10::optional<torch::Tensor> dy2,
+                  c10::optional<torch::Tensor> dres, int64_t M, int C) {
+  need_bf16(da, "da"); need_bf16(y, "y"); need_bf16(dy, "dy");
+  for (auto* t : {&da, &y, &dy}) need_numel(*t, M * C, "bn bwd tensor");
+  if (a.has_value() && a->defined()) need_numel(*a, M * C, "a");
+  if (y2.has_value() && y2->defined()) { need_numel(*y2, M * C, "y2"); need_numel(*dy2, M * C, "dy2"); }
+  if (dres.has_value() && dres->defined()) need_numel(*dres, M * C, "dres");
+  TORCH_CHECK(C % 8 == 0, "C%8");
+  check_rc(tfk_bn_bwd_apply(da.data_ptr(), opt_ptr<const void>(a), y.data_ptr(), mean.data_ptr<float>(),
+                            invstd.data_ptr<float>(), coef.data_ptr<float>(), dy.data_ptr(), opt_ptr<const void>(y2),
+                            opt_ptr<const float>(mean2), opt_ptr<const float>(invstd2), opt_ptr<const float>(coef2),
+                            opt_ptr<void>(dy2), opt_ptr<void>(dres), M, C, cur_stream()),
+           "bn_bwd_apply");
+}
+
+// geom = [N, H, W, C, P, Q, KH, KW, sh, sw, ph, pw]
+void maxpool_fwd(torch::Tensor x, torch::Tensor y, torch::Tensor idx, std::vector<int64_t> g) {
+  TORCH_CHECK(g.size() == 12, "geom");
+  need_bf16(x, "x"); need_bf16(y, "y"); need(idx, at::kByte, "idx");
+  TORCH_CHECK(g[3] % 8 == 0, "C%8");
+  need_numel(x, g[0] * g[1] * g[2] * g[3], "x");
+  need_numel(y, g[0] * g[4] * g[5] * g[3], "y");
+  need_numel(idx, g[0] * g[4] * g[5] * g[3], "idx");
+  TORCH_CHECK(g[6] * g[7] <= 255, "window too large");
+  check_rc(tfk_maxpool_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), g[0], g[1], g[2], g[3], g[4], g[5], g[6],
+                           g[7], g[8], g[9], g[10], g[11], cur_stream()),
+           "maxpool_fwd");
+}
+void maxpool_bwd(torch::Tensor dy, torch::Tensor idx, torch::Tensor dx, std::vector<int64_t> g) {
+  TORCH_CHECK(g.size() == 12, "geom");
+  need_bf16(dy, "dy"); need_bf16(dx, "dx"); need(idx, at::kByte, "idx");
+  need_numel(dx, g[0] * g[1] * g[2] * g[3], "dx");
+  need_numel(dy, g[0] * g[4] * g[5] * g[3], "dy");
+  check_rc(tfk_maxpool_bwd(dy.data_ptr(), idx.data_ptr<uint8_t>(), dx.data_ptr(), g[0], g[1], g[2], g[3], g[4], g[5], g[6],
+                           g[7], g[8], g[9], g[10], g[11], cur_stream()),
+           "maxpool_bwd");
+}
+void avgpool_fwd(torch::Tensor x, torch::Tensor y, int N, int HW, int C) {
+  need_bf16(x, "x"); need_bf16(y, "y"); TORCH_CHECK(C % 8 == 0, "C%8");
+  need_numel(x, (long long)N * HW * C, "x"); need_numel(y, (long long)N * C, "y");
+  check_rc(tfk_avgpool_fwd(x.data_ptr(), y.data_ptr(), N, HW, C, cur_stream()), "avgpool_fwd");
+}
+void avgpool_bwd(torch::Tensor dy, torch::Tensor dx, int N, int HW, int C) {
+  need_bf16(dy, "dy"); need_bf16(dx, "dx"); TORCH_CHECK(C % 8 == 0, "C%8");
+  need_numel(dx, (long long)N * HW * C, "dx"); need_numel(dy, (long long)N * C, "dy");
+  check_rc(tfk_avgpool_bwd(dy.data_ptr(), dx.data_ptr(), N, HW, C, cur_stream()), "avgpool_bwd");
+}
+
+void softmax_xent(torch::Tensor logits, torch::Tensor labels, int B, int V, int64_t ld, double smoothing, int ignore_index,
+                  double scale, torch::Tensor loss, c10::optional<torch::Tensor> dlogits,
+                  c10::optional<torch::Tensor> correct) {
+  need_bf16(logits, "logits"); need(labels, at::kInt, "labels"); need_f32(loss, "loss");
+  need_numel(logits, (long long)(B - 1) * ld + V, "logits"); need_numel(labels, B, "labels"); need_numel(loss, B, "loss");
+  if (dlogits.has_value() && dlogits->defined()) { need_bf16(*dlogits, "dlogits"); need_numel(*dlogits, (long long)(B - 1) * ld + V, "dlogits"); }
+  if (correct.has_value() && correct->defined()) need_numel(*correct, B, "correct");
+  check_rc(tfk_softmax_xent(logits.data_ptr(), labels.data_ptr<int>(), B, V, ld, (float)smoothing, ignore_index,
+                            (float)scale, loss.data_ptr<float>(), opt_ptr<void>(dlogits), opt_ptr<float>(correct),
+                            cur_stream()),
+           "softmax_xent");
+}
+
+void sgd(torch::Tensor w, c10::optional<torch::Tensor> wb, torch::Tensor g, torch::Tensor m, double lr, double mu,
+         double wd, bool nesterov, double gs, c10::optional<torch::Tensor> gs_dev) {
+  need_f32(w, "w"); need_f32(g, "g"); need_f32(m, "m");
+  long long n = w.numel();
+  need_numel(g, n, "g"); need_numel(m, n, "m");
+  need_aligned(w, 16, "w"); need_aligned(g, 16, "g"); need_aligned(m, 16, "m");
+  if (wb.has_value() && wb->defined()) { need_bf16(*wb, "wb"); need_numel(*wb, n, "wb"); need_aligned(*wb, 8, "wb"); }
+  check_rc(tfk_sgd(w.data_ptr<float>(), opt_ptr<void>(wb), g.data_ptr<float>(), m.data_ptr<float>(), n, (float)lr,
+                   (float)mu, (float)wd, nesterov ? 1 : 0, (float)gs, opt_ptr<const float>(gs_dev), cur_stream()),
+           "sgd");
+}
+void adamw(torch::Tensor w, c10::optional<torch::Tensor> wb, torch::Tensor g, torch::Tensor m, torch::Tensor v, double lr,
+           double b1, double b2, double eps, double wd, double bc1, double bc2, double gs,
+           c10::optional<torch::Tensor> gs_dev) {
+  need_f32(w, "w"); need_f32(g, "g"); need_f32(m, "m"); need_f32(v, "v");
+  long long n = w.numel();
+  need_numel(g, n, "g"); need_numel(m, n, "m"); need_numel(v, n, "v");
+  if (wb.has_value() && wb->defined()) { need_bf16(*wb, "wb"); need_numel(*wb, n, "wb"); }
+  check_rc(tfk_adamw(w.data_ptr<float>(), opt_ptr<void>(wb), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                     n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, (float)gs,
+                     opt_ptr<const float>(gs_dev), cur_stream()),
+           "adamw");
+}
+void lamb(torch::Tensor w, c10::optional<torch::Tensor> wb, torch::Tensor g, torch::Tensor m, torch::Tensor v,
+          torch::Tensor u, torch::Tensor cstart, torch::Tensor clen, torch::Tensor cseg, torch::Tensor seg_norms, double lr,
+          double b1, double b2, double eps, double wd, double bc1, double bc2, double gs,
+          c10::optional<torch::Tensor> gs_dev) {
+  need_f32(w, "w"); need_f32(g, "g"); need_f32(m, "m"); need_f32(v, "v"); need_f32(u, "u");
+  need(cstart, at::kLong, "cstart"); need(clen, at::kInt, "clen"); need(cseg, at::kInt, "cseg");
+  need_f32(seg_norms, "seg_norms");
+  long long n = w.numel();
+  for (auto* t : {&g, &m, &v, &u}) need_numel(*t, n, "lamb buf");
+  int nch = (int)cstart.numel();
+  TORCH_CHECK(clen.numel() == nch && cseg.numel() == nch, "chunk table");
+  check_rc(tfk_lamb(w.data_ptr<float>(), opt_ptr<void>(wb), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                    u.data_ptr<float>(), cstart.data_ptr<int64_t>() ? (const long long*)cstart.data_ptr<int64_t>() : nullptr,
+                    clen.data_ptr<int>(), cseg.data_ptr<int>(), nch, seg_norms.data_ptr<float>(), (float)lr, (float)b1,
+                    (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, (float)gs, opt_ptr<const float>(gs_dev),
+                    cur_stream()),
+           "lamb");
+}
+void sumsq(torch::Tensor x, torch::Tensor out) {
+  need_f32(x, "x"); need_f32(out, "out");
+  check_rc(tfk_sumsq(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), cur_stream()), "sumsq");
+}
+void clip_coef(torch::Tensor ss, double max_norm, torch::Tensor coef, c10::optional<torch::Tensor> norm) {
+  need_f32(ss, "ss"); need_f32(coef, "coef");
+  check_rc(tfk_clip_coef(ss.data_ptr<float>(), (float)max_norm, coef.data_ptr<float>(), opt_ptr<float>(norm), cur_stream()),
+           "clip_coef");
+}
+
+void splitk_reduce(torch::Tensor slabs, int S, int64_t stride, int64_t n, c10::optional<torch::Tensor> out,
+                   c10::optional<torch::Tensor> outb, bool accumulate, double alpha) {
+  need_f32(slabs, "slabs");
+  need_numel(slabs, (long long)(S - 1) * stride + n, "slabs");
+  TORCH_CHECK(stride % 4 == 0, "stride%4");
+  need_aligned(slabs, 16, "slabs");
+  if (out.has_value() && out->defined()) { need_f32(*out, "out"); need_numel(*out, n, "out"); need_aligned(*out, 16, "out"); }
+  else { TORCH_CHECK(outb.has_value() && outb->defined(), "need out"); need_bf16(*outb, "outb"); need_numel(*outb, n, "outb"); need_aligned(*outb, 8, "outb"); }
+  check_rc(tfk_splitk_reduce(slabs.data_ptr<float>(), S, stride, n, opt_ptr<float>(out), opt_ptr<void>(outb),
+                             accumulate ? 1 : 0, (float)alpha, cur_stream()),
+           "splitk_reduce");
+}
+void transpose_arb(torch::Tensor in, torch::Tensor out, int A, int R, int B) {
+  need_bf16(in, "in"); need_bf16(out, "out");
+  need_numel(in, (long long)A * R * B, "in"); need_numel(out, (long long)A * R * B, "out");
+  check_rc(tfk_transpose_arb(in.data_ptr(), out.data_ptr(), A, R, B, cur_stream()), "transpose_arb");
+}
+void transpose_f32(torch::Tensor in, torch::Tensor out, int rows, int cols) {
+  need_f32(in, "in"); need_f32(out, "out");
+  need_numel(in, (long long)rows * cols, "in"); need_numel(out, (long long)rows * cols, "out");
+  check_rc(tfk_transpose_f32(in.data_ptr<float>(), out.data_ptr<float>(), rows, cols, cur_stream()), "transpose_f32");
+}
+void cast_f32_bf16(torch::Tensor x, torch::Tensor y) {
+  need_f32(x, "x"); need_bf16(y, "y"); need_numel(y, x.numel(), "y");
+  check_rc(tfk_cast_f32_bf16(x.data_ptr<float>(), y.data_ptr(), x.numel(), cur_stream()), "cast_f32_bf16");
+}
+void cast_bf16_f32(torch::Tensor x, torch::Tensor y) {
+  need_bf16(x, "x"); need_f32(y, "y"); need_numel(y, x.numel(), "y");
+  check_rc(tfk_cast_bf16_f32(x.data_ptr(), y.data_ptr<float>(), x.numel(), cur_stream()), "cast_bf16_f32");
+}
+void synth_uniform(torch::Tensor y, int64_t rows, int Creal, int Cpad, double lo, double hi, int64_t seed) {
+  need_bf16(y, "y"); need_numel(y, rows * Cpad, "y");
+  check_rc(tfk_synth_uniform(y.data_ptr(), rows, Creal, Cpad, (float)lo, (float)hi, (unsigned long long)seed, cur_stream()),
+           "synth_uniform");
+}
+void synth_normal_f32(torch::Tensor y, double mean, double std, int64_t seed) {
+  need_f32(y, "y");
+  check_rc(tfk_synth_normal_f32(y.data_ptr<float>(), y.numel(), (float)mean, (float)std, (unsigned long long)seed,
+                                cur_stream()),
+           "synth_normal");
+}
+void synth_labels(torch::Tensor y, int classes, int64_t seed) {
+  need(y, at::kInt, "labels");
+  check_rc(tfk_synth_labels(y.data_ptr<int>(), y.numel(), classes, (unsigned long long)seed, cur_stream()), "synth_labels");
+}
+void colsum(torch::Tensor x, int64_t M, int N, int64_t ld, torch::Tensor out) {
+  need_bf16(x, "x"); need_f32(out, "out");
+  need_numel(x, (M - 1) * ld + N, "x"); need_numel(out, N, "out");
+  check_rc(tfk_colsum(x.data_ptr(), M, N, ld, out.data_ptr<float>(), cur_stream()), "colsum");
+}
+void act_fwd(torch::Tensor x, c10::optional<torch::Tensor> bias, int N, torch::Tensor y, int act) {
+  need_bf16(x, "x"); need_bf16(y, "y"); need_numel(y, x.numel(), "y");
+  if (bias.has_value() && bias->defined()) { need_f32(*bias, "bias"); need_numel(*bias, N, "bias"); TORCH_CHECK(x.numel() % N == 0, "bias N"); }
+  check_rc(tfk_act_fwd(x.data_ptr(), opt_ptr<const float>(bias), N, y.data_ptr(), x.numel(), act, cur_stream()), "act_fwd");
+}
+void act_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor dx, int act) {
+  need_bf16(dy, "dy"); need_bf16(x, "x"); need_bf16(dx, "dx");
+  need_numel(x, dy.numel(), "x"); need_numel(dx, dy.numel(), "dx");
+  check_rc(tfk_act_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), dy.numel(), act, cur_stream()), "act_bwd");
+}
+void dropout(torch::Tensor x, torch::Tensor y, double p, int64_t seed) {
+  need_bf16(x, "x"); need_bf16(y, "y"); need_numel(y, x.numel(), "y");
+  check_rc(tfk_dropout(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (unsigned long long)seed, cur_stream()), "dropout");
+}
+void add(torch::Tensor a, torch::Tensor b, torch::Tensor y, double alpha, double beta) {
+  need_bf16(a, "a"); need_bf16(b, "b"); need_bf16(y, "y");
+  need_numel(b, a.numel(), "b"); need_numel(y, a.numel(), "y");
+  check_rc(tfk_add(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), (float)alpha, (float)beta, cur_stream()), "add");
+}
+}  // namespace
+
+void register_transformer_ops(pybind11::module& m);
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "tfk gfx950 HIP kernel library";
+  m.def("gemm", &gemm);
+  m.def("gemm_splits", &gemm_splits);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_stats", &bn_stats);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_finalize", &bn_bwd_finalize);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("sgd", &sgd);
+  m.def("adamw", &adamw);
+  m.def("lamb", &lamb);
+  m.def("sumsq", &sumsq);
+  m.def("clip_coef", &clip_coef);
+  m.def("splitk_reduce", &splitk_reduce);
+  m.def("transpose_arb", &transpose_arb);
+  m.def("transpose_f32", &transpose_f32);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("cast_bf16_f32", &cast_bf16_f32);
+  m.def("synth_uniform", &synth_uniform);
+  m.def("synth_normal_f32", &synth_normal_f32);
+  m.def("synth_labels", &synth_labels);
+  m.def("colsum", &colsum);
+  m.def("act_fwd", &act_fwd);
+  m.def("act_bwd", &act_bwd);
+  m.def("dropout", &dropout);
+  m.def("add", &add);
+  register_transformer_ops(m);
+}

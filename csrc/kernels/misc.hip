@@ -1,0 +1,217 @@
+// Small utility kernels for the executor: split-K slab reduction, weight transposes for conv
+// dgrad, casts, fills, on-device synthetic data (no H2D in the hot loop), column sums (bias
+// grads), elementwise activation/dropout forward+backward.
+#include "common.h"
+
+namespace {
+constexpr int NT = 256;
+
+int grid_for(long long work, int cap = 8192) {
+  long long g = (work + NT - 1) / NT;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+// out[i] = (acc ? out[i] : 0) + sum_s slabs[s*stride + i]; optional bf16 output instead.
+__global__ void splitk_reduce_kernel(const float* __restrict__ slabs, int S, long long stride, long long n,
+                                     float* __restrict__ out, bf16* __restrict__ outb, int accumulate, float alpha) {
+  for (long long i = ((long long)blockIdx.x * NT + threadIdx.x) * 4; i < n; i += (long long)gridDim.x * NT * 4) {
+    if (i + 3 < n) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < S; ++s) a += *(const f32x4*)(slabs + s * stride + i);
+      a *= alpha;
+      if (out) {
+        if (accumulate) a += *(f32x4*)(out + i);
+        *(f32x4*)(out + i) = a;
+      } else {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(a[e] + (accumulate ? bf2f(outb[i + e]) : 0.f));
+        *(bf16x4*)(outb + i) = o;
+      }
+    } else {
+      for (long long j = i; j < n; ++j) {
+        float a = 0.f;
+        for (int s = 0; s < S; ++s) a += slabs[s * stride + j];
+        a *= alpha;
+        if (out) out[j] = a + (accumulate ? out[j] : 0.f);
+        else outb[j] = f2bf(a + (accumulate ? bf2f(outb[j]) : 0.f));
+      }
+    }
+  }
+}
+
+// in [A][R][B] -> out [B][R][A] (bf16), 32x32 LDS tiles; grid (ceil(B/32), ceil(A/32), R).
+__global__ void transpose_arb_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int A, int R, int B) {
+  __shared__ bf16 tile[32][33];
+  const int b0 = blockIdx.x * 32, a0 = blockIdx.y * 32, r = blockIdx.z;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads -> 8 rows per pass
+  for (int i = ty; i < 32; i += 8) {
+    int a = a0 + i, b = b0 + tx;
+    tile[i][tx] = (a < A && b < B) ? in[((long long)a * R + r) * B + b] : f2bf(0.f);
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    int b = b0 + i, a = a0 + tx;
+    if (a < A && b < B) out[((long long)b * R + r) * A + a] = tile[tx][i];
+  }
+}
+
+// 2D transpose [rows][cols] -> [cols][rows] for f32 (weight layout conversions for checkpoints).
+__global__ void transpose_f32_kernel(const float* __restrict__ in, float* __restrict__ out, int rows, int cols) {
+  __shared__ float tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    int r = r0 + i, c = c0 + tx;
+    if (r < rows && c < cols) tile[i][tx] = in[(long long)r * cols + c];
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    int c = c0 + i, r = r0 + tx;
+    if (r < rows && c < cols) out[(long long)c * rows + r] = tile[tx][i];
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) y[i] = f2bf(x[i]);
+}
+__global__ void cast_bf16_f32_kernel(const bf16* __restrict__ x, float* __restrict__ y, long long n) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) y[i] = bf2f(x[i]);
+}
+
+// Uniform [lo, hi) bf16 with channel padding: tensor [rows][Cpad], channels >= Creal are zero.
+__global__ void synth_uniform_kernel(bf16* __restrict__ y, long long rows, int Creal, int Cpad, float lo, float hi,
+                                     unsigned long long seed) {
+  const long long n = rows * Cpad;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    int c = (int)(i % Cpad);
+    y[i] = c < Creal ? f2bf(lo + (hi - lo) * u01(hash_u32(seed, i))) : f2bf(0.f);
+  }
+}
+__global__ void synth_normal_f32_kernel(float* __restrict__ y, long long n, float mean, float std, unsigned long long seed) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    float u1 = fmaxf(u01(hash_u32(seed, 2 * i)), 1e-7f), u2 = u01(hash_u32(seed, 2 * i + 1));
+    y[i] = mean + std * sqrtf(-2.f * __logf(u1)) * __cosf(6.2831853f * u2);
+  }
+}
+__global__ void synth_labels_kernel(int* __restrict__ y, long long n, int classes, unsigned long long seed) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
+    y[i] = (int)(hash_u32(seed, i) % (uint32_t)classes);
+}
+
+// Column sums of bf16 [M][N] -> f32 out[N] (bias grads). Block = 64 columns x 4 row-groups.
+__global__ void colsum_kernel(const bf16* __restrict__ x, long long M, int N, long long ld, float* __restrict__ out,
+                              int accumulate_atomic) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < N)
+    for (long long r = (long long)blockIdx.y * 4 + rg; r < M; r += (long long)gridDim.y * 4) s += bf2f(x[r * ld + c]);
+  __shared__ float red[4][64];
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && c < N) {
+    s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(out + c, s);
+  }
+}
+
+// act: 1 relu, 2 gelu(tanh). y = act(x [+ bias[col]]).
+__global__ void act_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ bias, int N, bf16* __restrict__ y,
+                               long long n, int act) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    float v = bf2f(x[i]) + (bias ? bias[i % N] : 0.f);
+    y[i] = f2bf(act == 1 ? fmaxf(v, 0.f) : (act == 2 ? gelu_tanh(v) : v));
+  }
+}
+// dx = dy * act'(x_preact)
+__global__ void act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, bf16* __restrict__ dx, long long n,
+                               int act) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    float v = bf2f(x[i]), g = bf2f(dy[i]);
+    dx[i] = f2bf(act == 1 ? (v > 0.f ? g : 0.f) : (act == 2 ? g * gelu_tanh_grad(v) : g));
+  }
+}
+
+// Inverted dropout; mask regenerated from (seed, index) in backward -> no mask tensor stored.
+__global__ void dropout_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long long n, float p,
+                               unsigned long long seed) {
+  const float keep = 1.f - p, inv = 1.f / keep;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    bool k = u01(hash_u32(seed, i)) < keep;
+    y[i] = f2bf(k ? bf2f(x[i]) * inv : 0.f);
+  }
+}
+
+__global__ void add_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b, bf16* __restrict__ y, long long n,
+                           float alpha, float beta) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
+    y[i] = f2bf(alpha * bf2f(a[i]) + beta * bf2f(b[i]));
+}
+}  // namespace
+
+extern "C" {
+int tfk_splitk_reduce(const float* slabs, int S, long long stride, long long n, float* out, bf16* outb, int accumulate,
+                      float alpha, hipStream_t s) {
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(n / 4 + 1)), dim3(NT), 0, s, slabs, S, stride, n, out, outb,
+                     accumulate, alpha);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_transpose_arb(const bf16* in, bf16* out, int A, int R, int B, hipStream_t s) {
+  dim3 grid((B + 31) / 32, (A + 31) / 32, R);
+  hipLaunchKernelGGL(transpose_arb_kernel, grid, dim3(NT), 0, s, in, out, A, R, B);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_transpose_f32(const float* in, float* out, int rows, int cols, hipStream_t s) {
+  dim3 grid((cols + 31) / 32, (rows + 31) / 32);
+  hipLaunchKernelGGL(transpose_f32_kernel, grid, dim3(NT), 0, s, in, out, rows, cols);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_cast_bf16_f32(const bf16* x, float* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_synth_uniform(bf16* y, long long rows, int Creal, int Cpad, float lo, float hi, unsigned long long seed,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(synth_uniform_kernel, dim3(grid_for(rows * Cpad)), dim3(NT), 0, s, y, rows, Creal, Cpad, lo, hi, seed);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_synth_normal_f32(float* y, long long n, float mean, float std, unsigned long long seed, hipStream_t s) {
+  hipLaunchKernelGGL(synth_normal_f32_kernel, dim3(grid_for(n)), dim3(NT), 0, s, y, n, mean, std, seed);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_synth_labels(int* y, long long n, int classes, unsigned long long seed, hipStream_t s) {
+  hipLaunchKernelGGL(synth_labels_kernel, dim3(grid_for(n)), dim3(NT), 0, s, y, n, classes, seed);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_colsum(const bf16* x, long long M, int N, long long ld, float* out, hipStream_t s) {
+  long long gy = (M + 255) / 256;
+  if (gy > 1024) gy = 1024;
+  if (gy < 1) gy = 1;
+  dim3 grid((N + 63) / 64, (unsigned)gy);
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(NT), 0, s, x, M, N, ld, out, 1);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_act_fwd(const bf16* x, const float* bias, int N, bf16* y, long long n, int act, hipStream_t s) {
+  hipLaunchKernelGGL(act_fwd_kernel, dim3(grid_for(n)), dim3(NT), 0, s, x, bias, N, y, n, act);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_act_bwd(const bf16* dy, const bf16* x, bf16* dx, long long n, int act, hipStream_t s) {
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(NT), 0, s, dy, x, dx, n, act);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_dropout(const bf16* x, bf16* y, long long n, float p, unsigned long long seed, hipStream_t s) {
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n, p, seed);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_add(const bf16* a, const bf16* b, bf16* y, long long n, float alpha, float beta, hipStream_t s) {
+  hipLaunchKernelGGL(add_kernel, dim3(grid_for(n)), dim3(NT), 0, s, a, b, y, n, alpha, beta);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

@@ -1,0 +1,166 @@
+// Fused optimizers over the executor's FLAT parameter arena (one launch per parameter group,
+// no per-tensor multi-tensor-apply lists needed): f32 master weights, f32 grads, f32 slots, and
+// the bf16 compute copy refreshed in the same pass. grad_scale may be a device scalar (global-norm
+// clipping / loss-scale) so nothing synchronises with the host.
+#include "common.h"
+
+namespace {
+constexpr int NT = 256;
+
+__device__ __forceinline__ float gscale_of(float host, const float* dev) { return dev ? host * dev[0] : host; }
+
+__global__ void sgd_kernel(float* __restrict__ w, bf16* __restrict__ wb, const float* __restrict__ g, float* __restrict__ m,
+                           long long n, float lr, float mu, float wd, int nesterov, float gs_host, const float* gs_dev) {
+  const float gs = gscale_of(gs_host, gs_dev);
+  for (long long i = ((long long)blockIdx.x * NT + threadIdx.x) * 4; i < n; i += (long long)gridDim.x * NT * 4) {
+    if (i + 3 < n) {
+      f32x4 wv = *(f32x4*)(w + i), gv = *(const f32x4*)(g + i), mv = *(f32x4*)(m + i);
+      f32x4 d = gv * gs + wd * wv;
+      mv = mu * mv + d;
+      f32x4 step = nesterov ? d + mu * mv : mv;
+      wv = wv - lr * step;
+      *(f32x4*)(w + i) = wv;
+      *(f32x4*)(m + i) = mv;
+      if (wb) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(wv[e]);
+        *(bf16x4*)(wb + i) = o;
+      }
+    } else {
+      for (long long j = i; j < n; ++j) {
+        float d = g[j] * gs + wd * w[j];
+        m[j] = mu * m[j] + d;
+        w[j] -= lr * (nesterov ? d + mu * m[j] : m[j]);
+        if (wb) wb[j] = f2bf(w[j]);
+      }
+    }
+  }
+}
+
+__global__ void adamw_kernel(float* __restrict__ w, bf16* __restrict__ wb, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, long long n, float lr, float b1, float b2, float eps, float wd,
+                             float bc1, float bc2, float gs_host, const float* gs_dev) {
+  const float gs = gscale_of(gs_host, gs_dev);
+  const float ibc1 = 1.f / bc1, ibc2 = 1.f / bc2;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    float gr = g[i] * gs;
+    float mm = b1 * m[i] + (1.f - b1) * gr;
+    float vv = b2 * v[i] + (1.f - b2) * gr * gr;
+    m[i] = mm;
+    v[i] = vv;
+    float ww = w[i];
+    ww -= lr * ((mm * ibc1) / (sqrtf(vv * ibc2) + eps) + wd * ww);
+    w[i] = ww;
+    if (wb) wb[i] = f2bf(ww);
+  }
+}
+
+// LAMB stage 1: u = adam_dir + wd*w written into `u`; per-segment ||w||^2, ||u||^2 via atomics.
+// seg_of_chunk: segment id of each 4096-element chunk (host-built; chunks never straddle segments).
+__global__ void lamb_stage1_kernel(const float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
+                                   float* __restrict__ v, float* __restrict__ u, const long long* __restrict__ chunk_start,
+                                   const int* __restrict__ chunk_len, const int* __restrict__ chunk_seg, int nchunks,
+                                   float b1, float b2, float eps, float wd, float bc1, float bc2,
+                                   float* __restrict__ seg_norms, float gs_host, const float* gs_dev) {
+  __shared__ float red[NT / 64];
+  const float gs = gscale_of(gs_host, gs_dev);
+  for (int c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const long long s0 = chunk_start[c];
+    const int len = chunk_len[c];
+    float wsq = 0.f, usq = 0.f;
+    for (int j = threadIdx.x; j < len; j += NT) {
+      long long i = s0 + j;
+      float gr = g[i] * gs;
+      float mm = b1 * m[i] + (1.f - b1) * gr;
+      float vv = b2 * v[i] + (1.f - b2) * gr * gr;
+      m[i] = mm;
+      v[i] = vv;
+      float uu = (mm / bc1) / (sqrtf(vv / bc2) + eps) + wd * w[i];
+      u[i] = uu;
+      wsq += w[i] * w[i];
+      usq += uu * uu;
+    }
+    wsq = block_sum<NT>(wsq, red);
+    usq = block_sum<NT>(usq, red);
+    if (threadIdx.x == 0) {
+      atomicAdd(seg_norms + 2 * chunk_seg[c], wsq);
+      atomicAdd(seg_norms + 2 * chunk_seg[c] + 1, usq);
+    }
+  }
+}
+
+__global__ void lamb_stage2_kernel(float* __restrict__ w, bf16* __restrict__ wb, const float* __restrict__ u,
+                                   const long long* __restrict__ chunk_start, const int* __restrict__ chunk_len,
+                                   const int* __restrict__ chunk_seg, int nchunks, const float* __restrict__ seg_norms,
+                                   float lr) {
+  for (int c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int sg = chunk_seg[c];
+    const float wn = sqrtf(seg_norms[2 * sg]), un = sqrtf(seg_norms[2 * sg + 1]);
+    const float ratio = (wn > 0.f && un > 0.f) ? wn / un : 1.f;
+    const long long s0 = chunk_start[c];
+    const int len = chunk_len[c];
+    for (int j = threadIdx.x; j < len; j += NT) {
+      long long i = s0 + j;
+      float ww = w[i] - lr * ratio * u[i];
+      w[i] = ww;
+      if (wb) wb[i] = f2bf(ww);
+    }
+  }
+}
+
+// out[0] += sum(x^2) (global grad norm)
+__global__ void sumsq_kernel(const float* __restrict__ x, long long n, float* __restrict__ out) {
+  __shared__ float red[NT / 64];
+  float s = 0.f;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) s += x[i] * x[i];
+  s = block_sum<NT>(s, red);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+// clip coefficient from sumsq: out = min(1, max_norm / (sqrt(ss) + 1e-6)); also stores the norm.
+__global__ void clip_coef_kernel(const float* ss, float max_norm, float* coef, float* norm) {
+  float nn = sqrtf(ss[0]);
+  if (norm) norm[0] = nn;
+  coef[0] = max_norm > 0.f ? fminf(1.f, max_norm / (nn + 1e-6f)) : 1.f;
+}
+
+int grid_for(long long work, int cap = 4096) {
+  long long g = (work + NT - 1) / NT;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+}  // namespace
+
+extern "C" {
+int tfk_sgd(float* w, bf16* wb, const float* g, float* m, long long n, float lr, float mu, float wd, int nesterov,
+            float gs, const float* gs_dev, hipStream_t s) {
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4 + 1)), dim3(NT), 0, s, w, wb, g, m, n, lr, mu, wd, nesterov, gs, gs_dev);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_adamw(float* w, bf16* wb, const float* g, float* m, float* v, long long n, float lr, float b1, float b2, float eps,
+              float wd, float bc1, float bc2, float gs, const float* gs_dev, hipStream_t s) {
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(NT), 0, s, w, wb, g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2, gs,
+                     gs_dev);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_lamb(float* w, bf16* wb, const float* g, float* m, float* v, float* u, const long long* cstart, const int* clen,
+             const int* cseg, int nchunks, float* seg_norms, float lr, float b1, float b2, float eps, float wd, float bc1,
+             float bc2, float gs, const float* gs_dev, hipStream_t s) {
+  int grid = nchunks < 4096 ? nchunks : 4096;
+  if (grid < 1) return 0;
+  hipLaunchKernelGGL(lamb_stage1_kernel, dim3(grid), dim3(NT), 0, s, w, g, m, v, u, cstart, clen, cseg, nchunks, b1, b2, eps,
+                     wd, bc1, bc2, seg_norms, gs, gs_dev);
+  hipLaunchKernelGGL(lamb_stage2_kernel, dim3(grid), dim3(NT), 0, s, w, wb, u, cstart, clen, cseg, nchunks, seg_norms, lr);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_sumsq(const float* x, long long n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n, 2048)), dim3(NT), 0, s, x, n, out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_clip_coef(const float* ss, float max_norm, float* coef, float* norm, hipStream_t s) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, s, ss, max_norm, coef, norm);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

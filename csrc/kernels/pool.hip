@@ -1,0 +1,155 @@
+// NHWC bf16 pooling for gfx950: max-pool (argmax byte recorded in forward, gather-form backward:
+// no atomics) and global average pool. 8 channels (16 B) per lane.
+#include "common.h"
+
+namespace {
+constexpr int NT = 256;
+
+__global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, uint8_t* __restrict__ idx, int N, int H,
+                                   int W, int C, int P, int Q, int KH, int KW, int sh, int sw, int ph, int pw) {
+  const int cpr = C >> 3;
+  const long long total = (long long)N * P * Q * cpr;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    int cc = (int)(i % cpr);
+    long long pix = i / cpr;
+    int q = (int)(pix % Q);
+    long long t = pix / Q;
+    int p = (int)(t % P);
+    int n = (int)(t / P);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int r = 0; r < KH; ++r) {
+      int h = p * sh - ph + r;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int s = 0; s < KW; ++s) {
+        int w = q * sw - pw + s;
+        if ((unsigned)w >= (unsigned)W) continue;
+        bf16x8 v = *(const bf16x8*)(x + (((long long)n * H + h) * W + w) * C + cc * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float f = bf2f(v[e]);
+          if (f > best[e]) { best[e] = f; bi[e] = (uint8_t)(r * KW + s); }
+        }
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
+    *(bf16x8*)(y + i * 8) = o;
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *(uint2*)(idx + i * 8) = packed;
+  }
+}
+
+__global__ void maxpool_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* __restrict__ idx, bf16* __restrict__ dx, int N,
+                                   int H, int W, int C, int P, int Q, int KH, int KW, int sh, int sw, int ph, int pw) {
+  const int cpr = C >> 3;
+  const long long total = (long long)N * H * W * cpr;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    int cc = (int)(i % cpr);
+    long long pix = i / cpr;
+    int w = (int)(pix % W);
+    long long t = pix / W;
+    int h = (int)(t % H);
+    int n = (int)(t / H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // outputs p with p*sh - ph <= h <= p*sh - ph + KH - 1
+    int p_lo = (h + ph - KH + 1 + sh - 1) / sh; if (h + ph - KH + 1 < 0) p_lo = 0;
+    int p_hi = (h + ph) / sh; if (p_hi > P - 1) p_hi = P - 1;
+    int q_lo = (w + pw - KW + 1 + sw - 1) / sw; if (w + pw - KW + 1 < 0) q_lo = 0;
+    int q_hi = (w + pw) / sw; if (q_hi > Q - 1) q_hi = Q - 1;
+    for (int p = p_lo; p <= p_hi; ++p) {
+      int r = h - (p * sh - ph);
+      for (int q = q_lo; q <= q_hi; ++q) {
+        int s = w - (q * sw - pw);
+        uint8_t want = (uint8_t)(r * KW + s);
+        long long o = (((long long)n * P + p) * Q + q) * C + cc * 8;
+        bf16x8 g = *(const bf16x8*)(dy + o);
+        uint2 packed = *(const uint2*)(idx + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          uint32_t word = e < 4 ? packed.x : packed.y;
+          uint8_t b = (word >> (8 * (e & 3))) & 0xff;
+          if (b == want) acc[e] += bf2f(g[e]);
+        }
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
+    *(bf16x8*)(dx + i * 8) = o;
+  }
+}
+
+// x [N][HW][C] -> y [N][C] (bf16), mean over HW. One block per (n, 8*NT channel slab).
+__global__ void avgpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int HW, int C) {
+  const int n = blockIdx.y;
+  const int c = (blockIdx.x * NT + threadIdx.x) * 8;
+  if (c >= C) return;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bf16* base = x + (long long)n * HW * C + c;
+  for (int i = 0; i < HW; ++i) {
+    bf16x8 v = *(const bf16x8*)(base + (long long)i * C);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[e]);
+  }
+  bf16x8 o;
+  const float inv = 1.f / HW;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e] * inv);
+  *(bf16x8*)(y + (long long)n * C + c) = o;
+}
+
+__global__ void avgpool_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N, int HW, int C) {
+  const int cpr = C >> 3;
+  const long long total = (long long)N * HW * cpr;
+  const float inv = 1.f / HW;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    int cc = (int)(i % cpr);
+    long long n = i / cpr / HW;
+    bf16x8 g = *(const bf16x8*)(dy + n * C + cc * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(g[e]) * inv);
+    *(bf16x8*)(dx + i * 8) = o;
+  }
+}
+
+int grid_for(long long work, int cap = 8192) {
+  long long g = (work + NT - 1) / NT;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+}  // namespace
+
+extern "C" {
+int tfk_maxpool_fwd(const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int KH, int KW, int sh,
+                    int sw, int ph, int pw, hipStream_t s) {
+  long long total = (long long)N * P * Q * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, x, y, idx, N, H, W, C, P, Q, KH, KW, sh, sw,
+                     ph, pw);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_maxpool_bwd(const bf16* dy, const uint8_t* idx, bf16* dx, int N, int H, int W, int C, int P, int Q, int KH, int KW,
+                    int sh, int sw, int ph, int pw, hipStream_t s) {
+  long long total = (long long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, dy, idx, dx, N, H, W, C, P, Q, KH, KW, sh,
+                     sw, ph, pw);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_avgpool_fwd(const bf16* x, bf16* y, int N, int HW, int C, hipStream_t s) {
+  dim3 grid((C / 8 + NT - 1) / NT, N);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, grid, dim3(NT), 0, s, x, y, HW, C);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_avgpool_bwd(const bf16* dy, bf16* dx, int N, int HW, int C, hipStream_t s) {
+  long long total = (long long)N * HW * (C / 8);
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, dy, dx, N, HW, C);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

@@ -1,0 +1,220 @@
+"""ResNet-50/101/152 (v1.5: stride on the 3x3 conv) for the tfk executor, NHWC bf16.
+
+Every conv feeds its BN's batch statistics from the GEMM epilogue; the block tail
+relu(bn3(y3) + bn_sc(y_sc) | + x) is ONE fused pass; backward fuses relu-mask + both BNs of the
+block tail and adds the identity-shortcut gradient inside the first conv's dgrad epilogue.
+Variable names follow the Keras/TF ResNet convention (conv1, bn_conv1, res2a_branch2a, ...,
+fc1000) so checkpoints line up with TF-era tooling.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import norm as BN
+from ..ops import pool as PL
+from ..ops.loss import softmax_xent
+from ..runtime.arena import ParamArena
+from ..runtime.layers import BatchNorm, Conv2d, Linear
+
+DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
+IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
+
+
+class Bottleneck:
+    def __init__(self, arena, stage: int, idx: int, cin: int, width: int, stride: int):
+        tag = f"{stage}{chr(ord('a') + idx)}"
+        cout = width * 4
+        self.stride = stride
+        self.conv1 = Conv2d(arena, f"res{tag}_branch2a", cin, width, 1)
+        self.bn1 = BatchNorm(arena, f"bn{tag}_branch2a", width)
+        self.conv2 = Conv2d(arena, f"res{tag}_branch2b", width, width, 3, stride=stride)
+        self.bn2 = BatchNorm(arena, f"bn{tag}_branch2b", width)
+        self.conv3 = Conv2d(arena, f"res{tag}_branch2c", width, cout, 1)
+        self.bn3 = BatchNorm(arena, f"bn{tag}_branch2c", cout, zero_gamma=False)
+        self.proj = stride != 1 or cin != cout
+        if self.proj:
+            self.conv_sc = Conv2d(arena, f"res{tag}_branch1", cin, cout, 1, stride=stride, pad=0)
+            self.bn_sc = BatchNorm(arena, f"bn{tag}_branch1", cout)
+        self.arena = arena
+
+    def bns(self):
+        return [self.bn1, self.bn2, self.bn3] + ([self.bn_sc] if self.proj else [])
+
+    def forward(self, x, training=True):
+        dev = x.device
+        s1, s2, s3 = self.bn1.state(dev), self.bn2.state(dev), self.bn3.state(dev)
+        y1 = self.conv1.forward(x, s1 if training else None)
+        if training:
+            self.bn1.finalize(y1.numel() // y1.shape[-1])
+        a1 = BN.bn_apply(y1, s1, relu=True)
+        y2 = self.conv2.forward(a1, s2 if training else None)
+        if training:
+            self.bn2.finalize(y2.numel() // y2.shape[-1])
+        a2 = BN.bn_apply(y2, s2, relu=True)
+        y3 = self.conv3.forward(a2, s3 if training else None)
+        if training:
+            self.bn3.finalize(y3.numel() // y3.shape[-1])
+        ysc = None
+        if self.proj:
+            ssc = self.bn_sc.state(dev)
+            ysc = self.conv_sc.forward(x, ssc if training else None)
+            if training:
+                self.bn_sc.finalize(ysc.numel() // ysc.shape[-1])
+            out = BN.bn_apply(y3, s3, relu=True, r=ysc, rst=ssc)
+        else:
+            out = BN.bn_apply(y3, s3, relu=True, r=x)
+        if training:
+            self.saved = (x, y1, a1, y2, a2, y3, ysc, out)
+        return out
+
+    def backward(self, dout, need_dx=True):
+        x, y1, a1, y2, a2, y3, ysc, out = self.saved
+        self.saved = None
+        cnt3 = y3.numel() // y3.shape[-1]
+        if self.proj:
+            dy3, dysc, _ = BN.bn_backward(dout, out, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
+                                          self.bn3.beta.grad, cnt3, y2=ysc, st2=self.bn_sc.st,
+                                          gamma2=self.bn_sc.gamma.master, dgamma2=self.bn_sc.gamma.grad,
+                                          dbeta2=self.bn_sc.beta.grad)
+            dres = None
+            self.arena.grad_ready(self.bn3.gamma, self.bn3.beta, self.bn_sc.gamma, self.bn_sc.beta)
+        else:
+            dy3, _, dres = BN.bn_backward(dout, out, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
+                                          self.bn3.beta.grad, cnt3, want_dres=True)
+            self.arena.grad_ready(self.bn3.gamma, self.bn3.beta)
+        da2 = self.conv3.backward(dy3, a2)
+        dy2, _, _ = BN.bn_backward(da2, a2, y2, self.bn2.st, self.bn2.gamma.master, self.bn2.gamma.grad,
+                                   self.bn2.beta.grad, y2.numel() // y2.shape[-1])
+        self.arena.grad_ready(self.bn2.gamma, self.bn2.beta)
+        da1 = self.conv2.backward(dy2, a1)
+        dy1, _, _ = BN.bn_backward(da1, a1, y1, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
+                                   self.bn1.beta.grad, y1.numel() // y1.shape[-1])
+        self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
+        if self.proj:
+            dx = self.conv1.backward(dy1, x, need_dx=need_dx)
+            dx = self.conv_sc.backward(dysc, x, need_dx=need_dx, resid=dx)
+        else:
+            dx = self.conv1.backward(dy1, x, need_dx=need_dx, resid=dres)
+        return dx
+
+
+class ResNet:
+    """ResNet v1.5 on the tfk executor. Input: NHWC bf16 [N,224,224,8] (RGB + zero pad)."""
+
+    def __init__(self, depth: int = 50, num_classes: int = 1000, width: int = 64, label_smoothing: float = 0.1):
+        if depth not in DEPTHS or DEPTHS[depth] is None:
+            raise ValueError(f"unsupported ResNet depth {depth}")
+        self.depth, self.num_classes, self.label_smoothing = depth, num_classes, label_smoothing
+        self.name = f"resnet{depth}"
+        a = self.arena = ParamArena()
+        self.conv1 = Conv2d(a, "conv1", IN_CH_PAD, width, 7, stride=2, pad=3, cin_real=3)
+        self.bn1 = BatchNorm(a, "bn_conv1", width)
+        self.blocks: list[Bottleneck] = []
+        cin = width
+        for si, n in enumerate(DEPTHS[depth]):
+            w = width * (2 ** si)
+            for bi in range(n):
+                stride = 2 if (bi == 0 and si > 0) else 1
+                self.blocks.append(Bottleneck(a, si + 2, bi, cin, w, stride))
+                cin = w * 4
+        self.fc = Linear(a, "fc1000", cin, num_classes, init="normal", std=0.01)
+        self.feat = cin
+        self.training = True
+
+    # ------------------------------------------------------------------ setup
+    def to(self, device, seed: int = 1234) -> "ResNet":
+        self.arena.finalize(device, seed)
+        return self
+
+    def batchnorms(self):
+        out = [self.bn1]
+        for b in self.blocks:
+            out += b.bns()
+        return out
+
+    def train(self, mode: bool = True) -> "ResNet":
+        self.training = mode
+        for bn in self.batchnorms():
+            bn.training = mode
+        return self
+
+    # ------------------------------------------------------------------ compute
+    def _features(self, x):
+        dev = x.device
+        st = self.bn1.state(dev)
+        y0 = self.conv1.forward(x, st if self.training else None)
+        if self.training:
+            self.bn1.finalize(y0.numel() // y0.shape[-1])
+        else:
+            self._eval_stats()
+        a0 = BN.bn_apply(y0, st, relu=True)
+        p0, idx = PL.maxpool_fwd(a0, 3, 2, 1)
+        h = p0
+        for b in self.blocks:
+            h = b.forward(h, self.training)
+        f = PL.avgpool_fwd(h)
+        if self.training:
+            self._saved = (x, y0, a0, idx, h.shape, f)
+        return f
+
+    def _eval_stats(self):
+        for bn in self.batchnorms():
+            bn.state(self.arena.device)
+            bn.use_running_stats()
+
+    def forward(self, x):
+        """Eval forward -> logits bf16 [N, classes]."""
+        if not self.training:
+            self._eval_stats()
+        f = self._features(x)
+        return self.fc.forward(f)
+
+    def forward_backward(self, x, labels, loss_scale: float = 1.0):
+        """One training forward + backward. Returns (loss_sum f32[N] per-row, correct f32[N]).
+        Gradients land in arena.grad (mean over the local batch)."""
+        f = self._features(x)
+        logits = self.fc.forward(f)
+        B = logits.shape[0]
+        loss, dlogits, corr = softmax_xent(logits, labels, smoothing=self.label_smoothing, scale=loss_scale / B,
+                                           want_correct=True)
+        df = self.fc.backward(dlogits, f)
+        x0, y0, a0, idx, hshape, _ = self._saved
+        self._saved = None
+        dh = PL.avgpool_bwd(df, hshape)
+        for i in range(len(self.blocks) - 1, -1, -1):
+            dh = self.blocks[i].backward(dh)
+        da0 = PL.maxpool_bwd(dh, idx, a0.shape, 3, 2, 1)
+        dy0, _, _ = BN.bn_backward(da0, a0, y0, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
+                                   self.bn1.beta.grad, y0.numel() // y0.shape[-1])
+        self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
+        self.conv1.backward(dy0, x0, need_dx=False)
+        return loss, corr
+
+
+def resnet50(**kw) -> ResNet:
+    return ResNet(50, **kw)
+
+
+def resnet101(**kw) -> ResNet:
+    return ResNet(101, **kw)
+
+
+def resnet152(**kw) -> ResNet:
+    return ResNet(152, **kw)
+
+
+def synthetic_imagenet(batch: int, device, image_size: int = 224, num_classes: int = 1000, seed: int = 0):
+    """On-device synthetic ImageNet-shaped batch: NHWC bf16 [B,224,224,8] (3 real channels,
+    uniform [-1,1)) + int32 labels. Generated by HIP kernels on GPU (no H2D)."""
+    x = torch.empty(batch, image_size, image_size, IN_CH_PAD, dtype=torch.bfloat16, device=device)
+    y = torch.empty(batch, dtype=torch.int32, device=device)
+    if x.is_cuda:
+        from ..ops._lib import lib
+        lib().synth_uniform(x, batch * image_size * image_size, 3, IN_CH_PAD, -1.0, 1.0, seed)
+        lib().synth_labels(y, num_classes, seed + 1)
+    else:
+        g = torch.Generator().manual_seed(seed)
+        x.zero_()
+        x[..., :3] = (torch.rand(batch, image_size, image_size, 3, generator=g) * 2 - 1).to(torch.bfloat16)
+        y.copy_(torch.randint(0, num_classes, (batch,), generator=g, dtype=torch.int32))
+    return x, y

@@ -1,0 +1,290 @@
+"""Matrix-multiply and NHWC convolution ops on the tfk MFMA implicit-GEMM engine (csrc/kernels/gemm.hip).
+
+Layouts (MI355X-first, not a translation of TF's): activations NHWC bf16, conv weights OHWI bf16
+([Cout][R][S][Cin], the K-contiguous "B" operand of the forward GEMM), linear weights [out][in].
+All weight gradients are produced in f32 directly into the caller's (flat-arena) grad view.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from ._lib import lib, on_gpu, workspace
+
+A_KIN, A_KOUT, A_CONV_FWD, A_CONV_DGRAD = 0, 1, 2, 3
+B_KIN, B_KOUT, B_CONV_WGRAD = 0, 1, 2
+EPI_BF16, EPI_F32 = 0, 1
+ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+NO_CONV = [0] * 15
+TARGET_BLOCKS = 1024  # ~4 blocks per CU on 256 CUs
+
+
+@dataclass(frozen=True)
+class ConvGeom:
+    N: int
+    H: int
+    W: int
+    C: int
+    K: int  # output channels
+    R: int
+    S: int
+    sh: int = 1
+    sw: int = 1
+    ph: int = 0
+    pw: int = 0
+    dh: int = 1
+    dw: int = 1
+
+    @property
+    def P(self) -> int:
+        return (self.H + 2 * self.ph - self.dh * (self.R - 1) - 1) // self.sh + 1
+
+    @property
+    def Q(self) -> int:
+        return (self.W + 2 * self.pw - self.dw * (self.S - 1) - 1) // self.sw + 1
+
+    def vec(self):
+        return [self.N, self.H, self.W, self.C, self.P, self.Q, self.K, self.R, self.S, self.sh, self.sw, self.ph,
+                self.pw, self.dh, self.dw]
+
+    @property
+    def pointwise(self) -> bool:
+        return self.R == 1 and self.S == 1 and self.sh == 1 and self.sw == 1 and self.ph == 0 and self.pw == 0
+
+    def flops(self) -> int:
+        return 2 * self.N * self.P * self.Q * self.K * self.R * self.S * self.C
+
+
+def pick_tile(M: int, N: int, splits_ok: bool = False):
+    """Largest tile that still yields enough blocks to fill 256 CUs (8 XCDs x 32)."""
+    def tiles(bm, bn):
+        return ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
+    if N <= 64:
+        return (128, 64) if tiles(128, 64) >= 256 or splits_ok else (64, 64)
+    if tiles(128, 128) >= 512 or splits_ok and M >= 128:
+        return (128, 128)
+    if tiles(128, 64) >= 512:
+        return (128, 64)
+    return (64, 64)
+
+
+def pick_splits(tiles: int, K: int, min_ktiles: int = 4) -> int:
+    nkt = (K + 63) // 64
+    if tiles >= TARGET_BLOCKS // 2:
+        return 1
+    s = max(1, TARGET_BLOCKS // max(tiles, 1))
+    s = min(s, max(1, nkt // min_ktiles))
+    return s
+
+
+def _gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile, *, alpha=1.0, beta=0.0, bias=None, resid=None,
+          act=0, stats=None, shards=1, splits=1, batch=1, sA=0, sB=0, sC=0, split_stride=0, conv=NO_CONV):
+    lib().gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile[0], tile[1], alpha, beta, bias, resid, act,
+               stats, shards, splits, batch, sA, sB, sC, split_stride, conv)
+
+
+def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, accumulate: bool, device,
+                    force_splits: int | None = None):
+    """Run an f32-epilogue GEMM with split-K into a workspace, then reduce into `out` ([M][N] f32)."""
+    splits = force_splits if force_splits is not None else pick_splits(tiles, K)
+    ns = int(lib().gemm_splits(K, splits))
+    if ns == 1:
+        run(out, 1, 0, 1.0 if accumulate else 0.0)
+        return
+    stride = ((M * N + 3) // 4) * 4
+    ws = workspace(device, ns * stride)
+    run(ws, splits, stride, 0.0)
+    lib().splitk_reduce(ws, ns, stride, M * N, out, None, accumulate, 1.0)
+
+
+# =========================================================================== linear
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
+               resid: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """y[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ resid). bf16 in/out, f32 accumulate."""
+    M, K = x.shape[0], x.shape[-1]
+    N = w.shape[0]
+    if not on_gpu(x):
+        y = x.float() @ w.float().t()
+        if bias is not None:
+            y = y + bias.float()
+        if ACT[act] == 1:
+            y = torch.relu(y)
+        elif ACT[act] == 2:
+            y = F.gelu(y, approximate="tanh")
+        y = y.to(torch.bfloat16)
+        if resid is not None:
+            y = (y.float() + resid.float()).to(torch.bfloat16)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    _gemm(x2, w, y, M, N, K, K, K, N, A_KIN, B_KIN, EPI_BF16, pick_tile(M, N), bias=bias, act=ACT[act],
+          resid=resid.reshape(-1, N) if resid is not None else None)
+    return y
+
+
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None = None) -> torch.Tensor:
+    """dx[M,K] = dy[M,N] @ w[N,K] (+ resid)."""
+    N, K = w.shape
+    dy2 = dy.reshape(-1, N)
+    M = dy2.shape[0]
+    if not on_gpu(dy):
+        dx = (dy2.float() @ w.float()).to(torch.bfloat16)
+        if resid is not None:
+            dx = (dx.float() + resid.reshape(-1, K).float()).to(torch.bfloat16)
+        return dx
+    dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
+    _gemm(dy2, w, dx, M, K, N, N, K, K, A_KIN, B_KOUT, EPI_BF16, pick_tile(M, K),
+          resid=resid.reshape(-1, K) if resid is not None else None)
+    return dx
+
+
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate: bool = False) -> None:
+    """gw[N,K] (f32) (+)= dy[M,N]^T @ x[M,K]."""
+    N = dy.shape[-1]
+    K = x.shape[-1]
+    dy2, x2 = dy.reshape(-1, N), x.reshape(-1, K)
+    M = dy2.shape[0]
+    if not on_gpu(dy):
+        g = dy2.float().t() @ x2.float()
+        if accumulate:
+            gw.view(N, K).add_(g)
+        else:
+            gw.view(N, K).copy_(g)
+        return
+    tile = pick_tile(N, K, splits_ok=True)
+    tiles = ((N + tile[0] - 1) // tile[0]) * ((K + tile[1] - 1) // tile[1])
+
+    def run(C, splits, stride, beta):
+        _gemm(dy2, x2, C, N, K, M, N, K, K, A_KOUT, B_KOUT, EPI_F32, tile, beta=beta, splits=splits,
+              split_stride=stride)
+    _f32_out_splitk(run, N, K, M, tiles, gw.view(-1), accumulate, dy.device)
+
+
+def bias_grad(dy: torch.Tensor, gb: torch.Tensor, accumulate: bool = False) -> None:
+    N = dy.shape[-1]
+    dy2 = dy.reshape(-1, N)
+    if not on_gpu(dy):
+        g = dy2.float().sum(0)
+        gb.add_(g) if accumulate else gb.copy_(g)
+        return
+    if not accumulate:
+        gb.zero_()
+    lib().colsum(dy2, dy2.shape[0], N, N, gb)
+
+
+def matmul_tn(a: torch.Tensor, b: torch.Tensor, out_f32: torch.Tensor | None = None) -> torch.Tensor:
+    """[M,N] = a[K,M]^T @ b[K,N]; f32 output."""
+    K, M = a.shape
+    N = b.shape[1]
+    out = out_f32 if out_f32 is not None else torch.empty(M, N, dtype=torch.float32, device=a.device)
+    if not on_gpu(a):
+        out.copy_(a.float().t() @ b.float())
+        return out
+    tile = pick_tile(M, N, splits_ok=True)
+    tiles = ((M + tile[0] - 1) // tile[0]) * ((N + tile[1] - 1) // tile[1])
+
+    def run(C, splits, stride, beta):
+        _gemm(a, b, C, M, N, K, M, N, N, A_KOUT, B_KOUT, EPI_F32, tile, beta=beta, splits=splits, split_stride=stride)
+    _f32_out_splitk(run, M, N, K, tiles, out.view(-1), False, a.device)
+    return out
+
+
+# =========================================================================== conv (NHWC)
+def _ref_conv(x, w, g: ConvGeom):
+    xn = x.float().permute(0, 3, 1, 2)
+    wn = w.float().permute(0, 3, 1, 2)
+    y = F.conv2d(xn, wn, stride=(g.sh, g.sw), padding=(g.ph, g.pw), dilation=(g.dh, g.dw))
+    return y.permute(0, 2, 3, 1)
+
+
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor | None = None,
+             shards: int = 1) -> torch.Tensor:
+    """y[N,P,Q,K] = conv(x[N,H,W,C], w[K,R,S,C]); optionally accumulates BN batch statistics
+    (sum, sumsq per output channel) of the f32 result into stats[shards][2][K]."""
+    if not on_gpu(x):
+        y = _ref_conv(x, w, g)
+        if stats is not None:
+            yf = y.reshape(-1, g.K)
+            stats.view(shards, 2, g.K)[0, 0] += yf.sum(0)
+            stats.view(shards, 2, g.K)[0, 1] += (yf * yf).sum(0)
+        return y.to(torch.bfloat16).contiguous()
+    M = g.N * g.P * g.Q
+    y = torch.empty(g.N, g.P, g.Q, g.K, dtype=torch.bfloat16, device=x.device)
+    tile = pick_tile(M, g.K)
+    if g.pointwise:
+        _gemm(x, w, y, M, g.K, g.C, g.C, g.C, g.K, A_KIN, B_KIN, EPI_BF16, tile, stats=stats, shards=shards)
+    else:
+        Kd = g.R * g.S * g.C
+        _gemm(x, w, y, M, g.K, Kd, 0, Kd, g.K, A_CONV_FWD, B_KIN, EPI_BF16, tile, stats=stats, shards=shards,
+              conv=g.vec())
+    return y
+
+
+def conv_weight_t(w: torch.Tensor, g: ConvGeom, out: torch.Tensor | None = None) -> torch.Tensor:
+    """OHWI [K][R][S][C] -> [C][R][S][K] (dgrad B operand)."""
+    if not on_gpu(w):
+        return w.permute(3, 1, 2, 0).contiguous()
+    out = out if out is not None else torch.empty(g.C, g.R, g.S, g.K, dtype=torch.bfloat16, device=w.device)
+    lib().transpose_arb(w, out, g.K, g.R * g.S, g.C)
+    return out
+
+
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tensor | None = None,
+               wt: torch.Tensor | None = None) -> torch.Tensor:
+    """dx[N,H,W,C] = conv_transpose(dy[N,P,Q,K], w) (+ resid)."""
+    if not on_gpu(dy):
+        dyn = dy.float().permute(0, 3, 1, 2)
+        wn = w.float().permute(0, 3, 1, 2)
+        out_pad = (g.H - ((g.P - 1) * g.sh - 2 * g.ph + g.dh * (g.R - 1) + 1),
+                   g.W - ((g.Q - 1) * g.sw - 2 * g.pw + g.dw * (g.S - 1) + 1))
+        dx = F.conv_transpose2d(dyn, wn, stride=(g.sh, g.sw), padding=(g.ph, g.pw), output_padding=out_pad,
+                                dilation=(g.dh, g.dw)).permute(0, 2, 3, 1)
+        if resid is not None:
+            dx = dx.to(torch.bfloat16).float() + resid.float()
+        return dx.to(torch.bfloat16).contiguous()
+    M = g.N * g.H * g.W
+    dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
+    tile = pick_tile(M, g.C)
+    if g.pointwise:
+        _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid)
+    elif g.R == 1 and g.S == 1:
+        # strided 1x1: B(n=c, k=co) = W[co][c] is K-outer with ldb = C; gather handles the stride
+        _gemm(dy, w, dx, M, g.C, g.K, 0, g.C, g.C, A_CONV_DGRAD, B_KOUT, EPI_BF16, tile, resid=resid,
+              conv=g.vec())
+    else:
+        wt = wt if wt is not None else conv_weight_t(w, g)
+        Kd = g.R * g.S * g.K
+        _gemm(dy, wt, dx, M, g.C, Kd, 0, Kd, g.C, A_CONV_DGRAD, B_KIN, EPI_BF16, tile, resid=resid, conv=g.vec())
+    return dx
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor, accumulate: bool = False,
+               splits: int | None = None) -> None:
+    """gw[K][R][S][C] (f32) (+)= sum over (n,p,q) dy[n,p,q,k] * x[n, p*sh-ph+r, q*sw-pw+s, c]."""
+    Nn = g.R * g.S * g.C
+    Kp = g.N * g.P * g.Q
+    if not on_gpu(dy):
+        xn = x.float().permute(0, 3, 1, 2)
+        dyn = dy.float().permute(0, 3, 1, 2)
+        gwt = torch.nn.grad.conv2d_weight(xn, (g.K, g.C, g.R, g.S), dyn, stride=(g.sh, g.sw), padding=(g.ph, g.pw),
+                                          dilation=(g.dh, g.dw)).permute(0, 2, 3, 1).reshape(g.K, Nn)
+        v = gw.view(g.K, Nn)
+        v.add_(gwt) if accumulate else v.copy_(gwt)
+        return
+    tile = pick_tile(g.K, Nn, splits_ok=True)
+    tiles = ((g.K + tile[0] - 1) // tile[0]) * ((Nn + tile[1] - 1) // tile[1])
+
+    def run(C, sp, stride, beta):
+        if g.pointwise:
+            _gemm(dy, x, C, g.K, Nn, Kp, g.K, g.C, Nn, A_KOUT, B_KOUT, EPI_F32, tile, beta=beta, splits=sp,
+                  split_stride=stride)
+        else:
+            _gemm(dy, x, C, g.K, Nn, Kp, g.K, 0, Nn, A_KOUT, B_CONV_WGRAD, EPI_F32, tile, beta=beta, splits=sp,
+                  split_stride=stride, conv=g.vec())
+    _f32_out_splitk(run, g.K, Nn, Kp, tiles, gw.view(-1), accumulate, dy.device, force_splits=splits)

@@ -1,0 +1,33 @@
+"""Fused softmax cross-entropy forward+backward (csrc/kernels/loss.hip)."""
+from __future__ import annotations
+
+import torch
+
+from ._lib import lib, on_gpu
+
+
+def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.0, ignore_index: int = -100,
+                 scale: float = 1.0, want_grad: bool = True, want_correct: bool = False):
+    """Returns (per-row loss f32 [B], dlogits bf16 [B,V] = scale*(softmax - target) or None, correct f32 [B] or None)."""
+    B, V = logits.shape
+    if not on_gpu(logits):
+        x = logits.float()
+        lse = torch.logsumexp(x, dim=1)
+        valid = (labels != ignore_index) & (labels >= 0) & (labels < V)
+        lab = labels.clamp(0, V - 1).long()
+        nll = lse - x.gather(1, lab[:, None])[:, 0]
+        smooth = lse - x.mean(1)
+        loss = torch.where(valid, (1 - smoothing) * nll + smoothing * smooth, torch.zeros_like(lse))
+        d = None
+        if want_grad:
+            p = torch.softmax(x, dim=1)
+            t = torch.full_like(p, smoothing / V)
+            t.scatter_add_(1, lab[:, None], torch.full((B, 1), 1 - smoothing))
+            d = (scale * (p - t) * valid[:, None]).to(torch.bfloat16)
+        corr = ((x.argmax(1) == lab) & valid).float() if want_correct else None
+        return loss, d, corr
+    loss = torch.empty(B, dtype=torch.float32, device=logits.device)
+    d = torch.empty_like(logits) if want_grad else None
+    corr = torch.empty(B, dtype=torch.float32, device=logits.device) if want_correct else None
+    lib().softmax_xent(logits, labels, B, V, V, smoothing, ignore_index, scale, loss, d, corr)
+    return loss, d, corr

@@ -1,0 +1,117 @@
+"""Training-mode BatchNorm for NHWC bf16 activations (csrc/kernels/bn.hip).
+
+Forward statistics come from the producing conv's GEMM epilogue (``stats`` buffer), so the
+forward is finalize + one fused apply pass; the projection-shortcut BN can be folded into the
+residual add of the same pass (dual form). Backward is reduce -> finalize -> apply.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import lib, on_gpu
+
+SHARDS = 32
+
+
+class BNState:
+    """Per-BN-layer device state: stats accumulators and the per-step saved statistics."""
+
+    def __init__(self, C: int, device, shards: int = SHARDS):
+        self.C = C
+        self.shards = shards if torch.device(device).type == "cuda" else 1
+        self.stats = torch.zeros(self.shards * 2 * C, dtype=torch.float32, device=device)
+        self.sums = torch.zeros(self.shards * 3 * C, dtype=torch.float32, device=device)
+        self.mean = torch.zeros(C, dtype=torch.float32, device=device)
+        self.invstd = torch.ones(C, dtype=torch.float32, device=device)
+        self.scale = torch.ones(C, dtype=torch.float32, device=device)
+        self.shift = torch.zeros(C, dtype=torch.float32, device=device)
+        self.coef = torch.zeros(3 * C, dtype=torch.float32, device=device)
+
+
+def bn_finalize(st: BNState, count: float, gamma, beta, eps, momentum, run_mean, run_var) -> None:
+    C = st.C
+    if not on_gpu(st.stats):
+        s = st.stats.view(st.shards, 2, C).sum(0)
+        mean = s[0] / count
+        var = (s[1] / count - mean * mean).clamp_min(0)
+        inv = torch.rsqrt(var + eps)
+        st.mean.copy_(mean); st.invstd.copy_(inv)
+        st.scale.copy_(gamma * inv); st.shift.copy_(beta - mean * gamma * inv)
+        if run_mean is not None:
+            unb = var * count / max(count - 1.0, 1.0)
+            run_mean.mul_(1 - momentum).add_(momentum * mean)
+            run_var.mul_(1 - momentum).add_(momentum * unb)
+        st.stats.zero_()
+        return
+    lib().bn_finalize(st.stats, st.shards, C, float(count), gamma, beta, eps, momentum, run_mean, run_var, st.mean,
+                      st.invstd, st.scale, st.shift)
+
+
+def bn_stats(y: torch.Tensor, st: BNState) -> None:
+    """Accumulate batch statistics of y (for producers without a fused-stats epilogue)."""
+    C = st.C
+    if not on_gpu(y):
+        yf = y.float().reshape(-1, C)
+        v = st.stats.view(st.shards, 2, C)
+        v[0, 0] += yf.sum(0); v[0, 1] += (yf * yf).sum(0)
+        return
+    lib().bn_stats(y, y.numel() // C, C, st.stats, st.shards)
+
+
+def bn_apply(y, st: BNState, relu: bool, r=None, rst: BNState | None = None, out=None) -> torch.Tensor:
+    """a = relu?(y*scale + shift [+ r | + r*rscale + rshift])."""
+    C = st.C
+    if not on_gpu(y):
+        o = y.float() * st.scale + st.shift
+        if r is not None:
+            o = o + (r.float() * rst.scale + rst.shift if rst is not None else r.float())
+        if relu:
+            o = torch.relu(o)
+        o = o.to(torch.bfloat16)
+        if out is not None:
+            out.copy_(o)
+            return out
+        return o
+    out = out if out is not None else torch.empty_like(y)
+    lib().bn_apply(y, st.scale, st.shift, r, rst.scale if rst is not None else None,
+                   rst.shift if rst is not None else None, relu, out, y.numel() // C, C)
+    return out
+
+
+def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=None, st2: BNState | None = None,
+                gamma2=None, dgamma2=None, dbeta2=None, want_dres: bool = False):
+    """Backward of a = relu?(bn(y) [+ bn2(y2) | + r]).
+
+    a: post-activation output used for the relu mask (None -> no relu). Returns (dy, dy2, dres).
+    Writes dgamma/dbeta (and the second BN's) into the given (arena) views."""
+    C = st.C
+    if not on_gpu(da):
+        dz = da.float()
+        if a is not None:
+            dz = dz * (a.float() > 0)
+        dz2 = dz.reshape(-1, C)
+        xh = (y.float().reshape(-1, C) - st.mean) * st.invstd
+        s0, s1 = dz2.sum(0), (dz2 * xh).sum(0)
+        dgamma.copy_(s1); dbeta.copy_(s0)
+        dy = (gamma * st.invstd) * (dz2 - s0 / count - xh * (s1 / count))
+        dy = dy.reshape(da.shape).to(torch.bfloat16)
+        dy2 = None
+        if y2 is not None:
+            xh2 = (y2.float().reshape(-1, C) - st2.mean) * st2.invstd
+            s2 = (dz2 * xh2).sum(0)
+            dgamma2.copy_(s2); dbeta2.copy_(s0)
+            dy2 = ((gamma2 * st2.invstd) * (dz2 - s0 / count - xh2 * (s2 / count))).reshape(da.shape).to(torch.bfloat16)
+        dres = dz.to(torch.bfloat16) if want_dres else None
+        return dy, dy2, dres
+    M = da.numel() // C
+    L = lib()
+    L.bn_bwd_reduce(da, a, y, st.mean, st.invstd, y2, st2.mean if st2 else None, st2.invstd if st2 else None, M, C,
+                    st.sums, st.shards)
+    L.bn_bwd_finalize(st.sums, st.shards, C, float(count), gamma, st.invstd, gamma2, st2.invstd if st2 else None,
+                      dgamma, dbeta, dgamma2, dbeta2, st.coef, st2.coef if st2 else None)
+    dy = torch.empty_like(da)
+    dy2 = torch.empty_like(da) if y2 is not None else None
+    dres = torch.empty_like(da) if want_dres else None
+    L.bn_bwd_apply(da, a, y, st.mean, st.invstd, st.coef, dy, y2, st2.mean if st2 else None,
+                   st2.invstd if st2 else None, st2.coef if st2 else None, dy2, dres, M, C)
+    return dy, dy2, dres

@@ -1,0 +1,54 @@
+"""NHWC pooling ops (csrc/kernels/pool.hip)."""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ._lib import lib, on_gpu
+
+
+def _out(n, k, s, p):
+    return (n + 2 * p - k) // s + 1
+
+
+def maxpool_fwd(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1):
+    N, H, W, C = x.shape
+    P, Q = _out(H, k, s, p), _out(W, k, s, p)
+    if not on_gpu(x):
+        xn = x.float().permute(0, 3, 1, 2)
+        y, idx = F.max_pool2d(xn, k, s, p, return_indices=True)
+        return y.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous(), (idx, xn.shape)
+    y = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=x.device)
+    idx = torch.empty(N, P, Q, C, dtype=torch.uint8, device=x.device)
+    lib().maxpool_fwd(x, y, idx, [N, H, W, C, P, Q, k, k, s, s, p, p])
+    return y, idx
+
+
+def maxpool_bwd(dy: torch.Tensor, idx, x_shape, k: int = 3, s: int = 2, p: int = 1) -> torch.Tensor:
+    N, H, W, C = x_shape
+    if not on_gpu(dy):
+        ind, nshape = idx
+        dx = F.max_unpool2d(dy.float().permute(0, 3, 1, 2), ind, k, s, p, output_size=nshape[-2:])
+        return dx.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+    P, Q = dy.shape[1], dy.shape[2]
+    dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
+    lib().maxpool_bwd(dy, idx, dx, [N, H, W, C, P, Q, k, k, s, s, p, p])
+    return dx
+
+
+def avgpool_fwd(x: torch.Tensor) -> torch.Tensor:
+    N, H, W, C = x.shape
+    if not on_gpu(x):
+        return x.float().mean(dim=(1, 2)).to(torch.bfloat16)
+    y = torch.empty(N, C, dtype=torch.bfloat16, device=x.device)
+    lib().avgpool_fwd(x, y, N, H * W, C)
+    return y
+
+
+def avgpool_bwd(dy: torch.Tensor, x_shape) -> torch.Tensor:
+    N, H, W, C = x_shape
+    if not on_gpu(dy):
+        return (dy.float()[:, None, None, :] / (H * W)).expand(N, H, W, C).to(torch.bfloat16).contiguous()
+    dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
+    lib().avgpool_bwd(dy, dx, N, H * W, C)
+    return dx

@@ -1,0 +1,122 @@
+"""Executor layers with explicit forward/backward on the tfk kernel library.
+
+No torch autograd in the hot path: each layer saves exactly what its backward needs, writes its
+weight gradients straight into the flat arena (f32) and signals readiness to the data-parallel
+strategy, so all-reduce of early buckets overlaps the rest of backward.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops import gemm as G
+from ..ops import norm as BN
+from .arena import ParamArena, ParamSpec
+
+
+def _ohwi_to_hwio(a: np.ndarray, cin_real: int | None = None) -> np.ndarray:
+    a = np.transpose(a, (1, 2, 3, 0))  # [R,S,C,K]
+    return a[:, :, :cin_real, :] if cin_real is not None else a
+
+
+def _hwio_to_ohwi(a: np.ndarray, cin_pad: int | None = None) -> np.ndarray:
+    if cin_pad is not None and a.shape[2] < cin_pad:
+        pad = np.zeros(a.shape[:2] + (cin_pad - a.shape[2], a.shape[3]), dtype=a.dtype)
+        a = np.concatenate([a, pad], axis=2)
+    return np.ascontiguousarray(np.transpose(a, (3, 0, 1, 2)))
+
+
+class Conv2d:
+    """NHWC conv, OHWI weight. TF variable: <name>/kernel in HWIO."""
+
+    def __init__(self, arena: ParamArena, name: str, cin: int, cout: int, k: int, stride: int = 1, pad: int | None = None,
+                 cin_real: int | None = None):
+        self.cin, self.cout, self.k, self.stride = cin, cout, k, stride
+        self.pad = (k - 1) // 2 if pad is None else pad
+        real = cin_real if cin_real is not None else cin
+        post = None
+        if real != cin:
+            def post(t, real=real):
+                t[..., real:] = 0
+                return t
+        self.w = arena.add(ParamSpec(
+            f"{name}/kernel", (cout, k, k, cin), init="he_normal", fan_in=k * k * real, fan_out=k * k * cout,
+            to_tf=lambda a, real=real: _ohwi_to_hwio(a, real), from_tf=lambda a, c=cin: _hwio_to_ohwi(a, c),
+            tf_shape=(k, k, real, cout), post_init=post))
+        self.arena = arena
+
+    def geom(self, x_shape) -> G.ConvGeom:
+        N, H, W, C = x_shape
+        assert C == self.cin, f"conv expects {self.cin} input channels, got {C}"
+        return G.ConvGeom(N, H, W, C, self.cout, self.k, self.k, self.stride, self.stride, self.pad, self.pad)
+
+    def forward(self, x, stats: BN.BNState | None = None):
+        g = self.geom(x.shape)
+        return G.conv_fwd(x, self.w.compute, g, stats.stats if stats else None, stats.shards if stats else 1)
+
+    def backward(self, dy, x, need_dx: bool = True, resid=None):
+        g = self.geom(x.shape)
+        G.conv_wgrad(dy, x, g, self.w.grad)
+        self.arena.grad_ready(self.w)
+        if not need_dx:
+            return None
+        return G.conv_dgrad(dy, self.w.compute, g, resid=resid)
+
+
+class BatchNorm:
+    """Training-mode BN; TF variables <name>/{gamma,beta,moving_mean,moving_variance}."""
+
+    def __init__(self, arena: ParamArena, name: str, C: int, eps: float = 1e-5, momentum: float = 0.1,
+                 zero_gamma: bool = False):
+        self.C, self.eps, self.momentum = C, eps, momentum
+        self.gamma = arena.add(ParamSpec(f"{name}/gamma", (C,), init="zeros" if zero_gamma else "ones", decay=False))
+        self.beta = arena.add(ParamSpec(f"{name}/beta", (C,), init="zeros", decay=False))
+        self.run_mean = arena.add_buffer(f"{name}/moving_mean", torch.zeros(C))
+        self.run_var = arena.add_buffer(f"{name}/moving_variance", torch.ones(C))
+        self.arena = arena
+        self.st: BN.BNState | None = None
+        self.training = True
+
+    def state(self, device) -> BN.BNState:
+        if self.st is None or self.st.mean.device != torch.device(device):
+            self.st = BN.BNState(self.C, device)
+        return self.st
+
+    def finalize(self, count: int) -> None:
+        BN.bn_finalize(self.st, float(count), self.gamma.master, self.beta.master, self.eps, self.momentum,
+                       self.run_mean if self.training else None, self.run_var if self.training else None)
+
+    def use_running_stats(self) -> None:
+        """Inference: scale/shift from the moving statistics."""
+        st = self.st
+        inv = torch.rsqrt(self.run_var + self.eps)
+        st.mean.copy_(self.run_mean); st.invstd.copy_(inv)
+        st.scale.copy_(self.gamma.master * inv)
+        st.shift.copy_(self.beta.master - self.run_mean * self.gamma.master * inv)
+
+
+class Linear:
+    """y = x W^T + b; W stored [out][in] (TF kernel is [in][out])."""
+
+    def __init__(self, arena: ParamArena, name: str, fin: int, fout: int, bias: bool = True, init: str = "xavier_uniform",
+                 std: float = 0.02, kernel_name: str = "kernel"):
+        self.fin, self.fout = fin, fout
+        self.w = arena.add(ParamSpec(f"{name}/{kernel_name}", (fout, fin), init=init, std=std, fan_in=fin, fan_out=fout,
+                                     to_tf=lambda a: np.ascontiguousarray(a.T),
+                                     from_tf=lambda a: np.ascontiguousarray(a.T), tf_shape=(fin, fout)))
+        self.b = arena.add(ParamSpec(f"{name}/bias", (fout,), init="zeros", decay=False)) if bias else None
+        self.arena = arena
+
+    def forward(self, x, act=None, resid=None):
+        return G.linear_fwd(x, self.w.compute, self.b.master if self.b else None, act=act, resid=resid)
+
+    def backward(self, dy, x, need_dx: bool = True, resid=None, accumulate: bool = False):
+        G.linear_wgrad(dy, x, self.w.grad, accumulate=accumulate)
+        if self.b is not None:
+            G.bias_grad(dy, self.b.grad, accumulate=accumulate)
+            self.arena.grad_ready(self.w, self.b)
+        else:
+            self.arena.grad_ready(self.w)
+        if not need_dx:
+            return None
+        return G.linear_dgrad(dy, self.w.compute, resid=resid)

@@ -1,0 +1,138 @@
+"""Optimizers over a ParamArena: one fused launch per parameter group (decay / no-decay).
+
+Slot names follow TF (`Momentum`, `Adam`, `Adam_1`) so checkpoints carry optimizer state the way
+TF-era TFJob workloads did.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import optim as O
+from .arena import ParamArena
+
+
+class LRSchedule:
+    """Linear warmup then cosine/poly/constant decay (per step)."""
+
+    def __init__(self, base_lr: float, warmup: int = 0, total: int = 0, kind: str = "constant", end_lr: float = 0.0,
+                 power: float = 1.0):
+        self.base, self.warmup, self.total, self.kind, self.end, self.power = base_lr, warmup, total, kind, end_lr, power
+
+    def __call__(self, step: int) -> float:
+        if self.warmup and step < self.warmup:
+            return self.base * (step + 1) / self.warmup
+        if self.kind == "constant" or self.total <= self.warmup:
+            return self.base
+        t = min(1.0, (step - self.warmup) / max(1, self.total - self.warmup))
+        if self.kind == "cosine":
+            return self.end + (self.base - self.end) * 0.5 * (1 + math.cos(math.pi * t))
+        if self.kind == "poly":
+            return self.end + (self.base - self.end) * (1 - t) ** self.power
+        return self.base
+
+
+class Optimizer:
+    slot_names: tuple = ()
+
+    def __init__(self, arena: ParamArena, lr, weight_decay: float = 0.0):
+        self.arena = arena
+        self.lr = lr if callable(lr) else LRSchedule(lr)
+        self.wd = weight_decay
+        self.step_count = 0
+        self.grad_scale = 1.0          # e.g. 1/world for gradient averaging
+        self.grad_scale_dev = None     # device scalar (global-norm clipping)
+        self.region = None             # (start, end) restrict to a shard (parameter-server)
+        for s in self.slot_names:
+            arena.slot(s)
+
+    def _regions(self):
+        lo, hi = self.region if self.region is not None else (0, self.arena.numel)
+        d0, d1 = self.arena.decay_region()
+        out = []
+        a, b = max(lo, d0), min(hi, d1)
+        if b > a:
+            out.append((a, b, self.wd))
+        n0, n1 = self.arena.nodecay_region()
+        a, b = max(lo, n0), min(hi, n1)
+        if b > a:
+            out.append((a, b, 0.0))
+        return out
+
+    def state_dict(self):
+        return {"step": self.step_count}
+
+    def load_state_dict(self, d):
+        self.step_count = int(d.get("step", 0))
+
+
+class SGD(Optimizer):
+    slot_names = ("Momentum",)
+
+    def __init__(self, arena, lr, momentum: float = 0.9, weight_decay: float = 5e-5, nesterov: bool = False):
+        super().__init__(arena, lr, weight_decay)
+        self.momentum, self.nesterov = momentum, nesterov
+
+    def step(self):
+        a = self.arena
+        lr = self.lr(self.step_count)
+        m = a.slot("Momentum")
+        for lo, hi, wd in self._regions():
+            O.sgd_(a.master[lo:hi], a.compute[lo:hi], a.grad[lo:hi], m[lo:hi], lr, self.momentum, wd, self.nesterov,
+                   self.grad_scale, self.grad_scale_dev)
+        self.step_count += 1
+
+
+class AdamW(Optimizer):
+    slot_names = ("Adam", "Adam_1")
+
+    def __init__(self, arena, lr, b1=0.9, b2=0.999, eps=1e-6, weight_decay=0.01):
+        super().__init__(arena, lr, weight_decay)
+        self.b1, self.b2, self.eps = b1, b2, eps
+
+    def step(self):
+        a = self.arena
+        self.step_count += 1
+        lr = self.lr(self.step_count - 1)
+        m, v = a.slot("Adam"), a.slot("Adam_1")
+        for lo, hi, wd in self._regions():
+            O.adamw_(a.master[lo:hi], a.compute[lo:hi], a.grad[lo:hi], m[lo:hi], v[lo:hi], lr, self.b1, self.b2,
+                     self.eps, wd, self.step_count, self.grad_scale, self.grad_scale_dev)
+
+
+class LAMB(Optimizer):
+    """Layer-wise adaptive moments (BERT pretraining); trust ratio per parameter tensor."""
+    slot_names = ("Adam", "Adam_1")
+    CHUNK = 4096
+
+    def __init__(self, arena, lr, b1=0.9, b2=0.999, eps=1e-6, weight_decay=0.01):
+        super().__init__(arena, lr, weight_decay)
+        self.b1, self.b2, self.eps = b1, b2, eps
+        self._tables = {}
+        self._u = torch.zeros(arena.numel, dtype=torch.float32, device=arena.device)
+        self._norms = torch.zeros(2 * len(arena.params), dtype=torch.float32, device=arena.device)
+
+    def _chunks(self, lo, hi):
+        key = (lo, hi)
+        if key not in self._tables:
+            starts, lens, segs = [], [], []
+            for p in self.arena.params:
+                s, e = max(p.offset, lo), min(p.offset + p.numel, hi)
+                for c in range(s, e, self.CHUNK):
+                    starts.append(c - lo); lens.append(min(self.CHUNK, e - c)); segs.append(p.index)
+            dev = self.arena.device
+            self._tables[key] = (torch.tensor(starts, dtype=torch.int64, device=dev),
+                                 torch.tensor(lens, dtype=torch.int32, device=dev),
+                                 torch.tensor(segs, dtype=torch.int32, device=dev))
+        return self._tables[key]
+
+    def step(self):
+        a = self.arena
+        self.step_count += 1
+        lr = self.lr(self.step_count - 1)
+        m, v = a.slot("Adam"), a.slot("Adam_1")
+        for lo, hi, wd in self._regions():
+            O.lamb_(a.master[lo:hi], a.compute[lo:hi], a.grad[lo:hi], m[lo:hi], v[lo:hi], self._u[lo:hi],
+                    self._chunks(lo, hi), self._norms, lr, self.b1, self.b2, self.eps, wd, self.step_count,
+                    self.grad_scale, self.grad_scale_dev)

@@ -1,0 +1,185 @@
+"""T5 kernel numerics: every gfx950 HIP kernel against the fp32 torch reference of the same op
+(the CPU path of each ops module), on random data, over the ResNet/BERT shape envelope plus
+ragged tails. Runs only on a real MI355X; the native library must be the thing under test."""
+import pytest
+import torch
+
+from tensorflow_k8s_amd.ops import gemm as G
+from tensorflow_k8s_amd.ops import loss as LS
+from tensorflow_k8s_amd.ops import norm as BN
+from tensorflow_k8s_amd.ops import optim as O
+from tensorflow_k8s_amd.ops import pool as PL
+from tensorflow_k8s_amd.ops._lib import lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16)
+
+
+def test_native_loaded():
+    L = lib()
+    assert hasattr(L, "gemm") and L.__file__.endswith(".so")
+
+
+CONVS = [
+    # N, H, W, C, K, R, S, stride, pad
+    (2, 8, 8, 64, 256, 1, 1, 1, 0),
+    (2, 9, 9, 64, 64, 3, 3, 1, 1),
+    (2, 16, 16, 128, 128, 3, 3, 2, 1),
+    (2, 14, 14, 256, 512, 1, 1, 2, 0),
+    (2, 32, 32, 8, 64, 7, 7, 2, 3),
+    (3, 7, 7, 24, 40, 3, 3, 1, 1),
+    (1, 5, 6, 16, 200, 3, 3, 2, 1),
+]
+
+
+@pytest.mark.parametrize("cfg", CONVS)
+def test_conv_fwd_dgrad_wgrad(cfg):
+    N, H, W, C, K, R, S, st, pd = cfg
+    g = G.ConvGeom(N, H, W, C, K, R, S, st, st, pd, pd)
+    x = bf(N, H, W, C, seed=1)
+    w = bf(K, R, S, C, scale=0.05, seed=2)
+    stats_ref = torch.zeros(2 * K)
+    y_ref = G.conv_fwd(x, w, g, stats_ref, 1)
+    stats = torch.zeros(4 * 2 * K, device=DEV)
+    y = G.conv_fwd(x.to(DEV), w.to(DEV), g, stats, 4)
+    assert y.shape == y_ref.shape
+    assert rel(y, y_ref) < 1e-2
+    s = stats.view(4, 2, K).sum(0).cpu()
+    assert rel(s[0], stats_ref.view(2, K)[0]) < 1e-3
+    assert rel(s[1], stats_ref.view(2, K)[1]) < 1e-3
+    dy = bf(*y_ref.shape, seed=3)
+    resid = bf(N, H, W, C, seed=4)
+    dx_ref = G.conv_dgrad(dy, w, g, resid=resid)
+    dx = G.conv_dgrad(dy.to(DEV), w.to(DEV), g, resid=resid.to(DEV))
+    assert rel(dx, dx_ref) < 1e-2
+    gw_ref = torch.zeros(K, R, S, C)
+    G.conv_wgrad(dy, x, g, gw_ref)
+    gw = torch.zeros(K, R, S, C, device=DEV)
+    G.conv_wgrad(dy.to(DEV), x.to(DEV), g, gw)
+    assert rel(gw, gw_ref) < 5e-3
+    # accumulate path
+    G.conv_wgrad(dy.to(DEV), x.to(DEV), g, gw, accumulate=True)
+    assert rel(gw, 2 * gw_ref) < 5e-3
+
+
+@pytest.mark.parametrize("M,K,N", [(37, 64, 200), (256, 2048, 1000), (512, 768, 3072), (128, 3072, 768), (8, 16, 24)])
+def test_linear(M, K, N):
+    x = bf(M, K, seed=5)
+    w = bf(N, K, scale=0.05, seed=6)
+    b = torch.randn(N)
+    for act in (None, "relu", "gelu"):
+        y_ref = G.linear_fwd(x, w, b, act=act)
+        y = G.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), act=act)
+        assert rel(y, y_ref) < 1e-2, act
+    dy = bf(M, N, seed=7)
+    if K % 8 == 0:
+        assert rel(G.linear_dgrad(dy.to(DEV), w.to(DEV)), G.linear_dgrad(dy, w)) < 1e-2
+    if N % 8 == 0 and K % 8 == 0:
+        gw_ref = torch.zeros(N, K)
+        G.linear_wgrad(dy, x, gw_ref)
+        gw = torch.zeros(N, K, device=DEV)
+        G.linear_wgrad(dy.to(DEV), x.to(DEV), gw)
+        assert rel(gw, gw_ref) < 5e-3
+    gb_ref = torch.zeros(N)
+    G.bias_grad(dy, gb_ref)
+    gb = torch.zeros(N, device=DEV)
+    G.bias_grad(dy.to(DEV), gb)
+    assert rel(gb, gb_ref) < 1e-3
+
+
+def test_gemm_asymmetric_identity():
+    """A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)."""
+    n = 64
+    eye = torch.eye(n).to(torch.bfloat16)
+    B = torch.arange(n * n, dtype=torch.float32).reshape(n, n).remainder(17).to(torch.bfloat16)
+    y = G.linear_fwd(eye.to(DEV), B.to(DEV))  # = I @ B^T
+    assert torch.equal(y.cpu().float(), B.float().t())
+
+
+@pytest.mark.parametrize("proj", [False, True])
+def test_bn_fused_forward_backward(proj):
+    N, H, W, C = 4, 10, 10, 64
+    M = N * H * W
+    y = bf(N, H, W, C, seed=8)
+    y2 = bf(N, H, W, C, seed=9)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C) * 0.1
+    gamma2, beta2 = torch.rand(C) + 0.5, torch.randn(C) * 0.1
+    out = {}
+    for dev in ("cpu", DEV):
+        st, st2 = BN.BNState(C, dev), BN.BNState(C, dev)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        BN.bn_stats(y.to(dev), st)
+        BN.bn_finalize(st, M, gamma.to(dev), beta.to(dev), 1e-5, 0.1, rm, rv)
+        r = y2.to(dev)
+        if proj:
+            BN.bn_stats(r, st2)
+            BN.bn_finalize(st2, M, gamma2.to(dev), beta2.to(dev), 1e-5, 0.1, None, None)
+        a = BN.bn_apply(y.to(dev), st, True, r=r, rst=st2 if proj else None)
+        da = bf(N, H, W, C, seed=10).to(dev)
+        dg, db, dg2, db2 = (torch.zeros(C, device=dev) for _ in range(4))
+        dy, dy2, dres = BN.bn_backward(da, a, y.to(dev), st, gamma.to(dev), dg, db, M,
+                                       y2=r if proj else None, st2=st2 if proj else None,
+                                       gamma2=gamma2.to(dev) if proj else None, dgamma2=dg2, dbeta2=db2,
+                                       want_dres=not proj)
+        out[dev] = dict(a=a, dy=dy, dy2=dy2, dres=dres, dg=dg, db=db, dg2=dg2, rm=rm, rv=rv)
+    for k, v in out["cpu"].items():
+        if v is None:
+            continue
+        assert rel(out[DEV][k], v) < 1e-2, k
+
+
+def test_pools():
+    x = bf(2, 17, 17, 64, seed=11)
+    y_ref, idx_ref = PL.maxpool_fwd(x)
+    y, idx = PL.maxpool_fwd(x.to(DEV))
+    assert torch.equal(y.cpu(), y_ref)
+    dy = bf(*y.shape, seed=12)
+    assert rel(PL.maxpool_bwd(dy.to(DEV), idx, x.shape), PL.maxpool_bwd(dy, idx_ref, x.shape)) < 1e-2
+    assert rel(PL.avgpool_fwd(x.to(DEV)), PL.avgpool_fwd(x)) < 1e-2
+    g = bf(2, 64, seed=13)
+    assert rel(PL.avgpool_bwd(g.to(DEV), x.shape), PL.avgpool_bwd(g, x.shape)) < 1e-2
+
+
+@pytest.mark.parametrize("B,V,smooth", [(64, 1000, 0.1), (33, 30522, 0.0), (16, 37, 0.1)])
+def test_softmax_xent(B, V, smooth):
+    x = bf(B, V, scale=3.0, seed=14)
+    lab = torch.randint(0, V, (B,), dtype=torch.int32)
+    lab[0] = -100
+    l_ref, d_ref, c_ref = LS.softmax_xent(x, lab, smooth, scale=1.0 / B, want_correct=True)
+    l, d, c = LS.softmax_xent(x.to(DEV), lab.to(DEV), smooth, scale=1.0 / B, want_correct=True)
+    assert rel(l, l_ref) < 1e-3
+    assert rel(d, d_ref) < 1e-2
+    assert torch.equal(c.cpu(), c_ref)
+
+
+def test_optimizers():
+    n = 10007
+    w = torch.randn(n); g = torch.randn(n); m = torch.randn(n) * 0.1; v = torch.rand(n) * 0.1
+    wc, mc = w.clone(), m.clone()
+    O.sgd_(wc, None, g, mc, 0.1, 0.9, 1e-4, True, 0.5)
+    wg, mg, wb = w.to(DEV), m.to(DEV), torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    O.sgd_(wg, wb, g.to(DEV), mg, 0.1, 0.9, 1e-4, True, 0.5)
+    assert rel(wg, wc) < 1e-6 and rel(mg, mc) < 1e-6 and rel(wb, wc) < 1e-2
+    wc, mc, vc = w.clone(), m.clone(), v.clone()
+    O.adamw_(wc, None, g, mc, vc, 1e-3, 0.9, 0.999, 1e-6, 0.01, 3)
+    wg, mg, vg = w.to(DEV), m.to(DEV), v.to(DEV)
+    O.adamw_(wg, None, g.to(DEV), mg, vg, 1e-3, 0.9, 0.999, 1e-6, 0.01, 3)
+    assert rel(wg, wc) < 1e-6 and rel(vg, vc) < 1e-6
+
+
+def test_global_norm_clip():
+    g = torch.randn(100000) * 3
+    ss, coef, nrm = (torch.zeros(1, device=DEV) for _ in range(3))
+    O.global_norm_clip_coef(g.to(DEV), 1.0, ss, coef, nrm)
+    assert abs(float(nrm) - float(g.norm())) / float(g.norm()) < 1e-4
+    assert abs(float(coef) - 1.0 / float(g.norm())) < 1e-5

@@ -1,0 +1,106 @@
+"""In-tree native build for tfk.
+
+Compiles every ``csrc/kernels/*.hip`` with hipcc for gfx950, the pybind11 bindings with the
+host compiler against torch's headers, and links ``tensorflow_k8s_amd/_C*.so``. Also builds the
+C++ control plane (``cpp/``) via its Makefile. Incremental (mtime based), parallel.
+No hipify, no JIT cache: the .so lives in the package directory so it travels with the repo.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OBJ = os.path.join(ROOT, "build", "obj")
+PKG = os.path.join(ROOT, "tensorflow_k8s_amd")
+ARCH = os.environ.get("TFK_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _torch_paths():
+    import torch  # noqa: F401
+    from torch.utils import cpp_extension as ce
+
+    return ce.include_paths(device_type="cuda"), ce.library_paths(device_type="cuda")
+
+
+def _stale(out: str, deps: list[str]) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("build failed: " + " ".join(cmd[:3]) + " ... " + cmd[-1])
+
+
+def ext_path() -> str:
+    return os.path.join(PKG, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_kernels(jobs: int | None = None, verbose: bool = False) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    inc, libs = _torch_paths()
+    headers = glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.h"))
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    tasks = []
+    objs = []
+    for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip"))):
+        out = os.path.join(OBJ, os.path.basename(src) + ".o")
+        objs.append(out)
+        if _stale(out, [src] + headers):
+            tasks.append([HIPCC, "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}",
+                          "-munsafe-fp-atomics", src, "-o", out])
+    py_inc = sysconfig.get_paths()["include"]
+    for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "bindings", "*.cpp"))):
+        out = os.path.join(OBJ, os.path.basename(src) + ".o")
+        objs.append(out)
+        if _stale(out, [src]):
+            cmd = ["g++", "-c", "-fPIC", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+                   "-D_GLIBCXX_USE_CXX11_ABI=1", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                   f"-I{py_inc}"] + [f"-I{p}" for p in inc] + [src, "-o", out]
+            tasks.append(cmd)
+    if tasks:
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            for f in [ex.submit(_run, t) for t in tasks]:
+                f.result()
+    so = ext_path()
+    if tasks or _stale(so, objs):
+        tlib = [p for p in libs if "torch" in p][0]
+        cmd = ["g++", "-shared", "-o", so] + objs + [f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
+                                                     "-ltorch_hip", "-ltorch_python", "-lamdhip64",
+                                                     f"-Wl,-rpath,{tlib}"]
+        _run(cmd)
+    if verbose:
+        print(f"[tfk build] {len(tasks)} objects rebuilt -> {so}")
+    return so
+
+
+def build_control_plane(jobs: int | None = None, verbose: bool = False) -> None:
+    mk = os.path.join(ROOT, "cpp", "Makefile")
+    if not os.path.exists(mk):
+        return
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    r = subprocess.run(["make", "-C", os.path.join(ROOT, "cpp"), f"-j{jobs}"], capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout[-4000:] + r.stderr[-8000:])
+        raise RuntimeError("control-plane build failed")
+    if verbose:
+        print("[tfk build] control plane ok")
+
+
+def build_all(verbose: bool = True) -> None:
+    build_kernels(verbose=verbose)
+    build_control_plane(verbose=verbose)
+
+
+if __name__ == "__main__":
+    build_all()

@@ -1,0 +1,170 @@
+// Single-node Kubernetes-semantics object store for the tfk control plane (the L0 substrate the
+// reference operator talks to: REST layout k8s-operator.md:33-34, List/Watch images/informer1.png,
+// finalizers + deletionTimestamp k8s-operator.md:35-43). Provides:
+//   resourceVersion (global, monotonic) + optimistic concurrency (409 on stale update),
+//   uid/creationTimestamp/generation, status subresource, label/field selectors,
+//   watch with replay from a resourceVersion (410 Gone when it fell out of the history window),
+//   finalizers (delete -> deletionTimestamp, removal when the list empties), ownerReference
+//   cascading garbage collection, CRD registry + TFJob version conversion, optional JSON-lines WAL.
+#pragma once
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../common/json.h"
+
+namespace tfk {
+
+struct ApiStatus {
+  int code = 200;
+  std::string reason, message;
+  bool ok() const { return code >= 200 && code < 300; }
+  static ApiStatus Ok(int c = 200) { return {c, "", ""}; }
+  static ApiStatus Err(int c, const std::string& reason, const std::string& msg) { return {c, reason, msg}; }
+  Json to_json() const;
+};
+
+struct ResourceInfo {
+  std::string group;  // "" for core
+  std::string version;
+  std::string plural, singular, kind;
+  bool namespaced = true;
+  std::vector<std::string> versions;  // served versions
+  std::vector<std::string> short_names;
+};
+
+// Label selector: "a=b,c!=d,e,!f,g in (x,y),h notin (z)"
+class LabelSelector {
+ public:
+  static LabelSelector parse(const std::string& s, std::string* err = nullptr);
+  static LabelSelector from_map(const Json& match_labels);
+  bool matches(const Json& labels) const;
+  bool empty() const { return reqs_.empty(); }
+  std::string str() const;
+
+ private:
+  struct Req {
+    std::string key, op;  // = != exists !exists in notin
+    std::set<std::string> vals;
+  };
+  std::vector<Req> reqs_;
+};
+
+// Field selector: "metadata.name=x,status.phase!=Failed,spec.nodeName="
+class FieldSelector {
+ public:
+  static FieldSelector parse(const std::string& s);
+  bool matches(const Json& obj) const;
+  bool empty() const { return reqs_.empty(); }
+
+ private:
+  struct Req {
+    std::string path, val;
+    bool neq;
+  };
+  std::vector<Req> reqs_;
+};
+
+struct WatchEvent {
+  std::string type;  // ADDED | MODIFIED | DELETED | BOOKMARK | ERROR
+  Json object;
+  int64_t rv = 0;
+};
+
+class Watcher {
+ public:
+  Watcher(std::string plural, std::string ns, LabelSelector ls, FieldSelector fs)
+      : plural_(std::move(plural)), ns_(std::move(ns)), ls_(std::move(ls)), fs_(std::move(fs)) {}
+  // Blocks up to timeout_ms; returns false on timeout or when closed with no events left.
+  bool next(WatchEvent* ev, int64_t timeout_ms);
+  void close();
+  bool closed() const { return closed_; }
+  void deliver(const WatchEvent& ev);  // applies ns/selector filters
+  const std::string& plural() const { return plural_; }
+  std::string requested_version;       // convert objects to this version (TFJobs)
+
+ private:
+  friend class Store;
+  std::string plural_, ns_;
+  LabelSelector ls_;
+  FieldSelector fs_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<WatchEvent> q_;
+  bool closed_ = false;
+  size_t max_queue_ = 100000;
+};
+
+class Store {
+ public:
+  explicit Store(const std::string& wal_path = "", size_t history = 10000);
+  ~Store();
+
+  void register_resource(const ResourceInfo& ri);
+  bool resource(const std::string& plural, ResourceInfo* out) const;
+  bool resource_by_kind(const std::string& kind, ResourceInfo* out) const;
+  std::vector<ResourceInfo> resources() const;
+
+  ApiStatus create(const std::string& plural, const std::string& ns, Json obj, Json* out);
+  ApiStatus get(const std::string& plural, const std::string& ns, const std::string& name, Json* out) const;
+  ApiStatus list(const std::string& plural, const std::string& ns, const LabelSelector& ls, const FieldSelector& fs,
+                 std::vector<Json>* items, int64_t* rv) const;
+  // Full replace. status_only: only .status changes (status subresource); otherwise .status is kept.
+  ApiStatus update(const std::string& plural, const std::string& ns, const std::string& name, Json obj,
+                   bool status_only, Json* out);
+  // RFC 7386 JSON merge patch.
+  ApiStatus patch(const std::string& plural, const std::string& ns, const std::string& name, const Json& patch,
+                  bool status_only, Json* out);
+  // propagation: Background (default) | Foreground | Orphan
+  ApiStatus remove(const std::string& plural, const std::string& ns, const std::string& name,
+                   const std::string& propagation, Json* out);
+  std::shared_ptr<Watcher> watch(const std::string& plural, const std::string& ns, int64_t from_rv,
+                                 const LabelSelector& ls, const FieldSelector& fs, ApiStatus* st);
+  int64_t resource_version() const;
+  size_t count(const std::string& plural) const;
+  std::map<std::string, long long> counters() const;  // for /metrics
+
+  // Version conversion hook for multi-version CRDs: (obj, target apiVersion) -> converted
+  using Converter = std::function<Json(const Json&, const std::string&)>;
+  void set_converter(const std::string& plural, Converter c);
+  Json convert_for(const std::string& plural, const Json& obj, const std::string& api_version) const;
+
+ private:
+  struct Obj {
+    Json data;
+    int64_t rv;
+  };
+  using Bucket = std::map<std::string, Obj>;  // key "ns/name"
+  static std::string key(const std::string& ns, const std::string& name) { return ns + "/" + name; }
+  void emit_locked(const std::string& plural, const std::string& type, const Json& obj, int64_t rv);
+  void wal_locked(const std::string& op, const std::string& plural, const Json& obj);
+  void replay_wal();
+  ApiStatus finish_delete_locked(const std::string& plural, const std::string& ns, const std::string& name,
+                                 const std::string& propagation, Json* out);
+  void gc_dependents_locked(const std::string& owner_uid, const std::string& ns);
+
+  mutable std::mutex mu_;
+  std::map<std::string, ResourceInfo> resources_;
+  std::map<std::string, Bucket> data_;
+  int64_t rv_ = 1;
+  std::deque<WatchEvent> history_;  // all resources, rv ordered
+  std::map<int64_t, std::string> history_plural_;
+  size_t history_cap_;
+  std::vector<std::weak_ptr<Watcher>> watchers_;
+  std::map<std::string, Converter> converters_;
+  std::string wal_path_;
+  FILE* wal_ = nullptr;
+  bool replaying_ = false;
+  std::map<std::string, long long> ops_;
+};
+
+// RFC 7386
+Json merge_patch(const Json& target, const Json& patch);
+
+}  // namespace tfk

@@ -1,0 +1,379 @@
+#include "kubelet.h"
+
+#include <dirent.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cstring>
+#include <fstream>
+#include <set>
+#include <sstream>
+
+extern char** environ;
+
+namespace tfk {
+
+int detect_gpus() {
+  int n = 0;
+  DIR* d = opendir("/sys/class/kfd/kfd/topology/nodes");
+  if (!d) return 0;
+  while (dirent* e = readdir(d)) {
+    if (e->d_name[0] == '.') continue;
+    std::ifstream f(std::string("/sys/class/kfd/kfd/topology/nodes/") + e->d_name + "/gpu_id");
+    int id = 0;
+    if (f >> id && id != 0) n++;
+  }
+  closedir(d);
+  return n;
+}
+
+static void mkdirs(const std::string& p) {
+  std::string cur;
+  for (auto& part : split(p, '/')) {
+    if (part.empty()) { cur += "/"; continue; }
+    cur += part + "/";
+    mkdir(cur.c_str(), 0755);
+  }
+}
+
+Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletOptions o) : client_(std::move(c)), opts_(std::move(o)) {
+  if (opts_.gpus < 0) opts_.gpus = detect_gpus();
+  if (opts_.cpu_milli <= 0) opts_.cpu_milli = (long long)sysconf(_SC_NPROCESSORS_ONLN) * 1000;
+  mkdirs(opts_.root_dir + "/logs");
+  mkdirs(opts_.root_dir + "/term");
+  pods_inf_.reset(new SharedInformer(client_, "pods", "", 10000, "", "spec.nodeName=" + opts_.node_name));
+}
+
+Kubelet::~Kubelet() {
+  for (auto& kv : pods_) kill_pod(kv.second, SIGKILL);
+}
+
+void Kubelet::register_node(bool heartbeat) {
+  Json n = Json::object();
+  n["apiVersion"] = "v1";
+  n["kind"] = "Node";
+  n["metadata"]["name"] = opts_.node_name;
+  n["metadata"]["labels"]["kubernetes.io/hostname"] = opts_.node_name;
+  n["metadata"]["labels"]["amd.com/gpu.product"] = "MI355X";
+  Json cap = Json::object();
+  cap["amd.com/gpu"] = opts_.gpus;
+  cap["cpu"] = std::to_string(opts_.cpu_milli) + "m";
+  cap["pods"] = 110;
+  n["status"]["capacity"] = cap;
+  n["status"]["allocatable"] = cap;
+  Json cond = Json::object();
+  cond["type"] = "Ready";
+  cond["status"] = "True";
+  cond["reason"] = "KubeletReady";
+  cond["lastHeartbeatTime"] = rfc3339(now_ms());
+  n["status"]["conditions"] = Json(Json::array_t{cond});
+  Json addr = Json::object();
+  addr["type"] = "InternalIP";
+  addr["address"] = "127.0.0.1";
+  n["status"]["addresses"] = Json(Json::array_t{addr});
+  Json out;
+  if (!heartbeat) {
+    ApiStatus st = client_->create("nodes", "", n, &out);
+    if (st.code != 409) return;
+  }
+  Json cur;
+  if (client_->get("nodes", "", opts_.node_name, &cur).ok()) {
+    n["metadata"]["resourceVersion"] = cur.path("metadata.resourceVersion");
+    n["spec"] = cur.at("spec");
+    client_->update("nodes", "", n, &out);
+  }
+}
+
+void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
+  const Json* spec = nullptr;
+  for (auto& cs : pr.pod.path("spec.containers").items())
+    if (cs.at("name").str() == c.name) spec = &cs;
+  if (!spec) return;
+  c.log_path = opts_.root_dir + "/logs/" + pr.ns + "_" + pr.name + "_" + c.name + ".log";
+  c.term_path = opts_.root_dir + "/term/" + pr.uid + "_" + c.name;
+  unlink(c.term_path.c_str());
+  std::vector<std::string> argv;
+  for (auto& a : spec->at("command").items()) argv.push_back(a.str());
+  for (auto& a : spec->at("args").items()) argv.push_back(a.str());
+  if (argv.empty()) argv.push_back("/bin/true");
+  std::map<std::string, std::string> env;
+  for (char** e = environ; *e; ++e) {
+    std::string kv = *e;
+    size_t eq = kv.find('=');
+    if (eq != std::string::npos) env[kv.substr(0, eq)] = kv.substr(eq + 1);
+  }
+  for (auto& e : spec->at("env").items()) {
+    std::string v = e.at("value").str();
+    const Json& fr = e.path("valueFrom.fieldRef.fieldPath");
+    if (fr.is_string()) {
+      if (fr.str() == "metadata.name") v = pr.name;
+      else if (fr.str() == "metadata.namespace") v = pr.ns;
+      else if (fr.str() == "status.podIP") v = "127.0.0.1";
+      else if (fr.str() == "spec.nodeName") v = opts_.node_name;
+    }
+    env[e.at("name").str()] = v;
+  }
+  std::string gpu_ids = pr.pod.path("metadata.annotations").at("tfk.io/gpu-ids").str();
+  if (!gpu_ids.empty()) env["HIP_VISIBLE_DEVICES"] = gpu_ids;
+  env["TFK_POD_NAME"] = pr.name;
+  env["TFK_POD_NAMESPACE"] = pr.ns;
+  env["TFK_NODE_NAME"] = opts_.node_name;
+  env["TFK_TERMINATION_LOG"] = c.term_path;
+  if (opts_.local_dns) env["TFK_LOCAL_DNS"] = "1";
+  std::string wd = spec->at("workingDir").str();
+  pid_t pid = fork();
+  if (pid == 0) {
+    setsid();
+    int fd = open(c.log_path.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
+    if (fd >= 0) { dup2(fd, 1); dup2(fd, 2); close(fd); }
+    int nul = open("/dev/null", O_RDONLY);
+    if (nul >= 0) { dup2(nul, 0); close(nul); }
+    if (!wd.empty() && chdir(wd.c_str()) != 0) { perror("chdir"); _exit(127); }
+    std::vector<std::string> envs;
+    for (auto& kv : env) envs.push_back(kv.first + "=" + kv.second);
+    std::vector<char*> ev, av;
+    for (auto& s : envs) ev.push_back((char*)s.c_str());
+    ev.push_back(nullptr);
+    for (auto& s : argv) av.push_back((char*)s.c_str());
+    av.push_back(nullptr);
+    environ = ev.data();
+    execvp(av[0], av.data());
+    fprintf(stderr, "exec %s failed: %s\n", av[0], strerror(errno));
+    _exit(127);
+  }
+  if (pid < 0) {
+    c.state = "waiting";
+    c.waiting_reason = "StartError";
+    c.next_start_ms = mono_ms() + opts_.restart_backoff_ms;
+    return;
+  }
+  c.pid = pid;
+  c.state = "running";
+  c.started_at = rfc3339(now_ms());
+  c.started_mono = mono_ms();
+  for (size_t i = 0; i < pr.containers.size(); ++i)
+    if (&pr.containers[i] == &c) pid_owner_[pid] = {pr.uid, i};
+  TFK_LOG(Info, "started container", Json(Json::object_t{{"pod", Json(pr.ns + "/" + pr.name)}, {"container", Json(c.name)},
+                                                         {"pid", Json((long long)pid)}, {"gpus", Json(gpu_ids)}}));
+}
+
+void Kubelet::kill_pod(PodRun& pr, int sig) {
+  for (auto& c : pr.containers)
+    if (c.pid > 0) kill(-c.pid, sig);
+}
+
+void Kubelet::reap() {
+  while (true) {
+    int status = 0;
+    pid_t pid = waitpid(-1, &status, WNOHANG);
+    if (pid <= 0) break;
+    auto it = pid_owner_.find(pid);
+    if (it == pid_owner_.end()) continue;
+    auto pit = pods_.find(it->second.first);
+    size_t ci = it->second.second;
+    pid_owner_.erase(it);
+    if (pit == pods_.end()) continue;
+    PodRun& pr = pit->second;
+    ContainerRun& c = pr.containers[ci];
+    c.pid = -1;
+    c.exit_code = WIFEXITED(status) ? WEXITSTATUS(status) : (WIFSIGNALED(status) ? 128 + WTERMSIG(status) : 1);
+    c.reason = c.exit_code == 0 ? "Completed" : "Error";
+    std::ifstream tf(c.term_path);
+    std::string msg((std::istreambuf_iterator<char>(tf)), std::istreambuf_iterator<char>());
+    if (msg.find("OOMKilled") != std::string::npos) c.reason = "OOMKilled";
+    c.finished_at = rfc3339(now_ms());
+    c.state = "terminated";
+    Json term = Json::object();
+    term["exitCode"] = c.exit_code;
+    term["reason"] = c.reason;
+    term["startedAt"] = c.started_at;
+    term["finishedAt"] = c.finished_at;
+    if (!msg.empty()) term["message"] = msg.substr(0, 4096);
+    c.last_terminated = term;
+    std::string policy = pr.pod.path("spec.restartPolicy").str("Always");
+    bool restart = !pr.killing && (policy == "Always" || (policy == "OnFailure" && c.exit_code != 0));
+    if (restart) {
+      int64_t backoff = opts_.restart_backoff_ms << std::min(c.restarts, 10);
+      c.next_start_ms = mono_ms() + std::min(backoff, opts_.max_backoff_ms);
+      c.waiting_reason = "CrashLoopBackOff";
+    } else {
+      c.done = true;
+    }
+    TFK_LOG(Info, "container exited", Json(Json::object_t{{"pod", Json(pr.ns + "/" + pr.name)}, {"container", Json(c.name)},
+                                                          {"exitCode", Json(c.exit_code)}, {"reason", Json(c.reason)},
+                                                          {"restart", Json(restart)}}));
+  }
+}
+
+Json Kubelet::build_status(PodRun& pr) {
+  Json st = Json::object();
+  bool all_done = true, any_failed = false, all_zero = true, any_running = false;
+  Json css = Json::array();
+  for (auto& c : pr.containers) {
+    Json cs = Json::object();
+    cs["name"] = c.name;
+    cs["restartCount"] = c.restarts;
+    cs["ready"] = c.state == "running";
+    cs["image"] = "";
+    if (c.state == "running") {
+      cs["state"]["running"]["startedAt"] = c.started_at;
+      any_running = true;
+    } else if (c.state == "terminated" && c.done) {
+      cs["state"]["terminated"] = c.last_terminated;
+    } else {
+      cs["state"]["waiting"]["reason"] = c.waiting_reason;
+    }
+    if (c.last_terminated.is_object() && !(c.state == "terminated" && c.done))
+      cs["lastState"]["terminated"] = c.last_terminated;
+    css.push_back(cs);
+    if (!c.done) all_done = false;
+    if (c.done && c.exit_code != 0) { any_failed = true; all_zero = false; }
+  }
+  std::string phase = "Pending";
+  if (all_done && !pr.containers.empty()) phase = (any_failed || !all_zero) ? "Failed" : "Succeeded";
+  else if (any_running || pr.containers.size()) {
+    bool started = false;
+    for (auto& c : pr.containers) started |= !c.started_at.empty();
+    phase = started ? "Running" : "Pending";
+  }
+  st["phase"] = phase;
+  st["hostIP"] = "127.0.0.1";
+  st["podIP"] = "127.0.0.1";
+  if (!pr.start_time.empty()) st["startTime"] = pr.start_time;
+  st["containerStatuses"] = css;
+  Json rc = Json::object();
+  rc["type"] = "Ready";
+  rc["status"] = any_running ? "True" : "False";
+  st["conditions"] = Json(Json::array_t{rc});
+  return st;
+}
+
+void Kubelet::update_status(PodRun& pr) {
+  Json st = build_status(pr);
+  std::string s = st.dump();
+  if (s == pr.last_status) return;
+  Json cur;
+  if (!pods_inf_->indexer().get_by_key(pr.ns + "/" + pr.name, &cur)) return;
+  if (cur.path("metadata.uid").str() != pr.uid) return;
+  Json next = cur.clone();
+  next["status"] = st;
+  Json out;
+  ApiStatus r = client_->update_status("pods", pr.ns, next, &out);
+  if (r.ok()) {
+    pr.last_status = s;
+    pods_inf_->indexer().upsert(pr.ns + "/" + pr.name, out);
+  }
+}
+
+void Kubelet::sync_once() {
+  reap();
+  std::set<std::string> live;
+  for (auto& p : pods_inf_->indexer().list()) {
+    if (p.path("spec.nodeName").str() != opts_.node_name) continue;
+    std::string uid = p.path("metadata.uid").str();
+    live.insert(uid);
+    auto it = pods_.find(uid);
+    if (it == pods_.end()) {
+      std::string phase = p.path("status.phase").str();
+      if (phase == "Succeeded" || phase == "Failed") continue;  // already terminal (kubelet restart)
+      PodRun pr;
+      pr.uid = uid;
+      pr.ns = p.path("metadata.namespace").str();
+      pr.name = p.path("metadata.name").str();
+      pr.pod = p;
+      pr.start_time = rfc3339(now_ms());
+      for (auto& cs : p.path("spec.containers").items()) {
+        ContainerRun c;
+        c.name = cs.at("name").str();
+        pr.containers.push_back(c);
+      }
+      auto& ref = pods_[uid] = pr;
+      std::string logp;
+      for (auto& c : ref.containers) {
+        start_container(ref, c);
+        if (logp.empty() || c.name == "tensorflow") logp = c.log_path;
+      }
+      Json patch = Json::object();
+      patch["metadata"]["annotations"]["tfk.io/log-path"] = logp;
+      Json out;
+      client_->patch("pods", ref.ns, ref.name, patch, &out);
+      update_status(ref);
+      continue;
+    }
+    PodRun& pr = it->second;
+    pr.pod = p;
+    if (p.path("metadata.deletionTimestamp").is_string() && !pr.killing) {
+      pr.killing = true;
+      pr.kill_deadline = mono_ms() + opts_.grace_ms;
+      kill_pod(pr, SIGTERM);
+    }
+    // fault injection (once per restart generation)
+    const Json& an = p.path("metadata.annotations");
+    if (!pr.fault_done && an.has("tfk.io/fault-kill-after-ms") &&
+        an.at("tfk.io/fault-generation").str("0") == an.at("tfk.io/restart-generation").str("0")) {
+      int64_t after = atoll(an.at("tfk.io/fault-kill-after-ms").str().c_str());
+      int sig = atoi(an.at("tfk.io/fault-signal").str("9").c_str());
+      for (auto& c : pr.containers)
+        if (c.pid > 0 && mono_ms() - c.started_mono >= after) {
+          TFK_LOG(Warn, "fault injection: killing container", Json(Json::object_t{{"pod", Json(pr.name)}, {"signal", Json(sig)}}));
+          kill(-c.pid, sig);
+          pr.fault_done = true;
+        }
+    }
+    for (auto& c : pr.containers)
+      if (c.state != "running" && !c.done && !pr.killing && c.next_start_ms > 0 && mono_ms() >= c.next_start_ms) {
+        c.restarts++;
+        c.next_start_ms = 0;
+        start_container(pr, c);
+      }
+    update_status(pr);
+  }
+  // pods removed from the API (or rebound elsewhere): stop their containers
+  for (auto it = pods_.begin(); it != pods_.end();) {
+    PodRun& pr = it->second;
+    if (!live.count(it->first) && !pr.killing) {
+      pr.killing = true;
+      pr.kill_deadline = mono_ms() + opts_.grace_ms;
+      kill_pod(pr, SIGTERM);
+    }
+    bool alive = false;
+    for (auto& c : pr.containers) alive |= c.pid > 0;
+    if (pr.killing && alive && mono_ms() > pr.kill_deadline) kill_pod(pr, SIGKILL);
+    if (pr.killing && !alive && !live.count(it->first)) it = pods_.erase(it);
+    else ++it;
+  }
+  if (mono_ms() - last_heartbeat_ > opts_.heartbeat_ms) {
+    register_node(true);
+    last_heartbeat_ = mono_ms();
+  }
+}
+
+void Kubelet::run(StopToken& stop) {
+  register_node(false);
+  last_heartbeat_ = mono_ms();
+  pods_inf_->start(stop);
+  while (!stop.stopped() && !pods_inf_->wait_for_sync(1000)) {
+  }
+  TFK_LOG(Info, "kubelet ready", Json(Json::object_t{{"node", Json(opts_.node_name)}, {"gpus", Json(opts_.gpus)}}));
+  while (!stop.stopped()) {
+    sync_once();
+    stop.wait_for(100);
+  }
+  for (auto& kv : pods_) kill_pod(kv.second, SIGTERM);
+  int64_t dl = mono_ms() + opts_.grace_ms;
+  while (mono_ms() < dl) {
+    reap();
+    bool alive = false;
+    for (auto& kv : pods_)
+      for (auto& c : kv.second.containers) alive |= c.pid > 0;
+    if (!alive) break;
+    usleep(50000);
+  }
+  for (auto& kv : pods_) kill_pod(kv.second, SIGKILL);
+  reap();
+}
+
+}  // namespace tfk

@@ -1,0 +1,84 @@
+// tfk node agent ("kubelet"): runs the containers of pods bound to this node as process groups,
+// pins GPUs (HIP_VISIBLE_DEVICES from the scheduler's tfk.io/gpu-ids), implements the pod
+// restart policies (k8s-operator.md:46-52: OnFailure restarts in place, Never leaves the failed
+// pod, completed pods are retained), reports containerStatuses (exitCode, reason incl.
+// OOMKilled via the termination-message file, restartCount, lastState), keeps per-container log
+// files (tfk.io/log-path), heartbeats its Node object, and injects faults on request
+// (annotation tfk.io/fault-kill-after-ms / tfk.io/fault-signal / tfk.io/fault-generation).
+#pragma once
+#include <sys/types.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../cache/informer.h"
+
+namespace tfk {
+
+struct KubeletOptions {
+  std::string node_name = "node-0";
+  int gpus = -1;  // -1 = detect from /sys/class/kfd
+  long long cpu_milli = 0;
+  std::string root_dir = "/tmp/tfk-kubelet";
+  int64_t restart_backoff_ms = 1000;
+  int64_t max_backoff_ms = 30000;
+  int64_t grace_ms = 5000;
+  int64_t heartbeat_ms = 10000;
+  bool local_dns = true;
+};
+
+struct ContainerRun {
+  std::string name;
+  pid_t pid = -1;
+  int restarts = 0;
+  std::string state = "waiting";  // waiting | running | terminated
+  std::string waiting_reason = "ContainerCreating";
+  int exit_code = 0;
+  std::string reason;
+  std::string started_at, finished_at;
+  int64_t next_start_ms = 0;
+  int64_t started_mono = 0;
+  Json last_terminated;
+  std::string log_path, term_path;
+  bool done = false;  // terminal, no more restarts
+};
+
+struct PodRun {
+  std::string uid, ns, name;
+  Json pod;
+  std::vector<ContainerRun> containers;
+  std::string start_time;
+  bool fault_done = false;
+  bool killing = false;
+  int64_t kill_deadline = 0;
+  std::string last_status;  // last status JSON written
+};
+
+int detect_gpus();
+
+class Kubelet {
+ public:
+  Kubelet(std::shared_ptr<Client> c, KubeletOptions o);
+  ~Kubelet();
+  void run(StopToken& stop);
+  void sync_once();  // exposed for tests
+  size_t running_pods() const { return pods_.size(); }
+
+ private:
+  void register_node(bool heartbeat);
+  void start_container(PodRun& pr, ContainerRun& c);
+  void reap();
+  void kill_pod(PodRun& pr, int sig);
+  void update_status(PodRun& pr);
+  Json build_status(PodRun& pr);
+  std::shared_ptr<Client> client_;
+  KubeletOptions opts_;
+  std::unique_ptr<SharedInformer> pods_inf_;
+  std::map<std::string, PodRun> pods_;  // uid -> run
+  std::map<pid_t, std::pair<std::string, size_t>> pid_owner_;
+  int64_t last_heartbeat_ = 0;
+};
+
+}  // namespace tfk

@@ -118,11 +118,11 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   // ---- operand A extents
   switch (amode) {
     case A_KIN:
-      TORCH_CHECK(K % 8 == 0 && lda % 8 == 0 && lda >= K, "A_KIN needs K%8==0, lda%8==0, lda>=K");
+      TORCH_CHECK(lda >= K, "A_KIN needs lda>=K");
       need_numel(A, bA + (long long)(M - 1) * lda + K, "A");
       break;
     case A_KOUT:
-      TORCH_CHECK(M % 8 == 0 && lda % 8 == 0 && lda >= M, "A_KOUT needs M%8==0, lda%8==0, lda>=M");
+      TORCH_CHECK(lda >= M, "A_KOUT needs lda>=M");
       need_numel(A, bA + (long long)(K - 1) * lda + M, "A");
       break;
     case A_CONV_FWD:
@@ -139,11 +139,11 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   }
   switch (bmode) {
     case B_KIN:
-      TORCH_CHECK(K % 8 == 0 && ldb % 8 == 0 && ldb >= K, "B_KIN needs K%8==0, ldb%8==0");
+      TORCH_CHECK(ldb >= K, "B_KIN needs ldb>=K");
       need_numel(B, bB + (long long)(N - 1) * ldb + K, "B");
       break;
     case B_KOUT:
-      TORCH_CHECK(N % 8 == 0 && ldb % 8 == 0 && ldb >= N, "B_KOUT needs N%8==0, ldb%8==0");
+      TORCH_CHECK(ldb >= N, "B_KOUT needs ldb>=N");
       need_numel(B, bB + (long long)(K - 1) * ldb + N, "B");
       break;
     case B_CONV_WGRAD:
@@ -157,10 +157,8 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   int ns = tfk_gemm_splits(K, splits);
   if (epi == 0) {
     TORCH_CHECK(ns == 1, "split-K requires the f32 epilogue");
-    TORCH_CHECK(ldc % 8 == 0, "bf16 C needs ldc%8==0");
     need_numel(C, bC + (long long)(M - 1) * ldc + N, "C");
   } else {
-    TORCH_CHECK(ldc % 4 == 0, "f32 C needs ldc%4==0");
     TORCH_CHECK(ns == 1 || batch == 1, "split-K with batch>1 unsupported");
     need_numel(C, bC + (long long)(ns - 1) * split_stride + (long long)(M - 1) * ldc + N, "C");
   }

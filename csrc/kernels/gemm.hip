@@ -44,6 +44,17 @@ __device__ __forceinline__ int kin_off(int row, int kc) { return row * 128 + ((k
 template <int ROWS>
 __device__ __forceinline__ int kout_off(int krow, int rc) { return krow * (ROWS * 2) + ((rc ^ swz_kout<ROWS>(krow)) << 4); }
 
+// Predicated scalar load of up to 8 consecutive bf16 (ragged tails / unaligned leading dims).
+__device__ __forceinline__ u32x4 load_partial(const bf16* src, int valid, int stride) {
+  union { u32x4 v; unsigned short h[8]; } u;
+  u.v = u32x4{0u, 0u, 0u, 0u};
+  const unsigned short* s = (const unsigned short*)src;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (e < valid) u.h[e] = s[e * stride];
+  return u.v;
+}
+
 // Per-operand loader state. ROWS = tile rows of this operand (BM for A, BN for B).
 template <int ROWS, int MODE, bool IS_A>
 struct Loader {
@@ -117,19 +128,25 @@ struct Loader {
     const u32x4 zero = {0u, 0u, 0u, 0u};
     if constexpr (MODE == 0 /*KIN dense (A_KIN==B_KIN==0)*/) {
       const int k = kt * BK + chunk_col() * 8;
+      const bool vec = (ld & 7) == 0;
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         int r = row0 + chunk_row(i);
         bool ok = (r < lim_rows) && (k < K);
-        regs[i] = ok ? *(const u32x4*)(base + (long long)r * ld + k) : zero;
+        const bf16* src = base + (long long)r * ld + k;
+        if (ok && vec && k + 8 <= K) regs[i] = *(const u32x4*)src;
+        else regs[i] = ok ? load_partial(src, K - k, 1) : zero;
       }
     } else if constexpr (MODE == 1 /*KOUT dense*/) {
       const int col = row0 + chunk_col() * 8;
+      const bool vec = (ld & 7) == 0;
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         int k = kt * BK + chunk_row(i);
         bool ok = (k < K) && (col < lim_rows);
-        regs[i] = ok ? *(const u32x4*)(base + (long long)k * ld + col) : zero;
+        const bf16* src = base + (long long)k * ld + col;
+        if (ok && vec && col + 8 <= lim_rows) regs[i] = *(const u32x4*)src;
+        else regs[i] = ok ? load_partial(src, lim_rows - col, 1) : zero;
       }
     } else if constexpr (IS_A && MODE == A_CONV_FWD) {
       const bool kok = cr < p.R;
@@ -291,7 +308,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
         const int n = n0 + wn * (BN / 2) + j * 16 + nl;
         float* dst = C + (long long)m * p.ldc + n;
         f32x4 v = acc[i][j] * p.alpha;
-        if (n + 3 < p.N) {
+        if (n + 3 < p.N && (p.ldc & 3) == 0) {
           if (p.beta != 0.f) v += p.beta * *(f32x4*)dst;
           *(f32x4*)dst = v;
         } else {
@@ -358,7 +375,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
       if (m >= p.M || n >= p.N) continue;
       bf16x8 v = *(const bf16x8*)(Cs + row * LDC_S + cc * 8);
       bf16* dst = C + (long long)m * p.ldc + n;
-      if (n + 7 < p.N) {
+      if (n + 7 < p.N && (p.ldc & 7) == 0) {
         if (p.resid) {
           bf16x8 rr = *(const bf16x8*)((const bf16*)p.resid + bz * p.sC + (long long)m * p.ldc + n);
 #pragma unroll

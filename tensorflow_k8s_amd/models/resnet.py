@@ -30,7 +30,7 @@ class Bottleneck:
         self.conv2 = Conv2d(arena, f"res{tag}_branch2b", width, width, 3, stride=stride)
         self.bn2 = BatchNorm(arena, f"bn{tag}_branch2b", width)
         self.conv3 = Conv2d(arena, f"res{tag}_branch2c", width, cout, 1)
-        self.bn3 = BatchNorm(arena, f"bn{tag}_branch2c", cout, zero_gamma=False)
+        self.bn3 = BatchNorm(arena, f"bn{tag}_branch2c", cout, zero_gamma=True)
         self.proj = stride != 1 or cin != cout
         if self.proj:
             self.conv_sc = Conv2d(arena, f"res{tag}_branch1", cin, cout, 1, stride=stride, pad=0)

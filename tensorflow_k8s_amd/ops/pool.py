@@ -27,9 +27,11 @@ def maxpool_fwd(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1):
 def maxpool_bwd(dy: torch.Tensor, idx, x_shape, k: int = 3, s: int = 2, p: int = 1) -> torch.Tensor:
     N, H, W, C = x_shape
     if not on_gpu(dy):
+        # overlapping windows: gradients of windows sharing an argmax must ACCUMULATE
         ind, nshape = idx
-        dx = F.max_unpool2d(dy.float().permute(0, 3, 1, 2), ind, k, s, p, output_size=nshape[-2:])
-        return dx.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+        g = dy.float().permute(0, 3, 1, 2).reshape(N, C, -1)
+        dx = torch.zeros(N, C, H * W).scatter_add_(2, ind.reshape(N, C, -1), g)
+        return dx.reshape(N, C, H, W).permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
     P, Q = dy.shape[1], dy.shape[2]
     dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
     lib().maxpool_bwd(dy, idx, dx, [N, H, W, C, P, Q, k, k, s, s, p, p])

@@ -20,11 +20,12 @@ int tfk_bn_stats(const void*, long long, int, float*, int, hipStream_t);
 int tfk_bn_apply(const void*, const float*, const float*, const void*, const float*, const float*, int, void*, long long,
                  int, hipStream_t);
 int tfk_bn_bwd_reduce(const void*, const void*, const void*, const float*, const float*, const void*, const float*,
-                      const float*, long long, int, float*, int, hipStream_t);
+                      const float*, long long, int, float*, int, const float*, const float*, hipStream_t);
 int tfk_bn_bwd_finalize(float*, int, int, float, const float*, const float*, const float*, const float*, float*, float*,
                         float*, float*, float*, float*, hipStream_t);
 int tfk_bn_bwd_apply(const void*, const void*, const void*, const float*, const float*, const float*, void*, const void*,
-                     const float*, const float*, const float*, void*, void*, long long, int, hipStream_t);
+                     const float*, const float*, const float*, void*, void*, long long, int, const float*, const float*,
+                     hipStream_t);
 int tfk_maxpool_fwd(const void*, void*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int tfk_maxpool_bwd(const void*, const uint8_t*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                     hipStream_t);
@@ -93,7 +94,8 @@ enum { B_KIN = 0, B_KOUT = 1, B_CONV_WGRAD = 2 };
 void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
           int amode, int bmode, int epi, int bm, int bn, double alpha, double beta, c10::optional<torch::Tensor> bias,
           c10::optional<torch::Tensor> resid, int act, c10::optional<torch::Tensor> stats, int shards, int splits,
-          int batch, int64_t sA, int64_t sB, int64_t sC, int64_t split_stride, std::vector<int64_t> conv) {
+          int batch, int64_t sA, int64_t sB, int64_t sC, int64_t split_stride, std::vector<int64_t> conv,
+          std::vector<c10::optional<torch::Tensor>> bnr, int bn_relu, int bn_shards) {
   need_bf16(A, "A");
   need_bf16(B, "B");
   TORCH_CHECK(epi == 0 || epi == 1, "epi");
@@ -172,6 +174,33 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
     TORCH_CHECK(shards >= 1, "shards");
     need_numel(*stats, (long long)shards * 2 * N, "stats");
   }
+  if (!bnr.empty()) {
+    // [y, a, mean, invstd, scale, shift, y2, mean2, invstd2, sums]
+    TORCH_CHECK(bnr.size() == 10, "bnr needs 10 entries");
+    TORCH_CHECK(epi == 0 && N % 8 == 0 && ldc == N && batch == 1, "fused BN reduce needs bf16 out, N%8==0, ldc==N");
+    for (int i : {0, 2, 3, 9}) TORCH_CHECK(bnr[i].has_value() && bnr[i]->defined(), "bnr missing required entry ", i);
+    need_bf16(*bnr[0], "bn_y"); need_numel(*bnr[0], (long long)M * N, "bn_y");
+    if (bnr[1].has_value() && bnr[1]->defined()) { need_bf16(*bnr[1], "bn_a"); need_numel(*bnr[1], (long long)M * N, "bn_a"); }
+    if (bnr[6].has_value() && bnr[6]->defined()) { need_bf16(*bnr[6], "bn_y2"); need_numel(*bnr[6], (long long)M * N, "bn_y2"); }
+    for (int i : {2, 3, 4, 5, 7, 8})
+      if (bnr[i].has_value() && bnr[i]->defined()) { need_f32(*bnr[i], "bn vec"); need_numel(*bnr[i], N, "bn vec"); }
+    need_f32(*bnr[9], "bn_sums");
+    TORCH_CHECK(bn_shards >= 1, "bn_shards");
+    need_numel(*bnr[9], (long long)bn_shards * 3 * N, "bn_sums");
+    p.bn_y = bnr[0]->data_ptr();
+    p.bn_a = opt_ptr<const void>(bnr[1]);
+    p.bn_mean = bnr[2]->data_ptr<float>();
+    p.bn_invstd = bnr[3]->data_ptr<float>();
+    p.bn_scale = opt_ptr<const float>(bnr[4]);
+    p.bn_shift = opt_ptr<const float>(bnr[5]);
+    p.bn_y2 = opt_ptr<const void>(bnr[6]);
+    p.bn_mean2 = opt_ptr<const float>(bnr[7]);
+    p.bn_invstd2 = opt_ptr<const float>(bnr[8]);
+    p.bn_sums = bnr[9]->data_ptr<float>();
+    p.bn_relu = bn_relu;
+    p.bn_shards = bn_shards;
+    TORCH_CHECK(!(p.bn_relu && !p.bn_a && !(p.bn_scale && p.bn_shift)), "relu mask needs a or scale/shift");
+  }
   p.bias = opt_ptr<const float>(bias);
   p.resid = opt_ptr<const void>(resid);
   p.stats = opt_ptr<float>(stats);
@@ -216,7 +245,8 @@ void bn_apply(torch::Tensor y, torch::Tensor scale, torch::Tensor shift, c10::op
 
 void bn_bwd_reduce(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tensor y, torch::Tensor mean,
                    torch::Tensor invstd, c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> mean2,
-                   c10::optional<torch::Tensor> invstd2, int64_t M, int C, torch::Tensor sums, int shards) {
+                   c10::optional<torch::Tensor> invstd2, int64_t M, int C, torch::Tensor sums, int shards,
+                   c10::optional<torch::Tensor> mscale, c10::optional<torch::Tensor> mshift) {
   need_bf16(da, "da"); need_bf16(y, "y"); need_numel(da, M * C, "da"); need_numel(y, M * C, "y");
   TORCH_CHECK(C % 8 == 0, "C%8");
   if (a.has_value() && a->defined()) need_numel(*a, M * C, "a");
@@ -224,7 +254,8 @@ void bn_bwd_reduce(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tens
   need_f32(sums, "sums"); need_numel(sums, (long long)shards * 3 * C, "sums");
   check_rc(tfk_bn_bwd_reduce(da.data_ptr(), opt_ptr<const void>(a), y.data_ptr(), mean.data_ptr<float>(),
                              invstd.data_ptr<float>(), opt_ptr<const void>(y2), opt_ptr<const float>(mean2),
-                             opt_ptr<const float>(invstd2), M, C, sums.data_ptr<float>(), shards, cur_stream()),
+                             opt_ptr<const float>(invstd2), M, C, sums.data_ptr<float>(), shards,
+                             opt_ptr<const float>(mscale), opt_ptr<const float>(mshift), cur_stream()),
            "bn_bwd_reduce");
 }
 
@@ -246,7 +277,8 @@ void bn_bwd_apply(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tenso
                   torch::Tensor invstd, torch::Tensor coef, torch::Tensor dy, c10::optional<torch::Tensor> y2,
                   c10::optional<torch::Tensor> mean2, c10::optional<torch::Tensor> invstd2,
                   c10::optional<torch::Tensor> coef2, c10::optional<torch::Tensor> dy2,
-                  c10::optional<torch::Tensor> dres, int64_t M, int C) {
+                  c10::optional<torch::Tensor> dres, int64_t M, int C, c10::optional<torch::Tensor> mscale,
+                  c10::optional<torch::Tensor> mshift) {
   need_bf16(da, "da"); need_bf16(y, "y"); need_bf16(dy, "dy");
   for (auto* t : {&da, &y, &dy}) need_numel(*t, M * C, "bn bwd tensor");
   if (a.has_value() && a->defined()) need_numel(*a, M * C, "a");
@@ -256,7 +288,8 @@ void bn_bwd_apply(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tenso
   check_rc(tfk_bn_bwd_apply(da.data_ptr(), opt_ptr<const void>(a), y.data_ptr(), mean.data_ptr<float>(),
                             invstd.data_ptr<float>(), coef.data_ptr<float>(), dy.data_ptr(), opt_ptr<const void>(y2),
                             opt_ptr<const float>(mean2), opt_ptr<const float>(invstd2), opt_ptr<const float>(coef2),
-                            opt_ptr<void>(dy2), opt_ptr<void>(dres), M, C, cur_stream()),
+                            opt_ptr<void>(dy2), opt_ptr<void>(dres), M, C, opt_ptr<const float>(mscale),
+                            opt_ptr<const float>(mshift), cur_stream()),
            "bn_bwd_apply");
 }
 
@@ -429,6 +462,7 @@ void add(torch::Tensor a, torch::Tensor b, torch::Tensor y, double alpha, double
 }  // namespace
 
 void register_transformer_ops(pybind11::module& m);
+void register_ckpt_ops(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "tfk gfx950 HIP kernel library";
@@ -464,4 +498,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("dropout", &dropout);
   m.def("add", &add);
   register_transformer_ops(m);
+  register_ckpt_ops(m);
 }

@@ -13,21 +13,25 @@ constexpr int NT = 256;
 
 // ---------------------------------------------------------------- forward
 // stats: [shards][2][C] (sum, sumsq), zeroed again after reading so the next conv can accumulate.
-__global__ void bn_finalize_kernel(float* __restrict__ stats, int shards, int C, float count, const float* __restrict__ gamma,
+__global__ void bn_finalize_kernel(float* stats, int shards, int C, float count, const float* __restrict__ gamma,
                                    const float* __restrict__ beta, float eps, float momentum, float* __restrict__ run_mean,
                                    float* __restrict__ run_var, float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                    float* __restrict__ scale_out, float* __restrict__ shift_out) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double s = 0.0, q = 0.0;
+  float s = 0.f, q = 0.f;
+#pragma unroll 8
   for (int i = 0; i < shards; ++i) {
     s += stats[(long long)i * 2 * C + c];
     q += stats[(long long)i * 2 * C + C + c];
+  }
+#pragma unroll 8
+  for (int i = 0; i < shards; ++i) {
     stats[(long long)i * 2 * C + c] = 0.f;
     stats[(long long)i * 2 * C + C + c] = 0.f;
   }
-  double mean = s / count;
-  double var = q / count - mean * mean;
+  double mean = (double)s / count;
+  double var = (double)q / count - mean * mean;
   if (var < 0) var = 0;
   float inv = rsqrtf((float)var + eps);
   mean_out[c] = (float)mean;
@@ -111,7 +115,7 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ da, const bf16* __
                                      const float* __restrict__ mean, const float* __restrict__ invstd,
                                      const bf16* __restrict__ y2, const float* __restrict__ mean2,
                                      const float* __restrict__ invstd2, long long M, int C, float* __restrict__ sums,
-                                     int shards) {
+                                     int shards, const float* __restrict__ mscale, const float* __restrict__ mshift) {
   const int cpr = C >> 3;
   const int rows_par = NT / cpr > 0 ? NT / cpr : 1;
   const int t = threadIdx.x;
@@ -119,10 +123,11 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ da, const bf16* __
   const int c0 = cchunk * 8;
   float s0[8] = {0}, s1[8] = {0}, s2[8] = {0};
   if (rsub < rows_par) {
-    float mu[8], is[8], mu2[8], is2[8];
+    float mu[8], is[8], mu2[8], is2[8], msc[8], msh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e];
+      msc[e] = mscale ? mscale[c0 + e] : 1.f; msh[e] = mshift ? mshift[c0 + e] : 0.f;
       mu2[e] = y2 ? mean2[c0 + e] : 0.f; is2[e] = y2 ? invstd2[c0 + e] : 0.f;
     }
     for (long long r = (long long)blockIdx.x * rows_par + rsub; r < M; r += (long long)gridDim.x * rows_par) {
@@ -137,6 +142,7 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ da, const bf16* __
       for (int e = 0; e < 8; ++e) {
         float dz = bf2f(g[e]);
         if (a && !(bf2f(av[e]) > 0.f)) dz = 0.f;
+        if (!a && mscale && !(bf2f(yv[e]) * msc[e] + msh[e] > 0.f)) dz = 0.f;
         s0[e] += dz;
         s1[e] += dz * (bf2f(yv[e]) - mu[e]) * is[e];
         if (y2) s2[e] += dz * (bf2f(y2v[e]) - mu2[e]) * is2[e];
@@ -164,7 +170,7 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ da, const bf16* __
 
 // Reduce shards; write dgamma/dbeta (+= if accumulate) and per-channel apply coefficients
 // coef: [k1, k2, k3][C] with dy = k1*(dz - k2 - xhat*k3); coef2 same for the second BN.
-__global__ void bn_bwd_finalize_kernel(float* __restrict__ sums, int shards, int C, float count,
+__global__ void bn_bwd_finalize_kernel(float* sums, int shards, int C, float count,
                                        const float* __restrict__ gamma, const float* __restrict__ invstd,
                                        const float* __restrict__ gamma2, const float* __restrict__ invstd2,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dgamma2,
@@ -172,9 +178,14 @@ __global__ void bn_bwd_finalize_kernel(float* __restrict__ sums, int shards, int
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+  for (int i = 0; i < shards; ++i) {
+    const float* p = sums + (long long)i * 3 * C;
+    s0 += p[c]; s1 += p[C + c]; s2 += p[2 * C + c];
+  }
+#pragma unroll 8
   for (int i = 0; i < shards; ++i) {
     float* p = sums + (long long)i * 3 * C;
-    s0 += p[c]; s1 += p[C + c]; s2 += p[2 * C + c];
     p[c] = 0.f; p[C + c] = 0.f; p[2 * C + c] = 0.f;
   }
   dgamma[c] = s1;
@@ -197,7 +208,8 @@ __global__ void bn_bwd_apply_kernel(const bf16* __restrict__ da, const bf16* __r
                                     const float* __restrict__ coef, bf16* __restrict__ dy, const bf16* __restrict__ y2,
                                     const float* __restrict__ mean2, const float* __restrict__ invstd2,
                                     const float* __restrict__ coef2, bf16* __restrict__ dy2, bf16* __restrict__ dres,
-                                    long long nchunks, int C) {
+                                    long long nchunks, int C, const float* __restrict__ mscale,
+                                    const float* __restrict__ mshift) {
   const int cpr = C >> 3;
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < nchunks; i += (long long)gridDim.x * NT) {
     const int c0 = (int)(i % cpr) * 8;
@@ -210,6 +222,7 @@ __global__ void bn_bwd_apply_kernel(const bf16* __restrict__ da, const bf16* __r
     for (int e = 0; e < 8; ++e) {
       dz[e] = bf2f(g[e]);
       if (a && !(bf2f(av[e]) > 0.f)) dz[e] = 0.f;
+      if (!a && mscale && !(bf2f(yv[e]) * mscale[c0 + e] + mshift[c0 + e] > 0.f)) dz[e] = 0.f;
     }
     bf16x8 o;
 #pragma unroll
@@ -249,7 +262,7 @@ extern "C" {
 int tfk_bn_finalize(float* stats, int shards, int C, float count, const float* gamma, const float* beta, float eps,
                     float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* scale,
                     float* shift, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, stats, shards, C, count, gamma, beta, eps,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, stats, shards, C, count, gamma, beta, eps,
                      momentum, run_mean, run_var, mean, invstd, scale, shift);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -267,25 +280,26 @@ int tfk_bn_apply(const bf16* y, const float* scale, const float* shift, const bf
 }
 int tfk_bn_bwd_reduce(const bf16* da, const bf16* a, const bf16* y, const float* mean, const float* invstd, const bf16* y2,
                       const float* mean2, const float* invstd2, long long M, int C, float* sums, int shards,
-                      hipStream_t s) {
+                      const float* mscale, const float* mshift, hipStream_t s) {
   int cpr = C / 8, rows_par = NT / cpr > 0 ? NT / cpr : 1;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_for(M, rows_par * 16, 2048)), dim3(NT), 0, s, da, a, y, mean, invstd,
-                     y2, mean2, invstd2, M, C, sums, shards);
+                     y2, mean2, invstd2, M, C, sums, shards, mscale, mshift);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_bn_bwd_finalize(float* sums, int shards, int C, float count, const float* gamma, const float* invstd,
                         const float* gamma2, const float* invstd2, float* dgamma, float* dbeta, float* dgamma2,
                         float* dbeta2, float* coef, float* coef2, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, shards, C, count, gamma, invstd,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, sums, shards, C, count, gamma, invstd,
                      gamma2, invstd2, dgamma, dbeta, dgamma2, dbeta2, coef, coef2);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_bn_bwd_apply(const bf16* da, const bf16* a, const bf16* y, const float* mean, const float* invstd,
                      const float* coef, bf16* dy, const bf16* y2, const float* mean2, const float* invstd2,
-                     const float* coef2, bf16* dy2, bf16* dres, long long M, int C, hipStream_t s) {
+                     const float* coef2, bf16* dy2, bf16* dres, long long M, int C, const float* mscale,
+                     const float* mshift, hipStream_t s) {
   long long nch = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(nch, NT * 4, 8192)), dim3(NT), 0, s, da, a, y, mean, invstd, coef,
-                     dy, y2, mean2, invstd2, coef2, dy2, dres, nch, C);
+                     dy, y2, mean2, invstd2, coef2, dy2, dres, nch, C, mscale, mshift);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }

@@ -367,6 +367,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
     __syncthreads();
     bf16* C = (bf16*)p.C + bz * p.sC;
     constexpr int CPR = BN / 8, TOT = BM * CPR;
+    const bool bnr = p.bn_sums != nullptr;
+    const int ccol = tid % CPR;  // this thread's 8-column chunk (fixed: NT % CPR == 0)
+    float r0[8], r1[8], r2[8], mu[8], is[8], sc[8], sh[8], mu2[8], is2[8];
+    if (bnr) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int n = min(n0 + ccol * 8 + e, p.N - 1);
+        r0[e] = r1[e] = r2[e] = 0.f;
+        mu[e] = p.bn_mean[n]; is[e] = p.bn_invstd[n];
+        sc[e] = p.bn_scale ? p.bn_scale[n] : 1.f; sh[e] = p.bn_shift ? p.bn_shift[n] : 0.f;
+        mu2[e] = p.bn_y2 ? p.bn_mean2[n] : 0.f; is2[e] = p.bn_y2 ? p.bn_invstd2[n] : 0.f;
+      }
+    }
 #pragma unroll
     for (int it = 0; it < TOT / NT; ++it) {
       const int idx = tid + it * NT;
@@ -376,18 +389,67 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
       bf16x8 v = *(const bf16x8*)(Cs + row * LDC_S + cc * 8);
       bf16* dst = C + (long long)m * p.ldc + n;
       if (n + 7 < p.N && (p.ldc & 7) == 0) {
+        const long long off = bz * p.sC + (long long)m * p.ldc + n;
         if (p.resid) {
-          bf16x8 rr = *(const bf16x8*)((const bf16*)p.resid + bz * p.sC + (long long)m * p.ldc + n);
+          bf16x8 rr = *(const bf16x8*)((const bf16*)p.resid + off);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[e]));
         }
         *(bf16x8*)dst = v;
+        if (bnr) {
+          bf16x8 yv = *(const bf16x8*)((const bf16*)p.bn_y + off);
+          bf16x8 av, y2v;
+          if (p.bn_a) av = *(const bf16x8*)((const bf16*)p.bn_a + off);
+          if (p.bn_y2) y2v = *(const bf16x8*)((const bf16*)p.bn_y2 + off);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float y = bf2f(yv[e]);
+            bool keep = p.bn_a ? (bf2f(av[e]) > 0.f) : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
+            const float dz = keep ? bf2f(v[e]) : 0.f;
+            r0[e] += dz;
+            r1[e] += dz * (y - mu[e]) * is[e];
+            if (p.bn_y2) r2[e] += dz * (bf2f(y2v[e]) - mu2[e]) * is2[e];
+          }
+        }
       } else {
         for (int e = 0; e < 8 && n + e < p.N; ++e) {
           float x = bf2f(v[e]);
           if (p.resid) x += bf2f(((const bf16*)p.resid)[bz * p.sC + (long long)m * p.ldc + n + e]);
           dst[e] = f2bf(x);
         }
+      }
+    }
+    if (bnr) {
+      // lanes sharing a column chunk: tid % CPR equal -> xor over the bits above log2(CPR)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = CPR; o < 64; o <<= 1) {
+          r0[e] += __shfl_xor(r0[e], o, 64);
+          r1[e] += __shfl_xor(r1[e], o, 64);
+          r2[e] += __shfl_xor(r2[e], o, 64);
+        }
+      __syncthreads();  // C tile no longer needed: reuse LDS for the cross-wave reduction
+      float* red = (float*)smem;  // [4 waves][3][CPR*8]
+      if (lane < CPR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[(wid * 3 + 0) * (CPR * 8) + lane * 8 + e] = r0[e];
+          red[(wid * 3 + 1) * (CPR * 8) + lane * 8 + e] = r1[e];
+          red[(wid * 3 + 2) * (CPR * 8) + lane * 8 + e] = r2[e];
+        }
+      }
+      __syncthreads();
+      const int nsum = p.bn_y2 ? 3 : 2;
+      float* st = p.bn_sums + (long long)(blockIdx.x % p.bn_shards) * 3 * p.N;
+      for (int k = tid; k < nsum * CPR * 8; k += NT) {
+        const int which = k / (CPR * 8), col = k - which * (CPR * 8);
+        const int n = n0 + col;
+        if (n >= p.N) continue;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) v += red[(w * 3 + which) * (CPR * 8) + col];
+        atomicAdd(st + which * p.N + n, v);
       }
     }
   }

@@ -20,5 +20,20 @@ struct GemmParams {
   int kt_per_split;
   long long split_stride;  // f32 elements between split-K slabs
   int tiles_n;
+  // Fused BatchNorm-backward reduction over the final bf16 output dA (bf16 epilogue only, N%8==0):
+  //   dz = dA * mask,  mask = bn_a ? (a > 0) : bn_relu ? (y*scale+shift > 0) : 1
+  //   bn_sums[shard][0][n] += dz,  [1][n] += dz*(y-mean)*invstd,  [2][n] += dz*(y2-mean2)*invstd2
+  const void* bn_y;
+  const void* bn_a;
+  const float* bn_mean;
+  const float* bn_invstd;
+  const float* bn_scale;
+  const float* bn_shift;
+  int bn_relu;
+  const void* bn_y2;
+  const float* bn_mean2;
+  const float* bn_invstd2;
+  float* bn_sums;
+  int bn_shards;
 };
 }  // namespace tfk

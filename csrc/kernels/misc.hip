@@ -13,31 +13,43 @@ int grid_for(long long work, int cap = 8192) {
   return (int)g;
 }
 
-// out[i] = (acc ? out[i] : 0) + sum_s slabs[s*stride + i]; optional bf16 output instead.
+// out[i] = (acc ? out[i] : 0) + alpha * sum_s slabs[s*stride + i]; optional bf16 output instead.
+// 2-D grid: x over 1024-element chunks (4 per lane, 16-B loads), y over groups of SG slabs, so a
+// small weight with hundreds of split-K slabs still spreads over the whole chip (the 1-D form was
+// latency-bound: 17 blocks each walking 256 slabs serially). Groups > 1 combine with f32 atomics
+// into `out` (pre-initialised by the first group's pass of the launcher below).
+constexpr int SG = 8;
 __global__ void splitk_reduce_kernel(const float* __restrict__ slabs, int S, long long stride, long long n,
-                                     float* __restrict__ out, bf16* __restrict__ outb, int accumulate, float alpha) {
-  for (long long i = ((long long)blockIdx.x * NT + threadIdx.x) * 4; i < n; i += (long long)gridDim.x * NT * 4) {
-    if (i + 3 < n) {
-      f32x4 a = {0.f, 0.f, 0.f, 0.f};
-      for (int s = 0; s < S; ++s) a += *(const f32x4*)(slabs + s * stride + i);
-      a *= alpha;
-      if (out) {
-        if (accumulate) a += *(f32x4*)(out + i);
-        *(f32x4*)(out + i) = a;
-      } else {
-        bf16x4 o;
+                                     float* __restrict__ out, bf16* __restrict__ outb, int accumulate, float alpha,
+                                     int atomic) {
+  const long long i = ((long long)blockIdx.x * NT + threadIdx.x) * 4;
+  if (i >= n) return;
+  const int s0 = blockIdx.y * SG, s1 = gridDim.y == 1 ? S : min(S, s0 + SG);
+  if (i + 3 < n) {
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int s = s0; s < s1; ++s) a += __builtin_nontemporal_load((const f32x4*)(slabs + s * stride + i));
+    a *= alpha;
+    if (atomic) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = f2bf(a[e] + (accumulate ? bf2f(outb[i + e]) : 0.f));
-        *(bf16x4*)(outb + i) = o;
-      }
+      for (int e = 0; e < 4; ++e) atomicAdd(out + i + e, a[e]);
+    } else if (out) {
+      if (accumulate) a += *(f32x4*)(out + i);
+      *(f32x4*)(out + i) = a;
     } else {
-      for (long long j = i; j < n; ++j) {
-        float a = 0.f;
-        for (int s = 0; s < S; ++s) a += slabs[s * stride + j];
-        a *= alpha;
-        if (out) out[j] = a + (accumulate ? out[j] : 0.f);
-        else outb[j] = f2bf(a + (accumulate ? bf2f(outb[j]) : 0.f));
-      }
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(a[e] + (accumulate ? bf2f(outb[i + e]) : 0.f));
+      *(bf16x4*)(outb + i) = o;
+    }
+  } else {
+    for (long long j = i; j < n; ++j) {
+      float a = 0.f;
+      for (int s = s0; s < s1; ++s) a += slabs[s * stride + j];
+      a *= alpha;
+      if (atomic) atomicAdd(out + j, a);
+      else if (out) out[j] = a + (accumulate ? out[j] : 0.f);
+      else outb[j] = f2bf(a + (accumulate ? bf2f(outb[j]) : 0.f));
     }
   }
 }
@@ -155,8 +167,19 @@ __global__ void add_kernel(const bf16* __restrict__ a, const bf16* __restrict__ 
 extern "C" {
 int tfk_splitk_reduce(const float* slabs, int S, long long stride, long long n, float* out, bf16* outb, int accumulate,
                       float alpha, hipStream_t s) {
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(n / 4 + 1)), dim3(NT), 0, s, slabs, S, stride, n, out, outb,
-                     accumulate, alpha);
+  const unsigned gx = (unsigned)((n + NT * 4 - 1) / (NT * 4));
+  const int groups = (S + SG - 1) / SG;
+  if (groups == 1 || !out) {
+    // bf16 output (rare) or few slabs: single pass over all slabs per element
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, 1), dim3(NT), 0, s, slabs, S, stride, n, out, outb, accumulate,
+                       alpha, 0);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  // first slab group initialises (or accumulates into) out; the remaining groups add atomically
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, 1), dim3(NT), 0, s, slabs, SG, stride, n, out, outb, accumulate,
+                     alpha, 0);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, (unsigned)(groups - 1)), dim3(NT), 0, s, slabs + SG * stride,
+                     S - SG, stride, n, out, outb, 1, alpha, 1);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_transpose_arb(const bf16* in, bf16* out, int A, int R, int B, hipStream_t s) {

@@ -67,7 +67,15 @@ class Bottleneck:
             self.saved = (x, y1, a1, y2, a2, y3, ysc, out)
         return out
 
-    def backward(self, dout, need_dx=True):
+    def tail_reduce(self) -> BN.BNReduce:
+        """BN-backward reduction spec of this block's tail (relu(bn3(y3) + shortcut)); fused into
+        the epilogue of the NEXT block's final dgrad, which produces this block's dout."""
+        x, y1, a1, y2, a2, y3, ysc, out = self.saved
+        return BN.BNReduce(y3, self.bn3.st, a=out, y2=ysc, st2=self.bn_sc.st if self.proj else None)
+
+    def backward(self, dout, need_dx=True, dout_reduced=False, next_bnr: BN.BNReduce | None = None):
+        """dout_reduced: the producer of dout already accumulated this block's tail BN sums.
+        next_bnr: reduction spec to fuse into the dgrad that produces dx (previous block's tail)."""
         x, y1, a1, y2, a2, y3, ysc, out = self.saved
         self.saved = None
         cnt3 = y3.numel() // y3.shape[-1]
@@ -75,34 +83,36 @@ class Bottleneck:
             dy3, dysc, _ = BN.bn_backward(dout, out, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
                                           self.bn3.beta.grad, cnt3, y2=ysc, st2=self.bn_sc.st,
                                           gamma2=self.bn_sc.gamma.master, dgamma2=self.bn_sc.gamma.grad,
-                                          dbeta2=self.bn_sc.beta.grad)
+                                          dbeta2=self.bn_sc.beta.grad, reduced=dout_reduced)
             dres = None
             self.arena.grad_ready(self.bn3.gamma, self.bn3.beta, self.bn_sc.gamma, self.bn_sc.beta)
         else:
             dy3, _, dres = BN.bn_backward(dout, out, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
-                                          self.bn3.beta.grad, cnt3, want_dres=True)
+                                          self.bn3.beta.grad, cnt3, want_dres=True, reduced=dout_reduced)
             self.arena.grad_ready(self.bn3.gamma, self.bn3.beta)
-        da2 = self.conv3.backward(dy3, a2)
-        dy2, _, _ = BN.bn_backward(da2, a2, y2, self.bn2.st, self.bn2.gamma.master, self.bn2.gamma.grad,
-                                   self.bn2.beta.grad, y2.numel() // y2.shape[-1])
+        # bn2/bn1 have no residual input: relu mask recomputed from y, sums fused into the dgrad epilogue
+        da2 = self.conv3.backward(dy3, a2, bnr=BN.BNReduce(y2, self.bn2.st))
+        dy2, _, _ = BN.bn_backward(da2, None, y2, self.bn2.st, self.bn2.gamma.master, self.bn2.gamma.grad,
+                                   self.bn2.beta.grad, y2.numel() // y2.shape[-1], relu_from_y=True, reduced=True)
         self.arena.grad_ready(self.bn2.gamma, self.bn2.beta)
-        da1 = self.conv2.backward(dy2, a1)
-        dy1, _, _ = BN.bn_backward(da1, a1, y1, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
-                                   self.bn1.beta.grad, y1.numel() // y1.shape[-1])
+        da1 = self.conv2.backward(dy2, a1, bnr=BN.BNReduce(y1, self.bn1.st))
+        dy1, _, _ = BN.bn_backward(da1, None, y1, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
+                                   self.bn1.beta.grad, y1.numel() // y1.shape[-1], relu_from_y=True, reduced=True)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
         if self.proj:
             dx = self.conv1.backward(dy1, x, need_dx=need_dx)
-            dx = self.conv_sc.backward(dysc, x, need_dx=need_dx, resid=dx)
+            dx = self.conv_sc.backward(dysc, x, need_dx=need_dx, resid=dx, bnr=next_bnr)
         else:
-            dx = self.conv1.backward(dy1, x, need_dx=need_dx, resid=dres)
+            dx = self.conv1.backward(dy1, x, need_dx=need_dx, resid=dres, bnr=next_bnr)
         return dx
 
 
 class ResNet:
     """ResNet v1.5 on the tfk executor. Input: NHWC bf16 [N,224,224,8] (RGB + zero pad)."""
 
-    def __init__(self, depth: int = 50, num_classes: int = 1000, width: int = 64, label_smoothing: float = 0.1):
-        if depth not in DEPTHS or DEPTHS[depth] is None:
+    def __init__(self, depth: int = 50, num_classes: int = 1000, width: int = 64, label_smoothing: float = 0.1,
+                 stages: list | None = None):
+        if stages is None and (depth not in DEPTHS or DEPTHS[depth] is None):
             raise ValueError(f"unsupported ResNet depth {depth}")
         self.depth, self.num_classes, self.label_smoothing = depth, num_classes, label_smoothing
         self.name = f"resnet{depth}"
@@ -111,7 +121,7 @@ class ResNet:
         self.bn1 = BatchNorm(a, "bn_conv1", width)
         self.blocks: list[Bottleneck] = []
         cin = width
-        for si, n in enumerate(DEPTHS[depth]):
+        for si, n in enumerate(stages or DEPTHS[depth]):
             w = width * (2 ** si)
             for bi in range(n):
                 stride = 2 if (bi == 0 and si > 0) else 1
@@ -181,11 +191,13 @@ class ResNet:
         x0, y0, a0, idx, hshape, _ = self._saved
         self._saved = None
         dh = PL.avgpool_bwd(df, hshape)
-        for i in range(len(self.blocks) - 1, -1, -1):
-            dh = self.blocks[i].backward(dh)
+        nb = len(self.blocks)
+        for i in range(nb - 1, -1, -1):
+            nxt = self.blocks[i - 1].tail_reduce() if i > 0 else None
+            dh = self.blocks[i].backward(dh, dout_reduced=i < nb - 1, next_bnr=nxt)
         da0 = PL.maxpool_bwd(dh, idx, a0.shape, 3, 2, 1)
-        dy0, _, _ = BN.bn_backward(da0, a0, y0, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
-                                   self.bn1.beta.grad, y0.numel() // y0.shape[-1])
+        dy0, _, _ = BN.bn_backward(da0, None, y0, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
+                                   self.bn1.beta.grad, y0.numel() // y0.shape[-1], relu_from_y=True)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
         self.conv1.backward(dy0, x0, need_dx=False)
         return loss, corr

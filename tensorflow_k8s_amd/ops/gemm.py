@@ -80,9 +80,11 @@ def pick_splits(tiles: int, K: int, min_ktiles: int = 4) -> int:
 
 
 def _gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile, *, alpha=1.0, beta=0.0, bias=None, resid=None,
-          act=0, stats=None, shards=1, splits=1, batch=1, sA=0, sB=0, sC=0, split_stride=0, conv=NO_CONV):
+          act=0, stats=None, shards=1, splits=1, batch=1, sA=0, sB=0, sC=0, split_stride=0, conv=NO_CONV, bnr=None):
     lib().gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile[0], tile[1], alpha, beta, bias, resid, act,
-               stats, shards, splits, batch, sA, sB, sC, split_stride, conv)
+               stats, shards, splits, batch, sA, sB, sC, split_stride, conv,
+               bnr.gemm_args() if bnr is not None else [], int(bnr.relu) if bnr is not None else 0,
+               bnr.st.shards if bnr is not None else 1)
 
 
 def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, accumulate: bool, device,
@@ -236,8 +238,9 @@ def conv_weight_t(w: torch.Tensor, g: ConvGeom, out: torch.Tensor | None = None)
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tensor | None = None,
-               wt: torch.Tensor | None = None) -> torch.Tensor:
-    """dx[N,H,W,C] = conv_transpose(dy[N,P,Q,K], w) (+ resid)."""
+               wt: torch.Tensor | None = None, bnr=None) -> torch.Tensor:
+    """dx[N,H,W,C] = conv_transpose(dy[N,P,Q,K], w) (+ resid). bnr (ops.norm.BNReduce): also
+    accumulate the BN-backward channel sums of the layer that produced x, from the final dx."""
     if not on_gpu(dy):
         dyn = dy.float().permute(0, 3, 1, 2)
         wn = w.float().permute(0, 3, 1, 2)
@@ -247,20 +250,24 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
                                 dilation=(g.dh, g.dw)).permute(0, 2, 3, 1)
         if resid is not None:
             dx = dx.to(torch.bfloat16).float() + resid.float()
-        return dx.to(torch.bfloat16).contiguous()
+        dx = dx.to(torch.bfloat16).contiguous()
+        if bnr is not None:
+            bnr.reference_accumulate(dx)
+        return dx
     M = g.N * g.H * g.W
     dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
     tile = pick_tile(M, g.C)
     if g.pointwise:
-        _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid)
+        _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid, bnr=bnr)
     elif g.R == 1 and g.S == 1:
         # strided 1x1: B(n=c, k=co) = W[co][c] is K-outer with ldb = C; gather handles the stride
         _gemm(dy, w, dx, M, g.C, g.K, 0, g.C, g.C, A_CONV_DGRAD, B_KOUT, EPI_BF16, tile, resid=resid,
-              conv=g.vec())
+              conv=g.vec(), bnr=bnr)
     else:
         wt = wt if wt is not None else conv_weight_t(w, g)
         Kd = g.R * g.S * g.K
-        _gemm(dy, wt, dx, M, g.C, Kd, 0, Kd, g.C, A_CONV_DGRAD, B_KIN, EPI_BF16, tile, resid=resid, conv=g.vec())
+        _gemm(dy, wt, dx, M, g.C, Kd, 0, Kd, g.C, A_CONV_DGRAD, B_KIN, EPI_BF16, tile, resid=resid, conv=g.vec(),
+              bnr=bnr)
     return dx
 
 

@@ -78,17 +78,53 @@ def bn_apply(y, st: BNState, relu: bool, r=None, rst: BNState | None = None, out
     return out
 
 
+class BNReduce:
+    """Spec for fusing a BN-backward reduction into the epilogue of the GEMM that produces dA
+    (dz = dA * mask; sums into st.sums). mask: `a > 0` if a is given, else `y*scale+shift > 0`
+    when relu, else 1. y2/st2: projection-shortcut BN sharing the same dz."""
+
+    def __init__(self, y, st: BNState, a=None, relu: bool = True, y2=None, st2: BNState | None = None):
+        self.y, self.st, self.a, self.relu, self.y2, self.st2 = y, st, a, relu, y2, st2
+
+    def gemm_args(self):
+        st, st2 = self.st, self.st2
+        return [self.y, self.a, st.mean, st.invstd, st.scale if (self.relu and self.a is None) else None,
+                st.shift if (self.relu and self.a is None) else None, self.y2, st2.mean if st2 else None,
+                st2.invstd if st2 else None, st.sums]
+
+    def reference_accumulate(self, dA: torch.Tensor) -> None:
+        """CPU oracle of the fused reduction (shard 0 of st.sums)."""
+        C = self.st.C
+        dz = dA.float().reshape(-1, C)
+        y = self.y.float().reshape(-1, C)
+        if self.a is not None:
+            dz = dz * (self.a.float().reshape(-1, C) > 0)
+        elif self.relu:
+            dz = dz * ((y * self.st.scale + self.st.shift) > 0)
+        v = self.st.sums.view(self.st.shards, 3, C)
+        v[0, 0] += dz.sum(0)
+        v[0, 1] += (dz * (y - self.st.mean) * self.st.invstd).sum(0)
+        if self.y2 is not None:
+            y2 = self.y2.float().reshape(-1, C)
+            v[0, 2] += (dz * (y2 - self.st2.mean) * self.st2.invstd).sum(0)
+
+
 def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=None, st2: BNState | None = None,
-                gamma2=None, dgamma2=None, dbeta2=None, want_dres: bool = False):
+                gamma2=None, dgamma2=None, dbeta2=None, want_dres: bool = False, relu_from_y: bool = False,
+                reduced: bool = False):
     """Backward of a = relu?(bn(y) [+ bn2(y2) | + r]).
 
-    a: post-activation output used for the relu mask (None -> no relu). Returns (dy, dy2, dres).
-    Writes dgamma/dbeta (and the second BN's) into the given (arena) views."""
+    a: post-activation output used for the relu mask (None -> no relu, unless relu_from_y: the mask
+    is recomputed as y*scale+shift > 0, valid when there is no residual input). reduced: the
+    per-channel sums were already accumulated into st.sums by the producer's GEMM epilogue
+    (BNReduce). Returns (dy, dy2, dres). Writes dgamma/dbeta (and the second BN's)."""
     C = st.C
     if not on_gpu(da):
         dz = da.float()
         if a is not None:
             dz = dz * (a.float() > 0)
+        elif relu_from_y:
+            dz = dz * ((y.float() * st.scale + st.shift) > 0)
         dz2 = dz.reshape(-1, C)
         xh = (y.float().reshape(-1, C) - st.mean) * st.invstd
         s0, s1 = dz2.sum(0), (dz2 * xh).sum(0)
@@ -105,13 +141,16 @@ def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=No
         return dy, dy2, dres
     M = da.numel() // C
     L = lib()
-    L.bn_bwd_reduce(da, a, y, st.mean, st.invstd, y2, st2.mean if st2 else None, st2.invstd if st2 else None, M, C,
-                    st.sums, st.shards)
+    msc = st.scale if (a is None and relu_from_y) else None
+    msh = st.shift if (a is None and relu_from_y) else None
+    if not reduced:
+        L.bn_bwd_reduce(da, a, y, st.mean, st.invstd, y2, st2.mean if st2 else None, st2.invstd if st2 else None, M, C,
+                        st.sums, st.shards, msc, msh)
     L.bn_bwd_finalize(st.sums, st.shards, C, float(count), gamma, st.invstd, gamma2, st2.invstd if st2 else None,
                       dgamma, dbeta, dgamma2, dbeta2, st.coef, st2.coef if st2 else None)
     dy = torch.empty_like(da)
     dy2 = torch.empty_like(da) if y2 is not None else None
     dres = torch.empty_like(da) if want_dres else None
     L.bn_bwd_apply(da, a, y, st.mean, st.invstd, st.coef, dy, y2, st2.mean if st2 else None,
-                   st2.invstd if st2 else None, st2.coef if st2 else None, dy2, dres, M, C)
+                   st2.invstd if st2 else None, st2.coef if st2 else None, dy2, dres, M, C, msc, msh)
     return dy, dy2, dres

@@ -54,13 +54,13 @@ class Conv2d:
         g = self.geom(x.shape)
         return G.conv_fwd(x, self.w.compute, g, stats.stats if stats else None, stats.shards if stats else 1)
 
-    def backward(self, dy, x, need_dx: bool = True, resid=None):
+    def backward(self, dy, x, need_dx: bool = True, resid=None, bnr=None):
         g = self.geom(x.shape)
         G.conv_wgrad(dy, x, g, self.w.grad)
         self.arena.grad_ready(self.w)
         if not need_dx:
             return None
-        return G.conv_dgrad(dy, self.w.compute, g, resid=resid)
+        return G.conv_dgrad(dy, self.w.compute, g, resid=resid, bnr=bnr)
 
 
 class BatchNorm:

@@ -183,3 +183,33 @@ def test_global_norm_clip():
     O.global_norm_clip_coef(g.to(DEV), 1.0, ss, coef, nrm)
     assert abs(float(nrm) - float(g.norm())) / float(g.norm()) < 1e-4
     assert abs(float(coef) - 1.0 / float(g.norm())) < 1e-5
+
+
+@pytest.mark.parametrize("mode", ["relu_from_y", "mask_a", "dual"])
+@pytest.mark.parametrize("cfg", [(2, 8, 8, 64, 256, 1, 1, 1, 0), (2, 9, 9, 64, 64, 3, 3, 1, 1), (2, 14, 14, 256, 512, 1, 1, 2, 0)])
+def test_dgrad_fused_bn_reduce(cfg, mode):
+    """BN-backward channel sums fused into the dgrad epilogue == the standalone reduction."""
+    N, H, W, C, K, R, S, st_, pd = cfg
+    g = G.ConvGeom(N, H, W, C, K, R, S, st_, st_, pd, pd)
+    w = bf(K, R, S, C, scale=0.05, seed=2)
+    dy = bf(N, g.P, g.Q, K, seed=3)
+    y = bf(N, H, W, C, seed=4)
+    y2 = bf(N, H, W, C, seed=5)
+    a = bf(N, H, W, C, seed=6)
+    res = {}
+    for dev in ("cpu", DEV):
+        st, st2 = BN.BNState(C, dev), BN.BNState(C, dev)
+        for s_ in (st, st2):
+            s_.mean.copy_(torch.randn(C) * 0.1); s_.invstd.copy_(torch.rand(C) + 0.5)
+            s_.scale.copy_(torch.randn(C)); s_.shift.copy_(torch.randn(C) * 0.1)
+        if mode == "relu_from_y":
+            spec = BN.BNReduce(y.to(dev), st)
+        elif mode == "mask_a":
+            spec = BN.BNReduce(y.to(dev), st, a=a.to(dev))
+        else:
+            spec = BN.BNReduce(y.to(dev), st, a=a.to(dev), y2=y2.to(dev), st2=st2)
+        dx = G.conv_dgrad(dy.to(dev), w.to(dev), g, bnr=spec)
+        res[dev] = (dx, st.sums.view(st.shards, 3, C).sum(0).cpu())
+    assert rel(res[DEV][0], res["cpu"][0]) < 1e-2
+    for k in range(3 if mode == "dual" else 2):
+        assert rel(res[DEV][1][k], res["cpu"][1][k]) < 2e-2, k

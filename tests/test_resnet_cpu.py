@@ -1,0 +1,85 @@
+"""CPU tier: the executor's hand-written ResNet backward (incl. the fused BN-reduce plumbing and
+mask-from-y) against torch autograd on the same arena weights."""
+import torch
+import torch.nn.functional as F
+
+from reference_models import _bn, resnet_loss
+from tensorflow_k8s_amd.models.resnet import Bottleneck, ResNet, synthetic_imagenet
+from tensorflow_k8s_amd.runtime.arena import ParamArena
+
+
+class _Round(torch.autograd.Function):
+    """Emulates bf16 storage of activations and of their gradients (what the executor keeps)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+def _block_case(cin, width, stride, prev_tail=False):
+    torch.manual_seed(0)
+    a = ParamArena()
+    b = Bottleneck(a, 2, 0, cin, width, stride)
+    a.finalize("cpu")
+    with torch.no_grad():
+        for bn in b.bns():
+            bn.gamma.master.uniform_(0.5, 1.5)
+            bn.beta.master.uniform_(-0.2, 0.2)
+    x = torch.randn(4, 16, 16, cin).relu().to(torch.bfloat16)
+    out = b.forward(x)
+    dout = torch.randn(out.shape).to(torch.bfloat16)
+    dx = b.backward(dout)
+    rd = _Round.apply
+    L = {p.name: p.master.clone().requires_grad_(True) for p in a.params}
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+
+    def conv(l, h):
+        return rd(F.conv2d(h, L[l.w.name].to(torch.bfloat16).float().permute(0, 3, 1, 2), stride=l.stride, padding=l.pad))
+
+    def bn(l, h):
+        return _bn(h, L[l.gamma.name], L[l.beta.name], l.eps)
+
+    o = rd(F.relu(bn(b.bn1, conv(b.conv1, xr))))
+    o = rd(F.relu(bn(b.bn2, conv(b.conv2, o))))
+    o = bn(b.bn3, conv(b.conv3, o))
+    sc = bn(b.bn_sc, conv(b.conv_sc, xr)) if b.proj else xr
+    r = rd(F.relu(o + sc))
+    (r * dout.float().permute(0, 3, 1, 2)).sum().backward()
+    assert float((r.permute(0, 2, 3, 1) - out.float()).norm() / r.norm()) < 1e-2
+    assert float((xr.grad.permute(0, 2, 3, 1) - dx.float()).norm() / xr.grad.norm()) < 0.1
+    for p in a.params:
+        ref = L[p.name].grad
+        assert float((p.grad - ref).norm() / (ref.norm() + 1e-12)) < 0.15, p.name
+
+
+def test_bottleneck_identity():
+    _block_case(256, 64, 1)
+
+
+def test_bottleneck_projection_strided():
+    _block_case(256, 128, 2)
+
+
+def test_resnet_gradients_track_autograd():
+    # shallow (one bottleneck per stage): full-depth random-init ResNets are chaotic enough that two
+    # bf16 runs with different summation orders decorrelate (measured), which says nothing about
+    # the backward implementation; the per-block tests above cover every block type at depth 1.
+    torch.manual_seed(0)
+    m = ResNet(50, num_classes=10, stages=[1, 1, 1, 1]).to("cpu")
+    with torch.no_grad():  # non-zero residual branches so every layer gets gradient
+        for bn in m.batchnorms():
+            bn.gamma.master.fill_(1.0)
+    m.arena.refresh_compute()
+    x, y = synthetic_imagenet(8, "cpu", image_size=96, num_classes=10)
+    loss, _ = m.forward_backward(x, y)
+    rl, leaves = resnet_loss(m, x, y, m.label_smoothing, emulate_bf16=True)
+    rl.backward()
+    assert abs(float(loss.mean()) - float(rl)) < 0.05
+    g = torch.cat([p.grad.reshape(-1) for p in m.arena.params])
+    r = torch.cat([leaves[p.name].grad.reshape(-1) for p in m.arena.params])
+    cos = float(F.cosine_similarity(g, r, dim=0))
+    assert cos > 0.9, cos

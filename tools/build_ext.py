@@ -60,14 +60,22 @@ def build_kernels(jobs: int | None = None, verbose: bool = False) -> str:
             tasks.append([HIPCC, "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}",
                           "-munsafe-fp-atomics", src, "-o", out])
     py_inc = sysconfig.get_paths()["include"]
+    cpp_hdrs = glob.glob(os.path.join(ROOT, "cpp", "*", "*.h"))
     for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "bindings", "*.cpp"))):
         out = os.path.join(OBJ, os.path.basename(src) + ".o")
         objs.append(out)
-        if _stale(out, [src]):
+        if _stale(out, [src] + headers + cpp_hdrs):
             cmd = ["g++", "-c", "-fPIC", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                    "-D_GLIBCXX_USE_CXX11_ABI=1", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
                    f"-I{py_inc}"] + [f"-I{p}" for p in inc] + [src, "-o", out]
             tasks.append(cmd)
+    # native checkpoint (TF bundle) + its deps from the control-plane tree, linked into _C
+    for rel in ("cpp/runtime/tfbundle.cc", "cpp/common/util.cc", "cpp/common/json.cc"):
+        src = os.path.join(ROOT, rel)
+        out = os.path.join(OBJ, "cp_" + os.path.basename(src) + ".o")
+        objs.append(out)
+        if _stale(out, [src] + cpp_hdrs):
+            tasks.append(["g++", "-c", "-fPIC", "-O2", "-std=c++17", "-pthread", src, "-o", out])
     if tasks:
         with cf.ThreadPoolExecutor(jobs) as ex:
             for f in [ex.submit(_run, t) for t in tasks]:

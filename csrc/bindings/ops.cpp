@@ -21,11 +21,10 @@ int tfk_bn_apply(const void*, const float*, const float*, const void*, const flo
                  int, hipStream_t);
 int tfk_bn_bwd_reduce(const void*, const void*, const void*, const float*, const float*, const void*, const float*,
                       const float*, long long, int, float*, int, const float*, const float*, hipStream_t);
-int tfk_bn_bwd_finalize(float*, int, int, float, const float*, const float*, const float*, const float*, float*, float*,
-                        float*, float*, float*, float*, hipStream_t);
-int tfk_bn_bwd_apply(const void*, const void*, const void*, const float*, const float*, const float*, void*, const void*,
-                     const float*, const float*, const float*, void*, void*, long long, int, const float*, const float*,
-                     hipStream_t);
+int tfk_bn_bwd_finalize(float*, int, int, float, const float*, const float*, const float*, const float*, const float*,
+                        const float*, float*, float*, float*, float*, float*, float*, hipStream_t);
+int tfk_bn_bwd_apply(const void*, const void*, const void*, const float*, void*, const void*, const float*, void*, void*,
+                     long long, int, const float*, const float*, hipStream_t);
 int tfk_maxpool_fwd(const void*, void*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int tfk_maxpool_bwd(const void*, const uint8_t*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                     hipStream_t);
@@ -259,37 +258,46 @@ void bn_bwd_reduce(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tens
            "bn_bwd_reduce");
 }
 
-void bn_bwd_finalize(torch::Tensor sums, int shards, int C, double count, torch::Tensor gamma, torch::Tensor invstd,
-                     c10::optional<torch::Tensor> gamma2, c10::optional<torch::Tensor> invstd2, torch::Tensor dgamma,
-                     torch::Tensor dbeta, c10::optional<torch::Tensor> dgamma2, c10::optional<torch::Tensor> dbeta2,
-                     torch::Tensor coef, c10::optional<torch::Tensor> coef2) {
+void bn_bwd_finalize(torch::Tensor sums, int shards, int C, double count, torch::Tensor gamma, torch::Tensor mean,
+                     torch::Tensor invstd, c10::optional<torch::Tensor> gamma2, c10::optional<torch::Tensor> mean2,
+                     c10::optional<torch::Tensor> invstd2, torch::Tensor dgamma, torch::Tensor dbeta,
+                     c10::optional<torch::Tensor> dgamma2, c10::optional<torch::Tensor> dbeta2, torch::Tensor coef,
+                     c10::optional<torch::Tensor> coef2) {
   need_f32(sums, "sums"); need_numel(sums, (long long)shards * 3 * C, "sums");
-  need_numel(dgamma, C, "dgamma"); need_numel(dbeta, C, "dbeta"); need_numel(coef, 3 * C, "coef");
-  if (coef2.has_value() && coef2->defined()) need_numel(*coef2, 3 * C, "coef2");
+  for (auto* t : {&gamma, &mean, &invstd, &dgamma, &dbeta}) { need_f32(*t, "bn vector"); need_numel(*t, C, "bn vector"); }
+  need_numel(coef, 3 * C, "coef");
+  if (coef2.has_value() && coef2->defined()) {
+    need_numel(*coef2, 3 * C, "coef2");
+    TORCH_CHECK(gamma2.has_value() && mean2.has_value() && invstd2.has_value() && dgamma2.has_value() &&
+                    dbeta2.has_value(), "bn_bwd_finalize: second BN needs gamma2/mean2/invstd2/dgamma2/dbeta2");
+  }
   check_rc(tfk_bn_bwd_finalize(sums.data_ptr<float>(), shards, C, (float)count, gamma.data_ptr<float>(),
-                               invstd.data_ptr<float>(), opt_ptr<const float>(gamma2), opt_ptr<const float>(invstd2),
-                               dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), opt_ptr<float>(dgamma2),
-                               opt_ptr<float>(dbeta2), coef.data_ptr<float>(), opt_ptr<float>(coef2), cur_stream()),
+                               mean.data_ptr<float>(), invstd.data_ptr<float>(), opt_ptr<const float>(gamma2),
+                               opt_ptr<const float>(mean2), opt_ptr<const float>(invstd2), dgamma.data_ptr<float>(),
+                               dbeta.data_ptr<float>(), opt_ptr<float>(dgamma2), opt_ptr<float>(dbeta2),
+                               coef.data_ptr<float>(), opt_ptr<float>(coef2), cur_stream()),
            "bn_bwd_finalize");
 }
 
-void bn_bwd_apply(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tensor y, torch::Tensor mean,
-                  torch::Tensor invstd, torch::Tensor coef, torch::Tensor dy, c10::optional<torch::Tensor> y2,
-                  c10::optional<torch::Tensor> mean2, c10::optional<torch::Tensor> invstd2,
-                  c10::optional<torch::Tensor> coef2, c10::optional<torch::Tensor> dy2,
+void bn_bwd_apply(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tensor y, torch::Tensor coef, torch::Tensor dy,
+                  c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> coef2, c10::optional<torch::Tensor> dy2,
                   c10::optional<torch::Tensor> dres, int64_t M, int C, c10::optional<torch::Tensor> mscale,
                   c10::optional<torch::Tensor> mshift) {
   need_bf16(da, "da"); need_bf16(y, "y"); need_bf16(dy, "dy");
   for (auto* t : {&da, &y, &dy}) need_numel(*t, M * C, "bn bwd tensor");
+  need_f32(coef, "coef"); need_numel(coef, 3 * C, "coef");
   if (a.has_value() && a->defined()) need_numel(*a, M * C, "a");
-  if (y2.has_value() && y2->defined()) { need_numel(*y2, M * C, "y2"); need_numel(*dy2, M * C, "dy2"); }
+  if (y2.has_value() && y2->defined()) {
+    TORCH_CHECK(coef2.has_value() && dy2.has_value(), "bn_bwd_apply: y2 needs coef2 and dy2");
+    need_numel(*y2, M * C, "y2"); need_numel(*dy2, M * C, "dy2"); need_numel(*coef2, 3 * C, "coef2");
+  }
   if (dres.has_value() && dres->defined()) need_numel(*dres, M * C, "dres");
+  if (mscale.has_value() && mscale->defined()) { need_numel(*mscale, C, "mscale"); need_numel(*mshift, C, "mshift"); }
   TORCH_CHECK(C % 8 == 0, "C%8");
-  check_rc(tfk_bn_bwd_apply(da.data_ptr(), opt_ptr<const void>(a), y.data_ptr(), mean.data_ptr<float>(),
-                            invstd.data_ptr<float>(), coef.data_ptr<float>(), dy.data_ptr(), opt_ptr<const void>(y2),
-                            opt_ptr<const float>(mean2), opt_ptr<const float>(invstd2), opt_ptr<const float>(coef2),
-                            opt_ptr<void>(dy2), opt_ptr<void>(dres), M, C, opt_ptr<const float>(mscale),
-                            opt_ptr<const float>(mshift), cur_stream()),
+  check_rc(tfk_bn_bwd_apply(da.data_ptr(), opt_ptr<const void>(a), y.data_ptr(), coef.data_ptr<float>(), dy.data_ptr(),
+                            opt_ptr<const void>(y2), opt_ptr<const float>(coef2), opt_ptr<void>(dy2),
+                            opt_ptr<void>(dres), M, C, opt_ptr<const float>(mscale), opt_ptr<const float>(mshift),
+                            cur_stream()),
            "bn_bwd_apply");
 }
 

@@ -78,25 +78,53 @@ __global__ void bn_stats_kernel(const bf16* __restrict__ y, long long M, int C, 
   }
 }
 
+__device__ __forceinline__ void load8(const float* __restrict__ p, float (&v)[8]) {
+  f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[e + 4] = b[e]; }
+}
+
+// Streaming passes: with FIXED a thread owns one 8-channel chunk (tid % cpr) and walks rows, so
+// per-channel coefficients are loaded once into registers; needs NT % cpr == 0 (C | 2048). Other
+// C use the flat layout and reload the chunk's coefficients per element group.
+template <bool FIXED>
 __global__ void bn_apply_kernel(const bf16* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
                                 const bf16* __restrict__ r, const float* __restrict__ rscale, const float* __restrict__ rshift,
-                                int relu, bf16* __restrict__ out, long long nchunks, int C) {
+                                int relu, bf16* __restrict__ out, long long M, int C) {
   const int cpr = C >> 3;
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < nchunks; i += (long long)gridDim.x * NT) {
-    const int c0 = (int)(i % cpr) * 8;
-    bf16x8 v = *(const bf16x8*)(y + i * 8);
-    f32x4 s0 = *(const f32x4*)(scale + c0), s1 = *(const f32x4*)(scale + c0 + 4);
-    f32x4 b0 = *(const f32x4*)(shift + c0), b1 = *(const f32x4*)(shift + c0 + 4);
+  long long i, step;
+  int c0;
+  if (FIXED) {
+    const int rows_par = NT / cpr;
+    c0 = (threadIdx.x % cpr) * 8;
+    i = ((long long)blockIdx.x * rows_par + threadIdx.x / cpr) * C + c0;
+    step = (long long)gridDim.x * rows_par * C;
+  } else {
+    i = ((long long)blockIdx.x * NT + threadIdx.x) * 8;
+    step = (long long)gridDim.x * NT * 8;
+    c0 = 0;
+  }
+  const long long end = M * C;
+  float s[8], b[8], rs[8], rb[8];
+  if (FIXED) {
+    load8(scale + c0, s); load8(shift + c0, b);
+    if (rscale) { load8(rscale + c0, rs); load8(rshift + c0, rb); }
+  }
+  for (; i < end; i += step) {
+    if (!FIXED) {
+      c0 = (int)((i >> 3) % cpr) * 8;
+      load8(scale + c0, s); load8(shift + c0, b);
+      if (rscale) { load8(rscale + c0, rs); load8(rshift + c0, rb); }
+    }
+    bf16x8 v = *(const bf16x8*)(y + i);
     float o[8];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { o[e] = bf2f(v[e]) * s0[e] + b0[e]; o[e + 4] = bf2f(v[e + 4]) * s1[e] + b1[e]; }
+    for (int e = 0; e < 8; ++e) o[e] = bf2f(v[e]) * s[e] + b[e];
     if (r) {
-      bf16x8 rv = *(const bf16x8*)(r + i * 8);
+      bf16x8 rv = *(const bf16x8*)(r + i);
       if (rscale) {
-        f32x4 rs0 = *(const f32x4*)(rscale + c0), rs1 = *(const f32x4*)(rscale + c0 + 4);
-        f32x4 rb0 = *(const f32x4*)(rshift + c0), rb1 = *(const f32x4*)(rshift + c0 + 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { o[e] += bf2f(rv[e]) * rs0[e] + rb0[e]; o[e + 4] += bf2f(rv[e + 4]) * rs1[e] + rb1[e]; }
+        for (int e = 0; e < 8; ++e) o[e] += bf2f(rv[e]) * rs[e] + rb[e];
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] += bf2f(rv[e]);
@@ -105,7 +133,7 @@ __global__ void bn_apply_kernel(const bf16* __restrict__ y, const float* __restr
     bf16x8 w;
 #pragma unroll
     for (int e = 0; e < 8; ++e) w[e] = f2bf(relu ? fmaxf(o[e], 0.f) : o[e]);
-    *(bf16x8*)(out + i * 8) = w;
+    *(bf16x8*)(out + i) = w;
   }
 }
 
@@ -168,11 +196,13 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ da, const bf16* __
   }
 }
 
-// Reduce shards; write dgamma/dbeta (+= if accumulate) and per-channel apply coefficients
-// coef: [k1, k2, k3][C] with dy = k1*(dz - k2 - xhat*k3); coef2 same for the second BN.
+// Reduce shards; write dgamma/dbeta (+= if accumulate) and per-channel apply coefficients.
+// With k1 = gamma*invstd, dy = k1*(dz - mean(dz) - xhat*mean(dz*xhat)) is affine in (dz, y):
+// coef = [k1, A, B][C] with dy = k1*dz + A*y + B; coef2 the same for the second BN.
 __global__ void bn_bwd_finalize_kernel(float* sums, int shards, int C, float count,
-                                       const float* __restrict__ gamma, const float* __restrict__ invstd,
-                                       const float* __restrict__ gamma2, const float* __restrict__ invstd2,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, const float* __restrict__ gamma2,
+                                       const float* __restrict__ mean2, const float* __restrict__ invstd2,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dgamma2,
                                        float* __restrict__ dbeta2, float* __restrict__ coef, float* __restrict__ coef2) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -190,62 +220,84 @@ __global__ void bn_bwd_finalize_kernel(float* sums, int shards, int C, float cou
   }
   dgamma[c] = s1;
   dbeta[c] = s0;
-  coef[c] = gamma[c] * invstd[c];
-  coef[C + c] = s0 / count;
-  coef[2 * C + c] = s1 / count;
+  {
+    const float inv = invstd[c], k1 = gamma[c] * inv, k3 = s1 / count;
+    coef[c] = k1;
+    coef[C + c] = -k1 * k3 * inv;
+    coef[2 * C + c] = k1 * (k3 * inv * mean[c] - s0 / count);
+  }
   if (coef2) {
     dgamma2[c] = s2;
     dbeta2[c] = s0;
-    coef2[c] = gamma2[c] * invstd2[c];
-    coef2[C + c] = s0 / count;
-    coef2[2 * C + c] = s2 / count;
+    const float inv = invstd2[c], k1 = gamma2[c] * inv, k3 = s2 / count;
+    coef2[c] = k1;
+    coef2[C + c] = -k1 * k3 * inv;
+    coef2[2 * C + c] = k1 * (k3 * inv * mean2[c] - s0 / count);
   }
 }
 
-// dy = k1*(dz - k2 - xhat*k3); optional dy2 (projection-shortcut BN) or dres = dz (identity shortcut).
+// dy = k1*dz + A*y + B; optional dy2 (projection-shortcut BN) or dres = dz (identity shortcut).
+// Relu mask: a > 0 if a is given, else y*mscale + mshift > 0 if mscale is given, else none.
+template <bool FIXED>
 __global__ void bn_bwd_apply_kernel(const bf16* __restrict__ da, const bf16* __restrict__ a, const bf16* __restrict__ y,
-                                    const float* __restrict__ mean, const float* __restrict__ invstd,
                                     const float* __restrict__ coef, bf16* __restrict__ dy, const bf16* __restrict__ y2,
-                                    const float* __restrict__ mean2, const float* __restrict__ invstd2,
                                     const float* __restrict__ coef2, bf16* __restrict__ dy2, bf16* __restrict__ dres,
-                                    long long nchunks, int C, const float* __restrict__ mscale,
+                                    long long M, int C, const float* __restrict__ mscale,
                                     const float* __restrict__ mshift) {
   const int cpr = C >> 3;
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < nchunks; i += (long long)gridDim.x * NT) {
-    const int c0 = (int)(i % cpr) * 8;
-    bf16x8 g = *(const bf16x8*)(da + i * 8);
-    bf16x8 yv = *(const bf16x8*)(y + i * 8);
+  long long i, step;
+  int c0;
+  if (FIXED) {
+    const int rows_par = NT / cpr;
+    c0 = (threadIdx.x % cpr) * 8;
+    i = ((long long)blockIdx.x * rows_par + threadIdx.x / cpr) * C + c0;
+    step = (long long)gridDim.x * rows_par * C;
+  } else {
+    i = ((long long)blockIdx.x * NT + threadIdx.x) * 8;
+    step = (long long)gridDim.x * NT * 8;
+    c0 = 0;
+  }
+  const long long end = M * C;
+  float k1[8], A[8], B[8], k1b[8], A2[8], B2[8], ms[8], mh[8];
+  auto load_coefs = [&]() {
+    load8(coef + c0, k1); load8(coef + C + c0, A); load8(coef + 2 * C + c0, B);
+    if (y2) { load8(coef2 + c0, k1b); load8(coef2 + C + c0, A2); load8(coef2 + 2 * C + c0, B2); }
+    if (!a && mscale) { load8(mscale + c0, ms); load8(mshift + c0, mh); }
+  };
+  if (FIXED) load_coefs();
+  for (; i < end; i += step) {
+    if (!FIXED) {
+      c0 = (int)((i >> 3) % cpr) * 8;
+      load_coefs();
+    }
+    bf16x8 g = *(const bf16x8*)(da + i);
+    bf16x8 yv = *(const bf16x8*)(y + i);
     bf16x8 av;
-    if (a) av = *(const bf16x8*)(a + i * 8);
+    if (a) av = *(const bf16x8*)(a + i);
     float dz[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       dz[e] = bf2f(g[e]);
-      if (a && !(bf2f(av[e]) > 0.f)) dz[e] = 0.f;
-      if (!a && mscale && !(bf2f(yv[e]) * mscale[c0 + e] + mshift[c0 + e] > 0.f)) dz[e] = 0.f;
+      if (a) {
+        if (!(bf2f(av[e]) > 0.f)) dz[e] = 0.f;
+      } else if (mscale) {
+        if (!(bf2f(yv[e]) * ms[e] + mh[e] > 0.f)) dz[e] = 0.f;
+      }
     }
     bf16x8 o;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = c0 + e;
-      float xh = (bf2f(yv[e]) - mean[c]) * invstd[c];
-      o[e] = f2bf(coef[c] * (dz[e] - coef[C + c] - xh * coef[2 * C + c]));
-    }
-    *(bf16x8*)(dy + i * 8) = o;
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(k1[e] * dz[e] + A[e] * bf2f(yv[e]) + B[e]);
+    *(bf16x8*)(dy + i) = o;
     if (y2) {
-      bf16x8 y2v = *(const bf16x8*)(y2 + i * 8);
+      bf16x8 y2v = *(const bf16x8*)(y2 + i);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = c0 + e;
-        float xh = (bf2f(y2v[e]) - mean2[c]) * invstd2[c];
-        o[e] = f2bf(coef2[c] * (dz[e] - coef2[C + c] - xh * coef2[2 * C + c]));
-      }
-      *(bf16x8*)(dy2 + i * 8) = o;
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(k1b[e] * dz[e] + A2[e] * bf2f(y2v[e]) + B2[e]);
+      *(bf16x8*)(dy2 + i) = o;
     }
     if (dres) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = f2bf(dz[e]);
-      *(bf16x8*)(dres + i * 8) = o;
+      *(bf16x8*)(dres + i) = o;
     }
   }
 }
@@ -273,9 +325,14 @@ int tfk_bn_stats(const bf16* y, long long M, int C, float* stats, int shards, hi
 }
 int tfk_bn_apply(const bf16* y, const float* scale, const float* shift, const bf16* r, const float* rscale,
                  const float* rshift, int relu, bf16* out, long long M, int C, hipStream_t s) {
-  long long nch = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(nch, NT * 4, 8192)), dim3(NT), 0, s, y, scale, shift, r, rscale, rshift,
-                     relu, out, nch, C);
+  const int cpr = C / 8;
+  if (NT % cpr == 0) {
+    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(grid_for(M, (NT / cpr) * 4, 8192)), dim3(NT), 0, s, y, scale, shift, r,
+                       rscale, rshift, relu, out, M, C);
+  } else {
+    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(grid_for(M * cpr, NT * 4, 8192)), dim3(NT), 0, s, y, scale, shift,
+                       r, rscale, rshift, relu, out, M, C);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_bn_bwd_reduce(const bf16* da, const bf16* a, const bf16* y, const float* mean, const float* invstd, const bf16* y2,
@@ -286,20 +343,25 @@ int tfk_bn_bwd_reduce(const bf16* da, const bf16* a, const bf16* y, const float*
                      y2, mean2, invstd2, M, C, sums, shards, mscale, mshift);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int tfk_bn_bwd_finalize(float* sums, int shards, int C, float count, const float* gamma, const float* invstd,
-                        const float* gamma2, const float* invstd2, float* dgamma, float* dbeta, float* dgamma2,
-                        float* dbeta2, float* coef, float* coef2, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, sums, shards, C, count, gamma, invstd,
-                     gamma2, invstd2, dgamma, dbeta, dgamma2, dbeta2, coef, coef2);
+int tfk_bn_bwd_finalize(float* sums, int shards, int C, float count, const float* gamma, const float* mean,
+                        const float* invstd, const float* gamma2, const float* mean2, const float* invstd2,
+                        float* dgamma, float* dbeta, float* dgamma2, float* dbeta2, float* coef, float* coef2,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, sums, shards, C, count, gamma, mean,
+                     invstd, gamma2, mean2, invstd2, dgamma, dbeta, dgamma2, dbeta2, coef, coef2);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int tfk_bn_bwd_apply(const bf16* da, const bf16* a, const bf16* y, const float* mean, const float* invstd,
-                     const float* coef, bf16* dy, const bf16* y2, const float* mean2, const float* invstd2,
+int tfk_bn_bwd_apply(const bf16* da, const bf16* a, const bf16* y, const float* coef, bf16* dy, const bf16* y2,
                      const float* coef2, bf16* dy2, bf16* dres, long long M, int C, const float* mscale,
                      const float* mshift, hipStream_t s) {
-  long long nch = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(nch, NT * 4, 8192)), dim3(NT), 0, s, da, a, y, mean, invstd, coef,
-                     dy, y2, mean2, invstd2, coef2, dy2, dres, nch, C, mscale, mshift);
+  const int cpr = C / 8;
+  if (NT % cpr == 0) {
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid_for(M, (NT / cpr) * 4, 8192)), dim3(NT), 0, s, da, a, y, coef,
+                       dy, y2, coef2, dy2, dres, M, C, mscale, mshift);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid_for(M * cpr, NT * 4, 8192)), dim3(NT), 0, s, da, a, y,
+                       coef, dy, y2, coef2, dy2, dres, M, C, mscale, mshift);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }

@@ -206,11 +206,17 @@ def _ref_conv(x, w, g: ConvGeom):
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor | None = None,
-             shards: int = 1) -> torch.Tensor:
-    """y[N,P,Q,K] = conv(x[N,H,W,C], w[K,R,S,C]); optionally accumulates BN batch statistics
-    (sum, sumsq per output channel) of the f32 result into stats[shards][2][K]."""
+             shards: int = 1, bias: torch.Tensor | None = None, act: str | None = None) -> torch.Tensor:
+    """y[N,P,Q,K] = act(conv(x[N,H,W,C], w[K,R,S,C]) + bias); optionally accumulates BN batch
+    statistics (sum, sumsq per output channel) of the f32 result into stats[shards][2][K]."""
     if not on_gpu(x):
         y = _ref_conv(x, w, g)
+        if bias is not None:
+            y = y + bias.float()
+        if ACT[act] == 1:
+            y = torch.relu(y)
+        elif ACT[act] == 2:
+            y = F.gelu(y, approximate="tanh")
         if stats is not None:
             yf = y.reshape(-1, g.K)
             stats.view(shards, 2, g.K)[0, 0] += yf.sum(0)
@@ -220,11 +226,12 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
     y = torch.empty(g.N, g.P, g.Q, g.K, dtype=torch.bfloat16, device=x.device)
     tile = pick_tile(M, g.K)
     if g.pointwise:
-        _gemm(x, w, y, M, g.K, g.C, g.C, g.C, g.K, A_KIN, B_KIN, EPI_BF16, tile, stats=stats, shards=shards)
+        _gemm(x, w, y, M, g.K, g.C, g.C, g.C, g.K, A_KIN, B_KIN, EPI_BF16, tile, stats=stats, shards=shards,
+              bias=bias, act=ACT[act])
     else:
         Kd = g.R * g.S * g.C
         _gemm(x, w, y, M, g.K, Kd, 0, Kd, g.K, A_CONV_FWD, B_KIN, EPI_BF16, tile, stats=stats, shards=shards,
-              conv=g.vec())
+              conv=g.vec(), bias=bias, act=ACT[act])
     return y
 
 

@@ -146,11 +146,11 @@ def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=No
     if not reduced:
         L.bn_bwd_reduce(da, a, y, st.mean, st.invstd, y2, st2.mean if st2 else None, st2.invstd if st2 else None, M, C,
                         st.sums, st.shards, msc, msh)
-    L.bn_bwd_finalize(st.sums, st.shards, C, float(count), gamma, st.invstd, gamma2, st2.invstd if st2 else None,
-                      dgamma, dbeta, dgamma2, dbeta2, st.coef, st2.coef if st2 else None)
+    L.bn_bwd_finalize(st.sums, st.shards, C, float(count), gamma, st.mean, st.invstd, gamma2,
+                      st2.mean if st2 else None, st2.invstd if st2 else None, dgamma, dbeta, dgamma2, dbeta2, st.coef,
+                      st2.coef if st2 else None)
     dy = torch.empty_like(da)
     dy2 = torch.empty_like(da) if y2 is not None else None
     dres = torch.empty_like(da) if want_dres else None
-    L.bn_bwd_apply(da, a, y, st.mean, st.invstd, st.coef, dy, y2, st2.mean if st2 else None,
-                   st2.invstd if st2 else None, st2.coef if st2 else None, dy2, dres, M, C, msc, msh)
+    L.bn_bwd_apply(da, a, y, st.coef, dy, y2, st2.coef if st2 else None, dy2, dres, M, C, msc, msh)
     return dy, dy2, dres

@@ -1,0 +1,221 @@
+"""ParameterServerStrategy: variables sharded over "ps" tasks, gradients pushed by workers.
+
+TF's ParameterServerStrategy (the reference's PS-style TFJobs, e.g. tf_cnn_benchmarks with
+``--variable_update=parameter_server`` / examples/dist-mnist) places variables
+on ps tasks; workers read them, compute gradients and send updates back, synchronously or
+asynchronously. tfk equivalent:
+
+* the flat parameter arena is split into ``len(ps)`` contiguous, ALIGN-aligned shards balanced by
+  size; ps task s owns shard s: the f32 master copy plus the optimizer slots, and runs the
+  optimizer for it (fused CPU path of ops.optim — ps tasks are CPU processes, as in TF);
+* workers (one per GPU) run forward/backward on the device, copy each gradient shard to pinned
+  host memory, push it to its owner and pull the updated shard back (gloo point-to-point over
+  TCP; GPU<->GPU traffic between workers does not exist in this strategy);
+* ``mode="sync"``: ps sums the pushes of all workers for step t, applies one update (mean
+  gradient) and answers everyone -> identical parameters everywhere (TF SyncReplicasOptimizer);
+  ``mode="async"``: ps applies each push as it arrives (Hogwild-style staleness, TF's default PS
+  behaviour) and answers that worker only.
+
+Message protocol per (worker, shard): header int64[4] = [cmd, step, worker_rank, 0] then payload.
+cmd PUSH=1 (payload grad shard f32) -> reply shard f32; DONE=2; FETCH=3 (reply master + slots, for
+checkpoints); LOAD=4 (payload master + slots, restore); PULL=5 (reply master shard).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..runtime.arena import ALIGN, ParamArena
+
+PUSH, DONE, FETCH, LOAD, PULL = 1, 2, 3, 4, 5
+
+
+def shard_bounds(numel: int, nshards: int) -> list[tuple[int, int]]:
+    """Contiguous ALIGN-aligned shards of [0, numel) with near-equal sizes."""
+    units = (numel + ALIGN - 1) // ALIGN
+    out, lo = [], 0
+    for s in range(nshards):
+        n = units // nshards + (1 if s < units % nshards else 0)
+        hi = min(numel, lo + n * ALIGN)
+        out.append((lo, hi))
+        lo = hi
+    return out
+
+
+def _hdr(cmd: int, step: int = 0, rank: int = 0) -> torch.Tensor:
+    return torch.tensor([cmd, step, rank, 0], dtype=torch.int64)
+
+
+class ParameterServerStrategy:
+    """Worker side."""
+    name = "ps"
+
+    def __init__(self, arena: ParamArena, ps_ranks: list[int], worker_ranks: list[int], mode: str = "sync",
+                 group=None):
+        if mode not in ("sync", "async"):
+            raise ValueError(f"ps mode must be sync|async, got {mode}")
+        self.arena, self.ps_ranks, self.worker_ranks, self.mode, self.group = arena, list(ps_ranks), list(worker_ranks), mode, group
+        self.rank = dist.get_rank()
+        self.shards = shard_bounds(arena.numel, len(self.ps_ranks))
+        pin = arena.grad.is_cuda
+        self._g = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
+        self._p = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
+        self.step_count = 0
+
+    @property
+    def num_workers(self) -> int:
+        return len(self.worker_ranks)
+
+    def begin_step(self):
+        pass
+
+    def finish_step(self):
+        pass
+
+    def configure_optimizer(self, opt) -> None:
+        """The optimizer runs on the ps tasks; the worker-side instance only provides slot names
+        and the step counter for checkpoints."""
+        self.opt = opt
+
+    def _exchange(self, cmd: int, send: list[torch.Tensor] | None, recv: list[torch.Tensor] | None):
+        reqs = []
+        for s, ps in enumerate(self.ps_ranks):
+            reqs.append(dist.isend(_hdr(cmd, self.step_count, self.rank), ps, group=self.group))
+            if send is not None:
+                reqs.append(dist.isend(send[s], ps, group=self.group))
+        for r in reqs:
+            r.wait()
+        if recv is not None:
+            reqs = [dist.irecv(recv[s], ps, group=self.group) for s, ps in enumerate(self.ps_ranks)]
+            for r in reqs:
+                r.wait()
+
+    def apply_gradients(self, opt=None) -> None:
+        """Push local gradients, pull the updated parameters (replaces optimizer.step())."""
+        a = self.arena
+        for s, (lo, hi) in enumerate(self.shards):
+            self._g[s].copy_(a.grad[lo:hi], non_blocking=True)
+        if a.grad.is_cuda:
+            torch.cuda.current_stream().synchronize()
+        self._exchange(PUSH, self._g, self._p)
+        for s, (lo, hi) in enumerate(self.shards):
+            a.master[lo:hi].copy_(self._p[s], non_blocking=True)
+        a.refresh_compute()
+        self.step_count += 1
+        if opt is not None:
+            opt.step_count = self.step_count
+
+    def pull(self) -> None:
+        """Initial (or resync) read of every variable from the ps tasks."""
+        self._exchange(PULL, None, self._p)
+        for s, (lo, hi) in enumerate(self.shards):
+            self.arena.master[lo:hi].copy_(self._p[s])
+        self.arena.refresh_compute()
+
+    def fetch_state(self, opt) -> None:
+        """Copy master + optimizer slots from the ps tasks into the local arena (chief, before a
+        checkpoint save)."""
+        names = list(opt.slot_names)
+        bufs = [torch.empty((1 + len(names)) * (hi - lo), dtype=torch.float32) for lo, hi in self.shards]
+        self._exchange(FETCH, None, bufs)
+        for s, (lo, hi) in enumerate(self.shards):
+            n = hi - lo
+            self.arena.master[lo:hi].copy_(bufs[s][:n])
+            for k, nm in enumerate(names):
+                self.arena.slot(nm)[lo:hi].copy_(bufs[s][(k + 1) * n:(k + 2) * n])
+
+    def load_state(self, opt, step: int) -> None:
+        """Push master + slots (restored from a checkpoint by the chief) to the ps tasks."""
+        names = list(opt.slot_names)
+        bufs = []
+        for lo, hi in self.shards:
+            parts = [self.arena.master[lo:hi].cpu()] + [self.arena.slot(nm)[lo:hi].cpu() for nm in names]
+            bufs.append(torch.cat(parts))
+        self.step_count = step
+        self._exchange(LOAD, bufs, None)
+
+    def shutdown(self) -> None:
+        self._exchange(DONE, None, None)
+
+    def broadcast_parameters(self, src: int = 0):
+        self.pull()
+
+    def all_reduce_metrics(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+
+class ParameterServer:
+    """ps-task side: owns one shard of the arena (master + slots) and runs the optimizer on it."""
+
+    def __init__(self, arena: ParamArena, opt, shard: int, ps_ranks: list[int], worker_ranks: list[int],
+                 mode: str = "sync", group=None):
+        self.arena, self.opt, self.mode, self.group = arena, opt, mode, group
+        self.worker_ranks = list(worker_ranks)
+        self.lo, self.hi = shard_bounds(arena.numel, len(ps_ranks))[shard]
+        opt.region = (self.lo, self.hi)
+        if mode == "sync":
+            opt.grad_scale = 1.0 / len(self.worker_ranks)
+        self.updates = 0
+
+    def _reply(self, dst: int, t: torch.Tensor):
+        dist.send(t, dst, group=self.group)
+
+    def _state(self) -> torch.Tensor:
+        a, lo, hi = self.arena, self.lo, self.hi
+        return torch.cat([a.master[lo:hi]] + [a.slot(nm)[lo:hi] for nm in self.opt.slot_names])
+
+    def _load(self, buf: torch.Tensor, step: int):
+        a, lo, hi = self.arena, self.lo, self.hi
+        n = hi - lo
+        a.master[lo:hi].copy_(buf[:n])
+        for k, nm in enumerate(self.opt.slot_names):
+            a.slot(nm)[lo:hi].copy_(buf[(k + 1) * n:(k + 2) * n])
+        self.opt.step_count = step
+
+    def serve(self) -> int:
+        """Serve until every worker has sent DONE. Returns the number of optimizer updates."""
+        a, lo, hi = self.arena, self.lo, self.hi
+        n = hi - lo
+        live = set(self.worker_ranks)
+        hdr = torch.empty(4, dtype=torch.int64)
+        gbuf = torch.empty(n, dtype=torch.float32)
+        pending: list[int] = []  # sync: workers whose push for the current step arrived
+        while live:
+            src = dist.recv(hdr, None, group=self.group)  # any source
+            cmd, step = int(hdr[0]), int(hdr[1])
+            if cmd == DONE:
+                live.discard(src)
+                continue
+            if cmd == PULL:
+                self._reply(src, a.master[lo:hi].contiguous())
+                continue
+            if cmd == FETCH:
+                self._reply(src, self._state())
+                continue
+            if cmd == LOAD:
+                buf = torch.empty((1 + len(self.opt.slot_names)) * n, dtype=torch.float32)
+                dist.recv(buf, src, group=self.group)
+                self._load(buf, step)
+                continue
+            if cmd != PUSH:
+                raise RuntimeError(f"ps: unknown command {cmd} from rank {src}")
+            dist.recv(gbuf, src, group=self.group)
+            if self.mode == "async":
+                a.grad[lo:hi].copy_(gbuf)
+                self.opt.step()
+                self.updates += 1
+                self._reply(src, a.master[lo:hi].contiguous())
+                continue
+            if not pending:
+                a.grad[lo:hi].copy_(gbuf)
+            else:
+                a.grad[lo:hi].add_(gbuf)
+            pending.append(src)
+            if len(pending) == len(live):
+                self.opt.step()
+                self.updates += 1
+                out = a.master[lo:hi].contiguous()
+                for w in pending:
+                    self._reply(w, out)
+                pending = []
+        return self.updates

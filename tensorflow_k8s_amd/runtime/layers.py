@@ -30,19 +30,36 @@ class Conv2d:
     """NHWC conv, OHWI weight. TF variable: <name>/kernel in HWIO."""
 
     def __init__(self, arena: ParamArena, name: str, cin: int, cout: int, k: int, stride: int = 1, pad: int | None = None,
-                 cin_real: int | None = None):
+                 cin_real: int | None = None, cout_real: int | None = None, bias: bool = False):
+        """cin_real/cout_real < cin/cout: channels padded to multiples of 8 for 16-B NHWC vectors
+        (e.g. RGB stem, LeNet's 1->6 conv); padded weights start and stay exactly zero, and the
+        checkpoint holds only the real [k, k, cin_real, cout_real] kernel."""
         self.cin, self.cout, self.k, self.stride = cin, cout, k, stride
         self.pad = (k - 1) // 2 if pad is None else pad
         real = cin_real if cin_real is not None else cin
+        oreal = cout_real if cout_real is not None else cout
         post = None
-        if real != cin:
-            def post(t, real=real):
+        if real != cin or oreal != cout:
+            def post(t, real=real, oreal=oreal):
                 t[..., real:] = 0
+                t[oreal:] = 0
                 return t
+
+        def to_tf(a, real=real, oreal=oreal):
+            return _ohwi_to_hwio(a, real)[..., :oreal]
+
+        def from_tf(a, c=cin, co=cout):
+            if a.shape[3] < co:
+                a = np.concatenate([a, np.zeros(a.shape[:3] + (co - a.shape[3],), dtype=a.dtype)], axis=3)
+            return _hwio_to_ohwi(a, c)
         self.w = arena.add(ParamSpec(
-            f"{name}/kernel", (cout, k, k, cin), init="he_normal", fan_in=k * k * real, fan_out=k * k * cout,
-            to_tf=lambda a, real=real: _ohwi_to_hwio(a, real), from_tf=lambda a, c=cin: _hwio_to_ohwi(a, c),
-            tf_shape=(k, k, real, cout), post_init=post))
+            f"{name}/kernel", (cout, k, k, cin), init="he_normal", fan_in=k * k * real, fan_out=k * k * oreal,
+            to_tf=to_tf, from_tf=from_tf, tf_shape=(k, k, real, oreal), post_init=post))
+        self.b = None
+        if bias:
+            self.b = arena.add(ParamSpec(f"{name}/bias", (cout,), init="zeros", decay=False,
+                                         to_tf=lambda a, o=oreal: a[:o],
+                                         from_tf=lambda a, co=cout: np.concatenate([a, np.zeros(co - a.shape[0], a.dtype)])))
         self.arena = arena
 
     def geom(self, x_shape) -> G.ConvGeom:
@@ -50,14 +67,19 @@ class Conv2d:
         assert C == self.cin, f"conv expects {self.cin} input channels, got {C}"
         return G.ConvGeom(N, H, W, C, self.cout, self.k, self.k, self.stride, self.stride, self.pad, self.pad)
 
-    def forward(self, x, stats: BN.BNState | None = None):
+    def forward(self, x, stats: BN.BNState | None = None, act: str | None = None):
         g = self.geom(x.shape)
-        return G.conv_fwd(x, self.w.compute, g, stats.stats if stats else None, stats.shards if stats else 1)
+        return G.conv_fwd(x, self.w.compute, g, stats.stats if stats else None, stats.shards if stats else 1,
+                          bias=self.b.master if self.b is not None else None, act=act)
 
     def backward(self, dy, x, need_dx: bool = True, resid=None, bnr=None):
         g = self.geom(x.shape)
         G.conv_wgrad(dy, x, g, self.w.grad)
-        self.arena.grad_ready(self.w)
+        if self.b is not None:
+            G.bias_grad(dy, self.b.grad)
+            self.arena.grad_ready(self.w, self.b)
+        else:
+            self.arena.grad_ready(self.w)
         if not need_dx:
             return None
         return G.conv_dgrad(dy, self.w.compute, g, resid=resid, bnr=bnr)

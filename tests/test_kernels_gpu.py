@@ -106,9 +106,10 @@ def test_gemm_asymmetric_identity():
     assert torch.equal(y.cpu().float(), B.float().t())
 
 
+@pytest.mark.parametrize("C", [64, 24])  # 24: C does not divide 2048 -> flat (non-fixed-chunk) kernels
 @pytest.mark.parametrize("proj", [False, True])
-def test_bn_fused_forward_backward(proj):
-    N, H, W, C = 4, 10, 10, 64
+def test_bn_fused_forward_backward(proj, C):
+    N, H, W = 4, 10, 10
     M = N * H * W
     y = bf(N, H, W, C, seed=8)
     y2 = bf(N, H, W, C, seed=9)
@@ -132,6 +133,11 @@ def test_bn_fused_forward_backward(proj):
                                        gamma2=gamma2.to(dev) if proj else None, dgamma2=dg2, dbeta2=db2,
                                        want_dres=not proj)
         out[dev] = dict(a=a, dy=dy, dy2=dy2, dres=dres, dg=dg, db=db, dg2=dg2, rm=rm, rv=rv)
+        # relu mask recomputed from y (no residual input): a = relu(bn(y))
+        a1 = BN.bn_apply(y.to(dev), st, True)
+        dg3, db3 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        dy3, _, _ = BN.bn_backward(da, None, y.to(dev), st, gamma.to(dev), dg3, db3, M, relu_from_y=True)
+        out[dev].update(a1=a1, dy3=dy3, dg3=dg3, db3=db3)
     for k, v in out["cpu"].items():
         if v is None:
             continue
@@ -196,12 +202,14 @@ def test_dgrad_fused_bn_reduce(cfg, mode):
     y = bf(N, H, W, C, seed=4)
     y2 = bf(N, H, W, C, seed=5)
     a = bf(N, H, W, C, seed=6)
+    gen = torch.Generator().manual_seed(7)
+    stat_vals = [(torch.randn(C, generator=gen) * 0.1, torch.rand(C, generator=gen) + 0.5,
+                  torch.randn(C, generator=gen), torch.randn(C, generator=gen) * 0.1) for _ in range(2)]
     res = {}
     for dev in ("cpu", DEV):
         st, st2 = BN.BNState(C, dev), BN.BNState(C, dev)
-        for s_ in (st, st2):
-            s_.mean.copy_(torch.randn(C) * 0.1); s_.invstd.copy_(torch.rand(C) + 0.5)
-            s_.scale.copy_(torch.randn(C)); s_.shift.copy_(torch.randn(C) * 0.1)
+        for s_, (mu, inv, sc, sh) in zip((st, st2), stat_vals):
+            s_.mean.copy_(mu); s_.invstd.copy_(inv); s_.scale.copy_(sc); s_.shift.copy_(sh)
         if mode == "relu_from_y":
             spec = BN.BNReduce(y.to(dev), st)
         elif mode == "mask_a":

@@ -159,6 +159,7 @@ class LocalCluster:
                  log_path: str | None = None):
         import tempfile
         self.root = root_dir or tempfile.mkdtemp(prefix="tfk-cluster-")
+        os.makedirs(self.root, exist_ok=True)
         self.port_file = os.path.join(self.root, "port")
         self.log_path = log_path or os.path.join(self.root, "cluster.log")
         args = [os.path.join(BIN, "tfk-cluster"), "--port", "0", "--port-file", self.port_file, "--gpus", str(gpus),

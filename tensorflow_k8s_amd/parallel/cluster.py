@@ -93,7 +93,7 @@ def resolve(env: dict | None = None) -> ClusterInfo:
     return ClusterInfo(worker_ranks=[0], source="local")
 
 
-def init_process_group(info: ClusterInfo, backend: str, timeout_s: float = 600.0, retries: int = 5):
+def init_process_group(info: ClusterInfo, backend: str, timeout_s: float = 600.0, retries: int = 5, device_id=None):
     """Rendezvous on the chief's TCP store (torch's C++ TCPStore on tfPort) and create the
     RCCL/gloo world. A port-in-use at the chief (k8s-operator.md:5 failure mode, typically the
     previous restart generation still shutting down) is retried, then reported as a retryable
@@ -109,8 +109,9 @@ def init_process_group(info: ClusterInfo, backend: str, timeout_s: float = 600.0
         try:
             store = dist.TCPStore(info.master_addr, info.master_port, info.world_size, info.rank == 0,
                                   timeout=datetime.timedelta(seconds=timeout_s))
+            kw = {"device_id": device_id} if device_id is not None else {}
             dist.init_process_group(backend, store=store, rank=info.rank, world_size=info.world_size,
-                                    timeout=datetime.timedelta(seconds=timeout_s))
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
             return True
         except (RuntimeError, OSError) as e:
             last = e

@@ -1,0 +1,296 @@
+"""In-pod training entrypoint: ``python -m tensorflow_k8s_amd.runtime.train --model resnet50 ...``.
+
+This is the program a TFJob replica runs (the reference's pods run a TF script that builds a
+``TFConfigClusterResolver`` + ``MultiWorkerMirroredStrategy`` / ``ParameterServerStrategy`` from
+the operator-injected TF_CONFIG). Per role:
+
+* chief / worker: one process per GPU (HIP_VISIBLE_DEVICES set by the node agent), RCCL world over
+  all workers (MWMS) or gloo point-to-point to the ps tasks (PS strategy); restore-or-init, train
+  ``--steps`` global steps on synthetic data of the model's shape, chief writes TF-bundle
+  checkpoints every ``--checkpoint-every`` steps and at the end, JSON-lines metrics on stdout;
+* ps: holds one shard of the variables + optimizer slots on the CPU and serves push/pull;
+* evaluator: not in the training world; follows the checkpoint directory (runtime/evaluator.py).
+
+Exit codes follow the operator's restart policy (ExitCode): 0 success; 1 permanent user error;
+137 OOM (termination message "OOMKilled", permanent) ; 143 peer/rendezvous failure (retryable ->
+gang restart, resume from the latest checkpoint). Fault injection for the failure-recovery tests:
+TFK_FAULT_AT_STEP=<n> [TFK_FAULT_EXIT=<code>|137=SIGKILL] [TFK_FAULT_RANK=<r>]
+[TFK_FAULT_GENERATION=<g>|any, compared with the operator's TFK_RESTART_GENERATION, default 0].
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import sys
+import time
+
+import torch
+
+EXIT_OK, EXIT_USER, EXIT_OOM, EXIT_RETRY = 0, 1, 137, 143
+
+
+def _log(obj: dict, fh=None):
+    line = json.dumps(obj, sort_keys=True)
+    print(line, flush=True)
+    if fh is not None:
+        fh.write(line + "\n")
+        fh.flush()
+
+
+def _termination_message(msg: str):
+    path = os.environ.get("TFK_TERMINATION_LOG")
+    if path:
+        try:
+            with open(path, "w") as f:
+                f.write(msg)
+        except OSError:
+            pass
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--model", default="lenet")
+    ap.add_argument("--batch", type=int, default=64, help="per-worker batch")
+    ap.add_argument("--steps", type=int, default=100, help="total global steps")
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adamw", "lamb"])
+    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--momentum", type=float, default=0.9)
+    ap.add_argument("--weight-decay", type=float, default=0.0)
+    ap.add_argument("--warmup-steps", type=int, default=0)
+    ap.add_argument("--lr-schedule", default="constant", choices=["constant", "cosine", "poly"])
+    ap.add_argument("--strategy", default="auto", choices=["auto", "mwms", "ps"])
+    ap.add_argument("--ps-mode", default="sync", choices=["sync", "async"])
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--device", default="auto", choices=["auto", "cpu", "cuda"])
+    ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph (1 GPU, MWMS)")
+    ap.add_argument("--checkpoint-dir", default="")
+    ap.add_argument("--checkpoint-every", type=int, default=0)
+    ap.add_argument("--keep", type=int, default=5)
+    ap.add_argument("--log-every", type=int, default=10)
+    ap.add_argument("--metrics-file", default="")
+    ap.add_argument("--data-batches", type=int, default=4, help="distinct synthetic batches per worker")
+    ap.add_argument("--image-size", type=int, default=0, help="override input resolution (ResNet)")
+    ap.add_argument("--num-classes", type=int, default=0)
+    ap.add_argument("--seq-len", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--rendezvous-timeout", type=float, default=300.0)
+    # evaluator
+    ap.add_argument("--eval-batches", type=int, default=4)
+    ap.add_argument("--eval-timeout", type=float, default=600.0)
+    return ap.parse_args(argv)
+
+
+def model_kwargs(args) -> dict:
+    kw = {}
+    if args.num_classes:
+        kw["num_classes"] = args.num_classes
+    if args.model.startswith("lenet") and args.image_size:
+        kw["image_size"] = args.image_size
+    return kw
+
+
+def data_kwargs(args) -> dict:
+    kw = {}
+    if args.image_size:
+        kw["image_size"] = args.image_size
+    if args.seq_len:
+        kw["seq_len"] = args.seq_len
+    return kw
+
+
+def make_optimizer(args, arena):
+    from .optimizer import LAMB, SGD, AdamW, LRSchedule
+    lr = LRSchedule(args.lr, warmup=args.warmup_steps, total=args.steps, kind=args.lr_schedule)
+    if args.optimizer == "sgd":
+        return SGD(arena, lr, momentum=args.momentum, weight_decay=args.weight_decay)
+    if args.optimizer == "adamw":
+        return AdamW(arena, lr, weight_decay=args.weight_decay)
+    return LAMB(arena, lr, weight_decay=args.weight_decay)
+
+
+def pick_device(args, info) -> torch.device:
+    if info.is_ps or args.device == "cpu":
+        return torch.device("cpu")
+    want_cuda = args.device == "cuda" or (args.device == "auto" and torch.cuda.is_available())
+    if not want_cuda:
+        return torch.device("cpu")
+    if not torch.cuda.is_available():
+        raise SystemExit("--device cuda but no GPU is visible")
+    local = int(os.environ.get("LOCAL_RANK", "0")) if info.source == "torchrun" else 0
+    torch.cuda.set_device(local)
+    return torch.device("cuda", local)
+
+
+def maybe_fault(step: int, rank: int):
+    at = os.environ.get("TFK_FAULT_AT_STEP")
+    if not at or int(at) != step:
+        return
+    if int(os.environ.get("TFK_FAULT_RANK", "0")) != rank:
+        return
+    gen = os.environ.get("TFK_FAULT_GENERATION", "0")
+    if gen != "any" and gen != os.environ.get("TFK_RESTART_GENERATION", "0"):
+        return
+    code = int(os.environ.get("TFK_FAULT_EXIT", "1"))
+    _log({"event": "fault_injected", "step": step, "rank": rank, "exit": code})
+    sys.stdout.flush()
+    if code == 137:
+        os.kill(os.getpid(), signal.SIGKILL)
+    os._exit(code)
+
+
+def run_ps(args, info) -> int:
+    import torch.distributed as dist
+
+    from ..models import build_model
+    from ..parallel.ps import ParameterServer
+    from .checkpoint import CheckpointManager
+    model = build_model(args.model, **model_kwargs(args)).to("cpu", seed=args.seed)
+    opt = make_optimizer(args, model.arena)
+    if args.checkpoint_dir:
+        step = CheckpointManager(args.checkpoint_dir, args.keep).restore(model.arena, opt)
+        if step is not None:
+            _log({"event": "restored", "role": "ps", "step": step, "index": info.task_index})
+    shard = info.ps_ranks.index(info.rank)
+    server = ParameterServer(model.arena, opt, shard, info.ps_ranks, info.worker_ranks, args.ps_mode)
+    _log({"event": "ps_ready", "index": info.task_index, "shard": [server.lo, server.hi]})
+    n = server.serve()
+    _log({"event": "done", "role": "ps", "index": info.task_index, "updates": n})
+    dist.destroy_process_group()
+    return EXIT_OK
+
+
+def run_worker(args, info, dev) -> int:
+    import torch.distributed as dist
+
+    from ..models import build_model, synthetic_batch
+    from .checkpoint import CheckpointManager
+    from .trainer import StepRunner
+
+    use_ps = args.strategy == "ps" or (args.strategy == "auto" and info.ps_ranks)
+    model = build_model(args.model, **model_kwargs(args)).to(dev, seed=args.seed)
+    opt = make_optimizer(args, model.arena)
+    if use_ps:
+        from ..parallel.ps import ParameterServerStrategy
+        if not info.ps_ranks:
+            raise SystemExit("--strategy ps needs ps tasks in TF_CONFIG")
+        strat = ParameterServerStrategy(model.arena, info.ps_ranks, info.worker_ranks, args.ps_mode)
+        strat.configure_optimizer(opt)
+    else:
+        from ..parallel.mwms import MultiWorkerMirroredStrategy
+        strat = MultiWorkerMirroredStrategy(model.arena, bucket_mb=args.bucket_mb)
+        strat.configure_optimizer(opt)
+    nworkers = max(1, len(info.worker_ranks))
+    wrank = info.worker_ranks.index(info.rank) if info.rank in info.worker_ranks else 0
+
+    ckpt = CheckpointManager(args.checkpoint_dir, args.keep) if args.checkpoint_dir else None
+    start = 0
+    if ckpt is not None:
+        s = ckpt.restore(model.arena, opt)
+        if s is not None:
+            start = s
+            _log({"event": "restored", "step": s, "rank": info.rank, "path": ckpt.latest()})
+    strat.broadcast_parameters()  # MWMS: chief's weights everywhere; PS: pull from the ps tasks
+    if use_ps:
+        strat.step_count = start
+
+    batches = [synthetic_batch(model, args.batch, dev, seed=args.seed * 7919 + wrank * 1009 + i, **data_kwargs(args))
+               for i in range(max(1, args.data_batches))]
+    static = tuple(t.clone() for t in batches[0])
+    runner = StepRunner(model, opt, strat, static, use_graph=bool(args.graph) and nworkers == 1)
+    metrics_fh = open(args.metrics_file, "a") if (args.metrics_file and info.is_chief) else None
+    gb = args.batch * nworkers
+    _log({"event": "start", "rank": info.rank, "world": info.world_size, "workers": nworkers, "model": model.name,
+          "params": model.arena.num_parameters(), "device": str(dev), "strategy": strat.name, "start_step": start,
+          "global_batch": gb, "restart_generation": int(os.environ.get("TFK_RESTART_GENERATION", "0"))})
+    t_last, n_last = time.perf_counter(), 0
+    step = start
+    while step < args.steps:
+        runner.set_batch(*batches[step % len(batches)])
+        runner.step()
+        step += 1
+        n_last += 1
+        if step % max(1, args.log_every) == 0 or step == args.steps:
+            m = torch.tensor([runner.last_loss() or 0.0, runner.last_accuracy() or 0.0], dtype=torch.float32,
+                             device=dev if strat.name == "mwms" else "cpu")
+            strat.all_reduce_metrics(m)
+            if strat.name == "mwms":
+                m /= nworkers
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            now = time.perf_counter()
+            if info.is_chief:
+                _log({"event": "train", "step": step, "loss": round(float(m[0]), 6), "accuracy": round(float(m[1]), 6),
+                      "examples_per_sec": round(gb * n_last / max(now - t_last, 1e-9), 2),
+                      "lr": opt.lr(step - 1)}, metrics_fh)
+            t_last, n_last = now, 0
+        if ckpt is not None and info.is_chief and args.checkpoint_every and step % args.checkpoint_every == 0 \
+                and step < args.steps:
+            if use_ps:
+                strat.fetch_state(opt)
+            path = ckpt.save(model.arena, opt, step)
+            _log({"event": "checkpoint", "step": step, "path": path}, metrics_fh)
+        maybe_fault(step, info.rank)
+    if ckpt is not None and info.is_chief:
+        if use_ps:
+            strat.fetch_state(opt)
+        path = ckpt.save(model.arena, opt, step, blocking=True)
+        _log({"event": "checkpoint", "step": step, "path": path, "final": True}, metrics_fh)
+        with open(os.path.join(args.checkpoint_dir, "DONE"), "w") as f:
+            f.write(str(step))
+    if use_ps:
+        strat.shutdown()
+    if dist.is_initialized():
+        if not use_ps:
+            dist.barrier()
+        dist.destroy_process_group()
+    if info.is_chief:
+        _log({"event": "done", "step": step, "loss": runner.last_loss()}, metrics_fh)
+    return EXIT_OK
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    from ..parallel import cluster
+    info = cluster.resolve()
+    if info.is_evaluator:
+        from .evaluator import run_evaluator
+        return run_evaluator(args)
+    try:
+        dev = pick_device(args, info)
+        if dev.type == "cpu" and info.world_size > 1 and "OMP_NUM_THREADS" not in os.environ:
+            # co-located CPU replicas: split the cores instead of oversubscribing them
+            torch.set_num_threads(max(1, (os.cpu_count() or 1) // info.world_size))
+        if info.world_size > 1:
+            use_ps = args.strategy == "ps" or (args.strategy == "auto" and info.ps_ranks)
+            backend = "nccl" if (dev.type == "cuda" and not use_ps) else "gloo"
+            cluster.init_process_group(info, backend, timeout_s=args.rendezvous_timeout,
+                                       device_id=dev if backend == "nccl" else None)
+        if info.is_ps:
+            return run_ps(args, info)
+        return run_worker(args, info, dev)
+    except torch.cuda.OutOfMemoryError as e:
+        _termination_message("OOMKilled")
+        _log({"event": "error", "kind": "oom", "message": str(e)[:500]})
+        return EXIT_OOM
+    except cluster.RendezvousError as e:
+        _termination_message(str(e))
+        _log({"event": "error", "kind": "rendezvous", "message": str(e)[:500]})
+        return EXIT_RETRY
+    except (RuntimeError, ConnectionError, OSError) as e:
+        msg = str(e)
+        import torch.distributed as dist
+        peer = isinstance(e, getattr(dist, "DistBackendError", ())) or any(
+            k in msg for k in ("Connection reset", "Connection closed", "timed out", "Timeout", "NCCL", "RCCL",
+                               "gloo", "Broken pipe", "peer"))
+        _termination_message(msg[:2000])
+        _log({"event": "error", "kind": "peer" if peer else "runtime", "message": msg[:500]})
+        return EXIT_RETRY if peer else EXIT_USER
+
+
+if __name__ == "__main__":
+    code = main()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code)

@@ -15,7 +15,8 @@ class StepRunner:
     def __init__(self, model, opt, strategy, batch, use_graph: bool = False, warmup_eager: int = 2):
         self.model, self.opt, self.strategy = model, opt, strategy
         self.batch = batch
-        self.use_graph = use_graph and torch.cuda.is_available() and batch[0].is_cuda
+        self.use_graph = (use_graph and torch.cuda.is_available() and batch[0].is_cuda
+                          and not hasattr(strategy, "apply_gradients"))
         self.warmup_eager = warmup_eager
         self.graph = None
         self.n = 0
@@ -29,8 +30,17 @@ class StepRunner:
         loss, corr = self.model.forward_backward(*self.batch)
         if s is not None:
             s.finish_step()
-        self.opt.step()
+        if s is not None and hasattr(s, "apply_gradients"):
+            s.apply_gradients(self.opt)  # parameter-server: the update runs on the ps tasks
+        else:
+            self.opt.step()
         return loss, corr
+
+    def set_batch(self, *tensors):
+        """Copy a new batch into the static input buffers (keeps captured graphs valid)."""
+        for dst, src in zip(self.batch, tensors):
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src, non_blocking=True)
 
     def step(self):
         self.n += 1

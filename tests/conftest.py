@@ -28,3 +28,27 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(scope="session")
+def native_ext():
+    """The _C extension (kernels + checkpoint/bundle bindings); built in-tree if stale/missing."""
+    from tools.build_ext import build_kernels
+    build_kernels()
+    from tensorflow_k8s_amd.ops._lib import lib
+    return lib()
+
+
+@pytest.fixture(scope="session")
+def control_plane_bin():
+    """Native control-plane binaries (cpp/ -> build/bin), built incrementally."""
+    from tools.build_ext import build_control_plane
+    build_control_plane()
+    return os.path.join(ROOT, "build", "bin")
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]

@@ -1,0 +1,89 @@
+"""End-to-end: native control plane (tfk-cluster: apiserver + TFJob operator + gang scheduler +
+kubelet, cpp/) running real training replicas (runtime/train.py) on CPU.
+
+Covers SURVEY §4.2 T3/T4: TFJob -> pods/services with TF_CONFIG -> MWMS training -> Succeeded;
+retryable failure (exit 137) -> gang restart -> resume from the chief's checkpoint -> Succeeded
+with the same final loss as an uninterrupted run; permanent failure (exit 1) -> Failed;
+backoffLimit exhaustion -> Failed.
+"""
+import json
+import os
+
+import pytest
+
+from tensorflow_k8s_amd.control.client import LocalCluster, tfjob_condition
+
+TRAIN = ["python3", "-m", "tensorflow_k8s_amd.runtime.train"]
+
+
+def _rs(n, args, env=(), policy="ExitCode"):
+    return {"replicas": n, "restartPolicy": policy, "template": {"spec": {"containers": [{
+        "name": "tensorflow", "image": "tfk/runtime", "command": TRAIN, "args": args,
+        "env": [{"name": k, "value": v} for k, v in env]}]}}}
+
+
+def _job(name, specs, backoff=3):
+    return {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": name, "namespace": "default"},
+            "spec": {"tfReplicaSpecs": specs, "runPolicy": {"backoffLimit": backoff, "cleanPodPolicy": "None"}}}
+
+
+def _events(text):
+    return [json.loads(l) for l in text.splitlines() if l.startswith("{")]
+
+
+@pytest.fixture
+def cluster(tmp_path, control_plane_bin, native_ext):
+    with LocalCluster(root_dir=str(tmp_path / "cluster")) as c:
+        yield c
+
+
+def _args(ck, steps=16):
+    return ["--model", "lenet", "--steps", str(steps), "--batch", "16", "--device", "cpu", "--log-every", "4",
+            "--checkpoint-dir", ck, "--checkpoint-every", "4"]
+
+
+def test_mnist_job_gang_restart_resumes_exactly(cluster, tmp_path):
+    c = cluster.client
+    # uninterrupted reference run
+    ck0 = str(tmp_path / "ck0")
+    c.create(_job("ref", {"Chief": _rs(1, _args(ck0)), "Worker": _rs(1, _args(ck0))}))
+    j = c.wait_tfjob("ref", timeout=240)
+    assert tfjob_condition(j) == "Succeeded", j["status"]
+    ref_loss = [e for e in _events(c.logs("ref-chief-0")) if e["event"] == "done"][-1]["loss"]
+    # worker 0 is SIGKILLed at step 10 in restart generation 0 -> retryable -> gang restart
+    ck1 = str(tmp_path / "ck1")
+    fault = [("TFK_FAULT_AT_STEP", "10"), ("TFK_FAULT_EXIT", "137"), ("TFK_FAULT_RANK", "1")]
+    c.create(_job("flaky", {"Chief": _rs(1, _args(ck1), fault), "Worker": _rs(1, _args(ck1), fault)}))
+    j = c.wait_tfjob("flaky", timeout=240)
+    st = j["status"]
+    assert tfjob_condition(j) == "Succeeded", st
+    assert any(cd["type"] == "Restarting" for cd in st["conditions"]), st
+    ev = _events(c.logs("flaky-chief-0"))
+    restored = [e for e in ev if e["event"] == "restored"]
+    assert restored and restored[-1]["step"] == 8
+    loss = [e for e in ev if e["event"] == "done"][-1]["loss"]
+    assert abs(loss - ref_loss) <= 1e-6 * max(1.0, abs(ref_loss)), (loss, ref_loss)
+    # every replica got a TF_CONFIG with both roles and its own task
+    pod = c.get("pods", "flaky-worker-0")
+    env = {e["name"]: e.get("value") for e in pod["spec"]["containers"][0]["env"]}
+    tf = json.loads(env["TF_CONFIG"])
+    assert tf["task"] == {"type": "worker", "index": 0} and len(tf["cluster"]["chief"]) == 1
+
+
+def test_permanent_failure_fails_job(cluster, tmp_path):
+    c = cluster.client
+    fault = [("TFK_FAULT_AT_STEP", "2"), ("TFK_FAULT_EXIT", "1"), ("TFK_FAULT_RANK", "0")]
+    c.create(_job("bad", {"Chief": _rs(1, _args(str(tmp_path / "ck")), fault)}))
+    j = c.wait_tfjob("bad", timeout=180)
+    assert tfjob_condition(j) == "Failed", j["status"]
+
+
+def test_backoff_limit_exhausted(cluster, tmp_path):
+    c = cluster.client
+    fault = [("TFK_FAULT_AT_STEP", "1"), ("TFK_FAULT_EXIT", "137"), ("TFK_FAULT_RANK", "0"),
+             ("TFK_FAULT_GENERATION", "any")]
+    c.create(_job("crashloop", {"Chief": _rs(1, _args(str(tmp_path / "ck")), fault)}, backoff=2))
+    j = c.wait_tfjob("crashloop", timeout=240)
+    assert tfjob_condition(j) == "Failed", j["status"]
+    msg = [cd for cd in j["status"]["conditions"] if cd["type"] == "Failed"][0]["message"]
+    assert "backoff" in msg.lower(), msg

@@ -1,0 +1,31 @@
+// Shared host-side validation helpers of the _C bindings: every op checks device, dtype,
+// contiguity, alignment and extents before a kernel launch, so a bad call fails loudly in Python
+// instead of faulting the GPU.
+#pragma once
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+namespace {
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+inline void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, "tfk kernel launch failed: ", what, " rc=", rc); }
+
+inline void need(const torch::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+inline void need_bf16(const torch::Tensor& t, const char* n) { need(t, at::kBFloat16, n); }
+inline void need_f32(const torch::Tensor& t, const char* n) { need(t, at::kFloat, n); }
+inline void need_aligned(const torch::Tensor& t, int bytes, const char* n) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % bytes == 0, n, " must be ", bytes, "-byte aligned");
+}
+inline void need_numel(const torch::Tensor& t, long long n, const char* name) {
+  TORCH_CHECK(t.numel() >= n, name, " too small: numel=", t.numel(), " < required ", n);
+}
+template <typename T>
+T* opt_ptr(const c10::optional<torch::Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+}  // namespace

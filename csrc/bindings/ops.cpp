@@ -7,8 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <vector>
 
-
-
+#include "bind_util.h"
 #include "../kernels/gemm_params.h"
 
 extern "C" {
@@ -51,41 +50,9 @@ int tfk_act_fwd(const void*, const float*, int, void*, long long, int, hipStream
 int tfk_act_bwd(const void*, const void*, void*, long long, int, hipStream_t);
 int tfk_dropout(const void*, void*, long long, float, unsigned long long, hipStream_t);
 int tfk_add(const void*, const void*, void*, long long, float, float, hipStream_t);
-int tfk_layernorm_fwd(const void*, const void*, const float*, const float*, void*, void*, float*, float*, int, int, float,
-                      hipStream_t);
-int tfk_layernorm_bwd(const void*, const void*, const float*, const float*, const float*, void*, float*, float*, int, int,
-                      hipStream_t);
-int tfk_embedding_fwd(const int*, const void*, void*, long long, int, int, hipStream_t);
-int tfk_embedding_bwd(const int*, const void*, float*, long long, int, int, hipStream_t);
-int tfk_attn_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, long long, long long,
-                 long long, long long, float, int, const int*, hipStream_t);
-int tfk_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, void*, void*, void*, float*,
-                 int, int, int, int, int, long long, long long, long long, long long, float, int, const int*, hipStream_t);
 }
 
 namespace {
-hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
-
-void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, "tfk kernel launch failed: ", what, " rc=", rc); }
-
-void need(const torch::Tensor& t, at::ScalarType dt, const char* name) {
-  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
-  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
-  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
-}
-void need_bf16(const torch::Tensor& t, const char* n) { need(t, at::kBFloat16, n); }
-void need_f32(const torch::Tensor& t, const char* n) { need(t, at::kFloat, n); }
-void need_aligned(const torch::Tensor& t, int bytes, const char* n) {
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % bytes == 0, n, " must be ", bytes, "-byte aligned");
-}
-void need_numel(const torch::Tensor& t, long long n, const char* name) {
-  TORCH_CHECK(t.numel() >= n, name, " too small: numel=", t.numel(), " < required ", n);
-}
-template <typename T>
-T* opt_ptr(const c10::optional<torch::Tensor>& t) {
-  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
-}
-
 enum { A_KIN = 0, A_KOUT = 1, A_CONV_FWD = 2, A_CONV_DGRAD = 3 };
 enum { B_KIN = 0, B_KOUT = 1, B_CONV_WGRAD = 2 };
 
@@ -94,7 +61,8 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
           int amode, int bmode, int epi, int bm, int bn, double alpha, double beta, c10::optional<torch::Tensor> bias,
           c10::optional<torch::Tensor> resid, int act, c10::optional<torch::Tensor> stats, int shards, int splits,
           int batch, int64_t sA, int64_t sB, int64_t sC, int64_t split_stride, std::vector<int64_t> conv,
-          std::vector<c10::optional<torch::Tensor>> bnr, int bn_relu, int bn_shards) {
+          std::vector<c10::optional<torch::Tensor>> bnr, int bn_relu, int bn_shards, c10::optional<torch::Tensor> aux,
+          c10::optional<torch::Tensor> dact_src, int dact, double drop_p, int64_t drop_seed) {
   need_bf16(A, "A");
   need_bf16(B, "B");
   TORCH_CHECK(epi == 0 || epi == 1, "epi");
@@ -203,6 +171,23 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   p.bias = opt_ptr<const float>(bias);
   p.resid = opt_ptr<const void>(resid);
   p.stats = opt_ptr<float>(stats);
+  for (auto* t : {&aux, &dact_src}) {
+    if (t->has_value() && (*t)->defined()) {
+      TORCH_CHECK(epi == 0, "aux/dact need the bf16 epilogue");
+      need_bf16(**t, "aux/dact_src");
+      need_numel(**t, bC + (long long)(M - 1) * ldc + N, "aux/dact_src");
+    }
+  }
+  p.aux = opt_ptr<void>(aux);
+  p.dact_src = opt_ptr<const void>(dact_src);
+  p.dact = dact;
+  TORCH_CHECK(!p.dact_src || (dact >= 1 && dact <= 3), "dact must be 1 (relu), 2 (gelu) or 3 (tanh) with dact_src");
+  TORCH_CHECK(act >= 0 && act <= 3, "act");
+  TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "drop_p");
+  TORCH_CHECK(drop_p == 0.0 || (epi == 0 && ldc == N && batch == 1), "fused dropout needs bf16 out, ldc==N, batch 1");
+  p.drop_p = (float)drop_p;
+  p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
+  p.drop_seed = (unsigned long long)drop_seed;
   TORCH_CHECK((bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64), "unsupported tile");
   check_rc(tfk_gemm_launch(p, bm, bn, amode, bmode, epi, batch, splits, cur_stream()), "gemm");
 }

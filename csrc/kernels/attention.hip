@@ -1,0 +1,419 @@
+// Fused multi-head attention (flash style) for gfx950: forward, dQ pass, dK/dV pass.
+//
+// Head dim D = 64. Q/K/V/O/dO are bf16 [B, S, H, 64] views with arbitrary token (row) and batch
+// strides, so Q, K and V can be read straight out of a fused QKV projection ([B*S, 3*H*64]) and O
+// is written in the [B*S, H*64] layout the output projection consumes: no head transposes.
+// lse/delta are f32 [B, H, Sq]. Options: causal mask, per-batch key length (padding mask),
+// attention-probability dropout (hash RNG of (seed, b, h, q, key) regenerated in backward).
+//
+// MFMA mapping (v_mfma_f32_16x16x32_bf16, wave64). mfma(X, Y) gives lane l, slot r:
+//   sum_k X[4*(l>>4) + r][k] * Y[l & 15][k]
+// where an operand fragment puts row (l & 15), k-slots 8*(l>>4)..+7 in lane l. Rows of Q (or K in
+// the dK/dV pass) stay lane-fixed ((l&15) = query), so softmax statistics are per-lane scalars and
+// row reductions are 4 register values + 2 shuffles. Within each 32-key chunk the 16-row blocks
+// of the "X" operand are read with the row permutation  i -> 8*(i>>2) + 4*half + (i&3)  so that
+// the P / dS accumulators of two blocks, packed to bf16, are directly the k-slots 8g..8g+7 of the
+// next MFMA (P*V, dS*K, ...) whose other operand is a transposed LDS read (ds_read_b64_tr_b16).
+// LDS tiles are [64 rows][72] bf16 (144-B rows: conflict-free 16-B row reads and tr reads).
+//
+// Backward = two kernels (no atomics, deterministic): dQ pass (grid over query tiles, recompute
+// P and dP, dQ = dS K) and dK/dV pass (grid over key tiles, dV = P^T dO, dK = dS^T Q).
+#include "common.h"
+
+namespace {
+constexpr int D = 64;
+constexpr int TILE = 64;
+constexpr int LS = 72;  // LDS row stride (elements)
+constexpr int NT = 256;
+constexpr float LOG2E = 1.4426950408889634f;
+
+struct AttnParams {
+  const bf16 *q, *k, *v, *o, *dout;
+  bf16 *out, *dq, *dk, *dv;
+  float *lse, *delta;
+  long long q_bs, k_bs, v_bs, o_bs, dq_bs, dk_bs, dv_bs;  // batch strides (elements)
+  int q_rs, k_rs, v_rs, o_rs, dq_rs, dk_rs, dv_rs;        // token strides (elements)
+  int B, H, Sq, Sk;
+  const int* kv_len;  // [B] valid keys per batch (padding mask) or null
+  float scale;
+  int causal;
+  float p_drop;
+  unsigned long long seed;
+};
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 x, bf16x8 y, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, c, 0, 0, 0);
+}
+
+// permuted row of 16-row block b inside a 64-row tile for lane-row i (see header)
+__device__ __forceinline__ int prow(int b, int i) { return 32 * (b >> 1) + 8 * (i >> 2) + 4 * (b & 1) + (i & 3); }
+// tile-relative row held by accumulator slot r of lane group g for block b
+__device__ __forceinline__ int arow(int b, int g, int r) { return 32 * (b >> 1) + 8 * g + 4 * (b & 1) + r; }
+
+// ---- global tile <-> registers <-> LDS (64 rows x 64 bf16; 2 x 16 B per thread)
+struct TileRegs {
+  u32x4 v[2];
+};
+__device__ __forceinline__ void tile_load(TileRegs& t, const bf16* base, int rs, int row0, int nvalid) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = threadIdx.x + it * NT, row = c >> 3, col = (c & 7) * 8;
+    if (row0 + row < nvalid)
+      t.v[it] = *(const u32x4*)(base + (long long)(row0 + row) * rs + col);
+    else
+      t.v[it] = u32x4{0u, 0u, 0u, 0u};
+  }
+}
+__device__ __forceinline__ void tile_store(const TileRegs& t, bf16* lds) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = threadIdx.x + it * NT, row = c >> 3, col = (c & 7) * 8;
+    *(u32x4*)(lds + row * LS + col) = t.v[it];
+  }
+}
+// row fragment: lane -> row `row`, k-slots = columns kk*32 + 8g .. +7
+__device__ __forceinline__ bf16x8 frag_row(const bf16* lds, int row, int kk) {
+  const int g = (threadIdx.x & 63) >> 4;
+  return *(const bf16x8*)(lds + row * LS + kk * 32 + 8 * g);
+}
+// transposed fragment: lane -> column cbase + (l&15), k-slots = tile rows kbase + 8g .. +7
+__device__ __forceinline__ bf16x8 frag_tr(const bf16* lds, int kbase, int cbase) {
+  const int l = threadIdx.x & 63, g = l >> 4, i = l & 15, qq = i >> 2, pc = i & 3;
+  const bf16* p0 = lds + (kbase + 8 * g + qq) * LS + cbase + 4 * pc;
+  const bf16* p1 = p0 + 4 * LS;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p1);
+  bf16x8 r;
+  r.lo = lo;
+  r.hi = hi;
+  return r;
+}
+// register row fragment straight from global (rows of this wave): row `row` (global), k-slots kk
+__device__ __forceinline__ bf16x8 frag_global(const bf16* base, int rs, int row, int nvalid, int kk) {
+  const int g = (threadIdx.x & 63) >> 4;
+  if (row >= nvalid) {
+    bf16x8 z;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z[e] = f2bf(0.f);
+    return z;
+  }
+  return *(const bf16x8*)(base + (long long)row * rs + kk * 32 + 8 * g);
+}
+__device__ __forceinline__ bf16x8 pack2(const f32x4& a, const f32x4& b) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { r[e] = f2bf(a[e]); r[4 + e] = f2bf(b[e]); }
+  return r;
+}
+__device__ __forceinline__ bool keep_elem(const AttnParams& p, int bh, int q, int key) {
+  return u01(hash_u32(p.seed ^ ((unsigned long long)bh * 0x9E3779B97F4A7C15ull), (unsigned long long)q * p.Sk + key)) >=
+         p.p_drop;
+}
+__device__ __forceinline__ void store_rowvec4(bf16* dst, const f32x4& v, float s) {
+  bf16x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e] * s);
+  *(bf16x4*)dst = o;
+}
+
+// =============================================================================== forward
+__global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) bf16 Ks[TILE * LS];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[TILE * LS];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * TILE;
+  const int bh = b * p.H + h;
+  const bf16* Qb = p.q + b * p.q_bs + h * D;
+  const bf16* Kb = p.k + b * p.k_bs + h * D;
+  const bf16* Vb = p.v + b * p.v_bs + h * D;
+  const int kvl = p.kv_len ? min(p.kv_len[b], p.Sk) : p.Sk;
+  const int qrow = q0 + 16 * w + li;  // this lane's query
+  const bf16x8 qf0 = frag_global(Qb, p.q_rs, qrow, p.Sq, 0), qf1 = frag_global(Qb, p.q_rs, qrow, p.Sq, 1);
+  const float sl2 = p.scale * LOG2E;
+  const float keep_scale = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+  float m = -INFINITY, lsum = 0.f;
+  f32x4 oacc[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) oacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int kend = kvl;
+  if (p.causal) kend = min(kend, q0 + TILE);
+  const int ntiles = (kend + TILE - 1) / TILE;
+  TileRegs kr, vr;
+  if (ntiles > 0) { tile_load(kr, Kb, p.k_rs, 0, kvl); tile_load(vr, Vb, p.v_rs, 0, kvl); }
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * TILE;
+    __syncthreads();
+    tile_store(kr, Ks);
+    tile_store(vr, Vs);
+    __syncthreads();
+    if (t + 1 < ntiles) { tile_load(kr, Kb, p.k_rs, k0 + TILE, kvl); tile_load(vr, Vb, p.v_rs, k0 + TILE, kvl); }
+    // S^T blocks: lane (g, r) of block bb = score(key k0 + arow(bb,g,r), query qrow)
+    f32x4 s[4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int kr_ = prow(bb, li);
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+      a = mfma(frag_row(Ks, kr_, 0), qf0, a);
+      a = mfma(frag_row(Ks, kr_, 1), qf1, a);
+      s[bb] = a;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + arow(bb, g, r);
+        float v = s[bb][r] * sl2;
+        if (key >= kvl || (p.causal && key > qrow)) v = -INFINITY;
+        s[bb][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float muse = mnew == -INFINITY ? 0.f : mnew;
+    const float alpha = exp2f(m - muse);
+    float rs = 0.f;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = exp2f(s[bb][r] - muse);
+        rs += e;
+        s[bb][r] = e;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    lsum = lsum * alpha + rs;
+    m = mnew;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) oacc[db] *= alpha;
+    if (p.p_drop > 0.f) {
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          s[bb][r] = keep_elem(p, bh, qrow, k0 + arow(bb, g, r)) ? s[bb][r] * keep_scale : 0.f;
+    }
+    const bf16x8 pf0 = pack2(s[0], s[1]), pf1 = pack2(s[2], s[3]);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      oacc[db] = mfma(frag_tr(Vs, 0, db * 16), pf0, oacc[db]);
+      oacc[db] = mfma(frag_tr(Vs, 32, db * 16), pf1, oacc[db]);
+    }
+  }
+  if (qrow < p.Sq) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16* O = p.out + b * p.o_bs + (long long)qrow * p.o_rs + h * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) store_rowvec4(O + db * 16 + 4 * g, oacc[db], inv);
+    if (g == 0 && p.lse)
+      p.lse[(long long)bh * p.Sq + qrow] = lsum > 0.f ? (m + log2f(lsum)) / LOG2E : INFINITY;
+  }
+}
+
+// delta[b,h,q] = sum_d dO * O
+__global__ void attn_delta_kernel(AttnParams p) {
+  const long long i = (long long)blockIdx.x * NT + threadIdx.x;
+  const long long n = (long long)p.B * p.H * p.Sq;
+  if (i >= n) return;
+  const int q = (int)(i % p.Sq), bh = (int)(i / p.Sq), b = bh / p.H, h = bh % p.H;
+  const bf16* o = p.o + b * p.o_bs + (long long)q * p.o_rs + h * D;
+  const bf16* d = p.dout + b * p.o_bs + (long long)q * p.o_rs + h * D;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < D / 8; ++c) {
+    bf16x8 a = *(const bf16x8*)(o + c * 8), bb = *(const bf16x8*)(d + c * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += bf2f(a[e]) * bf2f(bb[e]);
+  }
+  p.delta[i] = s;
+}
+
+// =============================================================================== dQ pass
+__global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) bf16 Ks[TILE * LS];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[TILE * LS];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * TILE;
+  const int bh = b * p.H + h;
+  const bf16* Qb = p.q + b * p.q_bs + h * D;
+  const bf16* Kb = p.k + b * p.k_bs + h * D;
+  const bf16* Vb = p.v + b * p.v_bs + h * D;
+  const bf16* dOb = p.dout + b * p.o_bs + h * D;
+  const int kvl = p.kv_len ? min(p.kv_len[b], p.Sk) : p.Sk;
+  const int qrow = q0 + 16 * w + li;
+  const bf16x8 qf0 = frag_global(Qb, p.q_rs, qrow, p.Sq, 0), qf1 = frag_global(Qb, p.q_rs, qrow, p.Sq, 1);
+  const bf16x8 df0 = frag_global(dOb, p.o_rs, qrow, p.Sq, 0), df1 = frag_global(dOb, p.o_rs, qrow, p.Sq, 1);
+  const float sl2 = p.scale * LOG2E;
+  const float keep_scale = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+  const float lse2 = qrow < p.Sq ? p.lse[(long long)bh * p.Sq + qrow] * LOG2E : INFINITY;
+  const float dlt = qrow < p.Sq ? p.delta[(long long)bh * p.Sq + qrow] : 0.f;
+  f32x4 acc[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) acc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int kend = kvl;
+  if (p.causal) kend = min(kend, q0 + TILE);
+  const int ntiles = (kend + TILE - 1) / TILE;
+  TileRegs kr, vr;
+  if (ntiles > 0) { tile_load(kr, Kb, p.k_rs, 0, kvl); tile_load(vr, Vb, p.v_rs, 0, kvl); }
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * TILE;
+    __syncthreads();
+    tile_store(kr, Ks);
+    tile_store(vr, Vs);
+    __syncthreads();
+    if (t + 1 < ntiles) { tile_load(kr, Kb, p.k_rs, k0 + TILE, kvl); tile_load(vr, Vb, p.v_rs, k0 + TILE, kvl); }
+    f32x4 ds[4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int kr_ = prow(bb, li);
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+      s = mfma(frag_row(Ks, kr_, 0), qf0, s);
+      s = mfma(frag_row(Ks, kr_, 1), qf1, s);
+      dp = mfma(frag_row(Vs, kr_, 0), df0, dp);
+      dp = mfma(frag_row(Vs, kr_, 1), df1, dp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + arow(bb, g, r);
+        const bool valid = key < kvl && !(p.causal && key > qrow);
+        const float pr = valid ? exp2f(s[r] * sl2 - lse2) : 0.f;
+        float dpv = dp[r];
+        if (p.p_drop > 0.f) dpv = keep_elem(p, bh, qrow, key) ? dpv * keep_scale : 0.f;
+        ds[bb][r] = pr * (dpv - dlt);
+      }
+    }
+    const bf16x8 sf0 = pack2(ds[0], ds[1]), sf1 = pack2(ds[2], ds[3]);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      acc[db] = mfma(frag_tr(Ks, 0, db * 16), sf0, acc[db]);
+      acc[db] = mfma(frag_tr(Ks, 32, db * 16), sf1, acc[db]);
+    }
+  }
+  if (qrow < p.Sq) {
+    bf16* dQ = p.dq + b * p.dq_bs + (long long)qrow * p.dq_rs + h * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) store_rowvec4(dQ + db * 16 + 4 * g, acc[db], p.scale);
+  }
+}
+
+// =============================================================================== dK/dV pass
+__global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) bf16 Qs[TILE * LS];
+  __shared__ __attribute__((aligned(16))) bf16 dOs[TILE * LS];
+  __shared__ float lse_s[TILE], dlt_s[TILE];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
+  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * TILE;
+  const int bh = b * p.H + h;
+  const bf16* Qb = p.q + b * p.q_bs + h * D;
+  const bf16* Kb = p.k + b * p.k_bs + h * D;
+  const bf16* Vb = p.v + b * p.v_bs + h * D;
+  const bf16* dOb = p.dout + b * p.o_bs + h * D;
+  const int kvl = p.kv_len ? min(p.kv_len[b], p.Sk) : p.Sk;
+  const int krow = k0 + 16 * w + li;  // this lane's key
+  const bf16x8 kf0 = frag_global(Kb, p.k_rs, krow, kvl, 0), kf1 = frag_global(Kb, p.k_rs, krow, kvl, 1);
+  const bf16x8 vf0 = frag_global(Vb, p.v_rs, krow, kvl, 0), vf1 = frag_global(Vb, p.v_rs, krow, kvl, 1);
+  const float sl2 = p.scale * LOG2E;
+  const float keep_scale = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) { dk[db] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[db] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  const int qstart = p.causal ? (k0 / TILE) * TILE : 0;
+  const int ntiles = k0 < kvl ? (p.Sq - qstart + TILE - 1) / TILE : 0;
+  TileRegs qr, dr;
+  if (ntiles > 0) { tile_load(qr, Qb, p.q_rs, qstart, p.Sq); tile_load(dr, dOb, p.o_rs, qstart, p.Sq); }
+  for (int t = 0; t < ntiles; ++t) {
+    const int q0 = qstart + t * TILE;
+    __syncthreads();
+    tile_store(qr, Qs);
+    tile_store(dr, dOs);
+    if (threadIdx.x < TILE) {
+      const int qq = q0 + threadIdx.x;
+      lse_s[threadIdx.x] = qq < p.Sq ? p.lse[(long long)bh * p.Sq + qq] * LOG2E : INFINITY;
+      dlt_s[threadIdx.x] = qq < p.Sq ? p.delta[(long long)bh * p.Sq + qq] : 0.f;
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) { tile_load(qr, Qb, p.q_rs, q0 + TILE, p.Sq); tile_load(dr, dOb, p.o_rs, q0 + TILE, p.Sq); }
+    f32x4 pp[4], ds[4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int qr_ = prow(bb, li);
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+      s = mfma(frag_row(Qs, qr_, 0), kf0, s);
+      s = mfma(frag_row(Qs, qr_, 1), kf1, s);
+      dp = mfma(frag_row(dOs, qr_, 0), vf0, dp);
+      dp = mfma(frag_row(dOs, qr_, 1), vf1, dp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qt = arow(bb, g, r), qq = q0 + qt;
+        const bool valid = krow < kvl && qq < p.Sq && !(p.causal && krow > qq);
+        const float pr = valid ? exp2f(s[r] * sl2 - lse_s[qt]) : 0.f;
+        float pd = pr, dpv = dp[r];
+        if (p.p_drop > 0.f) {
+          const bool kp = keep_elem(p, bh, qq, krow);
+          pd = kp ? pr * keep_scale : 0.f;
+          dpv = kp ? dpv * keep_scale : 0.f;
+        }
+        pp[bb][r] = pd;
+        ds[bb][r] = pr * (dpv - dlt_s[qt]);
+      }
+    }
+    const bf16x8 pf0 = pack2(pp[0], pp[1]), pf1 = pack2(pp[2], pp[3]);
+    const bf16x8 sf0 = pack2(ds[0], ds[1]), sf1 = pack2(ds[2], ds[3]);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      dv[db] = mfma(frag_tr(dOs, 0, db * 16), pf0, dv[db]);
+      dv[db] = mfma(frag_tr(dOs, 32, db * 16), pf1, dv[db]);
+      dk[db] = mfma(frag_tr(Qs, 0, db * 16), sf0, dk[db]);
+      dk[db] = mfma(frag_tr(Qs, 32, db * 16), sf1, dk[db]);
+    }
+  }
+  if (krow < p.Sk) {
+    bf16* dK = p.dk + b * p.dk_bs + (long long)krow * p.dk_rs + h * D;
+    bf16* dV = p.dv + b * p.dv_bs + (long long)krow * p.dv_rs + h * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      store_rowvec4(dK + db * 16 + 4 * g, dk[db], p.scale);
+      store_rowvec4(dV + db * 16 + 4 * g, dv[db], 1.f);
+    }
+  }
+}
+}  // namespace
+
+extern "C" {
+// shape: [B, H, Sq, Sk]; strides: [q_bs, q_rs, k_bs, k_rs, v_bs, v_rs, o_bs, o_rs]
+int tfk_attn_fwd(const void* q, const void* k, const void* v, void* out, float* lse, const long long* shape,
+                 const long long* strides, const int* kv_len, float scale, int causal, float p_drop,
+                 unsigned long long seed, hipStream_t s) {
+  AttnParams p{};
+  p.q = (const bf16*)q; p.k = (const bf16*)k; p.v = (const bf16*)v; p.out = (bf16*)out; p.lse = lse;
+  p.B = (int)shape[0]; p.H = (int)shape[1]; p.Sq = (int)shape[2]; p.Sk = (int)shape[3];
+  p.q_bs = strides[0]; p.q_rs = (int)strides[1]; p.k_bs = strides[2]; p.k_rs = (int)strides[3];
+  p.v_bs = strides[4]; p.v_rs = (int)strides[5]; p.o_bs = strides[6]; p.o_rs = (int)strides[7];
+  p.kv_len = kv_len; p.scale = scale; p.causal = causal; p.p_drop = p_drop; p.seed = seed;
+  dim3 grid((p.Sq + TILE - 1) / TILE, p.H, p.B);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(NT), 0, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// grads: dq/dk/dv with strides [dq_bs, dq_rs, dk_bs, dk_rs, dv_bs, dv_rs]; delta: [B*H*Sq] scratch
+int tfk_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
+                 float* delta, void* dq, void* dk, void* dv, const long long* shape, const long long* strides,
+                 const long long* gstrides, const int* kv_len, float scale, int causal, float p_drop,
+                 unsigned long long seed, hipStream_t s) {
+  AttnParams p{};
+  p.q = (const bf16*)q; p.k = (const bf16*)k; p.v = (const bf16*)v; p.o = (const bf16*)o; p.dout = (const bf16*)dout;
+  p.lse = (float*)lse; p.delta = delta; p.dq = (bf16*)dq; p.dk = (bf16*)dk; p.dv = (bf16*)dv;
+  p.B = (int)shape[0]; p.H = (int)shape[1]; p.Sq = (int)shape[2]; p.Sk = (int)shape[3];
+  p.q_bs = strides[0]; p.q_rs = (int)strides[1]; p.k_bs = strides[2]; p.k_rs = (int)strides[3];
+  p.v_bs = strides[4]; p.v_rs = (int)strides[5]; p.o_bs = strides[6]; p.o_rs = (int)strides[7];
+  p.dq_bs = gstrides[0]; p.dq_rs = (int)gstrides[1]; p.dk_bs = gstrides[2]; p.dk_rs = (int)gstrides[3];
+  p.dv_bs = gstrides[4]; p.dv_rs = (int)gstrides[5];
+  p.kv_len = kv_len; p.scale = scale; p.causal = causal; p.p_drop = p_drop; p.seed = seed;
+  const long long n = (long long)p.B * p.H * p.Sq;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, s, p);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((p.Sq + TILE - 1) / TILE, p.H, p.B), dim3(NT), 0, s, p);
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((p.Sk + TILE - 1) / TILE, p.H, p.B), dim3(NT), 0, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

@@ -69,6 +69,18 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
 }
 
+// Activation codes shared by GEMM epilogues and elementwise kernels: 0 none, 1 relu, 2 gelu(tanh), 3 tanh.
+__device__ __forceinline__ float act_apply(float v, int act) {
+  return act == 1 ? fmaxf(v, 0.f) : (act == 2 ? gelu_tanh(v) : (act == 3 ? tanhf(v) : v));
+}
+// derivative at the PRE-activation z
+__device__ __forceinline__ float act_grad(float z, int act) {
+  if (act == 1) return z > 0.f ? 1.f : 0.f;
+  if (act == 2) return gelu_tanh_grad(z);
+  if (act == 3) { const float t = tanhf(z); return 1.f - t * t; }
+  return 1.f;
+}
+
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 'XCD swizzle must be bijective'):
 // blocks b and b+8 share an XCD under round-robin dispatch, so give each XCD a contiguous range
 // of logical tile ids -> neighbouring tiles (sharing an A panel) hit the same 4 MiB L2.

@@ -337,15 +337,35 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int mloc = wm * (BM / 2) + i * 16 + ml;
-        bf16x4 o;
+        const int mg = m0 + mloc, ng = n0 + nloc;
+        const bool full = mg < p.M && ng + 3 < p.N && (p.ldc & 3) == 0;
+        const long long goff = bz * p.sC + (long long)mg * p.ldc + ng;
+        float dz[4] = {1.f, 1.f, 1.f, 1.f};
+        if (p.dact_src && mg < p.M) {
+          const bf16* zs = (const bf16*)p.dact_src + goff;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float z = ng + r < p.N ? bf2f(zs[r]) : 0.f;
+            dz[r] = act_grad(z, p.dact);
+          }
+        }
+        bf16x4 o, pre;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = acc[i][j][r] * p.alpha + bv[r];
-          if (p.act == 1) v = fmaxf(v, 0.f);
-          else if (p.act == 2) v = gelu_tanh(v);
+          float v = (acc[i][j][r] * p.alpha + bv[r]) * dz[r];
+          pre[r] = f2bf(v);
+          v = act_apply(v, p.act);
+          if (p.drop_p > 0.f && mg < p.M)
+            v = u01(hash_u32(p.drop_seed, (unsigned long long)mg * p.N + ng + r)) < 1.f - p.drop_p ? v * p.drop_scale : 0.f;
           csum[j][r] += v;
           csq[j][r] += v * v;
           o[r] = f2bf(v);
+        }
+        if (p.aux && mg < p.M) {
+          bf16* ad = (bf16*)p.aux + goff;
+          if (full) *(bf16x4*)ad = pre;
+          else
+            for (int r = 0; r < 4 && ng + r < p.N; ++r) ad[r] = pre[r];
         }
         *(bf16x4*)(Cs + mloc * LDC_S + nloc) = o;
       }

@@ -35,5 +35,14 @@ struct GemmParams {
   const float* bn_invstd2;
   float* bn_sums;
   int bn_shards;
+  // bf16 epilogue extras: aux = pre-activation copy of C (e.g. GELU input saved for backward);
+  // dact_src/dact: C = (A*B) * act'(dact_src) (activation backward fused into a dgrad GEMM).
+  void* aux;
+  const void* dact_src;
+  int dact;
+  // inverted dropout after the activation, before the residual add; mask = hash(seed, m*N + n),
+  // identical to misc.hip's dropout kernel on the contiguous [M][N] output (backward regenerates it)
+  float drop_p, drop_scale;
+  unsigned long long drop_seed;
 };
 }  // namespace tfk

@@ -135,7 +135,7 @@ __global__ void act_fwd_kernel(const bf16* __restrict__ x, const float* __restri
                                long long n, int act) {
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
     float v = bf2f(x[i]) + (bias ? bias[i % N] : 0.f);
-    y[i] = f2bf(act == 1 ? fmaxf(v, 0.f) : (act == 2 ? gelu_tanh(v) : v));
+    y[i] = f2bf(act_apply(v, act));
   }
 }
 // dx = dy * act'(x_preact)
@@ -143,7 +143,7 @@ __global__ void act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restri
                                int act) {
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
     float v = bf2f(x[i]), g = bf2f(dy[i]);
-    dx[i] = f2bf(act == 1 ? (v > 0.f ? g : 0.f) : (act == 2 ? g * gelu_tanh_grad(v) : g));
+    dx[i] = f2bf(g * act_grad(v, act));
   }
 }
 

@@ -1,0 +1,249 @@
+// LayerNorm and embedding kernels for the transformer models (BERT, Transformer-big).
+//
+// LayerNorm over the last dim W (W % 8 == 0, W <= 2048): one wave64 per row, the row lives in
+// registers (16-B bf16 vectors), exact two-pass mean/variance; saves mean and rstd (f32) for
+// backward. Backward: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*gamma, plus an optional
+// residual-stream gradient added in the same pass; dgamma/dbeta are accumulated per lane across
+// the rows a wave visits, reduced across the block in LDS, then one f32 atomic per column/block.
+//
+// Embedding: out[t] = word[ids[t]]*scale (+ pos[t % S]) (+ type[tt[t]]), 8 columns per thread;
+// backward scatters into f32 gradient tables with atomics (rows shared by many tokens).
+#include "common.h"
+
+namespace {
+constexpr int NT = 256;
+
+template <int CPL>
+__global__ __launch_bounds__(NT) void ln_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, bf16* __restrict__ y,
+                                                    float* __restrict__ mean, float* __restrict__ rstd, int M, int W,
+                                                    float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nch = W >> 3;
+  const bf16* xr = x + (long long)row * W;
+  float v[CPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nch) {
+      bf16x8 t = *(const bf16x8*)(xr + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { v[j][e] = bf2f(t[e]); s += v[j][e]; }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[j][e] = 0.f;
+    }
+  }
+  const float mu = wave_sum(s) / W;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j)
+    if (lane + 64 * j < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = v[j][e] - mu; q += d * d; }
+  const float rs = rsqrtf(wave_sum(q) / W + eps);
+  bf16* yr = y + (long long)row * W;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nch) {
+      f32x4 g0 = *(const f32x4*)(gamma + c * 8), g1 = *(const f32x4*)(gamma + c * 8 + 4);
+      f32x4 b0 = *(const f32x4*)(beta + c * 8), b1 = *(const f32x4*)(beta + c * 8 + 4);
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = f2bf((v[j][e] - mu) * rs * g0[e] + b0[e]);
+        o[e + 4] = f2bf((v[j][e + 4] - mu) * rs * g1[e] + b1[e]);
+      }
+      *(bf16x8*)(yr + c * 8) = o;
+    }
+  }
+  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+}
+
+template <int CPL>
+__global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                    const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd, const bf16* __restrict__ dres,
+                                                    bf16* __restrict__ dx, float* __restrict__ dgamma,
+                                                    float* __restrict__ dbeta, int M, int W) {
+  extern __shared__ float red[];  // [NT/64][2][W]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nch = W >> 3;
+  float dg[CPL][8], db[CPL][8], gm[CPL][8];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { dg[j][e] = 0.f; db[j][e] = 0.f; gm[j][e] = c < nch ? gamma[c * 8 + e] : 0.f; }
+  }
+  for (int row = blockIdx.x * (NT / 64) + wid; row < M; row += gridDim.x * (NT / 64)) {
+    const float mu = mean[row], rs = rstd[row];
+    float g[CPL][8], xh[CPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        bf16x8 dv = *(const bf16x8*)(dy + (long long)row * W + c * 8);
+        bf16x8 xv = *(const bf16x8*)(x + (long long)row * W + c * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = bf2f(dv[e]);
+          xh[j][e] = (bf2f(xv[e]) - mu) * rs;
+          g[j][e] = d * gm[j][e];
+          s1 += g[j][e];
+          s2 += g[j][e] * xh[j][e];
+          dg[j][e] += d * xh[j][e];
+          db[j][e] += d;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { g[j][e] = 0.f; xh[j][e] = 0.f; }
+      }
+    }
+    s1 = wave_sum(s1) / W;
+    s2 = wave_sum(s2) / W;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        bf16x8 rv;
+        if (dres) rv = *(const bf16x8*)(dres + (long long)row * W + c * 8);
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v = rs * (g[j][e] - s1 - xh[j][e] * s2);
+          if (dres) v += bf2f(rv[e]);
+          o[e] = f2bf(v);
+        }
+        *(bf16x8*)(dx + (long long)row * W + c * 8) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wid * 2 + 0) * W + c * 8 + e] = dg[j][e];
+        red[(wid * 2 + 1) * W + c * 8 + e] = db[j][e];
+      }
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < W; col += NT) {
+    float a = 0.f, b2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) { a += red[(w * 2) * W + col]; b2 += red[(w * 2 + 1) * W + col]; }
+    atomicAdd(dgamma + col, a);
+    atomicAdd(dbeta + col, b2);
+  }
+}
+
+__global__ void embed_fwd_kernel(const int* __restrict__ ids, const bf16* __restrict__ word, int V,
+                                 const bf16* __restrict__ pos, int S, const int* __restrict__ tt,
+                                 const bf16* __restrict__ type, int T, bf16* __restrict__ out, long long ntok, int W,
+                                 float scale) {
+  const int cpr = W >> 3;
+  const long long n = ntok * cpr;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const long long t = i / cpr;
+    const int c = (int)(i - t * cpr) * 8;
+    const int id = min(max(ids[t], 0), V - 1);
+    bf16x8 wv = *(const bf16x8*)(word + (long long)id * W + c);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = bf2f(wv[e]) * scale;
+    if (pos) {
+      bf16x8 pv = *(const bf16x8*)(pos + (long long)(t % S) * W + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += bf2f(pv[e]);
+    }
+    if (type) {
+      const int ty = min(max(tt[t], 0), T - 1);
+      bf16x8 tv = *(const bf16x8*)(type + (long long)ty * W + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += bf2f(tv[e]);
+    }
+    bf16x8 r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = f2bf(o[e]);
+    *(bf16x8*)(out + t * W + c) = r;
+  }
+}
+
+__global__ void embed_bwd_kernel(const int* __restrict__ ids, const bf16* __restrict__ dy, int V,
+                                 float* __restrict__ dword, float* __restrict__ dpos, int S, const int* __restrict__ tt,
+                                 float* __restrict__ dtype, int T, long long ntok, int W, float scale) {
+  const int cpr = W >> 3;
+  const long long n = ntok * cpr;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const long long t = i / cpr;
+    const int c = (int)(i - t * cpr) * 8;
+    bf16x8 g = *(const bf16x8*)(dy + t * W + c);
+    const int id = min(max(ids[t], 0), V - 1);
+    float* dw = dword + (long long)id * W + c;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(dw + e, bf2f(g[e]) * scale);
+    if (dpos) {
+      float* dp = dpos + (long long)(t % S) * W + c;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(dp + e, bf2f(g[e]));
+    }
+    if (dtype) {
+      const int ty = min(max(tt[t], 0), T - 1);
+      float* dt = dtype + (long long)ty * W + c;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(dt + e, bf2f(g[e]));
+    }
+  }
+}
+
+int grid_for(long long work, int per_block, int cap) {
+  long long g = (work + per_block - 1) / per_block;
+  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+}  // namespace
+
+extern "C" {
+int tfk_layernorm_fwd(const bf16* x, const float* gamma, const float* beta, bf16* y, float* mean, float* rstd, int M,
+                      int W, float eps, hipStream_t s) {
+  const int cpl = (W / 8 + 63) / 64;
+  dim3 grid((M + NT / 64 - 1) / (NT / 64));
+  if (cpl <= 1) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(NT), 0, s, x, gamma, beta, y, mean, rstd, M, W, eps);
+  else if (cpl <= 2) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(NT), 0, s, x, gamma, beta, y, mean, rstd, M, W, eps);
+  else if (cpl <= 4) hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(NT), 0, s, x, gamma, beta, y, mean, rstd, M, W, eps);
+  else return -3;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const float* mean, const float* rstd,
+                      const bf16* dres, bf16* dx, float* dgamma, float* dbeta, int M, int W, hipStream_t s) {
+  const int cpl = (W / 8 + 63) / 64;
+  dim3 grid(grid_for(M, (NT / 64) * 8, 1024));
+  const size_t sh = (size_t)(NT / 64) * 2 * W * sizeof(float);
+  if (cpl <= 1)
+    hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W);
+  else if (cpl <= 2)
+    hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W);
+  else if (cpl <= 4)
+    hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W);
+  else return -3;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_embedding_fwd(const int* ids, const bf16* word, int V, const bf16* pos, int S, const int* tt, const bf16* type,
+                      int T, bf16* out, long long ntok, int W, float scale, hipStream_t s) {
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(ntok * (W / 8), NT, 8192)), dim3(NT), 0, s, ids, word, V, pos, S,
+                     tt, type, T, out, ntok, W, scale);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_embedding_bwd(const int* ids, const bf16* dy, int V, float* dword, float* dpos, int S, const int* tt,
+                      float* dtype, int T, long long ntok, int W, float scale, hipStream_t s) {
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_for(ntok * (W / 8), NT, 8192)), dim3(NT), 0, s, ids, dy, V, dword,
+                     dpos, S, tt, dtype, T, ntok, W, scale);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

@@ -1,26 +1,52 @@
 """Elementwise ops (csrc/kernels/misc.hip): bias+activation, activation backward, dropout, add.
 
 Most activations are fused into GEMM epilogues (ops.gemm act=...); these standalone passes cover
-the remaining producers. act: None | "relu" | "gelu" (tanh form, as TF's gelu(approximate=True)).
+the remaining producers. act: None | "relu" | "gelu" (tanh form, as TF's gelu(approximate=True)) | "tanh".
 """
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
 from ._lib import lib, on_gpu
+from .gemm import ACT, act_grad_ref, act_ref
 
-ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+_M64 = (1 << 64) - 1
+
+
+def _s64(v: int) -> int:
+    v &= _M64
+    return v - (1 << 64) if v >> 63 else v
+
+
+def _shr(x: torch.Tensor, k: int) -> torch.Tensor:
+    return (x >> k) & ((1 << (64 - k)) - 1)
+
+
+def hash_u32(seed, idx: torch.Tensor) -> torch.Tensor:
+    """Bit-exact torch (int64) copy of common.h hash_u32(seed, idx); seed: int or int64 tensor."""
+    sd = seed if torch.is_tensor(seed) else torch.tensor(_s64(int(seed)), dtype=torch.int64)
+    x = (idx * _s64(0x9E3779B97F4A7C15)) ^ (sd + _s64(0xD1B54A32D192ED03))
+    x = x ^ _shr(x, 31)
+    x = x * _s64(0xBF58476D1CE4E5B9)
+    x = x ^ _shr(x, 27)
+    x = x * _s64(0x94D049BB133111EB)
+    x = x ^ _shr(x, 33)
+    return x & 0xFFFFFFFF
+
+
+def u01(h: torch.Tensor) -> torch.Tensor:
+    return (h >> 8).float() * (1.0 / 16777216.0)
+
+
+def dropout_keep(seed: int, n: int, p: float) -> torch.Tensor:
+    """Keep-mask of the dropout kernel / fused GEMM dropout over a contiguous tensor of n elements."""
+    return u01(hash_u32(seed, torch.arange(n, dtype=torch.int64))) < (1.0 - p)
 
 
 def act_fwd(x: torch.Tensor, act: str | None, bias: torch.Tensor | None = None) -> torch.Tensor:
     if not on_gpu(x):
         v = x.float() + (bias.float() if bias is not None else 0.0)
-        if ACT[act] == 1:
-            v = torch.relu(v)
-        elif ACT[act] == 2:
-            v = F.gelu(v, approximate="tanh")
-        return v.to(torch.bfloat16)
+        return act_ref(v, act).to(torch.bfloat16)
     y = torch.empty_like(x)
     lib().act_fwd(x, bias, x.shape[-1], y, ACT[act])
     return y
@@ -29,15 +55,7 @@ def act_fwd(x: torch.Tensor, act: str | None, bias: torch.Tensor | None = None) 
 def act_bwd(dy: torch.Tensor, x: torch.Tensor, act: str | None) -> torch.Tensor:
     """dx = dy * act'(x). For relu, x may be the pre- or post-activation (same sign test)."""
     if not on_gpu(dy):
-        g = dy.float()
-        if ACT[act] == 1:
-            g = g * (x.float() > 0)
-        elif ACT[act] == 2:
-            xf = x.float().requires_grad_(True)
-            with torch.enable_grad():
-                (gx,) = torch.autograd.grad(F.gelu(xf, approximate="tanh"), xf, g)
-            g = gx
-        return g.to(torch.bfloat16)
+        return (dy.float() * act_grad_ref(x, act)).to(torch.bfloat16)
     dx = torch.empty_like(dy)
     lib().act_bwd(dy, x, dx, ACT[act])
     return dx
@@ -48,8 +66,7 @@ def dropout(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
     if p <= 0.0:
         return x
     if not on_gpu(x):
-        g = torch.Generator().manual_seed(int(seed))
-        keep = torch.rand(x.shape, generator=g) >= p
+        keep = dropout_keep(seed, x.numel(), p).reshape(x.shape)
         return (x.float() * keep / (1 - p)).to(torch.bfloat16)
     y = torch.empty_like(x)
     lib().dropout(x, y, p, int(seed))

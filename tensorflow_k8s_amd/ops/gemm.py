@@ -16,7 +16,19 @@ from ._lib import lib, on_gpu, workspace
 A_KIN, A_KOUT, A_CONV_FWD, A_CONV_DGRAD = 0, 1, 2, 3
 B_KIN, B_KOUT, B_CONV_WGRAD = 0, 1, 2
 EPI_BF16, EPI_F32 = 0, 1
-ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2, "tanh": 3}
+
+
+def act_ref(y: torch.Tensor, act) -> torch.Tensor:
+    """f32 reference of the epilogue activations."""
+    a = ACT[act]
+    if a == 1:
+        return torch.relu(y)
+    if a == 2:
+        return F.gelu(y, approximate="tanh")
+    if a == 3:
+        return torch.tanh(y)
+    return y
 NO_CONV = [0] * 15
 TARGET_BLOCKS = 1024  # ~4 blocks per CU on 256 CUs
 
@@ -80,11 +92,12 @@ def pick_splits(tiles: int, K: int, min_ktiles: int = 4) -> int:
 
 
 def _gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile, *, alpha=1.0, beta=0.0, bias=None, resid=None,
-          act=0, stats=None, shards=1, splits=1, batch=1, sA=0, sB=0, sC=0, split_stride=0, conv=NO_CONV, bnr=None):
+          act=0, stats=None, shards=1, splits=1, batch=1, sA=0, sB=0, sC=0, split_stride=0, conv=NO_CONV, bnr=None,
+          aux=None, dact_src=None, dact=0, drop_p=0.0, drop_seed=0):
     lib().gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile[0], tile[1], alpha, beta, bias, resid, act,
                stats, shards, splits, batch, sA, sB, sC, split_stride, conv,
                bnr.gemm_args() if bnr is not None else [], int(bnr.relu) if bnr is not None else 0,
-               bnr.st.shards if bnr is not None else 1)
+               bnr.st.shards if bnr is not None else 1, aux, dact_src, dact, drop_p, drop_seed)
 
 
 def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, accumulate: bool, device,
@@ -103,18 +116,23 @@ def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, 
 
 # =========================================================================== linear
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
-               resid: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """y[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ resid). bf16 in/out, f32 accumulate."""
+               resid: torch.Tensor | None = None, out: torch.Tensor | None = None,
+               aux: torch.Tensor | None = None, drop_p: float = 0.0, drop_seed: int = 0) -> torch.Tensor:
+    """y[M,N] = dropout(act(x[M,K] @ w[N,K]^T + bias)) (+ resid). bf16 in/out, f32 accumulate.
+    aux: also store the pre-activation (bf16) there, for the activation backward. Dropout mask =
+    ops.elementwise.dropout_keep(drop_seed, M*N, drop_p) (backward: elementwise.dropout(dy))."""
     M, K = x.shape[0], x.shape[-1]
     N = w.shape[0]
     if not on_gpu(x):
-        y = x.float() @ w.float().t()
+        y = x.float().reshape(-1, K) @ w.float().t()
         if bias is not None:
             y = y + bias.float()
-        if ACT[act] == 1:
-            y = torch.relu(y)
-        elif ACT[act] == 2:
-            y = F.gelu(y, approximate="tanh")
+        if aux is not None:
+            aux.view(-1, N).copy_(y)
+        y = act_ref(y, act)
+        if drop_p > 0:
+            from .elementwise import dropout_keep
+            y = y * dropout_keep(drop_seed, y.numel(), drop_p).reshape(y.shape) / (1 - drop_p)
         y = y.to(torch.bfloat16)
         if resid is not None:
             y = (y.float() + resid.float()).to(torch.bfloat16)
@@ -126,23 +144,43 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
     M = x2.shape[0]
     y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
     _gemm(x2, w, y, M, N, K, K, K, N, A_KIN, B_KIN, EPI_BF16, pick_tile(M, N), bias=bias, act=ACT[act],
-          resid=resid.reshape(-1, N) if resid is not None else None)
+          resid=resid.reshape(-1, N) if resid is not None else None, aux=aux, drop_p=drop_p, drop_seed=drop_seed)
     return y
 
 
-def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None = None) -> torch.Tensor:
-    """dx[M,K] = dy[M,N] @ w[N,K] (+ resid)."""
+def act_grad_ref(z: torch.Tensor, act: str | None) -> torch.Tensor:
+    """f32 derivative of the activation at pre-activation z (CPU reference)."""
+    z = z.float()
+    if ACT[act] == 1:
+        return (z > 0).float()
+    if ACT[act] == 2:
+        k0, k1 = 0.7978845608028654, 0.044715
+        t = torch.tanh(k0 * (z + k1 * z ** 3))
+        return 0.5 * (1 + t) + 0.5 * z * (1 - t * t) * k0 * (1 + 3 * k1 * z * z)
+    if ACT[act] == 3:
+        return 1 - torch.tanh(z) ** 2
+    return torch.ones_like(z)
+
+
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None = None,
+                 dact_src: torch.Tensor | None = None, dact: str | None = None) -> torch.Tensor:
+    """dx[M,K] = (dy[M,N] @ w[N,K]) * act'(dact_src) (+ resid)."""
     N, K = w.shape
     dy2 = dy.reshape(-1, N)
     M = dy2.shape[0]
     if not on_gpu(dy):
-        dx = (dy2.float() @ w.float()).to(torch.bfloat16)
+        dx = dy2.float() @ w.float()
+        if dact_src is not None:
+            dx = dx * act_grad_ref(dact_src.reshape(-1, K), dact)
+        dx = dx.to(torch.bfloat16)
         if resid is not None:
             dx = (dx.float() + resid.reshape(-1, K).float()).to(torch.bfloat16)
         return dx
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
     _gemm(dy2, w, dx, M, K, N, N, K, K, A_KIN, B_KOUT, EPI_BF16, pick_tile(M, K),
-          resid=resid.reshape(-1, K) if resid is not None else None)
+          resid=resid.reshape(-1, K) if resid is not None else None,
+          dact_src=dact_src.reshape(-1, K) if dact_src is not None else None,
+          dact=ACT[dact] if dact_src is not None else 0)
     return dx
 
 
@@ -213,10 +251,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
         y = _ref_conv(x, w, g)
         if bias is not None:
             y = y + bias.float()
-        if ACT[act] == 1:
-            y = torch.relu(y)
-        elif ACT[act] == 2:
-            y = F.gelu(y, approximate="tanh")
+        y = act_ref(y, act)
         if stats is not None:
             yf = y.reshape(-1, g.K)
             stats.view(shards, 2, g.K)[0, 0] += yf.sum(0)

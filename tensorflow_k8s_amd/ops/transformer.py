@@ -1,0 +1,186 @@
+"""Transformer ops (csrc/kernels/attention.hip, transformer.hip): LayerNorm, embeddings, fused
+multi-head attention. bf16 activations, f32 statistics/gradients of parameters.
+
+Attention operands are *column views* of 2-D token-major buffers: ``(buf, col)`` means the
+[B*S, H*64] block of ``buf[:, col:col + H*64]`` -- e.g. q/k/v straight out of a fused QKV
+projection ``qkv[B*S, 3*H*64]`` (q at col 0, k at H*64, v at 2*H*64). No head transposes.
+CPU paths are fp32 references with the same rounding points and (for dropout) the same hash RNG.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._lib import lib, on_gpu
+
+HEAD_DIM = 64
+
+# ----------------------------------------------------------------------------- LayerNorm
+
+
+def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12):
+    """Returns (y bf16, mean f32 [M], rstd f32 [M])."""
+    W = x.shape[-1]
+    x2 = x.reshape(-1, W)
+    M = x2.shape[0]
+    if not on_gpu(x):
+        xf = x2.float()
+        mu = xf.mean(1)
+        var = ((xf - mu[:, None]) ** 2).mean(1)
+        rs = torch.rsqrt(var + eps)
+        y = ((xf - mu[:, None]) * rs[:, None] * gamma + beta).to(torch.bfloat16)
+        return y.reshape(x.shape), mu, rs
+    y = torch.empty_like(x)
+    mean = torch.empty(M, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+    lib().layernorm_fwd(x2, gamma, beta, y, mean, rstd, M, W, eps)
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate: bool = False):
+    """dx (+ dres) bf16; dgamma/dbeta (f32, written or accumulated)."""
+    W = x.shape[-1]
+    M = x.numel() // W
+    if not on_gpu(dy):
+        d = dy.reshape(-1, W).float()
+        xh = (x.reshape(-1, W).float() - mean[:, None]) * rstd[:, None]
+        g = d * gamma
+        dx = rstd[:, None] * (g - g.mean(1, keepdim=True) - xh * (g * xh).mean(1, keepdim=True))
+        if dres is not None:
+            dx = dx + dres.reshape(-1, W).float()
+        dg, db = (d * xh).sum(0), d.sum(0)
+        if accumulate:
+            dgamma.add_(dg); dbeta.add_(db)
+        else:
+            dgamma.copy_(dg); dbeta.copy_(db)
+        return dx.to(torch.bfloat16).reshape(dy.shape)
+    if not accumulate:
+        dgamma.zero_(); dbeta.zero_()
+    dx = torch.empty_like(dy)
+    lib().layernorm_bwd(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W)
+    return dx
+
+
+# ----------------------------------------------------------------------------- embeddings
+
+
+def embedding_fwd(ids, word, pos=None, seq_len: int = 1, type_ids=None, type_table=None, scale: float = 1.0):
+    """out[t] = word[ids[t]]*scale (+ pos[t % seq_len]) (+ type_table[type_ids[t]]); bf16 [T, W]."""
+    T = ids.numel()
+    W = word.shape[1]
+    if not on_gpu(word):
+        o = word.float()[ids.reshape(-1).long().clamp(0, word.shape[0] - 1)] * scale
+        if pos is not None:
+            o = o + pos.float()[:seq_len].repeat(T // seq_len, 1)
+        if type_table is not None:
+            o = o + type_table.float()[type_ids.reshape(-1).long()]
+        return o.to(torch.bfloat16)
+    out = torch.empty(T, W, dtype=torch.bfloat16, device=word.device)
+    lib().embedding_fwd(ids, word, pos, seq_len, type_ids, type_table, out, scale)
+    return out
+
+
+def embedding_bwd(ids, dy, dword, dpos=None, seq_len: int = 1, type_ids=None, dtype_table=None, scale: float = 1.0):
+    """Scatter-add into f32 gradient tables (caller zeroes / overwrites them first)."""
+    W = dy.shape[-1]
+    if not on_gpu(dy):
+        d = dy.reshape(-1, W).float()
+        dword.view(-1, W).index_add_(0, ids.reshape(-1).long(), d * scale)
+        if dpos is not None:
+            dpos.view(-1, W)[:seq_len].add_(d.view(-1, seq_len, W).sum(0))
+        if dtype_table is not None:
+            dtype_table.view(-1, W).index_add_(0, type_ids.reshape(-1).long(), d)
+        return
+    lib().embedding_bwd(ids, dy, dword, dpos, seq_len, type_ids, dtype_table, W, scale)
+
+
+# ----------------------------------------------------------------------------- attention
+
+def dropout_keep_mask(seed: int, B: int, H: int, Sq: int, Sk: int, p: float) -> torch.Tensor:
+    """The kernels' attention-dropout mask (bool [B,H,Sq,Sk]), bit-exact (hash_u32 in common.h)."""
+    from .elementwise import _s64, hash_u32, u01
+    bh = torch.arange(B * H, dtype=torch.int64)
+    sd = torch.tensor(_s64(seed), dtype=torch.int64) ^ (bh * _s64(0x9E3779B97F4A7C15))
+    idx = torch.arange(Sq * Sk, dtype=torch.int64)
+    return (u01(hash_u32(sd[:, None], idx[None, :])) >= p).reshape(B, H, Sq, Sk)
+
+
+def _view(buf, col, B, S, H):
+    return buf.reshape(B * S, -1)[:, col:col + H * HEAD_DIM].reshape(B, S, H, HEAD_DIM)
+
+
+def _ref_probs(q, k, kv_len, causal, scale):
+    B, Sq, H, _ = q.shape
+    Sk = k.shape[1]
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) * scale
+    mask = torch.zeros(B, 1, Sq, Sk, dtype=torch.bool)
+    if kv_len is not None:
+        mask |= torch.arange(Sk)[None, None, None, :] >= kv_len.long().cpu()[:, None, None, None]
+    if causal:
+        mask |= torch.arange(Sk)[None, :] > torch.arange(Sq)[:, None]
+    s = s.masked_fill(mask, float("-inf"))
+    return torch.softmax(s, -1).nan_to_num(0.0)
+
+
+class AttnSpec:
+    """Geometry of one attention call: q/k/v column views of token-major buffers."""
+
+    def __init__(self, B, H, Sq, Sk, q, k, v, kv_len=None, causal=False, p_drop=0.0, seed=0, scale=None):
+        self.B, self.H, self.Sq, self.Sk = B, H, Sq, Sk
+        self.q, self.k, self.v = q, k, v  # (buf, col)
+        self.kv_len, self.causal, self.p_drop, self.seed = kv_len, causal, p_drop, seed
+        self.scale = scale if scale is not None else 1.0 / math.sqrt(HEAD_DIM)
+
+    def strides(self):
+        out = []
+        for (buf, _), S in ((self.q, self.Sq), (self.k, self.Sk), (self.v, self.Sk)):
+            rs = buf.shape[-1]
+            out += [S * rs, rs]
+        return out
+
+
+def attention_fwd(sp: AttnSpec):
+    """Returns (out bf16 [B*Sq, H*64], lse f32 [B,H,Sq])."""
+    B, H, Sq, Sk = sp.B, sp.H, sp.Sq, sp.Sk
+    dev = sp.q[0].device
+    if not on_gpu(sp.q[0]):
+        q, k, v = (_view(b, c, B, S, H).float() for (b, c), S in ((sp.q, Sq), (sp.k, Sk), (sp.v, Sk)))
+        pr = _ref_probs(q, k, sp.kv_len, sp.causal, sp.scale)
+        s = torch.einsum("bqhd,bkhd->bhqk", q, k) * sp.scale
+        lse = torch.logsumexp(s.masked_fill(pr == 0, float("-inf")), -1)
+        if sp.p_drop > 0:
+            pr = pr * dropout_keep_mask(sp.seed, B, H, Sq, Sk, sp.p_drop) / (1 - sp.p_drop)
+        o = torch.einsum("bhqk,bkhd->bqhd", pr, v).reshape(B * Sq, H * HEAD_DIM)
+        return o.to(torch.bfloat16), lse
+    out = torch.empty(B * Sq, H * HEAD_DIM, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B, H, Sq, dtype=torch.float32, device=dev)
+    st = sp.strides() + [Sq * H * HEAD_DIM, H * HEAD_DIM]
+    lib().attn_fwd(sp.q[0], sp.q[1], sp.k[0], sp.k[1], sp.v[0], sp.v[1], out, lse, [B, H, Sq, Sk], st, sp.kv_len,
+                   sp.scale, sp.causal, sp.p_drop, sp.seed)
+    return out, lse
+
+
+def attention_bwd(sp: AttnSpec, out, dout, lse, dq, dk, dv):
+    """dq/dk/dv: (buf, col) views to write (e.g. column slices of a fused dQKV buffer)."""
+    B, H, Sq, Sk = sp.B, sp.H, sp.Sq, sp.Sk
+    if not on_gpu(out):
+        q, k, v = (_view(b, c, B, S, H).float().requires_grad_(True)
+                   for (b, c), S in ((sp.q, Sq), (sp.k, Sk), (sp.v, Sk)))
+        with torch.enable_grad():
+            pr = _ref_probs(q, k, sp.kv_len, sp.causal, sp.scale)
+            if sp.p_drop > 0:
+                pr = pr * dropout_keep_mask(sp.seed, B, H, Sq, Sk, sp.p_drop) / (1 - sp.p_drop)
+            o = torch.einsum("bhqk,bkhd->bqhd", pr, v)
+            gq, gk, gv = torch.autograd.grad(o, (q, k, v), dout.float().reshape(B, Sq, H, HEAD_DIM))
+        for (buf, col), g, S in ((dq, gq, Sq), (dk, gk, Sk), (dv, gv, Sk)):
+            _view(buf, col, B, S, H).copy_(g.to(torch.bfloat16))
+        return
+    delta = torch.empty(B, H, Sq, dtype=torch.float32, device=out.device)
+    st = sp.strides() + [Sq * H * HEAD_DIM, H * HEAD_DIM]
+    gst = []
+    for (buf, _), S in ((dq, Sq), (dk, Sk), (dv, Sk)):
+        rs = buf.shape[-1]
+        gst += [S * rs, rs]
+    lib().attn_bwd(sp.q[0], sp.q[1], sp.k[0], sp.k[1], sp.v[0], sp.v[1], out, dout, lse, delta, dq[0], dq[1], dk[0],
+                   dk[1], dv[0], dv[1], [B, H, Sq, Sk], st, gst, sp.kv_len, sp.scale, sp.causal, sp.p_drop, sp.seed)

@@ -27,11 +27,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: 256 ResNet, 64 BERT, 32 Transformer)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--graph", type=int, default=-1, help="capture step in a hipGraph (default: on for 1 GPU)")
     args = ap.parse_args()
+    if not args.batch:
+        args.batch = 256 if args.model.startswith("resnet") else (64 if args.model.startswith("bert") else 32)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -46,20 +48,29 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
-    from tensorflow_k8s_amd.models.resnet import ResNet, synthetic_imagenet
+    from tensorflow_k8s_amd.models import build_model, synthetic_batch
     from tensorflow_k8s_amd.parallel.mwms import MultiWorkerMirroredStrategy
-    from tensorflow_k8s_amd.runtime.optimizer import SGD
+    from tensorflow_k8s_amd.runtime.optimizer import LAMB, SGD, AdamW
     from tensorflow_k8s_amd.runtime.trainer import StepRunner
 
-    depth = int(args.model.replace("resnet", ""))
-    model = ResNet(depth).to(dev)
-    opt = SGD(model.arena, lr=0.1 * args.batch * world / 256, momentum=0.9, weight_decay=5e-5)
+    is_cnn = args.model.startswith("resnet")
+    model = build_model(args.model).to(dev)
+    if is_cnn:
+        opt = SGD(model.arena, lr=0.1 * args.batch * world / 256, momentum=0.9, weight_decay=5e-5)
+        opt_name = "SGD momentum 0.9 (fused HIP)"
+    elif args.model.startswith("bert"):
+        opt = LAMB(model.arena, lr=1e-4, weight_decay=0.01)
+        opt_name = "LAMB (fused HIP)"
+    else:
+        opt = AdamW(model.arena, lr=1e-4, b2=0.98, eps=1e-9, weight_decay=0.0)
+        opt_name = "Adam (fused HIP)"
     strat = MultiWorkerMirroredStrategy(model.arena, bucket_mb=args.bucket_mb)
     strat.configure_optimizer(opt)
     strat.broadcast_parameters()
-    x, y = synthetic_imagenet(args.batch, dev, seed=1000 + rank)
-    use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
-    runner = StepRunner(model, opt, strat, (x, y), use_graph=use_graph)
+    batch = synthetic_batch(model, args.batch, dev, seed=1000 + rank)
+    # dropout seeds advance per step on the host -> transformer steps stay eager
+    use_graph = (world == 1 and is_cnn) if args.graph < 0 else bool(args.graph)
+    runner = StepRunner(model, opt, strat, batch, use_graph=use_graph)
 
     for _ in range(args.warmup):
         runner.step()
@@ -83,7 +94,19 @@ def main():
     gb = args.batch * world
     value = gb / (ms / 1000.0)
     loss = runner.last_loss()
-    if rank == 0:
+    if rank == 0 and not is_cnn:
+        seq = model.cfg.seq_len if args.model.startswith("bert") else model.cfg.tgt_len
+        toks = gb * (seq if args.model.startswith("bert") else model.cfg.src_len + model.cfg.tgt_len)
+        print(json.dumps({
+            "metric": f"{args.model} training throughput (whole node)", "value": round(toks / (ms / 1000.0), 1),
+            "unit": "tokens/sec", "sequences_per_sec": round(value, 2), "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic token ids, random-init weights",
+            "config": {"model": args.model, "global_batch": gb, "seq_len": seq, "per_gpu_batch": args.batch,
+                       "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (RCCL all-reduce)",
+                       "optimizer": opt_name, "hipgraph": use_graph},
+            "loss": loss}), flush=True)
+    elif rank == 0:
         base = _baseline(world)
         print(json.dumps({
             "metric": "images/sec (whole node) ResNet-50 TFJob at 1/2/4/8 MI355X workers",
@@ -93,7 +116,7 @@ def main():
             "data": "synthetic (on-device ImageNet-shaped 224x224x3 bf16 batch, random-init weights)",
             "config": {"model": args.model, "global_batch": gb, "seq_len": None, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (RCCL all-reduce)",
-                       "optimizer": "SGD momentum 0.9 (fused HIP)", "hipgraph": use_graph},
+                       "optimizer": opt_name, "hipgraph": use_graph},
             "loss": loss,
         }), flush=True)
     if world > 1:

@@ -1,0 +1,296 @@
+"""Transformer (big / base) encoder-decoder for WMT-shaped translation (BASELINE config 5:
+"Transformer-big (WMT-shape) bf16/fp8 MFMA, 8-worker ring all-reduce TFJob").
+
+Follows tensor2tensor's transformer_big hparams: d_model 1024, 16 heads, FFN 4096 (ReLU), 6+6
+layers, pre-LayerNorm residual blocks ("n" preprocess, "da" postprocess), sinusoidal timing
+signal, ONE shared embedding matrix for source, target and the softmax (scaled by sqrt(d)),
+label smoothing 0.1, dropouts 0.3 (residual) / 0.1 (attention, relu). Attention projections have
+no bias (as in T2T). TF variable names mirror T2T's ("transformer/body/encoder/layer_0/
+self_attention/multihead_attention/q/kernel", ...), so checkpoints map name-for-name.
+
+MI355X mapping as in models/bert.py: fused q|k|v (self-attention) and k|v (encoder-decoder
+attention, computed from the encoder memory) GEMMs, flash attention (causal for decoder self
+attention; cross attention with Sq != Sk), dropout + residual in GEMM epilogues, the ReLU mask
+applied in the FFN2 dgrad epilogue from the saved pre-activation.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from ..ops import elementwise as E
+from ..ops import gemm as G
+from ..ops import transformer as TR
+from ..ops.loss import softmax_xent
+from ..runtime.arena import ParamArena
+from ..runtime.layers import Embedding, FusedLinear, LayerNorm, Linear
+from .bert import _mix
+
+
+@dataclass
+class TransformerConfig:
+    vocab_size: int = 33708  # t2t translate_ende_wmt32k shared subword vocabulary
+    hidden: int = 1024
+    enc_layers: int = 6
+    dec_layers: int = 6
+    heads: int = 16
+    ffn: int = 4096
+    dropout: float = 0.3
+    attn_dropout: float = 0.1
+    relu_dropout: float = 0.1
+    label_smoothing: float = 0.1
+    ln_eps: float = 1e-6
+    src_len: int = 256
+    tgt_len: int = 256
+    max_len: int = 1024
+
+    @classmethod
+    def big(cls):
+        return cls()
+
+    @classmethod
+    def base(cls):
+        return cls(hidden=512, heads=8, ffn=2048, dropout=0.1)
+
+    @classmethod
+    def tiny(cls):  # tests
+        return cls(vocab_size=500, hidden=128, enc_layers=2, dec_layers=2, heads=2, ffn=256, src_len=24, tgt_len=20,
+                   max_len=64)
+
+
+def timing_signal(length: int, channels: int) -> torch.Tensor:
+    """tensor2tensor get_timing_signal_1d: [sin(p*inv_ts) | cos(p*inv_ts)], half the channels each."""
+    half = channels // 2
+    log_inc = math.log(1.0e4) / max(half - 1, 1)
+    inv = torch.exp(torch.arange(half, dtype=torch.float64) * -log_inc)
+    t = torch.arange(length, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.cat([torch.sin(t), torch.cos(t)], 1).float()
+
+
+class _Attn:
+    """Self attention (fused q|k|v) or encoder-decoder attention (q from x, fused k|v from memory)."""
+
+    def __init__(self, arena, pre: str, W: int, cross: bool):
+        self.cross = cross
+        base = f"{pre}/multihead_attention"
+        self.names = {n: f"{base}/{n}" for n in "qkv"}
+        if cross:
+            self.q = Linear(arena, self.names["q"], W, W, bias=False, init="trunc_normal", std=W ** -0.5)
+            self.kv = FusedLinear(arena, [self.names["k"], self.names["v"]], W, W, bias=False, std=W ** -0.5)
+        else:
+            self.qkv = FusedLinear(arena, [self.names[n] for n in "qkv"], W, W, bias=False, std=W ** -0.5)
+        self.out = Linear(arena, f"{base}/output_transform", W, W, bias=False, init="trunc_normal", std=W ** -0.5)
+
+
+class EncoderLayer:
+    def __init__(self, arena: ParamArena, cfg: TransformerConfig, pre: str):
+        W = cfg.hidden
+        self.cfg = cfg
+        self.ln1 = LayerNorm(arena, f"{pre}/self_attention/layer_prepostprocess/layer_norm", W, cfg.ln_eps,
+                             ("layer_norm_scale", "layer_norm_bias"))
+        self.att = _Attn(arena, f"{pre}/self_attention", W, cross=False)
+        self.ln2 = LayerNorm(arena, f"{pre}/ffn/layer_prepostprocess/layer_norm", W, cfg.ln_eps,
+                             ("layer_norm_scale", "layer_norm_bias"))
+        self.ff1 = Linear(arena, f"{pre}/ffn/conv1", W, cfg.ffn, init="trunc_normal", std=W ** -0.5)
+        self.ff2 = Linear(arena, f"{pre}/ffn/conv2", cfg.ffn, W, init="trunc_normal", std=cfg.ffn ** -0.5)
+        self.ffn_ln = self.ln2
+        self.saved = None
+
+    def _self_attn(self, x, B, S, kv_len, causal, seed, training):
+        cfg = self.cfg
+        a, st1 = self.ln1.forward(x)
+        qkv = self.att.qkv.forward(a)
+        n = self.att.names
+        sp = TR.AttnSpec(B, cfg.heads, S, S, (qkv, self.att.qkv.col(n["q"])), (qkv, self.att.qkv.col(n["k"])),
+                         (qkv, self.att.qkv.col(n["v"])), kv_len=kv_len, causal=causal,
+                         p_drop=cfg.attn_dropout if training else 0.0, seed=_mix(seed, 1))
+        o, lse = TR.attention_fwd(sp)
+        x1 = self.att.out.forward(o, resid=x, drop_p=cfg.dropout if training else 0.0, drop_seed=_mix(seed, 2))
+        return x1, (x, a, st1, qkv, sp, o, lse)
+
+    def _self_attn_bwd(self, dx1, saved, seed, training):
+        x, a, st1, qkv, sp, o, lse = saved
+        n = self.att.names
+        do = self.att.out.backward(E.dropout(dx1, self.cfg.dropout if training else 0.0, _mix(seed, 2)), o)
+        dqkv = torch.empty_like(qkv)
+        TR.attention_bwd(sp, o, do, lse, (dqkv, self.att.qkv.col(n["q"])), (dqkv, self.att.qkv.col(n["k"])),
+                         (dqkv, self.att.qkv.col(n["v"])))
+        da = self.att.qkv.backward(dqkv, a)
+        return self.ln1.backward(da, x, st1, dres=dx1)
+
+    def _ffn(self, x, seed, training):
+        cfg = self.cfg
+        b, st = self.ffn_ln.forward(x)
+        z = torch.empty(b.shape[0], cfg.ffn, dtype=torch.bfloat16, device=x.device)
+        f = self.ff1.forward(b, act="relu", aux=z, drop_p=cfg.relu_dropout if training else 0.0,
+                             drop_seed=_mix(seed, 5))
+        x2 = self.ff2.forward(f, resid=x, drop_p=cfg.dropout if training else 0.0, drop_seed=_mix(seed, 6))
+        return x2, (x, b, st, z, f)
+
+    def _ffn_bwd(self, dx2, saved, seed, training):
+        cfg = self.cfg
+        x, b, st, z, f = saved
+        dy = E.dropout(dx2, cfg.dropout if training else 0.0, _mix(seed, 6))
+        dfz = self.ff2.backward(dy, f, dact_src=z, dact="relu")
+        dz = E.dropout(dfz, cfg.relu_dropout if training else 0.0, _mix(seed, 5))
+        db = self.ff1.backward(dz, b)
+        return self.ffn_ln.backward(db, x, st, dres=dx2)
+
+    def forward(self, x, B, S, kv_len, seed, training):
+        x1, s1 = self._self_attn(x, B, S, kv_len, False, seed, training)
+        x2, s2 = self._ffn(x1, seed, training)
+        self.saved = (s1, s2, seed, training) if training else None
+        return x2
+
+    def backward(self, dx2):
+        s1, s2, seed, training = self.saved
+        self.saved = None
+        dx1 = self._ffn_bwd(dx2, s2, seed, training)
+        return self._self_attn_bwd(dx1, s1, seed, training)
+
+
+class DecoderLayer(EncoderLayer):
+    def __init__(self, arena: ParamArena, cfg: TransformerConfig, pre: str):
+        W = cfg.hidden
+        self.cfg = cfg
+        self.ln1 = LayerNorm(arena, f"{pre}/self_attention/layer_prepostprocess/layer_norm", W, cfg.ln_eps,
+                             ("layer_norm_scale", "layer_norm_bias"))
+        self.att = _Attn(arena, f"{pre}/self_attention", W, cross=False)
+        self.ln2 = LayerNorm(arena, f"{pre}/encdec_attention/layer_prepostprocess/layer_norm", W, cfg.ln_eps,
+                             ("layer_norm_scale", "layer_norm_bias"))
+        self.xatt = _Attn(arena, f"{pre}/encdec_attention", W, cross=True)
+        self.ln3 = LayerNorm(arena, f"{pre}/ffn/layer_prepostprocess/layer_norm", W, cfg.ln_eps,
+                             ("layer_norm_scale", "layer_norm_bias"))
+        self.ff1 = Linear(arena, f"{pre}/ffn/conv1", W, cfg.ffn, init="trunc_normal", std=W ** -0.5)
+        self.ff2 = Linear(arena, f"{pre}/ffn/conv2", cfg.ffn, W, init="trunc_normal", std=cfg.ffn ** -0.5)
+        self.ffn_ln = self.ln3
+        self.saved = None
+
+    def forward(self, y, mem, B, St, Ss, src_len, seed, training):
+        cfg = self.cfg
+        y1, s1 = self._self_attn(y, B, St, None, True, seed, training)
+        c, st2 = self.ln2.forward(y1)
+        q = self.xatt.q.forward(c)
+        kv = self.xatt.kv.forward(mem)
+        n = self.xatt.names
+        sp = TR.AttnSpec(B, cfg.heads, St, Ss, (q, 0), (kv, self.xatt.kv.col(n["k"])), (kv, self.xatt.kv.col(n["v"])),
+                         kv_len=src_len, p_drop=cfg.attn_dropout if training else 0.0, seed=_mix(seed, 3))
+        o2, lse2 = TR.attention_fwd(sp)
+        y2 = self.xatt.out.forward(o2, resid=y1, drop_p=cfg.dropout if training else 0.0, drop_seed=_mix(seed, 4))
+        y3, s3 = self._ffn(y2, seed, training)
+        self.saved = (s1, (y1, c, st2, q, kv, sp, o2, lse2), s3, seed, training) if training else None
+        return y3
+
+    def backward(self, dy3, mem, dmem):
+        """Returns dy; accumulates this layer's encoder-memory gradient into dmem (in place)."""
+        s1, s2, s3, seed, training = self.saved
+        self.saved = None
+        cfg = self.cfg
+        dy2 = self._ffn_bwd(dy3, s3, seed, training)
+        y1, c, st2, q, kv, sp, o2, lse2 = s2
+        n = self.xatt.names
+        do2 = self.xatt.out.backward(E.dropout(dy2, cfg.dropout if training else 0.0, _mix(seed, 4)), o2)
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        TR.attention_bwd(sp, o2, do2, lse2, (dq, 0), (dkv, self.xatt.kv.col(n["k"])), (dkv, self.xatt.kv.col(n["v"])))
+        dmem.copy_(self.xatt.kv.backward(dkv, mem, resid=dmem))
+        dc = self.xatt.q.backward(dq, c)
+        dy1 = self.ln2.backward(dc, y1, st2, dres=dy2)
+        return self._self_attn_bwd(dy1, s1, seed, training)
+
+
+class Transformer:
+    def __init__(self, cfg: TransformerConfig | None = None):
+        cfg = cfg or TransformerConfig.big()
+        if cfg.hidden != cfg.heads * TR.HEAD_DIM:
+            raise ValueError("tfk attention kernels use head_dim 64: hidden must equal heads*64")
+        self.cfg = cfg
+        self.name = {1024: "transformer-big", 512: "transformer-base"}.get(cfg.hidden, "transformer")
+        self.num_classes = cfg.vocab_size
+        self.training = True
+        self.step = 0
+        W = cfg.hidden
+        a = self.arena = ParamArena()
+        self.emb = Embedding(a, f"transformer/symbol_modality_{cfg.vocab_size}_{W}/shared/weights", cfg.vocab_size, W,
+                             std=W ** -0.5)
+        self.enc = [EncoderLayer(a, cfg, f"transformer/body/encoder/layer_{i}") for i in range(cfg.enc_layers)]
+        self.enc_ln = LayerNorm(a, "transformer/body/encoder/layer_prepostprocess/layer_norm", W, cfg.ln_eps,
+                                ("layer_norm_scale", "layer_norm_bias"))
+        self.dec = [DecoderLayer(a, cfg, f"transformer/body/decoder/layer_{i}") for i in range(cfg.dec_layers)]
+        self.dec_ln = LayerNorm(a, "transformer/body/decoder/layer_prepostprocess/layer_norm", W, cfg.ln_eps,
+                                ("layer_norm_scale", "layer_norm_bias"))
+        self._pos = None
+
+    def to(self, device, seed: int = 1234):
+        self.arena.finalize(device, seed)
+        self._pos = timing_signal(self.cfg.max_len, self.cfg.hidden).to(torch.bfloat16).to(device)
+        return self
+
+    def train(self, mode: bool = True):
+        self.training = mode
+        return self
+
+    def _embed(self, ids, S, seed, training):
+        cfg = self.cfg
+        x = TR.embedding_fwd(ids, self.emb.table.compute, self._pos, S, scale=math.sqrt(cfg.hidden))
+        return E.dropout(x, cfg.dropout if training else 0.0, seed)
+
+    def _forward(self, src, tgt_in, src_len, B, Ss, St, seed, training):
+        x = self._embed(src, Ss, _mix(seed, 0xE0), training)
+        for i, layer in enumerate(self.enc):
+            x = layer.forward(x, B, Ss, src_len, _mix(seed, 100 + i), training)
+        mem, st_m = self.enc_ln.forward(x)
+        y = self._embed(tgt_in, St, _mix(seed, 0xE1), training)
+        for i, layer in enumerate(self.dec):
+            y = layer.forward(y, mem, B, St, Ss, src_len, _mix(seed, 200 + i), training)
+        yo, st_y = self.dec_ln.forward(y)
+        logits = G.linear_fwd(yo, self.emb.table.compute)  # tied softmax weights
+        return logits, (x, mem, st_m, y, yo, st_y)
+
+    def forward_backward(self, src, tgt_in, tgt_out, src_len, loss_scale: float = 1.0):
+        cfg = self.cfg
+        B = src_len.shape[0]
+        Ss, St = src.numel() // B, tgt_in.numel() // B
+        self.step += 1
+        seed = _mix(0x7EA, self.step)
+        tr = self.training
+        logits, (x, mem, st_m, y, yo, st_y) = self._forward(src, tgt_in, src_len, B, Ss, St, seed, tr)
+        loss, dlogits, corr = softmax_xent(logits, tgt_out, smoothing=cfg.label_smoothing,
+                                           scale=loss_scale / tgt_out.numel(), want_correct=True, V=cfg.vocab_size)
+        G.linear_wgrad(dlogits, yo, self.emb.table.grad)  # first writer of the shared table's grad
+        dyo = G.linear_dgrad(dlogits, self.emb.table.compute)
+        dy = self.dec_ln.backward(dyo, y, st_y)
+        dmem = torch.zeros_like(mem)
+        for layer in reversed(self.dec):
+            dy = layer.backward(dy, mem, dmem)
+        scale = math.sqrt(cfg.hidden)
+        TR.embedding_bwd(tgt_in, E.dropout(dy, cfg.dropout if tr else 0.0, _mix(seed, 0xE1)), self.emb.table.grad,
+                         None, St, scale=scale)
+        dx = self.enc_ln.backward(dmem, x, st_m)
+        for layer in reversed(self.enc):
+            dx = layer.backward(dx)
+        TR.embedding_bwd(src, E.dropout(dx, cfg.dropout if tr else 0.0, _mix(seed, 0xE0)), self.emb.table.grad,
+                         None, Ss, scale=scale)
+        self.arena.grad_ready(self.emb.table)
+        return loss.view(B, St).mean(1), corr
+
+    def evaluate(self, src, tgt_in, tgt_out, src_len):
+        B = src_len.shape[0]
+        logits, _ = self._forward(src, tgt_in, src_len, B, src.numel() // B, tgt_in.numel() // B, 0, False)
+        loss, _, corr = softmax_xent(logits, tgt_out, want_grad=False, want_correct=True, V=self.cfg.vocab_size)
+        return float(loss.sum()), float(corr.sum()), int(corr.numel())
+
+    def synthetic_batch(self, batch: int, device, seed: int = 0, seq_len: int | None = None, **_):
+        """WMT-shaped synthetic batch: full-length source/target token ids (shifted target)."""
+        cfg = self.cfg
+        Ss = seq_len or cfg.src_len
+        St = seq_len or cfg.tgt_len
+        g = torch.Generator().manual_seed(seed)
+        src = torch.randint(2, cfg.vocab_size, (batch, Ss), generator=g, dtype=torch.int32)
+        tgt = torch.randint(2, cfg.vocab_size, (batch, St + 1), generator=g, dtype=torch.int32)
+        tgt[:, 0] = 0
+        src_len = torch.full((batch,), Ss, dtype=torch.int32)
+        return tuple(t.contiguous().to(device) for t in (src.reshape(-1), tgt[:, :-1].reshape(-1),
+                                                       tgt[:, 1:].reshape(-1), src_len))

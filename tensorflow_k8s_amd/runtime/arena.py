@@ -145,6 +145,15 @@ class ParamArena:
     def nodecay_region(self):
         return self.n_decay, self.numel
 
+    def span(self, params: list[Param]) -> tuple[int, int]:
+        """[lo, hi) of params that are laid out back-to-back (e.g. q/k/v kernels registered
+        consecutively -> one fused [3*W, W] GEMM weight). Raises if they are not contiguous."""
+        ps = sorted(params, key=lambda p: p.offset)
+        for a, b in zip(ps, ps[1:]):
+            if a.offset + a.numel != b.offset:
+                raise ValueError(f"{a.name} and {b.name} are not contiguous in the arena")
+        return ps[0].offset, ps[-1].offset + ps[-1].numel
+
     def num_parameters(self) -> int:
         return sum(p.numel for p in self.params)
 
@@ -165,6 +174,10 @@ def _init_raw(spec: ParamSpec, gen: torch.Generator) -> torch.Tensor:
         return torch.ones(shape)
     if spec.init == "normal":
         return torch.randn(shape, generator=gen) * spec.std
+    if spec.init == "trunc_normal":  # TF truncated_normal_initializer (BERT, Transformer)
+        t = torch.empty(shape)
+        torch.nn.init.trunc_normal_(t, 0.0, spec.std, -2 * spec.std, 2 * spec.std, generator=gen)
+        return t
     if spec.init == "he_normal":
         return torch.randn(shape, generator=gen) * math.sqrt(2.0 / max(spec.fan_in, 1))
     if spec.init == "xavier_uniform":

@@ -16,8 +16,13 @@ import torch
 
 def evaluate(model, batches) -> dict:
     from ..ops.loss import softmax_xent
-    model.train(False)
     tot_loss, tot_corr, n = 0.0, 0.0, 0
+    if hasattr(model, "evaluate"):  # sequence models: (loss sum, hits, predictions) per batch
+        for b in batches:
+            l_, c_, n_ = model.evaluate(*b)
+            tot_loss, tot_corr, n = tot_loss + l_, tot_corr + c_, n + n_
+        return {"loss": tot_loss / max(n, 1), "accuracy": tot_corr / max(n, 1), "examples": n}
+    model.train(False)
     for x, y in batches:
         logits = model.forward(x)
         loss, _, corr = softmax_xent(logits, y, want_grad=False, want_correct=True)

@@ -11,6 +11,7 @@ import torch
 
 from ..ops import gemm as G
 from ..ops import norm as BN
+from ..ops import transformer as TR
 from .arena import ParamArena, ParamSpec
 
 
@@ -129,10 +130,13 @@ class Linear:
         self.b = arena.add(ParamSpec(f"{name}/bias", (fout,), init="zeros", decay=False)) if bias else None
         self.arena = arena
 
-    def forward(self, x, act=None, resid=None):
-        return G.linear_fwd(x, self.w.compute, self.b.master if self.b else None, act=act, resid=resid)
+    def forward(self, x, act=None, resid=None, aux=None, drop_p: float = 0.0, drop_seed: int = 0):
+        return G.linear_fwd(x, self.w.compute, self.b.master if self.b else None, act=act, resid=resid, aux=aux,
+                            drop_p=drop_p, drop_seed=drop_seed)
 
-    def backward(self, dy, x, need_dx: bool = True, resid=None, accumulate: bool = False):
+    def backward(self, dy, x, need_dx: bool = True, resid=None, accumulate: bool = False, dact_src=None,
+                 dact=None):
+        """dy: gradient of this layer's (pre-dropout, post-activation-backward) output."""
         G.linear_wgrad(dy, x, self.w.grad, accumulate=accumulate)
         if self.b is not None:
             G.bias_grad(dy, self.b.grad, accumulate=accumulate)
@@ -141,4 +145,96 @@ class Linear:
             self.arena.grad_ready(self.w)
         if not need_dx:
             return None
-        return G.linear_dgrad(dy, self.w.compute, resid=resid)
+        return G.linear_dgrad(dy, self.w.compute, resid=resid, dact_src=dact_src, dact=dact)
+
+
+class FusedLinear:
+    """Several TF dense layers sharing one input, run as ONE GEMM (e.g. BERT's query/key/value ->
+    a [3W, W] weight, 3x fewer launches and a 3x wider N for MFMA occupancy). Each part keeps its
+    own TF variables (<name>/kernel [in, out], <name>/bias); registration back-to-back makes
+    the arena place them contiguously (in reverse registration order: see ``cols``)."""
+
+    def __init__(self, arena: ParamArena, names: list[str], fin: int, fout: int, init: str = "trunc_normal",
+                 std: float = 0.02, bias: bool = True):
+        self.arena, self.fin, self.fout, self.names = arena, fin, fout, names
+        self.parts = [Linear(arena, n, fin, fout, init=init, std=std, bias=bias) for n in names]
+        self.has_bias = bias
+        self._views = None
+
+    def _build(self):
+        a = self.arena
+        lo, hi = a.span([p.w for p in self.parts])
+        order = sorted(range(len(self.parts)), key=lambda i: self.parts[i].w.offset)
+        self.cols = {self.names[i]: k * self.fout for k, i in enumerate(order)}
+        n = len(self.parts) * self.fout
+        bm = bg = None
+        if self.has_bias:
+            blo, bhi = a.span([p.b for p in self.parts])
+            if sorted(range(len(self.parts)), key=lambda i: self.parts[i].b.offset) != order:
+                raise ValueError("fused bias order differs from kernel order")
+            bm, bg = a.master[blo:bhi], a.grad[blo:bhi]
+        self._views = (a.compute[lo:hi].view(n, self.fin), a.grad[lo:hi].view(n, self.fin), bm, bg)
+
+    def views(self):
+        if self._views is None:
+            self._build()
+        return self._views
+
+    def col(self, name: str) -> int:
+        self.views()
+        return self.cols[name]
+
+    def forward(self, x, act=None):
+        w, _, b, _ = self.views()
+        return G.linear_fwd(x, w, b, act=act)
+
+    def backward(self, dy, x, need_dx: bool = True, resid=None):
+        w, gw, _, gb = self.views()
+        G.linear_wgrad(dy, x, gw)
+        if gb is not None:
+            G.bias_grad(dy, gb)
+        self.arena.grad_ready(*[p.w for p in self.parts], *[p.b for p in self.parts if p.b is not None])
+        if not need_dx:
+            return None
+        return G.linear_dgrad(dy, w, resid=resid)
+
+
+class LayerNorm:
+    """TF variables <name>/gamma, <name>/beta (f32, no weight decay)."""
+
+    def __init__(self, arena: ParamArena, name: str, W: int, eps: float = 1e-12, names=("gamma", "beta")):
+        self.W, self.eps, self.arena = W, eps, arena
+        self.gamma = arena.add(ParamSpec(f"{name}/{names[0]}", (W,), init="ones", decay=False))
+        self.beta = arena.add(ParamSpec(f"{name}/{names[1]}", (W,), init="zeros", decay=False))
+
+    def forward(self, x):
+        y, mu, rs = TR.layernorm_fwd(x, self.gamma.master, self.beta.master, self.eps)
+        return y, (mu, rs)
+
+    def backward(self, dy, x, stats, dres=None):
+        """dx = LN'(x)^T dy (+ dres: gradient arriving through a residual connection)."""
+        mu, rs = stats
+        dx = TR.layernorm_bwd(dy, x, self.gamma.master, mu, rs, self.gamma.grad, self.beta.grad, dres=dres)
+        self.arena.grad_ready(self.gamma, self.beta)
+        return dx
+
+
+def _pad_rows(rows: int, to: int = 64) -> int:
+    return (rows + to - 1) // to * to
+
+
+class Embedding:
+    """Token embedding table [V, W] stored with V padded to a multiple of 64 rows (padding rows
+    stay zero; the TF variable is the real [V, W] table). Also used as the tied output
+    projection (logits = h @ table^T over the padded vocab, masked to V by the loss)."""
+
+    def __init__(self, arena: ParamArena, name: str, V: int, W: int, std: float = 0.02, decay: bool = True):
+        self.V, self.Vp, self.W = V, _pad_rows(V), W
+
+        def post(t, V=V):
+            t[V:] = 0
+            return t
+        self.table = arena.add(ParamSpec(name, (self.Vp, W), init="trunc_normal", std=std, decay=decay,
+                                         post_init=post, tf_shape=(V, W), to_tf=lambda a, V=V: a[:V],
+                                         from_tf=lambda a, Vp=self.Vp: np.concatenate(
+                                             [a, np.zeros((Vp - a.shape[0], a.shape[1]), a.dtype)])))

@@ -122,7 +122,7 @@ bool FieldSelector::matches(const Json& obj) const {
 // ------------------------------------------------------------------------------ watcher
 bool Watcher::next(WatchEvent* ev, int64_t timeout_ms) {
   std::unique_lock<std::mutex> l(mu_);
-  cv_.wait_for(l, std::chrono::milliseconds(timeout_ms), [&] { return !q_.empty() || closed_; });
+  cv_wait_ms(cv_, l, timeout_ms, [&] { return !q_.empty() || closed_; });
   if (q_.empty()) return false;
   *ev = q_.front();
   q_.pop_front();

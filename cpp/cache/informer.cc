@@ -119,7 +119,7 @@ void DeltaFIFO::add(DeltaType t, const std::string& key, const Json& obj) {
 
 bool DeltaFIFO::pop(std::string* key, std::vector<Delta>* deltas, int64_t timeout_ms) {
   std::unique_lock<std::mutex> l(mu_);
-  cv_.wait_for(l, std::chrono::milliseconds(timeout_ms), [&] { return !queue_.empty() || closed_; });
+  cv_wait_ms(cv_, l, timeout_ms, [&] { return !queue_.empty() || closed_; });
   if (queue_.empty()) return false;
   *key = queue_.front();
   queue_.pop_front();

@@ -125,7 +125,7 @@ class RestWatch : public WatchStream {
   }
   bool next(WatchEvent* ev, int64_t timeout_ms) override {
     std::unique_lock<std::mutex> l(mu_);
-    cv_.wait_for(l, std::chrono::milliseconds(timeout_ms), [&] { return !q_.empty() || done_; });
+    cv_wait_ms(cv_, l, timeout_ms, [&] { return !q_.empty() || done_; });
     if (q_.empty()) return false;
     *ev = q_.front();
     q_.pop_front();

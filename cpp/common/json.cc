@@ -13,6 +13,19 @@ const std::string& Json::as_string() const {
   return t_ == String ? s_ : empty;
 }
 
+Json::Json(const Json& o) : t_(o.t_), b_(o.b_), n_(o.n_), s_(o.s_) {
+  if (o.a_) a_ = std::make_shared<array_t>(*o.a_);
+  if (o.o_) o_ = std::make_shared<object_t>(*o.o_);
+}
+
+Json& Json::operator=(const Json& o) {
+  if (this != &o) {
+    Json tmp(o);
+    *this = std::move(tmp);
+  }
+  return *this;
+}
+
 void Json::ensure_unique() {
   if (t_ == Array && a_ && a_.use_count() > 1) a_ = std::make_shared<array_t>(*a_);
   if (t_ == Object && o_ && o_.use_count() > 1) o_ = std::make_shared<object_t>(*o_);
@@ -84,18 +97,6 @@ const Json& Json::path(const std::string& dotted) const {
     start = dot + 1;
   }
   return *cur;
-}
-
-Json Json::clone() const {
-  Json r = *this;
-  if (t_ == Array) {
-    r.a_ = std::make_shared<array_t>();
-    for (auto& v : *a_) r.a_->push_back(v.clone());
-  } else if (t_ == Object) {
-    r.o_ = std::make_shared<object_t>();
-    for (auto& kv : *o_) (*r.o_)[kv.first] = kv.second.clone();
-  }
-  return r;
 }
 
 bool Json::operator==(const Json& o) const {

@@ -18,6 +18,14 @@ class Json {
 
   Json() : t_(Null) {}
   Json(std::nullptr_t) : t_(Null) {}
+  // Value semantics with DEEP copies: no storage is ever shared between two Json values, so a
+  // copy handed to another thread (informer caches, watch fan-out, work queues) can never race
+  // with its source (copy-on-write sharing is a data race under the C++ memory model: the
+  // use_count() probe has no acquire ordering). Moves stay O(1).
+  Json(const Json& o);
+  Json(Json&& o) noexcept = default;
+  Json& operator=(const Json& o);
+  Json& operator=(Json&& o) noexcept = default;
   Json(bool b) : t_(Bool), b_(b) {}
   Json(int v) : t_(Number), n_(v) {}
   Json(long v) : t_(Number), n_((double)v) {}
@@ -70,7 +78,7 @@ class Json {
   const Json& path(const std::string& dotted) const;
 
   std::string dump(int indent = -1) const;
-  Json clone() const;  // deep copy (values share storage otherwise)
+  Json clone() const { return *this; }  // copies are deep (kept for call-site clarity)
 
   bool operator==(const Json& o) const;
   bool operator!=(const Json& o) const { return !(*this == o); }

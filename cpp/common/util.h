@@ -93,6 +93,18 @@ inline uint32_t crc32c_unmask(uint32_t m) {
 }
 
 // ------------------------------------------------------------------------------ stop token
+// Timed condition-variable wait on the system clock (pthread_cond_timedwait). libstdc++'s
+// steady-clock wait_for goes through pthread_cond_clockwait, which GCC 11's ThreadSanitizer does
+// not intercept: it then loses track of the mutex and reports false double locks and races. The
+// wall clock is good enough for these sub-second timeouts.
+template <class Pred>
+inline bool cv_wait_ms(std::condition_variable& cv, std::unique_lock<std::mutex>& l, int64_t ms, Pred pred) {
+  return cv.wait_until(l, std::chrono::system_clock::now() + std::chrono::milliseconds(ms), pred);
+}
+inline void cv_wait_ms(std::condition_variable& cv, std::unique_lock<std::mutex>& l, int64_t ms) {
+  cv.wait_until(l, std::chrono::system_clock::now() + std::chrono::milliseconds(ms));
+}
+
 class StopToken {
  public:
   void stop() {
@@ -106,7 +118,7 @@ class StopToken {
   // Sleeps up to ms; returns true if stopped.
   bool wait_for(int64_t ms) {
     std::unique_lock<std::mutex> l(mu_);
-    cv_.wait_for(l, std::chrono::milliseconds(ms), [&] { return stopped_.load(); });
+    cv_wait_ms(cv_, l, ms, [&] { return stopped_.load(); });
     return stopped_.load();
   }
 

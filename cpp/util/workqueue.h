@@ -204,7 +204,7 @@ class RateLimitingQueue {
         add_locked(top.second);
         continue;
       }
-      delay_cv_.wait_for(l, std::chrono::milliseconds(top.first - now));
+      cv_wait_ms(delay_cv_, l, top.first - now);
     }
   }
   std::string name_;

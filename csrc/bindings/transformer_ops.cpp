@@ -85,12 +85,16 @@ void embedding_bwd(torch::Tensor ids, torch::Tensor dy, torch::Tensor dword, c10
   need_numel(dy, ntok * W, "dy");
   const int V = (int)(dword.numel() / W);
   TORCH_CHECK(V >= 1, "dword");
-  if (dpos.has_value() && dpos->defined()) { need_f32(*dpos, "dpos"); need_numel(*dpos, S * W, "dpos"); }
+  if (dpos.has_value() && dpos->defined()) {
+    need_f32(*dpos, "dpos"); need_numel(*dpos, S * W, "dpos");
+    TORCH_CHECK(S >= 1 && ntok % S == 0, "tokens must be a multiple of S");
+  }
   int T = 0;
   if (dtype.has_value() && dtype->defined()) {
     need_f32(*dtype, "dtype"); TORCH_CHECK(tt.has_value() && tt->defined(), "type grads need type ids");
     need(*tt, at::kInt, "type ids"); need_numel(*tt, ntok, "type ids");
     T = (int)(dtype->numel() / W);
+    TORCH_CHECK(T >= 1 && T <= 4, "at most 4 token types");
   }
   check_rc(tfk_embedding_bwd(ids.data_ptr<int>(), dy.data_ptr(), V, dword.data_ptr<float>(), opt_ptr<float>(dpos),
                              (int)S, opt_ptr<const int>(tt), opt_ptr<float>(dtype), T, ntok, (int)W, (float)scale,

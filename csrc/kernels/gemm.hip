@@ -24,7 +24,10 @@ namespace tfk {
 
 enum AMode { A_KIN = 0, A_KOUT = 1, A_CONV_FWD = 2, A_CONV_DGRAD = 3 };
 enum BMode { B_KIN = 0, B_KOUT = 1, B_CONV_WGRAD = 2 };
-enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1 };
+// BNR: + fused BN-backward reduction; EXT: + aux (pre-activation) store, activation-backward
+// multiplier and dropout. Separate instantiations keep the common epilogue small enough to unroll
+// fully (a rolled epilogue indexes the accumulators dynamically -> they go to scratch).
+enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1, EPI_BF16_BNR = 2, EPI_BF16_EXT = 3 };
 
 // GemmParams lives in gemm_params.h (shared with the host bindings).
 
@@ -45,14 +48,18 @@ template <int ROWS>
 __device__ __forceinline__ int kout_off(int krow, int rc) { return krow * (ROWS * 2) + ((rc ^ swz_kout<ROWS>(krow)) << 4); }
 
 // Predicated scalar load of up to 8 consecutive bf16 (ragged tails / unaligned leading dims).
+// Built from constant-index register words: a union/array indexed by a loop variable would be
+// placed in scratch memory and drag the whole register-staged tile through it.
 __device__ __forceinline__ u32x4 load_partial(const bf16* src, int valid, int stride) {
-  union { u32x4 v; unsigned short h[8]; } u;
-  u.v = u32x4{0u, 0u, 0u, 0u};
   const unsigned short* s = (const unsigned short*)src;
+  unsigned int w[4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e)
-    if (e < valid) u.h[e] = s[e * stride];
-  return u.v;
+  for (int q = 0; q < 4; ++q) {
+    const unsigned int lo = (2 * q < valid) ? (unsigned int)s[(2 * q) * stride] : 0u;
+    const unsigned int hi = (2 * q + 1 < valid) ? (unsigned int)s[(2 * q + 1) * stride] : 0u;
+    w[q] = lo | (hi << 16);
+  }
+  return u32x4{w[0], w[1], w[2], w[3]};
 }
 
 // Per-operand loader state. ROWS = tile rows of this operand (BM for A, BN for B).
@@ -337,35 +344,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int mloc = wm * (BM / 2) + i * 16 + ml;
-        const int mg = m0 + mloc, ng = n0 + nloc;
-        const bool full = mg < p.M && ng + 3 < p.N && (p.ldc & 3) == 0;
-        const long long goff = bz * p.sC + (long long)mg * p.ldc + ng;
-        float dz[4] = {1.f, 1.f, 1.f, 1.f};
-        if (p.dact_src && mg < p.M) {
-          const bf16* zs = (const bf16*)p.dact_src + goff;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float z = ng + r < p.N ? bf2f(zs[r]) : 0.f;
-            dz[r] = act_grad(z, p.dact);
-          }
-        }
-        bf16x4 o, pre;
+        bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = (acc[i][j][r] * p.alpha + bv[r]) * dz[r];
-          pre[r] = f2bf(v);
-          v = act_apply(v, p.act);
-          if (p.drop_p > 0.f && mg < p.M)
-            v = u01(hash_u32(p.drop_seed, (unsigned long long)mg * p.N + ng + r)) < 1.f - p.drop_p ? v * p.drop_scale : 0.f;
+          float v = acc[i][j][r] * p.alpha + bv[r];
+          if constexpr (EPI != EPI_BF16_EXT) v = act_apply(v, p.act);  // EXT: in the store pass
           csum[j][r] += v;
           csq[j][r] += v * v;
           o[r] = f2bf(v);
-        }
-        if (p.aux && mg < p.M) {
-          bf16* ad = (bf16*)p.aux + goff;
-          if (full) *(bf16x4*)ad = pre;
-          else
-            for (int r = 0; r < 4 && ng + r < p.N; ++r) ad[r] = pre[r];
         }
         *(bf16x4*)(Cs + mloc * LDC_S + nloc) = o;
       }
@@ -387,10 +373,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
     __syncthreads();
     bf16* C = (bf16*)p.C + bz * p.sC;
     constexpr int CPR = BN / 8, TOT = BM * CPR;
-    const bool bnr = p.bn_sums != nullptr;
+    constexpr bool bnr = (EPI == EPI_BF16_BNR);
     const int ccol = tid % CPR;  // this thread's 8-column chunk (fixed: NT % CPR == 0)
     float r0[8], r1[8], r2[8], mu[8], is[8], sc[8], sh[8], mu2[8], is2[8];
-    if (bnr) {
+    if constexpr (bnr) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int n = min(n0 + ccol * 8 + e, p.N - 1);
@@ -410,13 +396,35 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
       bf16* dst = C + (long long)m * p.ldc + n;
       if (n + 7 < p.N && (p.ldc & 7) == 0) {
         const long long off = bz * p.sC + (long long)m * p.ldc + n;
+        if constexpr (EPI == EPI_BF16_EXT) {
+          // pre-activation chunk: [* act'(z)] -> [aux copy] -> act -> [dropout]; 16-B coalesced
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
+          if (p.dact_src) {
+            bf16x8 zv = *(const bf16x8*)((const bf16*)p.dact_src + off);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] *= act_grad(bf2f(zv[e]), p.dact);
+          }
+          if (p.aux) *(bf16x8*)((bf16*)p.aux + off) = v;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = act_apply(f[e], p.act);
+          if (p.drop_p > 0.f) {
+            const unsigned long long lin = (unsigned long long)m * p.N + n;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              f[e] = u01(hash_u32(p.drop_seed, lin + e)) < 1.f - p.drop_p ? f[e] * p.drop_scale : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = f2bf(f[e]);
+        }
         if (p.resid) {
           bf16x8 rr = *(const bf16x8*)((const bf16*)p.resid + off);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[e]));
         }
         *(bf16x8*)dst = v;
-        if (bnr) {
+        if constexpr (bnr) {
           bf16x8 yv = *(const bf16x8*)((const bf16*)p.bn_y + off);
           bf16x8 av, y2v;
           if (p.bn_a) av = *(const bf16x8*)((const bf16*)p.bn_a + off);
@@ -433,13 +441,22 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
         }
       } else {
         for (int e = 0; e < 8 && n + e < p.N; ++e) {
+          const long long off = bz * p.sC + (long long)m * p.ldc + n + e;
           float x = bf2f(v[e]);
-          if (p.resid) x += bf2f(((const bf16*)p.resid)[bz * p.sC + (long long)m * p.ldc + n + e]);
+          if constexpr (EPI == EPI_BF16_EXT) {
+            if (p.dact_src) x *= act_grad(bf2f(((const bf16*)p.dact_src)[off]), p.dact);
+            if (p.aux) ((bf16*)p.aux)[off] = v[e];
+            x = act_apply(x, p.act);
+            if (p.drop_p > 0.f)
+              x = u01(hash_u32(p.drop_seed, (unsigned long long)m * p.N + n + e)) < 1.f - p.drop_p ? x * p.drop_scale : 0.f;
+            x = bf2f(f2bf(x));
+          }
+          if (p.resid) x += bf2f(((const bf16*)p.resid)[off]);
           dst[e] = f2bf(x);
         }
       }
     }
-    if (bnr) {
+    if constexpr (bnr) {
       // lanes sharing a column chunk: tid % CPR equal -> xor over the bits above log2(CPR)
 #pragma unroll
       for (int e = 0; e < 8; ++e)
@@ -499,6 +516,8 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
   p.tiles_n = tiles_n;
   if (p.stats_shards < 1) p.stats_shards = 1;
   dim3 grid(tiles_m * tiles_n, batch, splits);
+  if (epi == EPI_BF16 && p.bn_sums) epi = EPI_BF16_BNR;
+  if (epi == EPI_BF16 && (p.aux || p.dact_src || p.drop_p > 0.f)) epi = EPI_BF16_EXT;
   TFK_GEMM_TILES(A_KIN, B_KIN, EPI_BF16)
   TFK_GEMM_TILES(A_KIN, B_KIN, EPI_F32)
   TFK_GEMM_TILES(A_KIN, B_KOUT, EPI_BF16)
@@ -509,6 +528,13 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
   TFK_GEMM_TILES(A_CONV_DGRAD, B_KIN, EPI_BF16)
   TFK_GEMM_TILES(A_CONV_DGRAD, B_KOUT, EPI_BF16)
   TFK_GEMM_TILES(A_KOUT, B_CONV_WGRAD, EPI_F32)
+  // transformer epilogue extras: fwd (aux/dropout) and dgrad (activation backward)
+  TFK_GEMM_TILES(A_KIN, B_KIN, EPI_BF16_EXT)
+  TFK_GEMM_TILES(A_KIN, B_KOUT, EPI_BF16_EXT)
+  // fused BN-backward reduction: only the dgrad producers of a BN input
+  TFK_GEMM_TILES(A_KIN, B_KOUT, EPI_BF16_BNR)
+  TFK_GEMM_TILES(A_CONV_DGRAD, B_KIN, EPI_BF16_BNR)
+  TFK_GEMM_TILES(A_CONV_DGRAD, B_KOUT, EPI_BF16_BNR)
   return -1;  // unsupported combination
 }
 

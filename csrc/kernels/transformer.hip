@@ -6,8 +6,10 @@
 // residual-stream gradient added in the same pass; dgamma/dbeta are accumulated per lane across
 // the rows a wave visits, reduced across the block in LDS, then one f32 atomic per column/block.
 //
-// Embedding: out[t] = word[ids[t]]*scale (+ pos[t % S]) (+ type[tt[t]]), 8 columns per thread;
-// backward scatters into f32 gradient tables with atomics (rows shared by many tokens).
+// Embedding: out[t] = word[ids[t]]*scale (+ pos[t % S]) (+ type[tt[t]]), 8 columns per thread.
+// Backward: word rows by scattered f32 atomics (random ids rarely collide); position rows (hit by
+// every sequence) by a plain batch reduction; token-type rows (2-4 rows hit by every token) by
+// per-thread partial sums and one atomic per block -- no hot-row atomic contention.
 #include "common.h"
 
 namespace {
@@ -176,9 +178,9 @@ __global__ void embed_fwd_kernel(const int* __restrict__ ids, const bf16* __rest
   }
 }
 
+// word rows: scattered f32 atomics (token ids rarely collide)
 __global__ void embed_bwd_kernel(const int* __restrict__ ids, const bf16* __restrict__ dy, int V,
-                                 float* __restrict__ dword, float* __restrict__ dpos, int S, const int* __restrict__ tt,
-                                 float* __restrict__ dtype, int T, long long ntok, int W, float scale) {
+                                 float* __restrict__ dword, long long ntok, int W, float scale) {
   const int cpr = W >> 3;
   const long long n = ntok * cpr;
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
@@ -189,17 +191,51 @@ __global__ void embed_bwd_kernel(const int* __restrict__ ids, const bf16* __rest
     float* dw = dword + (long long)id * W + c;
 #pragma unroll
     for (int e = 0; e < 8; ++e) atomicAdd(dw + e, bf2f(g[e]) * scale);
-    if (dpos) {
-      float* dp = dpos + (long long)(t % S) * W + c;
+  }
+}
+
+// position rows: every sequence hits every row -> a plain column reduction over the batch
+// (deterministic, no atomics). Thread = (position s, 8-column chunk).
+__global__ void embed_pos_bwd_kernel(const bf16* __restrict__ dy, float* __restrict__ dpos, int S, int nseq, int W) {
+  const int cpr = W >> 3;
+  const long long n = (long long)S * cpr;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const int s = (int)(i / cpr), c = (int)(i % cpr) * 8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < nseq; ++b) {
+      bf16x8 g = *(const bf16x8*)(dy + ((long long)b * S + s) * W + c);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) atomicAdd(dp + e, bf2f(g[e]));
+      for (int e = 0; e < 8; ++e) acc[e] += bf2f(g[e]);
     }
-    if (dtype) {
+    *(f32x4*)(dpos + (long long)s * W + c) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    *(f32x4*)(dpos + (long long)s * W + c + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+  }
+}
+
+// token-type rows (T <= 4): per-thread partial sums over a token range, one atomic per block.
+__global__ void embed_type_bwd_kernel(const bf16* __restrict__ dy, const int* __restrict__ tt, float* __restrict__ dtype,
+                                      int T, long long ntok, int W) {
+  const int cpr = W >> 3;
+  const long long per = (ntok + gridDim.y - 1) / gridDim.y;
+  const long long t0 = (long long)blockIdx.y * per, t1 = min(ntok, t0 + per);
+  for (int c8 = blockIdx.x * NT + threadIdx.x; c8 < cpr; c8 += gridDim.x * NT) {
+    float acc[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+    for (long long t = t0; t < t1; ++t) {
       const int ty = min(max(tt[t], 0), T - 1);
-      float* dt = dtype + (long long)ty * W + c;
+      bf16x8 g = *(const bf16x8*)(dy + t * W + c8 * 8);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) atomicAdd(dt + e, bf2f(g[e]));
+      for (int k = 0; k < 4; ++k)
+        if (k == ty)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[k][e] += bf2f(g[e]);
     }
+    for (int k = 0; k < T; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(dtype + (long long)k * W + c8 * 8 + e, acc[k][e]);
   }
 }
 
@@ -240,10 +276,18 @@ int tfk_embedding_fwd(const int* ids, const bf16* word, int V, const bf16* pos, 
                      tt, type, T, out, ntok, W, scale);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+// dpos (if given) is OVERWRITTEN for rows < S; dtype (T <= 4) is accumulated.
 int tfk_embedding_bwd(const int* ids, const bf16* dy, int V, float* dword, float* dpos, int S, const int* tt,
                       float* dtype, int T, long long ntok, int W, float scale, hipStream_t s) {
+  if (dtype && T > 4) return -3;
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_for(ntok * (W / 8), NT, 8192)), dim3(NT), 0, s, ids, dy, V, dword,
-                     dpos, S, tt, dtype, T, ntok, W, scale);
+                     ntok, W, scale);
+  if (dpos)
+    hipLaunchKernelGGL(embed_pos_bwd_kernel, dim3(grid_for((long long)S * (W / 8), NT, 4096)), dim3(NT), 0, s, dy, dpos,
+                       S, (int)(ntok / S), W);
+  if (dtype)
+    hipLaunchKernelGGL(embed_type_bwd_kernel, dim3((W / 8 + NT - 1) / NT, 128), dim3(NT), 0, s, dy, tt, dtype, T, ntok,
+                       W);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }

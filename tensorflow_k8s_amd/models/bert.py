@@ -218,7 +218,8 @@ class BertForPreTraining:
         de = self.ln_emb.backward(E.dropout(dh, hd, s_emb), e, st)
         self.pos.table.grad.zero_()
         self.typ.table.grad.zero_()
-        TR.embedding_bwd(ids, de, self.word.table.grad, self.pos.table.grad, S, tt, self.typ.table.grad)
+        TR.embedding_bwd(ids, de, self.word.table.grad, self.pos.table.grad, S, tt,
+                         self.typ.table.grad[:self.cfg.type_vocab])  # real rows only (table padded to 64)
         self.arena.grad_ready(self.word.table, self.pos.table, self.typ.table)
         loss = mlm_loss.view(B, P).mean(1) + nsp_loss
         return loss, corr

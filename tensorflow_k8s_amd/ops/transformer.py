@@ -82,13 +82,14 @@ def embedding_fwd(ids, word, pos=None, seq_len: int = 1, type_ids=None, type_tab
 
 
 def embedding_bwd(ids, dy, dword, dpos=None, seq_len: int = 1, type_ids=None, dtype_table=None, scale: float = 1.0):
-    """Scatter-add into f32 gradient tables (caller zeroes / overwrites them first)."""
+    """dword (+)= scatter of dy rows (f32 atomics: the caller zeroes or pre-writes dword);
+    dpos[:seq_len] = column sums over the batch (overwritten); dtype_table (+)= per-type sums."""
     W = dy.shape[-1]
     if not on_gpu(dy):
         d = dy.reshape(-1, W).float()
         dword.view(-1, W).index_add_(0, ids.reshape(-1).long(), d * scale)
         if dpos is not None:
-            dpos.view(-1, W)[:seq_len].add_(d.view(-1, seq_len, W).sum(0))
+            dpos.view(-1, W)[:seq_len].copy_(d.view(-1, seq_len, W).sum(0))
         if dtype_table is not None:
             dtype_table.view(-1, W).index_add_(0, type_ids.reshape(-1).long(), d)
         return

@@ -16,9 +16,16 @@ asynchronously. tfk equivalent:
   ``mode="async"``: ps applies each push as it arrives (Hogwild-style staleness, TF's default PS
   behaviour) and answers that worker only.
 
-Message protocol per (worker, shard): header int64[4] = [cmd, step, worker_rank, 0] then payload.
-cmd PUSH=1 (payload grad shard f32) -> reply shard f32; DONE=2; FETCH=3 (reply master + slots, for
-checkpoints); LOAD=4 (payload master + slots, restore); PULL=5 (reply master shard).
+Two transports:
+* ``transport="gloo"`` (ps tasks on CPU; sync or async): message protocol per (worker, shard):
+  header int64[4] = [cmd, step, worker_rank, 0] then payload. cmd PUSH=1 (payload grad shard f32)
+  -> reply shard f32; DONE=2; FETCH=3 (reply master + slots, for checkpoints); LOAD=4 (payload
+  master + slots, restore); PULL=5 (reply master shard).
+* ``transport="rccl"`` (ps tasks own a GPU, e.g. BASELINE's PS=2/worker=6 on one 8xMI355X node;
+  sync only): per step and shard one RCCL ``reduce`` of the gradient shard onto its owner over
+  xGMI, the owner's fused HIP optimizer update, one ``broadcast`` of the updated shard back. The
+  schedule is identical on every rank (steps and checkpoint steps are known), so no control
+  messages are needed; for a checkpoint the owners ``send`` master + slots to the chief.
 """
 from __future__ import annotations
 
@@ -51,15 +58,21 @@ class ParameterServerStrategy:
     name = "ps"
 
     def __init__(self, arena: ParamArena, ps_ranks: list[int], worker_ranks: list[int], mode: str = "sync",
-                 group=None):
+                 group=None, transport: str = "gloo"):
         if mode not in ("sync", "async"):
             raise ValueError(f"ps mode must be sync|async, got {mode}")
+        if transport not in ("gloo", "rccl"):
+            raise ValueError(f"ps transport must be gloo|rccl, got {transport}")
+        if transport == "rccl" and mode != "sync":
+            raise ValueError("the rccl (collective) transport is synchronous; use transport=gloo for async")
         self.arena, self.ps_ranks, self.worker_ranks, self.mode, self.group = arena, list(ps_ranks), list(worker_ranks), mode, group
+        self.transport = transport
         self.rank = dist.get_rank()
         self.shards = shard_bounds(arena.numel, len(self.ps_ranks))
-        pin = arena.grad.is_cuda
-        self._g = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
-        self._p = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
+        if transport == "gloo":
+            pin = arena.grad.is_cuda
+            self._g = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
+            self._p = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
         self.step_count = 0
 
     @property
@@ -93,6 +106,13 @@ class ParameterServerStrategy:
     def apply_gradients(self, opt=None) -> None:
         """Push local gradients, pull the updated parameters (replaces optimizer.step())."""
         a = self.arena
+        if self.transport == "rccl":
+            collective_exchange(a, self.shards, self.ps_ranks, self.group)
+            a.refresh_compute()
+            self.step_count += 1
+            if opt is not None:
+                opt.step_count = self.step_count
+            return
         for s, (lo, hi) in enumerate(self.shards):
             self._g[s].copy_(a.grad[lo:hi], non_blocking=True)
         if a.grad.is_cuda:
@@ -107,6 +127,11 @@ class ParameterServerStrategy:
 
     def pull(self) -> None:
         """Initial (or resync) read of every variable from the ps tasks."""
+        if self.transport == "rccl":
+            for (lo, hi), ps in zip(self.shards, self.ps_ranks):
+                dist.broadcast(self.arena.master[lo:hi], ps, group=self.group)
+            self.arena.refresh_compute()
+            return
         self._exchange(PULL, None, self._p)
         for s, (lo, hi) in enumerate(self.shards):
             self.arena.master[lo:hi].copy_(self._p[s])
@@ -116,8 +141,14 @@ class ParameterServerStrategy:
         """Copy master + optimizer slots from the ps tasks into the local arena (chief, before a
         checkpoint save)."""
         names = list(opt.slot_names)
-        bufs = [torch.empty((1 + len(names)) * (hi - lo), dtype=torch.float32) for lo, hi in self.shards]
-        self._exchange(FETCH, None, bufs)
+        if self.transport == "rccl":
+            dev = self.arena.master.device
+            bufs = [torch.empty((1 + len(names)) * (hi - lo), dtype=torch.float32, device=dev) for lo, hi in self.shards]
+            for b, ps in zip(bufs, self.ps_ranks):
+                dist.recv(b, ps, group=self.group)
+        else:
+            bufs = [torch.empty((1 + len(names)) * (hi - lo), dtype=torch.float32) for lo, hi in self.shards]
+            self._exchange(FETCH, None, bufs)
         for s, (lo, hi) in enumerate(self.shards):
             n = hi - lo
             self.arena.master[lo:hi].copy_(bufs[s][:n])
@@ -135,13 +166,26 @@ class ParameterServerStrategy:
         self._exchange(LOAD, bufs, None)
 
     def shutdown(self) -> None:
-        self._exchange(DONE, None, None)
+        if self.transport == "gloo":
+            self._exchange(DONE, None, None)
 
     def broadcast_parameters(self, src: int = 0):
         self.pull()
 
     def all_reduce_metrics(self, t: torch.Tensor) -> torch.Tensor:
         return t
+
+
+def collective_exchange(arena: ParamArena, shards, ps_ranks, group=None, update=None):
+    """One synchronous PS step over RCCL, executed identically by every rank: reduce each gradient
+    shard onto its owner, (owner updates), broadcast the shard back. Non-owners' buffers are
+    their local gradients (workers) or zeros (ps tasks)."""
+    for (lo, hi), ps in zip(shards, ps_ranks):
+        dist.reduce(arena.grad[lo:hi], ps, op=dist.ReduceOp.SUM, group=group)
+    if update is not None:
+        update()
+    for (lo, hi), ps in zip(shards, ps_ranks):
+        dist.broadcast(arena.master[lo:hi], ps, group=group)
 
 
 class ParameterServer:
@@ -151,7 +195,9 @@ class ParameterServer:
                  mode: str = "sync", group=None):
         self.arena, self.opt, self.mode, self.group = arena, opt, mode, group
         self.worker_ranks = list(worker_ranks)
-        self.lo, self.hi = shard_bounds(arena.numel, len(ps_ranks))[shard]
+        self.ps_ranks = list(ps_ranks)
+        self.shards = shard_bounds(arena.numel, len(ps_ranks))
+        self.lo, self.hi = self.shards[shard]
         opt.region = (self.lo, self.hi)
         if mode == "sync":
             opt.grad_scale = 1.0 / len(self.worker_ranks)
@@ -218,4 +264,24 @@ class ParameterServer:
                 for w in pending:
                     self._reply(w, out)
                 pending = []
+        return self.updates
+
+    # ------------------------------------------------------------------ rccl transport
+    def serve_collective(self, start_step: int, total_steps: int, checkpoint_every: int = 0,
+                         chief: int = 0, final_checkpoint: bool = True) -> int:
+        """Mirror of the workers' step schedule over RCCL: initial broadcast, then per step
+        reduce -> fused optimizer on the owned shard -> broadcast; ship master + slots to the
+        chief at its checkpoint steps."""
+        a = self.arena
+        a.grad.zero_()
+        for (lo, hi), ps in zip(self.shards, self.ps_ranks):
+            dist.broadcast(a.master[lo:hi], ps, group=self.group)
+        for step in range(start_step + 1, total_steps + 1):
+            a.grad.zero_()  # zero contribution to every shard's reduce (reduce may scribble on non-root inputs)
+            collective_exchange(a, self.shards, self.ps_ranks, self.group, update=self.opt.step)
+            self.updates += 1
+            ckpt = (checkpoint_every and step % checkpoint_every == 0 and step < total_steps) or \
+                (final_checkpoint and step == total_steps)
+            if ckpt:
+                dist.send(self._state(), chief, group=self.group)
         return self.updates

@@ -62,6 +62,8 @@ def parse_args(argv=None):
     ap.add_argument("--lr-schedule", default="constant", choices=["constant", "cosine", "poly"])
     ap.add_argument("--strategy", default="auto", choices=["auto", "mwms", "ps"])
     ap.add_argument("--ps-mode", default="sync", choices=["sync", "async"])
+    ap.add_argument("--ps-transport", default="gloo", choices=["gloo", "rccl"],
+                    help="gloo: ps tasks on CPU (sync/async); rccl: ps tasks own a GPU, RCCL reduce/broadcast (sync)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--device", default="auto", choices=["auto", "cpu", "cuda"])
     ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph (1 GPU, MWMS)")
@@ -111,7 +113,7 @@ def make_optimizer(args, arena):
 
 
 def pick_device(args, info) -> torch.device:
-    if info.is_ps or args.device == "cpu":
+    if (info.is_ps and args.ps_transport == "gloo") or args.device == "cpu":
         return torch.device("cpu")
     want_cuda = args.device == "cuda" or (args.device == "auto" and torch.cuda.is_available())
     if not want_cuda:
@@ -140,22 +142,29 @@ def maybe_fault(step: int, rank: int):
     os._exit(code)
 
 
-def run_ps(args, info) -> int:
+def run_ps(args, info, dev) -> int:
     import torch.distributed as dist
 
     from ..models import build_model
     from ..parallel.ps import ParameterServer
     from .checkpoint import CheckpointManager
-    model = build_model(args.model, **model_kwargs(args)).to("cpu", seed=args.seed)
+    model = build_model(args.model, **model_kwargs(args)).to(dev, seed=args.seed)
     opt = make_optimizer(args, model.arena)
+    start = 0
     if args.checkpoint_dir:
         step = CheckpointManager(args.checkpoint_dir, args.keep).restore(model.arena, opt)
         if step is not None:
+            start = step
             _log({"event": "restored", "role": "ps", "step": step, "index": info.task_index})
     shard = info.ps_ranks.index(info.rank)
     server = ParameterServer(model.arena, opt, shard, info.ps_ranks, info.worker_ranks, args.ps_mode)
-    _log({"event": "ps_ready", "index": info.task_index, "shard": [server.lo, server.hi]})
-    n = server.serve()
+    _log({"event": "ps_ready", "index": info.task_index, "shard": [server.lo, server.hi],
+          "transport": args.ps_transport, "device": str(dev)})
+    if args.ps_transport == "rccl":
+        n = server.serve_collective(start, args.steps, args.checkpoint_every if args.checkpoint_dir else 0,
+                                    chief=0, final_checkpoint=bool(args.checkpoint_dir))
+    else:
+        n = server.serve()
     _log({"event": "done", "role": "ps", "index": info.task_index, "updates": n})
     dist.destroy_process_group()
     return EXIT_OK
@@ -175,7 +184,8 @@ def run_worker(args, info, dev) -> int:
         from ..parallel.ps import ParameterServerStrategy
         if not info.ps_ranks:
             raise SystemExit("--strategy ps needs ps tasks in TF_CONFIG")
-        strat = ParameterServerStrategy(model.arena, info.ps_ranks, info.worker_ranks, args.ps_mode)
+        strat = ParameterServerStrategy(model.arena, info.ps_ranks, info.worker_ranks, args.ps_mode,
+                                        transport=args.ps_transport)
         strat.configure_optimizer(opt)
     else:
         from ..parallel.mwms import MultiWorkerMirroredStrategy
@@ -264,11 +274,11 @@ def main(argv=None) -> int:
             torch.set_num_threads(max(1, (os.cpu_count() or 1) // info.world_size))
         if info.world_size > 1:
             use_ps = args.strategy == "ps" or (args.strategy == "auto" and info.ps_ranks)
-            backend = "nccl" if (dev.type == "cuda" and not use_ps) else "gloo"
+            backend = "nccl" if (dev.type == "cuda" and (not use_ps or args.ps_transport == "rccl")) else "gloo"
             cluster.init_process_group(info, backend, timeout_s=args.rendezvous_timeout,
                                        device_id=dev if backend == "nccl" else None)
         if info.is_ps:
-            return run_ps(args, info)
+            return run_ps(args, info, dev)
         return run_worker(args, info, dev)
     except torch.cuda.OutOfMemoryError as e:
         _termination_message("OOMKilled")

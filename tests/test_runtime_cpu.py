@@ -192,3 +192,22 @@ def test_checkpoint_manager_roundtrip_exact(tmp_path, native_ext):
     assert tuple(t["conv1/kernel"].shape) == (7, 7, 3, 16)
     w = m.conv1.w.master.numpy()  # OHWI
     np.testing.assert_array_equal(t["conv1/kernel"].numpy(), np.transpose(w, (1, 2, 3, 0))[:, :, :3, :])
+
+
+def test_collective_ps_transport_matches_mwms(tmp_path, native_ext):
+    """transport=rccl (reduce -> owner update -> broadcast; run here over gloo collectives) gives the
+    same trajectory as MWMS, including the chief's checkpoint fetch of the ps-held slots."""
+    p = free_port()
+    mw = _launch([("chief", 0), ("worker", 0)], {"chief": [f"c.svc:{p}"], "worker": ["w.svc:1"]}, BASE, str(tmp_path))
+    assert all(v[0] == 0 for v in mw.values()), {k: v[2][-1500:] for k, v in mw.items()}
+    p = free_port()
+    ck = str(tmp_path / "ck")
+    out = _launch([("chief", 0), ("worker", 0), ("ps", 0), ("ps", 1)],
+                  {"chief": [f"c.svc:{p}"], "worker": ["w.svc:1"], "ps": ["p0.svc:1", "p1.svc:1"]},
+                  BASE + ["--ps-transport", "rccl", "--checkpoint-dir", ck, "--checkpoint-every", "4"], str(tmp_path))
+    assert all(v[0] == 0 for v in out.values()), {k: v[2][-1500:] for k, v in out.items()}
+    a, b = _final_loss(mw[("chief", 0)][1]), _final_loss(out[("chief", 0)][1])
+    assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (a, b)
+    from tensorflow_k8s_amd.ops._lib import lib
+    t = lib().ckpt_read(os.path.join(ck, "model.ckpt-12"))
+    assert float(t["fc1/kernel/Momentum"].abs().sum()) > 0  # slots came from the ps shards

@@ -35,11 +35,26 @@ def _stale(out: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _check_scratch(stderr: str, src: str) -> None:
+    """Kernels must not spill: a scratch-using GEMM/attention kernel runs several times slower."""
+    import re
+    fn = None
+    for line in stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            fn = m.group(1)
+        m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
+        if m and int(m.group(1)) > 0:
+            sys.stderr.write(f"[tfk build] WARNING: {os.path.basename(src)}: {fn} uses {m.group(1)} B/lane of scratch\n")
+
+
 def _run(cmd: list[str]) -> None:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("build failed: " + " ".join(cmd[:3]) + " ... " + cmd[-1])
+    if "-Rpass-analysis=kernel-resource-usage" in cmd:
+        _check_scratch(r.stderr, cmd[-3])
 
 
 def ext_path() -> str:
@@ -58,7 +73,7 @@ def build_kernels(jobs: int | None = None, verbose: bool = False) -> str:
         objs.append(out)
         if _stale(out, [src] + headers):
             tasks.append([HIPCC, "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}",
-                          "-munsafe-fp-atomics", src, "-o", out])
+                          "-munsafe-fp-atomics", "-Rpass-analysis=kernel-resource-usage", src, "-o", out])
     py_inc = sysconfig.get_paths()["include"]
     cpp_hdrs = glob.glob(os.path.join(ROOT, "cpp", "*", "*.h"))
     for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "bindings", "*.cpp"))):

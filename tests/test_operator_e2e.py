@@ -87,3 +87,31 @@ def test_backoff_limit_exhausted(cluster, tmp_path):
     assert tfjob_condition(j) == "Failed", j["status"]
     msg = [cd for cd in j["status"]["conditions"] if cd["type"] == "Failed"][0]["message"]
     assert "backoff" in msg.lower(), msg
+
+
+def test_deploy_examples_are_accepted(cluster):
+    """Every manifest under deploy/ is accepted by the apiserver (CRD schema, v1alpha1 conversion)
+    and picked up by the operator (Created condition); GPU jobs stay Pending on this GPU-less node."""
+    import glob
+
+    import yaml
+    c = cluster.client
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = []
+    for f in sorted(glob.glob(os.path.join(root, "deploy", "examples", "*.yaml"))):
+        obj = yaml.safe_load(open(f))
+        c.create(obj)
+        names.append(obj["metadata"]["name"])
+    import time
+    deadline = time.time() + 30
+    pending = set(names)
+    while pending and time.time() < deadline:
+        for n in list(pending):
+            j = c.get("tfjobs", n)
+            conds = j.get("status", {}).get("conditions", [])
+            if any(cd["type"] == "Created" for cd in conds) or j.get("status", {}).get("phase"):
+                pending.discard(n)
+        time.sleep(0.2)
+    for n in names:
+        c.delete("tfjobs", n)
+    assert not pending, pending

@@ -188,7 +188,9 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   p.drop_p = (float)drop_p;
   p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
   p.drop_seed = (unsigned long long)drop_seed;
-  TORCH_CHECK((bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64), "unsupported tile");
+  TORCH_CHECK((bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64) ||
+                  (bm == 256 && bn == 256 && (amode == A_KIN || amode == A_KOUT) && (bmode == B_KIN || bmode == B_KOUT)),
+              "unsupported tile ", bm, "x", bn, " for operand modes ", amode, "/", bmode);
   check_rc(tfk_gemm_launch(p, bm, bn, amode, bmode, epi, batch, splits, cur_stream()), "gemm");
 }
 

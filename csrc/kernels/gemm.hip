@@ -33,7 +33,11 @@ enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1, EPI_BF16_BNR = 2, EPI_BF16_EXT = 3 };
 
 
 constexpr int BK = 64;
-constexpr int NT = 256;
+// Threads per block: 8 waves (2x4 wave grid, 128x64 per wave) for the 256x256 tile, else 4 waves
+// (2x2). The big tile halves the LDS fragment reads per MFMA (12 ds_read per 32 MFMA vs 8 per 16)
+// and the global->LDS bytes per FLOP; 128 KiB of double-buffered LDS -> 1 block (8 waves) per CU.
+template <int BM, int BN>
+constexpr int threads_for() { return (BM >= 256 && BN >= 256) ? 512 : 256; }
 
 template <int ROWS>
 __device__ __forceinline__ int swz_kout(int k) {
@@ -63,14 +67,18 @@ __device__ __forceinline__ u32x4 load_partial(const bf16* src, int valid, int st
 }
 
 // Per-operand loader state. ROWS = tile rows of this operand (BM for A, BN for B).
-template <int ROWS, int MODE, bool IS_A>
+template <int ROWS, int MODE, bool IS_A, int NT>
 struct Loader {
   static constexpr bool KOUT = IS_A ? (MODE == A_KOUT) : (MODE == B_KOUT || MODE == B_CONV_WGRAD);
-  static constexpr int NCH = ROWS / 32;  // 16-B chunks per thread per K-tile
-  static constexpr int CPR = ROWS / 8;   // chunks per k-row (K-outer)
+  static constexpr int NCH = ROWS * 8 / NT;  // 16-B chunks per thread per K-tile
+  static constexpr int CPR = ROWS / 8;       // chunks per k-row (K-outer)
+  static_assert(NT % CPR == 0 || !KOUT, "K-outer loader needs NT % (ROWS/8) == 0");
   const bf16* base;
   long long ld;
   int lim_rows, K;
+  // dense fast path: block-uniform "every row of this tile is in range and 16-B aligned"
+  bool full;
+  const bf16* tbase;  // this thread's first chunk address (k = 0)
   // conv state
   long long rbase[NCH];
   int hb[NCH], wb[NCH];
@@ -81,7 +89,7 @@ struct Loader {
 
   __device__ __forceinline__ int chunk_row(int i) const {
     if constexpr (KOUT) return (threadIdx.x / CPR) + (NT / CPR) * i;
-    else return (threadIdx.x >> 3) + 32 * i;
+    else return (threadIdx.x >> 3) + (NT / 8) * i;
   }
   __device__ __forceinline__ int chunk_col() const {
     if constexpr (KOUT) return threadIdx.x % CPR;
@@ -90,6 +98,11 @@ struct Loader {
 
   __device__ __forceinline__ void init(const GemmParams& p, const bf16* b, long long ld_, int row0, int rows, int kt0) {
     base = b; ld = ld_; lim_rows = rows; K = p.K;
+    if constexpr (MODE == 0 || MODE == 1) {
+      full = (row0 + ROWS <= rows) && ((ld & 7) == 0);
+      if constexpr (!KOUT) tbase = b + (long long)(row0 + chunk_row(0)) * ld + chunk_col() * 8;
+      else tbase = b + (long long)chunk_row(0) * ld + row0 + chunk_col() * 8;
+    }
     if constexpr (IS_A && MODE == A_CONV_FWD) {
       const int PQ = p.P * p.Q;
 #pragma unroll
@@ -133,6 +146,21 @@ struct Loader {
 
   __device__ __forceinline__ void load(const GemmParams& p, int kt, int row0, u32x4 (&regs)[NCH]) {
     const u32x4 zero = {0u, 0u, 0u, 0u};
+    if constexpr (MODE == 0 || MODE == 1) {
+      // interior tile, full K-tile: unpredicated 16-B loads, scalar strides (one uniform branch)
+      if (full && (kt + 1) * BK <= K) {
+        if constexpr (!KOUT) {
+          const bf16* src = tbase + kt * BK;
+#pragma unroll
+          for (int i = 0; i < NCH; ++i) regs[i] = *(const u32x4*)(src + (long long)i * (NT / 8) * ld);
+        } else {
+          const bf16* src = tbase + (long long)kt * BK * ld;
+#pragma unroll
+          for (int i = 0; i < NCH; ++i) regs[i] = *(const u32x4*)(src + (long long)i * (NT / CPR) * ld);
+        }
+        return;
+      }
+    }
     if constexpr (MODE == 0 /*KIN dense (A_KIN==B_KIN==0)*/) {
       const int k = kt * BK + chunk_col() * 8;
       const bool vec = (ld & 7) == 0;
@@ -227,17 +255,23 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rb, int kk) {
 }
 
 template <int BM, int BN, int AM, int BMD, int EPI>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
-  constexpr int FM = BM / 32, FN = BN / 32;  // 16x16 fragments per wave (2x2 waves)
+__global__ __launch_bounds__((threads_for<BM, BN>()), (threads_for<BM, BN>() == 512 ? 1 : 2)) void gemm_kernel(GemmParams p) {
+  constexpr int NT = threads_for<BM, BN>();
+  constexpr int NW = NT / 64;                    // waves
+  constexpr int WM = 2, WN = NW / WM;            // wave grid
+  constexpr int TM = BM / WM, TN = BN / WN;      // wave tile
+  constexpr int FM = TM / 16, FN = TN / 16;      // 16x16 fragments per wave
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr bool A_KOUT_ = (AM == A_KOUT);
   constexpr bool B_KOUT_ = (BMD == B_KOUT || BMD == B_CONV_WGRAD);
-  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  constexpr int MAIN_BYTES = 2 * (A_BYTES + B_BYTES);
+  constexpr int EPI_BYTES = (EPI == EPI_F32) ? 0 : BM * (BN + 8) * 2;
+  __shared__ __attribute__((aligned(16))) char smem[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
   char* As = smem;
   char* Bs = smem + 2 * A_BYTES;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -249,8 +283,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
   const int kt0 = blockIdx.z * p.kt_per_split;
   const int kt1 = min(nkt, kt0 + p.kt_per_split);
 
-  Loader<BM, AM, true> la;
-  Loader<BN, BMD, false> lb;
+  Loader<BM, AM, true, NT> la;
+  Loader<BN, BMD, false, NT> lb;
   la.S_ = p.S; lb.S_ = p.S;
   la.init(p, Ab, p.lda, m0, p.M, kt0);
   lb.init(p, Bb, p.ldb, n0, p.N, kt0);
@@ -261,7 +295,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ra[Loader<BM, AM, true>::NCH], rb[Loader<BN, BMD, false>::NCH];
+  u32x4 ra[Loader<BM, AM, true, NT>::NCH], rb[Loader<BN, BMD, false, NT>::NCH];
   if (kt0 < kt1) {
     la.load(p, kt0, m0, ra);
     lb.load(p, kt0, n0, rb);
@@ -285,9 +319,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, A_KOUT_>(Ac, wm * (BM / 2) + i * 16, kk);
+      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, A_KOUT_>(Ac, wm * TM + i * 16, kk);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, B_KOUT_>(Bc, wn * (BN / 2) + j * 16, kk);
+      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, B_KOUT_>(Bc, wn * TN + j * 16, kk);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -302,17 +336,17 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
   }
 
   // Accumulator (i,j) of this lane holds C[m][n..n+3] with
-  //   m = m0 + wm*BM/2 + i*16 + (lane&15),  n = n0 + wn*BN/2 + j*16 + (lane>>4)*4.
+  //   m = m0 + wm*TM + i*16 + (lane&15),  n = n0 + wn*TN + j*16 + (lane>>4)*4.
   const int ml = lane & 15, nl = (lane >> 4) * 4;
   if constexpr (EPI == EPI_F32) {
     float* C = (float*)p.C + bz * p.sC + (long long)blockIdx.z * p.split_stride;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * (BM / 2) + i * 16 + ml;
+      const int m = m0 + wm * TM + i * 16 + ml;
       if (m >= p.M) continue;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wn * (BN / 2) + j * 16 + nl;
+        const int n = n0 + wn * TN + j * 16 + nl;
         float* dst = C + (long long)m * p.ldc + n;
         f32x4 v = acc[i][j] * p.alpha;
         if (n + 3 < p.N && (p.ldc & 3) == 0) {
@@ -335,7 +369,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
       for (int r = 0; r < 4; ++r) { csum[j][r] = 0.f; csq[j][r] = 0.f; }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int nloc = wn * (BN / 2) + j * 16 + nl;
+      const int nloc = wn * TN + j * 16 + nl;
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
       if (p.bias) {
 #pragma unroll
@@ -343,7 +377,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int mloc = wm * (BM / 2) + i * 16 + ml;
+        const int mloc = wm * TM + i * 16 + ml;
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -366,7 +400,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
           float s = csum[j][r], q = csq[j][r];
 #pragma unroll
           for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
-          const int n = n0 + wn * (BN / 2) + j * 16 + nl + r;
+          const int n = n0 + wn * TN + j * 16 + nl + r;
           if (ml == 0 && n < p.N) { atomicAdd(st + n, s); atomicAdd(st + p.N + n, q); }
         }
     }
@@ -467,7 +501,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
           r2[e] += __shfl_xor(r2[e], o, 64);
         }
       __syncthreads();  // C tile no longer needed: reuse LDS for the cross-wave reduction
-      float* red = (float*)smem;  // [4 waves][3][CPR*8]
+      float* red = (float*)smem;  // [NW waves][3][CPR*8]
       if (lane < CPR) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -485,7 +519,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
         if (n >= p.N) continue;
         float v = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) v += red[(w * 3 + which) * (CPR * 8) + col];
+        for (int w = 0; w < NW; ++w) v += red[(w * 3 + which) * (CPR * 8) + col];
         atomicAdd(st + which * p.N + n, v);
       }
     }
@@ -498,11 +532,13 @@ using namespace tfk;
 
 #define TFK_GEMM_CASE(BM_, BN_, AM_, BM2_, EPI_)                                                  \
   if (bm == BM_ && bn == BN_ && amode == AM_ && bmode == BM2_ && epi == EPI_) {                  \
-    hipLaunchKernelGGL((gemm_kernel<BM_, BN_, AM_, BM2_, EPI_>), grid, dim3(NT), 0, stream, p); \
+    hipLaunchKernelGGL((gemm_kernel<BM_, BN_, AM_, BM2_, EPI_>), grid, dim3((threads_for<BM_, BN_>())), 0, stream, p); \
     return hipGetLastError() == hipSuccess ? 0 : -2;                                              \
   }
 #define TFK_GEMM_TILES(AM_, BM2_, EPI_) \
   TFK_GEMM_CASE(128, 128, AM_, BM2_, EPI_) TFK_GEMM_CASE(128, 64, AM_, BM2_, EPI_) TFK_GEMM_CASE(64, 64, AM_, BM2_, EPI_)
+// + the 256x256 (8-wave) tile for the dense (non-gather) operand modes
+#define TFK_GEMM_TILES_BIG(AM_, BM2_, EPI_) TFK_GEMM_TILES(AM_, BM2_, EPI_) TFK_GEMM_CASE(256, 256, AM_, BM2_, EPI_)
 
 // Host launcher. Grid: x = tiles (M x N), y = batch, z = split-K. Returns 0 on success.
 extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits,
@@ -518,21 +554,21 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
   dim3 grid(tiles_m * tiles_n, batch, splits);
   if (epi == EPI_BF16 && p.bn_sums) epi = EPI_BF16_BNR;
   if (epi == EPI_BF16 && (p.aux || p.dact_src || p.drop_p > 0.f)) epi = EPI_BF16_EXT;
-  TFK_GEMM_TILES(A_KIN, B_KIN, EPI_BF16)
-  TFK_GEMM_TILES(A_KIN, B_KIN, EPI_F32)
-  TFK_GEMM_TILES(A_KIN, B_KOUT, EPI_BF16)
-  TFK_GEMM_TILES(A_KIN, B_KOUT, EPI_F32)
-  TFK_GEMM_TILES(A_KOUT, B_KOUT, EPI_F32)
-  TFK_GEMM_TILES(A_KOUT, B_KOUT, EPI_BF16)
+  TFK_GEMM_TILES_BIG(A_KIN, B_KIN, EPI_BF16)
+  TFK_GEMM_TILES_BIG(A_KIN, B_KIN, EPI_F32)
+  TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_BF16)
+  TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_F32)
+  TFK_GEMM_TILES_BIG(A_KOUT, B_KOUT, EPI_F32)
+  TFK_GEMM_TILES_BIG(A_KOUT, B_KOUT, EPI_BF16)
   TFK_GEMM_TILES(A_CONV_FWD, B_KIN, EPI_BF16)
   TFK_GEMM_TILES(A_CONV_DGRAD, B_KIN, EPI_BF16)
   TFK_GEMM_TILES(A_CONV_DGRAD, B_KOUT, EPI_BF16)
   TFK_GEMM_TILES(A_KOUT, B_CONV_WGRAD, EPI_F32)
   // transformer epilogue extras: fwd (aux/dropout) and dgrad (activation backward)
-  TFK_GEMM_TILES(A_KIN, B_KIN, EPI_BF16_EXT)
-  TFK_GEMM_TILES(A_KIN, B_KOUT, EPI_BF16_EXT)
+  TFK_GEMM_TILES_BIG(A_KIN, B_KIN, EPI_BF16_EXT)
+  TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_BF16_EXT)
   // fused BN-backward reduction: only the dgrad producers of a BN input
-  TFK_GEMM_TILES(A_KIN, B_KOUT, EPI_BF16_BNR)
+  TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_BF16_BNR)
   TFK_GEMM_TILES(A_CONV_DGRAD, B_KIN, EPI_BF16_BNR)
   TFK_GEMM_TILES(A_CONV_DGRAD, B_KOUT, EPI_BF16_BNR)
   return -1;  // unsupported combination

@@ -69,17 +69,30 @@ class ConvGeom:
         return 2 * self.N * self.P * self.Q * self.K * self.R * self.S * self.C
 
 
-def pick_tile(M: int, N: int, splits_ok: bool = False):
-    """Largest tile that still yields enough blocks to fill 256 CUs (8 XCDs x 32)."""
-    def tiles(bm, bn):
-        return ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
-    if N <= 64:
-        return (128, 64) if tiles(128, 64) >= 256 or splits_ok else (64, 64)
-    if tiles(128, 128) >= 512 or splits_ok and M >= 128:
-        return (128, 128)
-    if tiles(128, 64) >= 512:
-        return (128, 64)
-    return (64, 64)
+# (bm, bn): (concurrent blocks on the chip, relative MFMA efficiency measured by tools/gemm_bench.py)
+_TILES = {(256, 256): (256, 0.76), (128, 128): (512, 0.62), (128, 64): (768, 0.45), (64, 64): (1024, 0.30)}
+BIG_TILE_MIN_K = 2048  # one 8-wave block per CU: its prologue/epilogue is exposed, so it needs a long K loop
+
+
+def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: int = 0):
+    """Tile with the lowest modelled time: rounds of concurrent blocks x per-block work / efficiency
+    (a 256x256 tile runs one 8-wave block per CU; smaller tiles 2-4 blocks/CU at lower efficiency).
+    big_ok: operand modes that have the 256x256 instantiation (dense, non-gather); K: reduction
+    length (the big tile is only used without split-K and for K >= BIG_TILE_MIN_K)."""
+    best, best_cost = None, None
+    for (bm, bn), (slots, eff) in _TILES.items():
+        if (bm, bn) == (256, 256) and (not big_ok or splits_ok or M < 256 or N < 256 or K < BIG_TILE_MIN_K):
+            continue
+        if bn > 64 and N <= 64:
+            continue
+        tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
+        s = pick_splits(tiles, K) if (splits_ok and K) else 1
+        kfrac = 1.0 / s
+        rounds = -(-tiles * s // slots)
+        cost = rounds * (slots / 256) * bm * bn * kfrac / eff
+        if best_cost is None or cost < best_cost * 0.98:
+            best, best_cost = (bm, bn), cost
+    return best
 
 
 def pick_splits(tiles: int, K: int, min_ktiles: int = 4) -> int:
@@ -143,7 +156,7 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
     x2 = x.reshape(-1, K)
     M = x2.shape[0]
     y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-    _gemm(x2, w, y, M, N, K, K, K, N, A_KIN, B_KIN, EPI_BF16, pick_tile(M, N), bias=bias, act=ACT[act],
+    _gemm(x2, w, y, M, N, K, K, K, N, A_KIN, B_KIN, EPI_BF16, pick_tile(M, N, big_ok=True, K=K), bias=bias, act=ACT[act],
           resid=resid.reshape(-1, N) if resid is not None else None, aux=aux, drop_p=drop_p, drop_seed=drop_seed)
     return y
 
@@ -177,7 +190,7 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
             dx = (dx.float() + resid.reshape(-1, K).float()).to(torch.bfloat16)
         return dx
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
-    _gemm(dy2, w, dx, M, K, N, N, K, K, A_KIN, B_KOUT, EPI_BF16, pick_tile(M, K),
+    _gemm(dy2, w, dx, M, K, N, N, K, K, A_KIN, B_KOUT, EPI_BF16, pick_tile(M, K, big_ok=True, K=N),
           resid=resid.reshape(-1, K) if resid is not None else None,
           dact_src=dact_src.reshape(-1, K) if dact_src is not None else None,
           dact=ACT[dact] if dact_src is not None else 0)
@@ -197,7 +210,7 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
         else:
             gw.view(N, K).copy_(g)
         return
-    tile = pick_tile(N, K, splits_ok=True)
+    tile = pick_tile(N, K, splits_ok=True, big_ok=True, K=M)
     tiles = ((N + tile[0] - 1) // tile[0]) * ((K + tile[1] - 1) // tile[1])
 
     def run(C, splits, stride, beta):
@@ -226,7 +239,7 @@ def matmul_tn(a: torch.Tensor, b: torch.Tensor, out_f32: torch.Tensor | None = N
     if not on_gpu(a):
         out.copy_(a.float().t() @ b.float())
         return out
-    tile = pick_tile(M, N, splits_ok=True)
+    tile = pick_tile(M, N, splits_ok=True, big_ok=True, K=K)
     tiles = ((M + tile[0] - 1) // tile[0]) * ((N + tile[1] - 1) // tile[1])
 
     def run(C, splits, stride, beta):
@@ -259,7 +272,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
         return y.to(torch.bfloat16).contiguous()
     M = g.N * g.P * g.Q
     y = torch.empty(g.N, g.P, g.Q, g.K, dtype=torch.bfloat16, device=x.device)
-    tile = pick_tile(M, g.K)
+    tile = pick_tile(M, g.K, big_ok=g.pointwise, K=g.C)
     if g.pointwise:
         _gemm(x, w, y, M, g.K, g.C, g.C, g.C, g.K, A_KIN, B_KIN, EPI_BF16, tile, stats=stats, shards=shards,
               bias=bias, act=ACT[act])
@@ -298,7 +311,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
         return dx
     M = g.N * g.H * g.W
     dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
-    tile = pick_tile(M, g.C)
+    tile = pick_tile(M, g.C, big_ok=g.pointwise, K=g.K)
     if g.pointwise:
         _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid, bnr=bnr)
     elif g.R == 1 and g.S == 1:
@@ -326,7 +339,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
         v = gw.view(g.K, Nn)
         v.add_(gwt) if accumulate else v.copy_(gwt)
         return
-    tile = pick_tile(g.K, Nn, splits_ok=True)
+    tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp)
     tiles = ((g.K + tile[0] - 1) // tile[0]) * ((Nn + tile[1] - 1) // tile[1])
 
     def run(C, sp, stride, beta):

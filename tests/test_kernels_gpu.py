@@ -221,3 +221,28 @@ def test_dgrad_fused_bn_reduce(cfg, mode):
     assert rel(res[DEV][0], res["cpu"][0]) < 1e-2
     for k in range(3 if mode == "dual" else 2):
         assert rel(res[DEV][1][k], res["cpu"][1][k]) < 2e-2, k
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 512, 256), (520, 300, 200), (777, 1030, 136)])
+def test_big_tile_256(M, N, K, monkeypatch):
+    """The 8-wave 256x256 tile (dense operand modes) on interior and ragged shapes: fwd (bias+gelu
+    with aux) and dgrad (K-outer B, fused GELU backward); wgrad (split-K) stays on 128 tiles."""
+    real = G.pick_tile
+    monkeypatch.setattr(G, "pick_tile", lambda m, n, splits_ok=False, big_ok=False, K=0:
+                        (256, 256) if big_ok and not splits_ok and m >= 256 and n >= 256
+                        else real(m, n, splits_ok, big_ok, K))
+    x, w = bf(M, K, seed=1), bf(N, K, seed=2, scale=0.05)
+    b = torch.randn(N) * 0.1
+    dy = bf(M, N, seed=3)
+    w2 = bf(K, N, seed=4, scale=0.05)
+    out = {}
+    for dev in ("cpu", DEV):
+        z = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        y = G.linear_fwd(x.to(dev), w.to(dev), b.to(dev), act="gelu", aux=z)
+        dz = G.linear_dgrad(bf(M, K, seed=5).to(dev), w2.to(dev), dact_src=z, dact="gelu")
+        dx = G.linear_dgrad(dy.to(dev), w.to(dev))
+        gw = torch.zeros(N, K, device=dev)
+        G.linear_wgrad(dy.to(dev), x.to(dev), gw)
+        out[dev] = dict(y=y, z=z, dz=dz, dx=dx, gw=gw)
+    for k in out["cpu"]:
+        assert rel(out[DEV][k], out["cpu"][k]) < 1e-2, k

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--graph", type=int, default=-1, help="capture step in a hipGraph (default: on for 1 GPU)")
+    ap.add_argument("--fp8", type=int, default=0, help="transformer models: MX-fp8 forward GEMMs")
     args = ap.parse_args()
     if not args.batch:
         args.batch = 256 if args.model.startswith("resnet") else (64 if args.model.startswith("bert") else 32)
@@ -54,7 +55,7 @@ def main():
     from tensorflow_k8s_amd.runtime.trainer import StepRunner
 
     is_cnn = args.model.startswith("resnet")
-    model = build_model(args.model).to(dev)
+    model = build_model(args.model, **({"fp8": True} if args.fp8 else {})).to(dev)
     if is_cnn:
         opt = SGD(model.arena, lr=0.1 * args.batch * world / 256, momentum=0.9, weight_decay=5e-5)
         opt_name = "SGD momentum 0.9 (fused HIP)"
@@ -101,7 +102,8 @@ def main():
             "metric": f"{args.model} training throughput (whole node)", "value": round(toks / (ms / 1000.0), 1),
             "unit": "tokens/sec", "sequences_per_sec": round(value, 2), "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic token ids, random-init weights",
+            "vs_baseline": None, "dtype": "bf16+mxfp8-fwd" if args.fp8 else "bf16",
+            "data": "synthetic token ids, random-init weights",
             "config": {"model": args.model, "global_batch": gb, "seq_len": seq, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (RCCL all-reduce)",
                        "optimizer": opt_name, "hipgraph": use_graph},

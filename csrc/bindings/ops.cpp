@@ -13,6 +13,9 @@
 extern "C" {
 int tfk_gemm_launch(tfk::GemmParams p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits, hipStream_t s);
 int tfk_gemm_splits(int K, int splits);
+int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
+int tfk_mx_probe(const int*, const int*, const int*, const int*, float*, hipStream_t);
+int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, hipStream_t s);
 int tfk_bn_finalize(float*, int, int, float, const float*, const float*, float, float, float*, float*, float*, float*,
                     float*, float*, hipStream_t);
 int tfk_bn_stats(const void*, long long, int, float*, int, hipStream_t);
@@ -195,6 +198,55 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
 }
 
 int64_t gemm_splits(int K, int splits) { return tfk_gemm_splits(K, splits); }
+
+void mx_probe(torch::Tensor X, torch::Tensor Y, torch::Tensor sx, torch::Tensor sy, torch::Tensor D) {
+  for (auto* t : {&X, &Y}) { need(*t, at::kInt, "probe operand"); need_numel(*t, 64 * 8, "probe operand"); }
+  for (auto* t : {&sx, &sy}) { need(*t, at::kInt, "probe scale"); need_numel(*t, 64, "probe scale"); }
+  need_f32(D, "D"); need_numel(D, 256, "D");
+  check_rc(tfk_mx_probe(X.data_ptr<int>(), Y.data_ptr<int>(), sx.data_ptr<int>(), sy.data_ptr<int>(),
+                        D.data_ptr<float>(), cur_stream()), "mx_probe");
+}
+
+// MX-fp8: x bf16 [rows][K] -> q uint8 (e4m3) [rows][K], s uint8 (e8m0) [rows][K/32]
+void mx_quant(torch::Tensor x, torch::Tensor q, torch::Tensor s, int64_t rows, int64_t K) {
+  need_bf16(x, "x"); need(q, at::kByte, "q"); need(s, at::kByte, "s");
+  TORCH_CHECK(K % 32 == 0, "mx_quant needs K % 32 == 0");
+  need_numel(x, rows * K, "x"); need_numel(q, rows * K, "q"); need_numel(s, rows * K / 32, "s");
+  need_aligned(x, 16, "x"); need_aligned(q, 16, "q");
+  check_rc(tfk_mx_quant(x.data_ptr(), q.data_ptr(), s.data_ptr(), rows * K / 32, cur_stream()), "mx_quant");
+}
+
+// C[M][N] bf16 = epilogue(Aq[M][K] . Bq[N][K]^T) with e8m0 block scales (one per 32 K-elements).
+void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tensor Bs, torch::Tensor C, int M, int N, int K,
+                c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, int act,
+                c10::optional<torch::Tensor> aux, double drop_p, int64_t drop_seed) {
+  for (auto* t : {&A, &As, &B, &Bs}) need(*t, at::kByte, "mx operand");
+  need_bf16(C, "C");
+  TORCH_CHECK(M > 0 && N > 0 && K > 0 && K % 128 == 0, "gemm_mxfp8 needs K % 128 == 0, got ", K);
+  need_numel(A, (long long)M * K, "A"); need_numel(B, (long long)N * K, "B");
+  need_numel(As, (long long)M * K / 32, "As"); need_numel(Bs, (long long)N * K / 32, "Bs");
+  need_numel(C, (long long)M * N, "C");
+  for (auto* t : {&A, &B, &C}) need_aligned(*t, 16, "gemm_mxfp8 operand");
+  for (auto* t : {&As, &Bs}) need_aligned(*t, 4, "gemm_mxfp8 scales");
+  TORCH_CHECK(act >= 0 && act <= 3, "act");
+  TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "drop_p");
+  tfk::GemmParams p{};
+  p.A = A.data_ptr(); p.B = B.data_ptr(); p.C = C.data_ptr();
+  p.M = M; p.N = N; p.K = K; p.lda = K; p.ldb = K; p.ldc = N;
+  p.alpha = 1.f; p.act = act;
+  p.a_scale = As.data_ptr(); p.b_scale = Bs.data_ptr();
+  if (bias.has_value() && bias->defined()) { need_f32(*bias, "bias"); need_numel(*bias, N, "bias"); }
+  if (resid.has_value() && resid->defined()) { need_bf16(*resid, "resid"); need_numel(*resid, (long long)M * N, "resid"); }
+  if (aux.has_value() && aux->defined()) { need_bf16(*aux, "aux"); need_numel(*aux, (long long)M * N, "aux"); }
+  p.bias = opt_ptr<const float>(bias);
+  p.resid = opt_ptr<const void>(resid);
+  p.aux = opt_ptr<void>(aux);
+  p.drop_p = (float)drop_p;
+  p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
+  p.drop_seed = (unsigned long long)drop_seed;
+  const int ext = (p.aux || drop_p > 0.0) ? 1 : 0;
+  check_rc(tfk_gemm_mxfp8(p, ext, cur_stream()), "gemm_mxfp8");
+}
 
 void bn_finalize(torch::Tensor stats, int shards, int C, double count, torch::Tensor gamma, torch::Tensor beta, double eps,
                  double momentum, c10::optional<torch::Tensor> run_mean, c10::optional<torch::Tensor> run_var,
@@ -463,6 +515,9 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "tfk gfx950 HIP kernel library";
   m.def("gemm", &gemm);
   m.def("gemm_splits", &gemm_splits);
+  m.def("mx_quant", &mx_quant);
+  m.def("mx_probe", &mx_probe);
+  m.def("gemm_mxfp8", &gemm_mxfp8);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);

@@ -12,24 +12,49 @@ namespace {
 constexpr int NT = 256;
 
 // ---------------------------------------------------------------- forward
+// Sums NV per-channel vectors stored as [shards][NV][C] over the shards for channel c, zeroing the
+// shards for the next accumulation. 256-thread blocks = 64 channels x 4 shard groups: each thread
+// issues shards/4 independent loads (latency-bound otherwise), then a 4-way LDS reduction.
+template <int NV>
+__device__ __forceinline__ bool shard_sum(float* buf, int shards, int C, float (&out)[NV]) {
+  __shared__ float red[4][NV][64];
+  const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + l;
+  float acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = 0.f;
+  if (c < C) {
+    for (int i = g; i < shards; i += 4) {
+      float* p = buf + (long long)i * NV * C;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[v] += p[v * C + c];
+    }
+    for (int i = g; i < shards; i += 4) {
+      float* p = buf + (long long)i * NV * C;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) p[v * C + c] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) red[g][v][l] = acc[v];
+  __syncthreads();
+  if (g != 0 || c >= C) return false;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) out[v] = red[0][v][l] + red[1][v][l] + red[2][v][l] + red[3][v][l];
+  return true;
+}
+
 // stats: [shards][2][C] (sum, sumsq), zeroed again after reading so the next conv can accumulate.
-__global__ void bn_finalize_kernel(float* stats, int shards, int C, float count, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float eps, float momentum, float* __restrict__ run_mean,
-                                   float* __restrict__ run_var, float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                                   float* __restrict__ scale_out, float* __restrict__ shift_out) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f, q = 0.f;
-#pragma unroll 8
-  for (int i = 0; i < shards; ++i) {
-    s += stats[(long long)i * 2 * C + c];
-    q += stats[(long long)i * 2 * C + C + c];
-  }
-#pragma unroll 8
-  for (int i = 0; i < shards; ++i) {
-    stats[(long long)i * 2 * C + c] = 0.f;
-    stats[(long long)i * 2 * C + C + c] = 0.f;
-  }
+__global__ __launch_bounds__(256) void bn_finalize_kernel(float* stats, int shards, int C, float count,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          float eps, float momentum, float* __restrict__ run_mean,
+                                                          float* __restrict__ run_var, float* __restrict__ mean_out,
+                                                          float* __restrict__ invstd_out, float* __restrict__ scale_out,
+                                                          float* __restrict__ shift_out) {
+  float sq[2];
+  if (!shard_sum<2>(stats, shards, C, sq)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float s = sq[0], q = sq[1];
   double mean = (double)s / count;
   double var = (double)q / count - mean * mean;
   if (var < 0) var = 0;
@@ -177,21 +202,24 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ da, const bf16* __
       }
     }
   }
-  __shared__ float red[NT * 8];
-  float* st = sums + (long long)(blockIdx.x % shards) * 3 * C;
-  const int npass = y2 ? 3 : 2;
-  for (int pass = 0; pass < npass; ++pass) {
-    float* src = pass == 0 ? s0 : (pass == 1 ? s1 : s2);
-    __syncthreads();
+  // all three partial vectors to LDS at once (a pointer selecting between local arrays would put
+  // them in scratch)
+  __shared__ float red[3][NT * 8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) red[t * 8 + e] = src[e];
-    __syncthreads();
-    if (rsub == 0) {
+  for (int e = 0; e < 8; ++e) { red[0][t * 8 + e] = s0[e]; red[1][t * 8 + e] = s1[e]; red[2][t * 8 + e] = s2[e]; }
+  __syncthreads();
+  if (rsub == 0) {
+    float* st = sums + (long long)(blockIdx.x % shards) * 3 * C;
+    const int npass = y2 ? 3 : 2;
+    for (int pass = 0; pass < npass; ++pass) {
+      float acc[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = red[pass][cchunk * 8 + e];
       for (int rr = 1; rr < rows_par; ++rr)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) src[e] += red[(rr * cpr + cchunk) * 8 + e];
+        for (int e = 0; e < 8; ++e) acc[e] += red[pass][(rr * cpr + cchunk) * 8 + e];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) atomicAdd(st + pass * C + c0 + e, src[e]);
+      for (int e = 0; e < 8; ++e) atomicAdd(st + pass * C + c0 + e, acc[e]);
     }
   }
 }
@@ -199,25 +227,16 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ da, const bf16* __
 // Reduce shards; write dgamma/dbeta (+= if accumulate) and per-channel apply coefficients.
 // With k1 = gamma*invstd, dy = k1*(dz - mean(dz) - xhat*mean(dz*xhat)) is affine in (dz, y):
 // coef = [k1, A, B][C] with dy = k1*dz + A*y + B; coef2 the same for the second BN.
-__global__ void bn_bwd_finalize_kernel(float* sums, int shards, int C, float count,
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(float* sums, int shards, int C, float count,
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, const float* __restrict__ gamma2,
                                        const float* __restrict__ mean2, const float* __restrict__ invstd2,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dgamma2,
                                        float* __restrict__ dbeta2, float* __restrict__ coef, float* __restrict__ coef2) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-#pragma unroll 8
-  for (int i = 0; i < shards; ++i) {
-    const float* p = sums + (long long)i * 3 * C;
-    s0 += p[c]; s1 += p[C + c]; s2 += p[2 * C + c];
-  }
-#pragma unroll 8
-  for (int i = 0; i < shards; ++i) {
-    float* p = sums + (long long)i * 3 * C;
-    p[c] = 0.f; p[C + c] = 0.f; p[2 * C + c] = 0.f;
-  }
+  float sv[3];
+  if (!shard_sum<3>(sums, shards, C, sv)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float s0 = sv[0], s1 = sv[1], s2 = sv[2];
   dgamma[c] = s1;
   dbeta[c] = s0;
   {
@@ -314,7 +333,7 @@ extern "C" {
 int tfk_bn_finalize(float* stats, int shards, int C, float count, const float* gamma, const float* beta, float eps,
                     float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* scale,
                     float* shift, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, stats, shards, C, count, gamma, beta, eps,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, stats, shards, C, count, gamma, beta, eps,
                      momentum, run_mean, run_var, mean, invstd, scale, shift);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -347,7 +366,7 @@ int tfk_bn_bwd_finalize(float* sums, int shards, int C, float count, const float
                         const float* invstd, const float* gamma2, const float* mean2, const float* invstd2,
                         float* dgamma, float* dbeta, float* dgamma2, float* dbeta2, float* coef, float* coef2,
                         hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, sums, shards, C, count, gamma, mean,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, sums, shards, C, count, gamma, mean,
                      invstd, gamma2, mean2, invstd2, dgamma, dbeta, dgamma2, dbeta2, coef, coef2);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

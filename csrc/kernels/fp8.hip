@@ -1,0 +1,223 @@
+// MX-fp8 (OCP e4m3 + e8m0 block scales) GEMM and quantizer for gfx950.
+//
+// gfx950 runs non-scaled fp8 MFMA at the bf16 rate; the 2x fp8 rate comes only from the
+// block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (K = 128 per instruction, one e8m0 scale per
+// 32 K-elements of each row, applied in hardware). So the fp8 path is MX: operands are quantized
+// per (row, 32-wide K block) to e4m3 with a power-of-two scale chosen so the block max maps to
+// <= 448 (no saturation), and the GEMM feeds the bytes and scales straight into the scaled MFMA.
+//
+// GEMM layout: A [M][K] and B [N][K] bytes (K-inner, K % 128 == 0), scales [rows][K/32]. A K-tile
+// is 128 K-elements = 128 B per row: the same LDS image (128-B rows, XOR-swizzled 16-B chunks) and
+// loader pattern as the bf16 engine's BK=64 tiles, plus the tile's 4 scale bytes per row staged in
+// LDS. 256 threads (2x2 waves), 128x128 tiles, register-staged double buffering, one barrier per
+// K-tile, the shared bf16 epilogue (bias/act/aux/dropout/residual; gemm_epilogue.h).
+// MFMA operand map (verified against a dequantized fp32 reference in tests/test_fp8_gpu.py):
+// lane l holds row (l&15), K-elements 32*(l>>4) .. +31 of its 128-wide step, i.e. K block (l>>4),
+// whose scale byte it passes as the scale operand.
+#include "common.h"
+#include "gemm_params.h"
+#include "gemm_epilogue.h"
+
+namespace tfk {
+namespace {
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+constexpr int NTF = 256;
+constexpr int BKB = 128;  // K elements (bytes) per tile
+
+__device__ __forceinline__ int kin_off8(int row, int kc) { return row * 128 + ((kc ^ ((row >> 1) & 7)) << 4); }
+
+template <int ROWS>
+struct Fp8Loader {
+  static constexpr int NCH = ROWS * 8 / NTF;
+  const unsigned char* tb;  // this thread's first chunk (k = 0)
+  const unsigned char* sc;  // scale row of this thread (threads < ROWS), else null
+  long long ld;
+  int rows_valid;           // rows of this tile that exist
+  __device__ __forceinline__ void init(const unsigned char* base, const unsigned char* scales, long long ld_, int row0,
+                                       int lim, int sld, int sc_tid) {
+    ld = ld_;
+    rows_valid = lim - row0;
+    tb = base + (long long)(row0 + (threadIdx.x >> 3)) * ld + (threadIdx.x & 7) * 16;
+    sc = (sc_tid >= 0 && sc_tid < ROWS && row0 + sc_tid < lim) ? scales + (long long)(row0 + sc_tid) * sld : nullptr;
+  }
+  __device__ __forceinline__ void load(int kt, u32x4 (&r)[NCH], unsigned int& s) const {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int row = (threadIdx.x >> 3) + (NTF / 8) * i;
+      r[i] = row < rows_valid ? *(const u32x4*)(tb + (long long)i * (NTF / 8) * ld + kt * BKB) : u32x4{0u, 0u, 0u, 0u};
+    }
+    s = sc ? *(const unsigned int*)(sc + kt * 4) : 0u;
+  }
+  __device__ __forceinline__ void store(char* lds, unsigned int* slds, int sc_tid, const u32x4 (&r)[NCH],
+                                        unsigned int s) const {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int row = (threadIdx.x >> 3) + (NTF / 8) * i;
+      *(u32x4*)(lds + kin_off8(row, threadIdx.x & 7)) = r[i];
+    }
+    if (sc_tid >= 0 && sc_tid < ROWS) slds[sc_tid] = s;
+  }
+};
+
+__device__ __forceinline__ i32x8 frag8(const char* lds, int row, int g) {
+  const u32x4 lo = *(const u32x4*)(lds + kin_off8(row, 2 * g));
+  const u32x4 hi = *(const u32x4*)(lds + kin_off8(row, 2 * g + 1));
+  i32x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(NTF, 2) void mxfp8_gemm_kernel(GemmParams p) {
+  constexpr int WM = 2, WN = 2, TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * BKB, B_BYTES = BN * BKB;
+  constexpr int STAGE = A_BYTES + B_BYTES + (BM + BN) * 4;
+  constexpr int MAIN = 2 * STAGE;
+  constexpr int EPI_BYTES = BM * (BN + 8) * 2;
+  __shared__ __attribute__((aligned(16))) char smem[MAIN > EPI_BYTES ? MAIN : EPI_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int sld = p.K / 32;
+  const int nkt = p.K / BKB;
+
+  Fp8Loader<BM> la;
+  Fp8Loader<BN> lb;
+  la.init((const unsigned char*)p.A, (const unsigned char*)p.a_scale, p.lda, m0, p.M, sld, tid);
+  lb.init((const unsigned char*)p.B, (const unsigned char*)p.b_scale, p.ldb, n0, p.N, sld, tid - BM);
+
+  auto stage = [&](int b) { return smem + b * STAGE; };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[Fp8Loader<BM>::NCH], rb[Fp8Loader<BN>::NCH];
+  unsigned int sa = 0, sb = 0;
+  if (nkt > 0) {
+    la.load(0, ra, sa);
+    lb.load(0, rb, sb);
+    char* st = stage(0);
+    la.store(st, (unsigned int*)(st + A_BYTES + B_BYTES), tid, ra, sa);
+    lb.store(st + A_BYTES, (unsigned int*)(st + A_BYTES + B_BYTES) + BM, tid - BM, rb, sb);
+  }
+  __syncthreads();
+  const int g = lane >> 4, li = lane & 15;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      la.load(kt + 1, ra, sa);
+      lb.load(kt + 1, rb, sb);
+    }
+    const char* st = stage(cur);
+    const unsigned int* ssa = (const unsigned int*)(st + A_BYTES + B_BYTES);
+    const unsigned int* ssb = ssa + BM;
+    i32x8 af[FM], bfr[FN];
+    int sca[FM], scb[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm * TM + i * 16 + li;
+      af[i] = frag8(st, row, g);
+      sca[i] = (ssa[row] >> (8 * g)) & 0xff;
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * TN + j * 16 + li;
+      bfr[j] = frag8(st + A_BYTES, row, g);
+      scb[j] = (ssb[row] >> (8 * g)) & 0xff;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[i][j], 0, 0, 0, scb[j], 0,
+                                                                     sca[i]);
+    if (more) {
+      char* nx = stage(cur ^ 1);
+      la.store(nx, (unsigned int*)(nx + A_BYTES + B_BYTES), tid, ra, sa);
+      lb.store(nx + A_BYTES, (unsigned int*)(nx + A_BYTES + B_BYTES) + BM, tid - BM, rb, sb);
+    }
+    __syncthreads();
+  }
+  gemm_epilogue<BM, BN, NTF, WM, EPI>(p, acc, smem, m0, n0, 0);
+}
+
+// x bf16 [rows][K] -> q e4m3 [rows][K] + s e8m0 [rows][K/32]; one thread per 32-element block.
+// scale exponent e = ceil(log2(amax / 448)) so every |x| * 2^-e <= 448 (no saturation).
+__global__ void mx_quant_kernel(const bf16* __restrict__ x, unsigned char* __restrict__ q,
+                                unsigned char* __restrict__ s, long long nblocks) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nblocks; i += (long long)gridDim.x * 256) {
+    const bf16* src = x + i * 32;
+    float v[32];
+    float amax = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      bf16x8 t = *(const bf16x8*)(src + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { v[c * 8 + e] = bf2f(t[e]); amax = fmaxf(amax, fabsf(v[c * 8 + e])); }
+    }
+    int ex = amax > 0.f ? (int)ceilf(log2f(amax * (1.f / 448.f))) : -127;
+    ex = ex < -127 ? -127 : (ex > 127 ? 127 : ex);
+    const float inv = ldexpf(1.f, -ex);
+    unsigned int w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float a0 = fminf(fmaxf(v[4 * k] * inv, -448.f), 448.f), a1 = fminf(fmaxf(v[4 * k + 1] * inv, -448.f), 448.f);
+      float a2 = fminf(fmaxf(v[4 * k + 2] * inv, -448.f), 448.f), a3 = fminf(fmaxf(v[4 * k + 3] * inv, -448.f), 448.f);
+      int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+      pk = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, pk, true);
+      w[k] = (unsigned int)pk;
+    }
+    *(u32x4*)(q + i * 32) = u32x4{w[0], w[1], w[2], w[3]};
+    *(u32x4*)(q + i * 32 + 16) = u32x4{w[4], w[5], w[6], w[7]};
+    s[i] = (unsigned char)(ex + 127);
+  }
+}
+// One-wave self-test of the scaled MFMA operand maps: X/Y are [64 lanes][8] words, scales one per
+// lane, D [64 lanes][4] (lane-major) = mfma_scale(X, Y) (tests/test_fp8_gpu.py probes the layout).
+__global__ void mx_probe_kernel(const int* X, const int* Y, const int* sx, const int* sy, float* D) {
+  const int l = threadIdx.x;
+  i32x8 x, y;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { x[e] = X[l * 8 + e]; y[e] = Y[l * 8 + e]; }
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(x, y, acc, 0, 0, 0, sx[l], 0, sy[l]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) D[l * 4 + r] = acc[r];
+}
+}  // namespace
+}  // namespace tfk
+
+using namespace tfk;
+
+extern "C" {
+int tfk_mx_probe(const int* X, const int* Y, const int* sx, const int* sy, float* D, hipStream_t st) {
+  hipLaunchKernelGGL(mx_probe_kernel, dim3(1), dim3(64), 0, st, X, Y, sx, sy, D);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_mx_quant(const void* x, void* q, void* s, long long nblocks, hipStream_t st) {
+  long long g = (nblocks + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(mx_quant_kernel, dim3((unsigned)g), dim3(256), 0, st, (const bf16*)x, (unsigned char*)q,
+                     (unsigned char*)s, nblocks);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// C[M][N] bf16 = epilogue(A q[M][K] x B q[N][K]^T), scales in p.a_scale / p.b_scale.
+int tfk_gemm_mxfp8(GemmParams p, int ext, hipStream_t st) {
+  const int BM = 128, BN = 128;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  if (p.stats_shards < 1) p.stats_shards = 1;
+  dim3 grid(((p.M + BM - 1) / BM) * p.tiles_n, 1, 1);
+  if (ext)
+    hipLaunchKernelGGL((mxfp8_gemm_kernel<128, 128, EPI_BF16_EXT>), grid, dim3(NTF), 0, st, p);
+  else
+    hipLaunchKernelGGL((mxfp8_gemm_kernel<128, 128, EPI_BF16>), grid, dim3(NTF), 0, st, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

@@ -19,15 +19,13 @@
 // (split-K slabs / beta-accumulate) stored straight from the accumulators.
 #include "common.h"
 #include "gemm_params.h"
+#include "gemm_epilogue.h"
 
 namespace tfk {
 
 enum AMode { A_KIN = 0, A_KOUT = 1, A_CONV_FWD = 2, A_CONV_DGRAD = 3 };
 enum BMode { B_KIN = 0, B_KOUT = 1, B_CONV_WGRAD = 2 };
-// BNR: + fused BN-backward reduction; EXT: + aux (pre-activation) store, activation-backward
-// multiplier and dropout. Separate instantiations keep the common epilogue small enough to unroll
-// fully (a rolled epilogue indexes the accumulators dynamically -> they go to scratch).
-enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1, EPI_BF16_BNR = 2, EPI_BF16_EXT = 3 };
+
 
 // GemmParams lives in gemm_params.h (shared with the host bindings).
 
@@ -335,195 +333,7 @@ __global__ __launch_bounds__((threads_for<BM, BN>()), (threads_for<BM, BN>() == 
     __syncthreads();
   }
 
-  // Accumulator (i,j) of this lane holds C[m][n..n+3] with
-  //   m = m0 + wm*TM + i*16 + (lane&15),  n = n0 + wn*TN + j*16 + (lane>>4)*4.
-  const int ml = lane & 15, nl = (lane >> 4) * 4;
-  if constexpr (EPI == EPI_F32) {
-    float* C = (float*)p.C + bz * p.sC + (long long)blockIdx.z * p.split_stride;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * TM + i * 16 + ml;
-      if (m >= p.M) continue;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wn * TN + j * 16 + nl;
-        float* dst = C + (long long)m * p.ldc + n;
-        f32x4 v = acc[i][j] * p.alpha;
-        if (n + 3 < p.N && (p.ldc & 3) == 0) {
-          if (p.beta != 0.f) v += p.beta * *(f32x4*)dst;
-          *(f32x4*)dst = v;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) dst[r] = v[r] + (p.beta != 0.f ? p.beta * dst[r] : 0.f);
-        }
-      }
-    }
-  } else {
-    constexpr int LDC_S = BN + 8;  // padded bf16 row stride of the LDS C tile
-    bf16* Cs = (bf16*)smem;
-    float csum[FN][4], csq[FN][4];
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { csum[j][r] = 0.f; csq[j][r] = 0.f; }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int nloc = wn * TN + j * 16 + nl;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.bias) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = (n0 + nloc + r < p.N) ? p.bias[n0 + nloc + r] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int mloc = wm * TM + i * 16 + ml;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[i][j][r] * p.alpha + bv[r];
-          if constexpr (EPI != EPI_BF16_EXT) v = act_apply(v, p.act);  // EXT: in the store pass
-          csum[j][r] += v;
-          csq[j][r] += v * v;
-          o[r] = f2bf(v);
-        }
-        *(bf16x4*)(Cs + mloc * LDC_S + nloc) = o;
-      }
-    }
-    if (p.stats) {
-      // rows >= M were zero-filled -> contribute 0 (no bias in conv use).
-      float* st = p.stats + (long long)(blockIdx.x % p.stats_shards) * 2 * p.N;
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float s = csum[j][r], q = csq[j][r];
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
-          const int n = n0 + wn * TN + j * 16 + nl + r;
-          if (ml == 0 && n < p.N) { atomicAdd(st + n, s); atomicAdd(st + p.N + n, q); }
-        }
-    }
-    __syncthreads();
-    bf16* C = (bf16*)p.C + bz * p.sC;
-    constexpr int CPR = BN / 8, TOT = BM * CPR;
-    constexpr bool bnr = (EPI == EPI_BF16_BNR);
-    const int ccol = tid % CPR;  // this thread's 8-column chunk (fixed: NT % CPR == 0)
-    float r0[8], r1[8], r2[8], mu[8], is[8], sc[8], sh[8], mu2[8], is2[8];
-    if constexpr (bnr) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int n = min(n0 + ccol * 8 + e, p.N - 1);
-        r0[e] = r1[e] = r2[e] = 0.f;
-        mu[e] = p.bn_mean[n]; is[e] = p.bn_invstd[n];
-        sc[e] = p.bn_scale ? p.bn_scale[n] : 1.f; sh[e] = p.bn_shift ? p.bn_shift[n] : 0.f;
-        mu2[e] = p.bn_y2 ? p.bn_mean2[n] : 0.f; is2[e] = p.bn_y2 ? p.bn_invstd2[n] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < TOT / NT; ++it) {
-      const int idx = tid + it * NT;
-      const int row = idx / CPR, cc = idx - row * CPR;
-      const int m = m0 + row, n = n0 + cc * 8;
-      if (m >= p.M || n >= p.N) continue;
-      bf16x8 v = *(const bf16x8*)(Cs + row * LDC_S + cc * 8);
-      bf16* dst = C + (long long)m * p.ldc + n;
-      if (n + 7 < p.N && (p.ldc & 7) == 0) {
-        const long long off = bz * p.sC + (long long)m * p.ldc + n;
-        if constexpr (EPI == EPI_BF16_EXT) {
-          // pre-activation chunk: [* act'(z)] -> [aux copy] -> act -> [dropout]; 16-B coalesced
-          float f[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
-          if (p.dact_src) {
-            bf16x8 zv = *(const bf16x8*)((const bf16*)p.dact_src + off);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] *= act_grad(bf2f(zv[e]), p.dact);
-          }
-          if (p.aux) *(bf16x8*)((bf16*)p.aux + off) = v;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = act_apply(f[e], p.act);
-          if (p.drop_p > 0.f) {
-            const unsigned long long lin = (unsigned long long)m * p.N + n;
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              f[e] = u01(hash_u32(p.drop_seed, lin + e)) < 1.f - p.drop_p ? f[e] * p.drop_scale : 0.f;
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = f2bf(f[e]);
-        }
-        if (p.resid) {
-          bf16x8 rr = *(const bf16x8*)((const bf16*)p.resid + off);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[e]));
-        }
-        *(bf16x8*)dst = v;
-        if constexpr (bnr) {
-          bf16x8 yv = *(const bf16x8*)((const bf16*)p.bn_y + off);
-          bf16x8 av, y2v;
-          if (p.bn_a) av = *(const bf16x8*)((const bf16*)p.bn_a + off);
-          if (p.bn_y2) y2v = *(const bf16x8*)((const bf16*)p.bn_y2 + off);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float y = bf2f(yv[e]);
-            bool keep = p.bn_a ? (bf2f(av[e]) > 0.f) : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
-            const float dz = keep ? bf2f(v[e]) : 0.f;
-            r0[e] += dz;
-            r1[e] += dz * (y - mu[e]) * is[e];
-            if (p.bn_y2) r2[e] += dz * (bf2f(y2v[e]) - mu2[e]) * is2[e];
-          }
-        }
-      } else {
-        for (int e = 0; e < 8 && n + e < p.N; ++e) {
-          const long long off = bz * p.sC + (long long)m * p.ldc + n + e;
-          float x = bf2f(v[e]);
-          if constexpr (EPI == EPI_BF16_EXT) {
-            if (p.dact_src) x *= act_grad(bf2f(((const bf16*)p.dact_src)[off]), p.dact);
-            if (p.aux) ((bf16*)p.aux)[off] = v[e];
-            x = act_apply(x, p.act);
-            if (p.drop_p > 0.f)
-              x = u01(hash_u32(p.drop_seed, (unsigned long long)m * p.N + n + e)) < 1.f - p.drop_p ? x * p.drop_scale : 0.f;
-            x = bf2f(f2bf(x));
-          }
-          if (p.resid) x += bf2f(((const bf16*)p.resid)[off]);
-          dst[e] = f2bf(x);
-        }
-      }
-    }
-    if constexpr (bnr) {
-      // lanes sharing a column chunk: tid % CPR equal -> xor over the bits above log2(CPR)
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-#pragma unroll
-        for (int o = CPR; o < 64; o <<= 1) {
-          r0[e] += __shfl_xor(r0[e], o, 64);
-          r1[e] += __shfl_xor(r1[e], o, 64);
-          r2[e] += __shfl_xor(r2[e], o, 64);
-        }
-      __syncthreads();  // C tile no longer needed: reuse LDS for the cross-wave reduction
-      float* red = (float*)smem;  // [NW waves][3][CPR*8]
-      if (lane < CPR) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          red[(wid * 3 + 0) * (CPR * 8) + lane * 8 + e] = r0[e];
-          red[(wid * 3 + 1) * (CPR * 8) + lane * 8 + e] = r1[e];
-          red[(wid * 3 + 2) * (CPR * 8) + lane * 8 + e] = r2[e];
-        }
-      }
-      __syncthreads();
-      const int nsum = p.bn_y2 ? 3 : 2;
-      float* st = p.bn_sums + (long long)(blockIdx.x % p.bn_shards) * 3 * p.N;
-      for (int k = tid; k < nsum * CPR * 8; k += NT) {
-        const int which = k / (CPR * 8), col = k - which * (CPR * 8);
-        const int n = n0 + col;
-        if (n >= p.N) continue;
-        float v = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) v += red[(w * 3 + which) * (CPR * 8) + col];
-        atomicAdd(st + which * p.N + n, v);
-      }
-    }
-  }
+  gemm_epilogue<BM, BN, NT, WM, EPI>(p, acc, smem, m0, n0, bz);
 }
 
 }  // namespace tfk

@@ -44,5 +44,8 @@ struct GemmParams {
   // identical to misc.hip's dropout kernel on the contiguous [M][N] output (backward regenerates it)
   float drop_p, drop_scale;
   unsigned long long drop_seed;
+  // MX-fp8 engine (fp8.hip): e8m0 block scales, [rows][K/32] bytes, one per 32 K-elements
+  const void* a_scale;
+  const void* b_scale;
 };
 }  // namespace tfk

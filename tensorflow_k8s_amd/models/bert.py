@@ -43,6 +43,7 @@ class BertConfig:
     init_std: float = 0.02
     seq_len: int = 128
     max_predictions: int = 20
+    fp8: bool = False  # forward GEMMs in MX-fp8 (e4m3 + e8m0 block scales); backward bf16
 
     @classmethod
     def base(cls):
@@ -146,6 +147,10 @@ class BertForPreTraining:
         self.nsp.w.spec.from_tf = None
         self.nsp.w.spec.tf_shape = (2, W)
         self.nsp.b.spec.name = "cls/seq_relationship/output_bias"
+        if cfg.fp8:
+            for layer in self.layers:
+                for lin in (layer.qkv, layer.ao, layer.ff1, layer.ff2):
+                    lin.fp8 = True
 
     def to(self, device, seed: int = 1234):
         self.arena.finalize(device, seed)

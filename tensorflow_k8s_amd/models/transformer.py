@@ -45,6 +45,7 @@ class TransformerConfig:
     src_len: int = 256
     tgt_len: int = 256
     max_len: int = 1024
+    fp8: bool = False  # forward GEMMs in MX-fp8 (e4m3 + e8m0 block scales); backward bf16
 
     @classmethod
     def big(cls):
@@ -222,6 +223,11 @@ class Transformer:
         self.dec_ln = LayerNorm(a, "transformer/body/decoder/layer_prepostprocess/layer_norm", W, cfg.ln_eps,
                                 ("layer_norm_scale", "layer_norm_bias"))
         self._pos = None
+        if cfg.fp8:
+            for layer in self.enc + self.dec:
+                for lin in [layer.att.qkv, layer.att.out, layer.ff1, layer.ff2] + (
+                        [layer.xatt.q, layer.xatt.kv, layer.xatt.out] if isinstance(layer, DecoderLayer) else []):
+                    lin.fp8 = True
 
     def to(self, device, seed: int = 1234):
         self.arena.finalize(device, seed)
@@ -246,7 +252,8 @@ class Transformer:
         for i, layer in enumerate(self.dec):
             y = layer.forward(y, mem, B, St, Ss, src_len, _mix(seed, 200 + i), training)
         yo, st_y = self.dec_ln.forward(y)
-        logits = G.linear_fwd(yo, self.emb.table.compute)  # tied softmax weights
+        from ..runtime.layers import linear_forward
+        logits = linear_forward(yo, self.emb.table.compute, None, self.cfg.fp8)  # tied softmax weights
         return logits, (x, mem, st_m, y, yo, st_y)
 
     def forward_backward(self, src, tgt_in, tgt_out, src_len, loss_scale: float = 1.0):

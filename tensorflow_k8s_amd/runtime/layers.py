@@ -27,6 +27,14 @@ def _hwio_to_ohwi(a: np.ndarray, cin_pad: int | None = None) -> np.ndarray:
     return np.ascontiguousarray(np.transpose(a, (3, 0, 1, 2)))
 
 
+def linear_forward(x, w, b, fp8: bool, **kw):
+    """bf16 GEMM, or the MX-fp8 block-scaled MFMA GEMM when fp8 and K % 128 == 0."""
+    if fp8 and x.shape[-1] % 128 == 0:
+        from ..ops.fp8 import linear_fwd_mx
+        return linear_fwd_mx(x, w, b, **kw)
+    return G.linear_fwd(x, w, b, **kw)
+
+
 class Conv2d:
     """NHWC conv, OHWI weight. TF variable: <name>/kernel in HWIO."""
 
@@ -129,10 +137,11 @@ class Linear:
                                      from_tf=lambda a: np.ascontiguousarray(a.T), tf_shape=(fin, fout)))
         self.b = arena.add(ParamSpec(f"{name}/bias", (fout,), init="zeros", decay=False)) if bias else None
         self.arena = arena
+        self.fp8 = False  # forward GEMM in MX-fp8 (ops.fp8); backward stays bf16
 
     def forward(self, x, act=None, resid=None, aux=None, drop_p: float = 0.0, drop_seed: int = 0):
-        return G.linear_fwd(x, self.w.compute, self.b.master if self.b else None, act=act, resid=resid, aux=aux,
-                            drop_p=drop_p, drop_seed=drop_seed)
+        return linear_forward(x, self.w.compute, self.b.master if self.b else None, self.fp8, act=act, resid=resid,
+                              aux=aux, drop_p=drop_p, drop_seed=drop_seed)
 
     def backward(self, dy, x, need_dx: bool = True, resid=None, accumulate: bool = False, dact_src=None,
                  dact=None):
@@ -159,6 +168,7 @@ class FusedLinear:
         self.arena, self.fin, self.fout, self.names = arena, fin, fout, names
         self.parts = [Linear(arena, n, fin, fout, init=init, std=std, bias=bias) for n in names]
         self.has_bias = bias
+        self.fp8 = False
         self._views = None
 
     def _build(self):
@@ -186,7 +196,7 @@ class FusedLinear:
 
     def forward(self, x, act=None):
         w, _, b, _ = self.views()
-        return G.linear_fwd(x, w, b, act=act)
+        return linear_forward(x, w, b, self.fp8, act=act)
 
     def backward(self, dy, x, need_dx: bool = True, resid=None):
         w, gw, _, gb = self.views()

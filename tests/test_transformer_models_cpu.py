@@ -75,3 +75,18 @@ def test_transformer_trains_with_dropout():
         opt.step()
         losses.append(float(loss.mean()))
     assert losses[-1] < losses[0]
+
+
+def test_transformer_fp8_forward_close_to_bf16():
+    """MX-fp8 forward GEMMs (CPU reference of the quantized product) keep the loss and the
+    gradients close to the bf16 model."""
+    from tensorflow_k8s_amd.models.transformer import Transformer, TransformerConfig
+    res = {}
+    for fp8 in (False, True):
+        cfg = TransformerConfig(vocab_size=500, hidden=128, enc_layers=1, dec_layers=1, heads=2, ffn=256, src_len=16,
+                                tgt_len=16, max_len=32, dropout=0.0, attn_dropout=0.0, relu_dropout=0.0, fp8=fp8)
+        m = Transformer(cfg).to("cpu", seed=4)
+        loss, _ = m.forward_backward(*m.synthetic_batch(2, "cpu", seed=1))
+        res[fp8] = (float(loss.mean()), m.arena.grad.clone())
+    assert abs(res[True][0] - res[False][0]) / res[False][0] < 0.02
+    assert _cos(res[True][1], res[False][1]) > 0.98

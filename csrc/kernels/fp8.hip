@@ -11,9 +11,11 @@
 // loader pattern as the bf16 engine's BK=64 tiles, plus the tile's 4 scale bytes per row staged in
 // LDS. 256 threads (2x2 waves), 128x128 tiles, register-staged double buffering, one barrier per
 // K-tile, the shared bf16 epilogue (bias/act/aux/dropout/residual; gemm_epilogue.h).
-// MFMA operand map (verified against a dequantized fp32 reference in tests/test_fp8_gpu.py):
-// lane l holds row (l&15), K-elements 32*(l>>4) .. +31 of its 128-wide step, i.e. K block (l>>4),
-// whose scale byte it passes as the scale operand.
+// MFMA operand map (measured with tools/mx_probe.py / tools/mx_diag.py, checked against a
+// dequantized fp32 reference in tests/test_fp8_gpu.py): lane l holds row (l&15); its 32 operand
+// bytes are K-elements 16g..16g+15 (bytes 0-15) and 64+16g..64+16g+15 (bytes 16-31), g = l>>4,
+// i.e. 16-B chunks g and g+4 of the 128-B row. The scale operand of lane group g is the scale of
+// K block g (K-elements 32g..32g+31), so the four scale bytes of a row go to groups 0..3 in order.
 #include "common.h"
 #include "gemm_params.h"
 #include "gemm_epilogue.h"
@@ -60,8 +62,8 @@ struct Fp8Loader {
 };
 
 __device__ __forceinline__ i32x8 frag8(const char* lds, int row, int g) {
-  const u32x4 lo = *(const u32x4*)(lds + kin_off8(row, 2 * g));
-  const u32x4 hi = *(const u32x4*)(lds + kin_off8(row, 2 * g + 1));
+  const u32x4 lo = *(const u32x4*)(lds + kin_off8(row, g));
+  const u32x4 hi = *(const u32x4*)(lds + kin_off8(row, g + 4));
   i32x8 r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];

@@ -55,5 +55,5 @@ def test_mx_linear_epilogues(M, N, K):
     assert rel(out["cuda"][0], out["cpu"][0]) < 1e-2
     assert rel(out["cuda"][1], out["cpu"][1]) < 1e-2
     # fp8 vs bf16 GEMM: MX-e4m3 quantization error only
-    yb = (x.float() @ w.float().t())
+    yb = x.float() @ w.float().t() + b
     assert rel(out["cuda"][1].float(), yb) < 0.06

@@ -46,6 +46,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--only", default="")
+    ap.add_argument("--fp8", type=int, default=1, help="also time the MX-fp8 forward GEMM")
     args = ap.parse_args()
     dev = "cuda"
     for name, (M, N, K) in SHAPES.items():
@@ -60,6 +61,14 @@ def main():
         r["tfk_fwd"] = fl / timeit(lambda: G.linear_fwd(x, w), args.iters) / 1e12
         r["tfk_dgrad"] = fl / timeit(lambda: G.linear_dgrad(dy, w), args.iters) / 1e12
         r["tfk_wgrad"] = fl / timeit(lambda: G.linear_wgrad(dy, x, gw), args.iters) / 1e12
+        if args.fp8 and K % 128 == 0:
+            from tensorflow_k8s_amd.ops import fp8 as F8
+            xq, wq = F8.mx_quantize(x), F8.mx_quantize(w)
+            y8 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            G.lib().gemm_mxfp8(xq[0], xq[1], wq[0], wq[1], y8, M, N, K, None, None, 0, None, 0.0, 0)
+            gemm8 = lambda: G.lib().gemm_mxfp8(xq[0], xq[1], wq[0], wq[1], y8, M, N, K, None, None, 0, None, 0.0, 0)  # noqa: E731
+            r["tfk_mxfp8_gemm"] = fl / timeit(gemm8, args.iters) / 1e12
+            r["tfk_mxfp8_fwd_incl_quant"] = fl / timeit(lambda: F8.linear_fwd_mx(x, w, wq=wq), args.iters) / 1e12
         r["blas_fwd"] = fl / timeit(lambda: x @ w.t(), args.iters) / 1e12
         r["blas_dgrad"] = fl / timeit(lambda: dy @ w, args.iters) / 1e12
         r["blas_wgrad"] = fl / timeit(lambda: dy.t() @ x, args.iters) / 1e12

@@ -13,6 +13,7 @@
 extern "C" {
 int tfk_gemm_launch(tfk::GemmParams p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits, hipStream_t s);
 int tfk_gemm_splits(int K, int splits);
+void tfk_gemm_set_persist(int on);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_probe(const int*, const int*, const int*, const int*, float*, hipStream_t);
 int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, hipStream_t s);
@@ -65,7 +66,8 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
           c10::optional<torch::Tensor> resid, int act, c10::optional<torch::Tensor> stats, int shards, int splits,
           int batch, int64_t sA, int64_t sB, int64_t sC, int64_t split_stride, std::vector<int64_t> conv,
           std::vector<c10::optional<torch::Tensor>> bnr, int bn_relu, int bn_shards, c10::optional<torch::Tensor> aux,
-          c10::optional<torch::Tensor> dact_src, int dact, double drop_p, int64_t drop_seed) {
+          c10::optional<torch::Tensor> dact_src, int dact, double drop_p, int64_t drop_seed,
+          std::vector<int64_t> rowmap) {
   need_bf16(A, "A");
   need_bf16(B, "B");
   TORCH_CHECK(epi == 0 || epi == 1, "epi");
@@ -135,9 +137,10 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
     need_numel(C, bC + (long long)(ns - 1) * split_stride + (long long)(M - 1) * ldc + N, "C");
   }
   if (bias.has_value() && bias->defined()) { need_f32(*bias, "bias"); need_numel(*bias, N, "bias"); }
+  const bool resid_sub = rowmap.size() == 14 && rowmap[12] > 0;  // checked with the row maps below
   if (resid.has_value() && resid->defined()) {
     need_bf16(*resid, "resid");
-    need_numel(*resid, bC + (long long)(M - 1) * ldc + N, "resid");
+    if (!resid_sub) need_numel(*resid, bC + (long long)(M - 1) * ldc + N, "resid");
   }
   if (stats.has_value() && stats->defined()) {
     need_f32(*stats, "stats");
@@ -191,13 +194,44 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   p.drop_p = (float)drop_p;
   p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
   p.drop_seed = (unsigned long long)drop_seed;
+  const bool dense_a = amode == A_KIN || amode == A_KOUT;
   TORCH_CHECK((bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64) ||
-                  (bm == 256 && bn == 256 && (amode == A_KIN || amode == A_KOUT) && (bmode == B_KIN || bmode == B_KOUT)),
+                  (bm == 256 && bn == 256 && dense_a && (bmode == B_KIN || bmode == B_KOUT)) ||
+                  (bm == 256 && bn == 64 && dense_a && !(amode == A_KOUT && bmode == B_KOUT && epi == 0)),
               "unsupported tile ", bm, "x", bn, " for operand modes ", amode, "/", bmode);
+  // row maps: [om_hp, om_wp, om_h, om_w, om_sh, om_sw, om_a, om_b, rs_h, rs_w, rs_p, rs_q, rs_sh, rs_sw]
+  if (!rowmap.empty()) {
+    TORCH_CHECK(rowmap.size() == 14, "rowmap needs 14 ints");
+    TORCH_CHECK(!bnr.empty() && epi == 0 && batch == 1, "row maps need the fused BN-backward bf16 epilogue");
+    const auto& r = rowmap;
+    for (int i = 0; i < 14; ++i) TORCH_CHECK(r[i] >= 0, "rowmap entries must be >= 0");
+    if (r[0] > 0) {
+      TORCH_CHECK(r[4] >= 1 && r[5] >= 1 && r[6] < r[4] && r[7] < r[5], "out-map stride/phase");
+      TORCH_CHECK(M % (r[0] * r[1]) == 0, "out-map: M must be images x om_hp x om_wp");
+      TORCH_CHECK((r[0] - 1) * r[4] + r[6] < r[2] && (r[1] - 1) * r[5] + r[7] < r[3], "out-map exceeds the output grid");
+      const long long rows = (long long)(M / (r[0] * r[1])) * r[2] * r[3];
+      need_numel(C, (rows - 1) * ldc + N, "C (out-map)");
+      for (int i : {0, 1, 6})
+        if (bnr[i].has_value() && bnr[i]->defined()) need_numel(*bnr[i], rows * N, "bn tensor (out-map)");
+      if (resid.has_value() && resid->defined()) need_numel(*resid, (rows - 1) * ldc + N, "resid (out-map)");
+    }
+    if (r[12] > 0) {
+      TORCH_CHECK(r[13] >= 1 && r[8] > 0 && r[9] > 0 && r[10] == (r[8] + r[12] - 1) / r[12] &&
+                      r[11] == (r[9] + r[13] - 1) / r[13], "resid sub-sampling geometry");
+      TORCH_CHECK(r[0] == 0, "resid sub-sampling and out-map are exclusive");
+      TORCH_CHECK(M % (r[8] * r[9]) == 0, "resid sub-sampling: M must be images x rs_h x rs_w");
+      TORCH_CHECK(resid.has_value() && resid->defined(), "resid sub-sampling needs resid");
+      need_numel(*resid, (long long)(M / (r[8] * r[9])) * r[10] * r[11] * ldc, "resid (sub-sampled)");
+    }
+    p.om_hp = r[0]; p.om_wp = r[1]; p.om_h = r[2]; p.om_w = r[3]; p.om_sh = r[4]; p.om_sw = r[5]; p.om_a = r[6];
+    p.om_b = r[7]; p.rs_h = r[8]; p.rs_w = r[9]; p.rs_p = r[10]; p.rs_q = r[11]; p.rs_sh = r[12]; p.rs_sw = r[13];
+  }
   check_rc(tfk_gemm_launch(p, bm, bn, amode, bmode, epi, batch, splits, cur_stream()), "gemm");
 }
 
 int64_t gemm_splits(int K, int splits) { return tfk_gemm_splits(K, splits); }
+// A/B switch for the persistent GEMM grid (tools/op_profile.py); default on.
+void gemm_set_persist(int on) { tfk_gemm_set_persist(on); }
 
 void mx_probe(torch::Tensor X, torch::Tensor Y, torch::Tensor sx, torch::Tensor sy, torch::Tensor D) {
   for (auto* t : {&X, &Y}) { need(*t, at::kInt, "probe operand"); need_numel(*t, 64 * 8, "probe operand"); }
@@ -515,6 +549,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "tfk gfx950 HIP kernel library";
   m.def("gemm", &gemm);
   m.def("gemm_splits", &gemm_splits);
+  m.def("gemm_set_persist", &gemm_set_persist);
   m.def("mx_quant", &mx_quant);
   m.def("mx_probe", &mx_probe);
   m.def("gemm_mxfp8", &gemm_mxfp8);

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(NTF, 2) void mxfp8_gemm_kernel(GemmParams p) {
   constexpr int A_BYTES = BM * BKB, B_BYTES = BN * BKB;
   constexpr int STAGE = A_BYTES + B_BYTES + (BM + BN) * 4;
   constexpr int MAIN = 2 * STAGE;
-  constexpr int EPI_BYTES = BM * (BN + 8) * 2;
+  constexpr int EPI_BYTES = epi_lds_bytes<BM, BN, WM>();
   __shared__ __attribute__((aligned(16))) char smem[MAIN > EPI_BYTES ? MAIN : EPI_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;

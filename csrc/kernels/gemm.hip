@@ -252,9 +252,35 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rb, int kk) {
   }
 }
 
+// Tile walk. One-shot grid (gridDim.x == tiles): the XCD remap. Persistent grid (gridDim.x <
+// tiles, a multiple of 8 sized to the resident block count): block b serves a contiguous tile range
+// of its XCD (b & 7 under round-robin dispatch), striding by that XCD's block count, so the blocks
+// of one XCD walk neighbouring tiles together (shared A panels stay in that XCD's L2).
+struct TileWalk {
+  int cur, end, step;
+  __device__ __forceinline__ explicit TileWalk(int ntiles) {
+    const int G = gridDim.x, b = blockIdx.x;
+    if (G >= ntiles) {
+      cur = xcd_remap(b, G); end = cur + 1; step = 1;
+    } else {
+      const int x = b & 7, q = ntiles >> 3, r = ntiles & 7;
+      const int start = x * q + (x < r ? x : r);
+      cur = start + (b >> 3); end = start + q + (x < r ? 1 : 0); step = G >> 3;
+    }
+  }
+};
+
 template <int BM, int BN, int AM, int BMD, int EPI>
 __global__ __launch_bounds__((threads_for<BM, BN>()), (threads_for<BM, BN>() == 512 ? 1 : 2)) void gemm_kernel(GemmParams p) {
   constexpr int NT = threads_for<BM, BN>();
+  // Persistent walk over several tiles: the next tile's first K-tile is loaded into registers
+  // before this tile's last MFMAs and stays in flight through the epilogue, so a short-K
+  // (memory-bound) GEMM keeps HBM busy while it stores. The 8-wave 256x256 tile (long-K GEMMs,
+  // one block per CU, no registers to spare) stays one-shot.
+  // Dense A operands only: the conv gathers keep per-chunk geometry in registers and have none
+  // left for an in-flight next tile (they spill); their GEMMs are long-K (3x3) or strided anyway.
+  // (256x64 with the BN-backward epilogue: one-shot, its row maps + 8-chunk A prefetch spill)
+  constexpr bool PERSIST = NT == 256 && (AM == A_KIN || AM == A_KOUT) && !(BM == 256 && EPI == EPI_BF16_BNR);
   constexpr int NW = NT / 64;                    // waves
   constexpr int WM = 2, WN = NW / WM;            // wave grid
   constexpr int TM = BM / WM, TN = BN / WN;      // wave tile
@@ -263,91 +289,144 @@ __global__ __launch_bounds__((threads_for<BM, BN>()), (threads_for<BM, BN>() == 
   constexpr bool A_KOUT_ = (AM == A_KOUT);
   constexpr bool B_KOUT_ = (BMD == B_KOUT || BMD == B_CONV_WGRAD);
   constexpr int MAIN_BYTES = 2 * (A_BYTES + B_BYTES);
-  constexpr int EPI_BYTES = (EPI == EPI_F32) ? 0 : BM * (BN + 8) * 2;
+  constexpr int EPI_BYTES = (EPI == EPI_F32) ? 0 : epi_lds_bytes<BM, BN, WM>();
   __shared__ __attribute__((aligned(16))) char smem[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
   char* As = smem;
   char* Bs = smem + 2 * A_BYTES;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
   const int bz = blockIdx.y;
   const bf16* Ab = (const bf16*)p.A + bz * p.sA;
   const bf16* Bb = (const bf16*)p.B + bz * p.sB;
 
   const int nkt = (p.K + BK - 1) / BK;
   const int kt0 = blockIdx.z * p.kt_per_split;
-  const int kt1 = min(nkt, kt0 + p.kt_per_split);
+  const int kt1 = min(nkt, kt0 + p.kt_per_split);  // the launcher gives every split >= 1 K-tile
+
+  TileWalk walk(((p.M + BM - 1) / BM) * p.tiles_n);
+  if (walk.cur >= walk.end) return;  // block-uniform
+  int m0 = (walk.cur / p.tiles_n) * BM, n0 = (walk.cur % p.tiles_n) * BN;
 
   Loader<BM, AM, true, NT> la;
   Loader<BN, BMD, false, NT> lb;
   la.S_ = p.S; lb.S_ = p.S;
   la.init(p, Ab, p.lda, m0, p.M, kt0);
   lb.init(p, Bb, p.ldb, n0, p.N, kt0);
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   u32x4 ra[Loader<BM, AM, true, NT>::NCH], rb[Loader<BN, BMD, false, NT>::NCH];
-  if (kt0 < kt1) {
-    la.load(p, kt0, m0, ra);
-    lb.load(p, kt0, n0, rb);
+  la.load(p, kt0, m0, ra);
+  lb.load(p, kt0, n0, rb);
+
+  for (;;) {
     la.store_lds(As, ra);
     lb.store_lds(Bs, rb);
-  }
-  __syncthreads();
-
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) {
-      if constexpr (AM == A_CONV_FWD) la.advance(p.Cin);
-      if constexpr (AM == A_CONV_DGRAD) la.advance(p.Cout);
-      la.load(p, kt + 1, m0, ra);
-      lb.load(p, kt + 1, n0, rb);
-    }
-    const char* Ac = As + cur * A_BYTES;
-    const char* Bc = Bs + cur * B_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, A_KOUT_>(Ac, wm * TM + i * 16, kk);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, B_KOUT_>(Bc, wn * TN + j * 16, kk);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
-    if (more) {
-      la.store_lds(As + (cur ^ 1) * A_BYTES, ra);
-      lb.store_lds(Bs + (cur ^ 1) * B_BYTES, rb);
-    }
     __syncthreads();
-  }
 
-  gemm_epilogue<BM, BN, NT, WM, EPI>(p, acc, smem, m0, n0, bz);
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nxt = walk.cur + walk.step;
+    const bool has_next = PERSIST && nxt < walk.end;
+    const int nm0 = (nxt / p.tiles_n) * BM, nn0 = (nxt % p.tiles_n) * BN;
+
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      const bool more = kt + 1 < kt1;
+      if (more) {
+        if constexpr (AM == A_CONV_FWD) la.advance(p.Cin);
+        if constexpr (AM == A_CONV_DGRAD) la.advance(p.Cout);
+        la.load(p, kt + 1, m0, ra);
+        lb.load(p, kt + 1, n0, rb);
+      } else if (has_next) {
+        // issue-early: the next tile's first K-tile flies during the last MFMAs + epilogue
+        la.init(p, Ab, p.lda, nm0, p.M, kt0);
+        lb.init(p, Bb, p.ldb, nn0, p.N, kt0);
+        la.load(p, kt0, nm0, ra);
+        lb.load(p, kt0, nn0, rb);
+      }
+      const char* Ac = As + cur * A_BYTES;
+      const char* Bc = Bs + cur * B_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, A_KOUT_>(Ac, wm * TM + i * 16, kk);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, B_KOUT_>(Bc, wn * TN + j * 16, kk);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+      if (more) {
+        la.store_lds(As + (cur ^ 1) * A_BYTES, ra);
+        lb.store_lds(Bs + (cur ^ 1) * B_BYTES, rb);
+      }
+      __syncthreads();
+    }
+
+    gemm_epilogue<BM, BN, NT, WM, EPI>(p, acc, smem, m0, n0, bz);
+    if (!has_next) break;
+    walk.cur = nxt; m0 = nm0; n0 = nn0;
+    __syncthreads();  // every wave is done reading the epilogue's LDS before stage 0 is rewritten
+  }
 }
 
 }  // namespace tfk
 
 using namespace tfk;
 
-#define TFK_GEMM_CASE(BM_, BN_, AM_, BM2_, EPI_)                                                  \
-  if (bm == BM_ && bn == BN_ && amode == AM_ && bmode == BM2_ && epi == EPI_) {                  \
-    hipLaunchKernelGGL((gemm_kernel<BM_, BN_, AM_, BM2_, EPI_>), grid, dim3((threads_for<BM_, BN_>())), 0, stream, p); \
-    return hipGetLastError() == hipSuccess ? 0 : -2;                                              \
+// Persistent grids on (default) unless TFK_GEMM_PERSIST=0 or tfk_gemm_set_persist(0).
+static int g_persist = -1;
+static bool persist_on() {
+  if (g_persist < 0) {
+    const char* e = getenv("TFK_GEMM_PERSIST");
+    g_persist = (e && e[0] == '0') ? 0 : 1;
   }
-#define TFK_GEMM_TILES(AM_, BM2_, EPI_) \
+  return g_persist == 1;
+}
+extern "C" void tfk_gemm_set_persist(int on) { g_persist = on ? 1 : 0; }
+
+// Launch one instantiation. 4-wave tiles with more tiles than resident blocks get a persistent
+// grid of exactly the resident count (occupancy query, cached per instantiation; a multiple of 8
+// so TileWalk's XCD split holds).
+template <int BM_, int BN_, int AM_, int BM2_, int EPI_>
+static int launch_gemm(const GemmParams& p, int tiles, int batch, int splits, hipStream_t stream) {
+  constexpr int NT = threads_for<BM_, BN_>();
+  int gx = tiles;
+  constexpr bool can_persist = NT == 256 && (AM_ == A_KIN || AM_ == A_KOUT) && !(BM_ == 256 && EPI_ == EPI_BF16_BNR);
+  if (can_persist && persist_on()) {
+    static int resident = 0;
+    if (resident == 0) {
+      int dev = 0, cus = 0, per_cu = 0;
+      if (hipGetDevice(&dev) == hipSuccess &&
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_kernel<BM_, BN_, AM_, BM2_, EPI_>, NT, 0) ==
+              hipSuccess &&
+          cus > 0 && per_cu > 0)
+        resident = (cus * per_cu) & ~7;
+      else
+        resident = -1;
+    }
+    if (resident >= 8 && tiles > resident) gx = resident;
+  }
+  hipLaunchKernelGGL((gemm_kernel<BM_, BN_, AM_, BM2_, EPI_>), dim3(gx, batch, splits), dim3(NT), 0, stream, p);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+#define TFK_GEMM_CASE(BM_, BN_, AM_, BM2_, EPI_)                                 \
+  if (bm == BM_ && bn == BN_ && amode == AM_ && bmode == BM2_ && epi == EPI_) { \
+    return launch_gemm<BM_, BN_, AM_, BM2_, EPI_>(p, tiles_m * tiles_n, batch, splits, stream); \
+  }
+// gather A modes (conv fwd/dgrad): 3 tiles (a 256-row gather tile needs more registers than exist)
+#define TFK_GEMM_TILES3(AM_, BM2_, EPI_) \
   TFK_GEMM_CASE(128, 128, AM_, BM2_, EPI_) TFK_GEMM_CASE(128, 64, AM_, BM2_, EPI_) TFK_GEMM_CASE(64, 64, AM_, BM2_, EPI_)
-// + the 256x256 (8-wave) tile for the dense (non-gather) operand modes
+// + the 256x64 tile (narrow-N GEMMs: twice the MFMA work per K-tile barrier of 128x64)
+#define TFK_GEMM_TILES(AM_, BM2_, EPI_) TFK_GEMM_TILES3(AM_, BM2_, EPI_) TFK_GEMM_CASE(256, 64, AM_, BM2_, EPI_)
 #define TFK_GEMM_TILES_BIG(AM_, BM2_, EPI_) TFK_GEMM_TILES(AM_, BM2_, EPI_) TFK_GEMM_CASE(256, 256, AM_, BM2_, EPI_)
 
 // Host launcher. Grid: x = tiles (M x N), y = batch, z = split-K. Returns 0 on success.
@@ -361,7 +440,6 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
   splits = nkt > 0 ? (nkt + p.kt_per_split - 1) / p.kt_per_split : 1;
   p.tiles_n = tiles_n;
   if (p.stats_shards < 1) p.stats_shards = 1;
-  dim3 grid(tiles_m * tiles_n, batch, splits);
   if (epi == EPI_BF16 && p.bn_sums) epi = EPI_BF16_BNR;
   if (epi == EPI_BF16 && (p.aux || p.dact_src || p.drop_p > 0.f)) epi = EPI_BF16_EXT;
   TFK_GEMM_TILES_BIG(A_KIN, B_KIN, EPI_BF16)
@@ -369,18 +447,18 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
   TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_BF16)
   TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_F32)
   TFK_GEMM_TILES_BIG(A_KOUT, B_KOUT, EPI_F32)
-  TFK_GEMM_TILES_BIG(A_KOUT, B_KOUT, EPI_BF16)
-  TFK_GEMM_TILES(A_CONV_FWD, B_KIN, EPI_BF16)
-  TFK_GEMM_TILES(A_CONV_DGRAD, B_KIN, EPI_BF16)
-  TFK_GEMM_TILES(A_CONV_DGRAD, B_KOUT, EPI_BF16)
+  TFK_GEMM_TILES3(A_KOUT, B_KOUT, EPI_BF16) TFK_GEMM_CASE(256, 256, A_KOUT, B_KOUT, EPI_BF16)
+  TFK_GEMM_TILES3(A_CONV_FWD, B_KIN, EPI_BF16)
+  TFK_GEMM_TILES3(A_CONV_DGRAD, B_KIN, EPI_BF16)
+  TFK_GEMM_TILES3(A_CONV_DGRAD, B_KOUT, EPI_BF16)
   TFK_GEMM_TILES(A_KOUT, B_CONV_WGRAD, EPI_F32)
   // transformer epilogue extras: fwd (aux/dropout) and dgrad (activation backward)
   TFK_GEMM_TILES_BIG(A_KIN, B_KIN, EPI_BF16_EXT)
   TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_BF16_EXT)
   // fused BN-backward reduction: only the dgrad producers of a BN input
   TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_BF16_BNR)
-  TFK_GEMM_TILES(A_CONV_DGRAD, B_KIN, EPI_BF16_BNR)
-  TFK_GEMM_TILES(A_CONV_DGRAD, B_KOUT, EPI_BF16_BNR)
+  TFK_GEMM_TILES3(A_CONV_DGRAD, B_KIN, EPI_BF16_BNR)
+  TFK_GEMM_TILES3(A_CONV_DGRAD, B_KOUT, EPI_BF16_BNR)
   return -1;  // unsupported combination
 }
 

@@ -12,6 +12,41 @@ namespace tfk {
 // fully (a rolled epilogue indexes the accumulators dynamically -> they go to scratch).
 enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1, EPI_BF16_BNR = 2, EPI_BF16_EXT = 3 };
 
+// LDS the bf16 epilogues need: the padded C tile + the [2][WM][BN] f32 BN-statistics partials.
+template <int BM, int BN, int WM>
+constexpr int epi_lds_bytes() { return BM * (BN + 8) * 2 + 2 * WM * BN * 4; }
+
+// DPP row rotate (16-lane rows); rotates stay inside the row so every source lane is valid.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// Sum over the 16 lanes of a DPP row; every lane of the row gets the total (VALU only, no LDS).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f32<0x128>(v);  // row_ror:8
+  v += dpp_f32<0x124>(v);  // row_ror:4
+  v += dpp_f32<0x122>(v);  // row_ror:2
+  v += dpp_f32<0x121>(v);  // row_ror:1
+  return v;
+}
+
+// Output row of GEMM row m under the out-map (identity without one).
+__device__ __forceinline__ long long out_row(const GemmParams& p, int m) {
+  if (p.om_hp == 0) return m;
+  const int hw = p.om_hp * p.om_wp;
+  const int n = m / hw, rem = m - n * hw, h = rem / p.om_wp, w = rem - h * p.om_wp;
+  return ((long long)n * p.om_h + h * p.om_sh + p.om_a) * p.om_w + w * p.om_sw + p.om_b;
+}
+// Residual row of output row mo (-1: off the sub-sampling lattice -> no residual).
+__device__ __forceinline__ long long resid_row(const GemmParams& p, long long mo) {
+  if (p.rs_sh == 0) return mo;
+  const long long hw = (long long)p.rs_h * p.rs_w;
+  const long long n = mo / hw;
+  const int rem = (int)(mo - n * hw), h = rem / p.rs_w, w = rem - h * p.rs_w;
+  if (h % p.rs_sh != 0 || w % p.rs_sw != 0) return -1;
+  return (n * p.rs_p + h / p.rs_sh) * p.rs_q + w / p.rs_sw;
+}
+
 template <int BM, int BN, int NT, int WM, int EPI>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[BM / WM / 16][BN / (NT / 64 / WM) / 16],
                                               char* smem, int m0, int n0, int bz) {
@@ -73,21 +108,36 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         *(bf16x4*)(Cs + mloc * LDC_S + nloc) = o;
       }
     }
+    // BN batch statistics (rows >= M were zero-filled -> contribute 0; no bias in conv use):
+    // 16-lane row sums by DPP, the WM waves of a column meet in LDS behind the C tile, then ONE
+    // coalesced atomic per (column, stat) per block instead of 4-lane atomics per wave.
+    float* red = (float*)(smem + BM * LDC_S * 2);  // [2][WM][BN]
     if (p.stats) {
-      // rows >= M were zero-filled -> contribute 0 (no bias in conv use).
-      float* st = p.stats + (long long)(blockIdx.x % p.stats_shards) * 2 * p.N;
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float s = csum[j][r], q = csq[j][r];
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
-          const int n = n0 + wn * TN + j * 16 + nl + r;
-          if (ml == 0 && n < p.N) { atomicAdd(st + n, s); atomicAdd(st + p.N + n, q); }
+          const float s = row16_sum(csum[j][r]), q = row16_sum(csq[j][r]);
+          if (ml == 0) {
+            const int nloc = wn * TN + j * 16 + nl + r;
+            red[wm * BN + nloc] = s;
+            red[(WM + wm) * BN + nloc] = q;
+          }
         }
     }
     __syncthreads();
+    if (p.stats) {
+      float* st = p.stats + (long long)(blockIdx.x % p.stats_shards) * 2 * p.N;
+      for (int t = tid; t < 2 * BN; t += NT) {
+        const int w = t / BN, col = t - w * BN, n = n0 + col;
+        if (n < p.N) {
+          float v = 0.f;
+#pragma unroll
+          for (int k = 0; k < WM; ++k) v += red[(w * WM + k) * BN + col];
+          atomicAdd(st + (long long)w * p.N + n, v);
+        }
+      }
+    }
     bf16* C = (bf16*)p.C + bz * p.sC;
     constexpr int CPR = BN / 8, TOT = BM * CPR;
     constexpr bool bnr = (EPI == EPI_BF16_BNR);
@@ -103,16 +153,104 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         mu2[e] = p.bn_y2 ? p.bn_mean2[n] : 0.f; is2[e] = p.bn_y2 ? p.bn_invstd2[n] : 0.f;
       }
     }
+    // Interior tile (block-uniform): the store pass runs in groups of G chunks whose global loads
+    // (residual, BN inputs, activation-backward source) are ALL issued before the group's first
+    // store. Written load -> store per chunk, the compiler cannot hoist the next chunk's loads over
+    // a store that may alias them, and every chunk paid two full memory latencies (vmcnt(0) before
+    // and after its store: measured 3 TB/s on the BN-backward dgrads). Loads are unconditional from
+    // always-valid addresses (absent tensors alias y / C) so no per-element branch splits them.
+    const bool tile_fast = (m0 + BM <= p.M) && (n0 + BN <= p.N) && ((p.ldc & 7) == 0);
+    constexpr int NIT = TOT / NT;
+    constexpr int G = bnr ? 1 : (EPI == EPI_BF16_EXT ? (NIT < 2 ? NIT : 2) : (NIT < 4 ? NIT : 4));
+    if (tile_fast) {
+      const bf16* resid_b = p.resid ? (const bf16*)p.resid : (const bf16*)p.C;
+      const bf16* dsrc_b = (EPI == EPI_BF16_EXT && p.dact_src) ? (const bf16*)p.dact_src : (const bf16*)p.C;
+      const bf16* y_b = bnr ? (const bf16*)p.bn_y : nullptr;
+      const bf16* a_b = bnr ? (p.bn_a ? (const bf16*)p.bn_a : y_b) : nullptr;
+      const bf16* y2_b = bnr ? (p.bn_y2 ? (const bf16*)p.bn_y2 : y_b) : nullptr;
+#pragma unroll (bnr ? 1 : NIT)
+      for (int g0 = 0; g0 < NIT; g0 += G) {
+        bf16x8 cv[G], rr[G], zv[G], yv[G], av[G], y2v[G];
+        long long off[G];
+        bool rok[G];
+        int mlog[G], nlog[G];
 #pragma unroll
-    for (int it = 0; it < TOT / NT; ++it) {
+        for (int g = 0; g < G; ++g) {
+          const int idx = tid + (g0 + g) * NT;
+          const int row = idx / CPR, cc = idx - row * CPR;
+          const int m = m0 + row, n = n0 + cc * 8;
+          long long mo = m, mr = m;
+          if constexpr (bnr) { mo = out_row(p, m); mr = resid_row(p, mo); }
+          off[g] = bz * p.sC + mo * p.ldc + n;
+          rok[g] = p.resid && mr >= 0;
+          mlog[g] = m; nlog[g] = n;
+          cv[g] = *(const bf16x8*)(Cs + row * LDC_S + cc * 8);
+          rr[g] = *(const bf16x8*)(resid_b + (rok[g] ? bz * p.sC + mr * p.ldc + n : off[g]));
+          if constexpr (EPI == EPI_BF16_EXT) zv[g] = *(const bf16x8*)(dsrc_b + off[g]);
+          if constexpr (bnr) {
+            yv[g] = *(const bf16x8*)(y_b + off[g]);
+            av[g] = *(const bf16x8*)(a_b + off[g]);
+            y2v[g] = *(const bf16x8*)(y2_b + off[g]);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          bf16x8 v = cv[g];
+          if constexpr (EPI == EPI_BF16_EXT) {
+            // pre-activation chunk: [* act'(z)] -> [aux copy] -> act -> [dropout]
+            float f[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
+            if (p.dact_src) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) f[e] *= act_grad(bf2f(zv[g][e]), p.dact);
+            }
+            if (p.aux) *(bf16x8*)((bf16*)p.aux + off[g]) = v;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = act_apply(f[e], p.act);
+            if (p.drop_p > 0.f) {
+              const unsigned long long lin = (unsigned long long)mlog[g] * p.N + nlog[g];
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                f[e] = u01(hash_u32(p.drop_seed, lin + e)) < 1.f - p.drop_p ? f[e] * p.drop_scale : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = f2bf(f[e]);
+          }
+          if (rok[g]) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[g][e]));
+          }
+          *(bf16x8*)((bf16*)p.C + off[g]) = v;
+          if constexpr (bnr) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float y = bf2f(yv[g][e]);
+              const bool keep = p.bn_a ? (bf2f(av[g][e]) > 0.f) : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
+              const float dz = keep ? bf2f(v[e]) : 0.f;
+              r0[e] += dz;
+              r1[e] += dz * (y - mu[e]) * is[e];
+              if (p.bn_y2) r2[e] += dz * (bf2f(y2v[g][e]) - mu2[e]) * is2[e];
+            }
+          }
+        }
+      }
+    } else {
+#pragma unroll 1
+    for (int it = 0; it < NIT; ++it) {
       const int idx = tid + it * NT;
       const int row = idx / CPR, cc = idx - row * CPR;
       const int m = m0 + row, n = n0 + cc * 8;
       if (m >= p.M || n >= p.N) continue;
+      // row maps (strided-conv dgrad) exist on the BN-backward epilogue only: elsewhere they would
+      // cost registers the persistent kernels do not have
+      long long mo = m, mr = m;
+      if constexpr (bnr) { mo = out_row(p, m); mr = resid_row(p, mo); }
+      const bf16* rsrc = (p.resid && mr >= 0) ? (const bf16*)p.resid + bz * p.sC + mr * p.ldc + n : nullptr;
       bf16x8 v = *(const bf16x8*)(Cs + row * LDC_S + cc * 8);
-      bf16* dst = C + (long long)m * p.ldc + n;
+      bf16* dst = C + mo * p.ldc + n;
       if (n + 7 < p.N && (p.ldc & 7) == 0) {
-        const long long off = bz * p.sC + (long long)m * p.ldc + n;
+        const long long off = bz * p.sC + mo * p.ldc + n;
         if constexpr (EPI == EPI_BF16_EXT) {
           // pre-activation chunk: [* act'(z)] -> [aux copy] -> act -> [dropout]; 16-B coalesced
           float f[8];
@@ -135,8 +273,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = f2bf(f[e]);
         }
-        if (p.resid) {
-          bf16x8 rr = *(const bf16x8*)((const bf16*)p.resid + off);
+        if (rsrc) {
+          bf16x8 rr = *(const bf16x8*)rsrc;
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[e]));
         }
@@ -158,7 +296,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         }
       } else {
         for (int e = 0; e < 8 && n + e < p.N; ++e) {
-          const long long off = bz * p.sC + (long long)m * p.ldc + n + e;
+          const long long off = bz * p.sC + mo * p.ldc + n + e;
           float x = bf2f(v[e]);
           if constexpr (EPI == EPI_BF16_EXT) {
             if (p.dact_src) x *= act_grad(bf2f(((const bf16*)p.dact_src)[off]), p.dact);
@@ -168,11 +306,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
               x = u01(hash_u32(p.drop_seed, (unsigned long long)m * p.N + n + e)) < 1.f - p.drop_p ? x * p.drop_scale : 0.f;
             x = bf2f(f2bf(x));
           }
-          if (p.resid) x += bf2f(((const bf16*)p.resid)[off]);
+          if (rsrc) x += bf2f(rsrc[e]);
           dst[e] = f2bf(x);
         }
       }
     }
+    }  // ragged tile
     if constexpr (bnr) {
       // lanes sharing a column chunk: tid % CPR equal -> xor over the bits above log2(CPR)
 #pragma unroll

@@ -47,5 +47,12 @@ struct GemmParams {
   // MX-fp8 engine (fp8.hip): e8m0 block scales, [rows][K/32] bytes, one per 32 K-elements
   const void* a_scale;
   const void* b_scale;
+  // bf16-epilogue row maps (strided-conv dgrad, gemm_epilogue.h out_row/resid_row):
+  //  out-map (om_hp > 0): GEMM row m = (n, h', w') of an [om_hp][om_wp] phase grid is output row
+  //    (n, h'*om_sh + om_a, w'*om_sw + om_b) of the [om_h][om_w] grid (C, resid, bn_* share it);
+  //  resid sub-sampling (rs_sh > 0): output row (n, h, w) of [rs_h][rs_w] reads resid row
+  //    (n, h/rs_sh, w/rs_sw) of [rs_p][rs_q] on the stride lattice and no resid elsewhere.
+  int om_hp, om_wp, om_h, om_w, om_sh, om_sw, om_a, om_b;
+  int rs_h, rs_w, rs_p, rs_q, rs_sh, rs_sw;
 };
 }  // namespace tfk

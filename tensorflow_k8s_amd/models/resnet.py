@@ -99,7 +99,13 @@ class Bottleneck:
         dy1, _, _ = BN.bn_backward(da1, None, y1, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
                                    self.bn1.beta.grad, y1.numel() // y1.shape[-1], relu_from_y=True, reduced=True)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
-        if self.proj:
+        if self.proj and self.stride > 1 and need_dx and next_bnr is not None:
+            # strided projection: its dgrad only touches the stride lattice -> a dense GEMM over the
+            # P x Q rows, added on the lattice inside conv1's dgrad epilogue (which also carries the
+            # previous block's fused BN reduction) instead of a 3/4-zero strided gather
+            t = self.conv_sc.backward_lattice(dysc, x)
+            dx = self.conv1.backward(dy1, x, need_dx=True, resid=t, resid_stride=self.stride, bnr=next_bnr)
+        elif self.proj:
             dx = self.conv1.backward(dy1, x, need_dx=need_dx)
             dx = self.conv_sc.backward(dysc, x, need_dx=need_dx, resid=dx, bnr=next_bnr)
         else:

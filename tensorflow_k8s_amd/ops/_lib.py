@@ -22,8 +22,52 @@ def lib():
             raise RuntimeError(
                 "tfk native extension tensorflow_k8s_amd/_C is not built; run `python tools/build_ext.py` "
                 f"(import error: {e})") from e
-        _C = C
+        _C = _OpProfiler(C) if os.environ.get("TFK_OPPROF") else C
     return _C
+
+
+class _OpProfiler:
+    """TFK_OPPROF=1: wraps every native entry point with a pair of device events on the current
+    stream and records (name, compact args, elapsed ms) per call; ``records()`` synchronizes and
+    resolves them. Used by tools/op_profile.py for per-layer kernel times; off in normal runs."""
+
+    def __init__(self, mod):
+        self._mod = mod
+        self._pending = []
+        self.__file__ = getattr(mod, "__file__", "")
+
+    @staticmethod
+    def _desc(a):
+        if isinstance(a, torch.Tensor):
+            return {"shape": list(a.shape), "esize": a.element_size()}
+        if isinstance(a, (int, float, str, bool)) or a is None:
+            return a
+        if isinstance(a, (list, tuple)):
+            return [_OpProfiler._desc(x) for x in a]
+        return type(a).__name__
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+        if not callable(fn):
+            return fn
+
+        def wrapped(*args, **kw):
+            if not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+                return fn(*args, **kw)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = fn(*args, **kw)
+            e1.record()
+            self._pending.append((name, [self._desc(a) for a in args], e0, e1))
+            return r
+        return wrapped
+
+    def records(self, clear: bool = True):
+        torch.cuda.synchronize()
+        out = [{"op": n, "args": a, "ms": e0.elapsed_time(e1)} for n, a, e0, e1 in self._pending]
+        if clear:
+            self._pending = []
+        return out
 
 
 def available() -> bool:

@@ -70,18 +70,22 @@ class ConvGeom:
 
 
 # (bm, bn): (concurrent blocks on the chip, relative MFMA efficiency measured by tools/gemm_bench.py)
-_TILES = {(256, 256): (256, 0.76), (128, 128): (512, 0.62), (128, 64): (768, 0.45), (64, 64): (1024, 0.30)}
+_TILES = {(256, 256): (256, 0.76), (128, 128): (512, 0.62), (256, 64): (512, 0.60), (128, 64): (768, 0.45),
+          (64, 64): (1024, 0.30)}
 BIG_TILE_MIN_K = 2048  # one 8-wave block per CU: its prologue/epilogue is exposed, so it needs a long K loop
 
 
-def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: int = 0):
+def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: int = 0, mid_ok: bool = True):
     """Tile with the lowest modelled time: rounds of concurrent blocks x per-block work / efficiency
     (a 256x256 tile runs one 8-wave block per CU; smaller tiles 2-4 blocks/CU at lower efficiency).
     big_ok: operand modes that have the 256x256 instantiation (dense, non-gather); K: reduction
-    length (the big tile is only used without split-K and for K >= BIG_TILE_MIN_K)."""
+    length (the big tile is only used without split-K and for K >= BIG_TILE_MIN_K). mid_ok: the
+    mode has the 256x64 tile (every mode except the conv fwd/dgrad gathers)."""
     best, best_cost = None, None
     for (bm, bn), (slots, eff) in _TILES.items():
         if (bm, bn) == (256, 256) and (not big_ok or splits_ok or M < 256 or N < 256 or K < BIG_TILE_MIN_K):
+            continue
+        if (bm, bn) == (256, 64) and (not mid_ok or M < 256):
             continue
         if bn > 64 and N <= 64:
             continue
@@ -106,11 +110,11 @@ def pick_splits(tiles: int, K: int, min_ktiles: int = 4) -> int:
 
 def _gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile, *, alpha=1.0, beta=0.0, bias=None, resid=None,
           act=0, stats=None, shards=1, splits=1, batch=1, sA=0, sB=0, sC=0, split_stride=0, conv=NO_CONV, bnr=None,
-          aux=None, dact_src=None, dact=0, drop_p=0.0, drop_seed=0):
+          aux=None, dact_src=None, dact=0, drop_p=0.0, drop_seed=0, rowmap=()):
     lib().gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile[0], tile[1], alpha, beta, bias, resid, act,
                stats, shards, splits, batch, sA, sB, sC, split_stride, conv,
                bnr.gemm_args() if bnr is not None else [], int(bnr.relu) if bnr is not None else 0,
-               bnr.st.shards if bnr is not None else 1, aux, dact_src, dact, drop_p, drop_seed)
+               bnr.st.shards if bnr is not None else 1, aux, dact_src, dact, drop_p, drop_seed, list(rowmap))
 
 
 def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, accumulate: bool, device,
@@ -272,7 +276,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
         return y.to(torch.bfloat16).contiguous()
     M = g.N * g.P * g.Q
     y = torch.empty(g.N, g.P, g.Q, g.K, dtype=torch.bfloat16, device=x.device)
-    tile = pick_tile(M, g.K, big_ok=g.pointwise, K=g.C)
+    tile = pick_tile(M, g.K, big_ok=g.pointwise, K=g.C, mid_ok=g.pointwise)
     if g.pointwise:
         _gemm(x, w, y, M, g.K, g.C, g.C, g.C, g.K, A_KIN, B_KIN, EPI_BF16, tile, stats=stats, shards=shards,
               bias=bias, act=ACT[act])
@@ -292,10 +296,36 @@ def conv_weight_t(w: torch.Tensor, g: ConvGeom, out: torch.Tensor | None = None)
     return out
 
 
+def _phases(g: ConvGeom):
+    """Sub-pixel decomposition of a strided conv's dgrad: output phase (a, b) (rows h = a + sh*i)
+    only receives the taps r = r0 + sh*i with r0 = (a + ph) % sh, and those read dY row
+    i_h + (a + ph - r0)/sh - i -- a stride-1 dgrad with Rp x Sp taps on the phase grid. Returns
+    [(a, b, Ha, Wb, r0, s0, Rp, Sp, ph', pw')]; None if some non-empty phase has no taps or the
+    conv is dilated (-> gather path)."""
+    if g.dh != 1 or g.dw != 1:
+        return None
+    out = []
+    for a in range(g.sh):
+        for b in range(g.sw):
+            Ha, Wb = len(range(a, g.H, g.sh)), len(range(b, g.W, g.sw))
+            if Ha == 0 or Wb == 0:
+                continue
+            r0, s0 = (a + g.ph) % g.sh, (b + g.pw) % g.sw
+            Rp, Sp = len(range(r0, g.R, g.sh)), len(range(s0, g.S, g.sw))
+            if Rp == 0 or Sp == 0:
+                return None
+            out.append((a, b, Ha, Wb, r0, s0, Rp, Sp, (a + g.ph - r0) // g.sh, (b + g.pw - s0) // g.sw))
+    return out
+
+
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tensor | None = None,
-               wt: torch.Tensor | None = None, bnr=None) -> torch.Tensor:
+               wt: torch.Tensor | None = None, bnr=None, resid_stride: int = 1) -> torch.Tensor:
     """dx[N,H,W,C] = conv_transpose(dy[N,P,Q,K], w) (+ resid). bnr (ops.norm.BNReduce): also
-    accumulate the BN-backward channel sums of the layer that produced x, from the final dx."""
+    accumulate the BN-backward channel sums of the layer that produced x, from the final dx.
+    resid_stride > 1 (pointwise convs with bnr): resid is [N, ceil(H/s), ceil(W/s), C] and is added
+    on the stride-s lattice only -- the dgrad of a strided 1x1 projection shortcut computed densely
+    on its own rows (no 3/4-zero gather), folded into the sibling conv's dgrad epilogue.
+    Strided convs with bnr run as one stride-1 dgrad GEMM per output phase (``_phases``)."""
     if not on_gpu(dy):
         dyn = dy.float().permute(0, 3, 1, 2)
         wn = w.float().permute(0, 3, 1, 2)
@@ -304,6 +334,10 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
         dx = F.conv_transpose2d(dyn, wn, stride=(g.sh, g.sw), padding=(g.ph, g.pw), output_padding=out_pad,
                                 dilation=(g.dh, g.dw)).permute(0, 2, 3, 1)
         if resid is not None:
+            if resid_stride > 1:
+                full = torch.zeros_like(dx)
+                full[:, ::resid_stride, ::resid_stride, :] = resid.float()
+                resid = full
             dx = dx.to(torch.bfloat16).float() + resid.float()
         dx = dx.to(torch.bfloat16).contiguous()
         if bnr is not None:
@@ -311,10 +345,30 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
         return dx
     M = g.N * g.H * g.W
     dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
-    tile = pick_tile(M, g.C, big_ok=g.pointwise, K=g.K)
+    tile = pick_tile(M, g.C, big_ok=g.pointwise, K=g.K, mid_ok=g.pointwise)
+    if resid_stride > 1:
+        if not g.pointwise or bnr is None or resid is None:
+            raise ValueError("resid_stride needs a pointwise conv, a resid and the fused BN reduction")
+        s = resid_stride
+        rmap = [0] * 8 + [g.H, g.W, -(-g.H // s), -(-g.W // s), s, s]
+        _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid, bnr=bnr,
+              rowmap=rmap)
+        return dx
     if g.pointwise:
         _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid, bnr=bnr)
-    elif g.R == 1 and g.S == 1:
+        return dx
+    phases = _phases(g) if (bnr is not None and (g.sh > 1 or g.sw > 1)) else None
+    if phases is not None:
+        wt = wt if wt is not None else conv_weight_t(w, g)
+        for a, b, Ha, Wb, r0, s0, Rp, Sp, php, pwp in phases:
+            wp = wt[:, r0::g.sh, s0::g.sw, :].contiguous()  # [C][Rp][Sp][K] sub-kernel (weights only)
+            Mp, Kd = g.N * Ha * Wb, Rp * Sp * g.K
+            conv = [g.N, Ha, Wb, g.C, g.P, g.Q, g.K, Rp, Sp, 1, 1, php, pwp, 1, 1]
+            rmap = [Ha, Wb, g.H, g.W, g.sh, g.sw, a, b] + [0] * 6
+            _gemm(dy, wp, dx, Mp, g.C, Kd, 0, Kd, g.C, A_CONV_DGRAD, B_KIN, EPI_BF16,
+                  pick_tile(Mp, g.C, K=Kd, mid_ok=False), resid=resid, conv=conv, bnr=bnr, rowmap=rmap)
+        return dx
+    if g.R == 1 and g.S == 1:
         # strided 1x1: B(n=c, k=co) = W[co][c] is K-outer with ldb = C; gather handles the stride
         _gemm(dy, w, dx, M, g.C, g.K, 0, g.C, g.C, A_CONV_DGRAD, B_KOUT, EPI_BF16, tile, resid=resid,
               conv=g.vec(), bnr=bnr)

@@ -81,7 +81,7 @@ class Conv2d:
         return G.conv_fwd(x, self.w.compute, g, stats.stats if stats else None, stats.shards if stats else 1,
                           bias=self.b.master if self.b is not None else None, act=act)
 
-    def backward(self, dy, x, need_dx: bool = True, resid=None, bnr=None):
+    def backward(self, dy, x, need_dx: bool = True, resid=None, bnr=None, resid_stride: int = 1):
         g = self.geom(x.shape)
         G.conv_wgrad(dy, x, g, self.w.grad)
         if self.b is not None:
@@ -91,7 +91,19 @@ class Conv2d:
             self.arena.grad_ready(self.w)
         if not need_dx:
             return None
-        return G.conv_dgrad(dy, self.w.compute, g, resid=resid, bnr=bnr)
+        return G.conv_dgrad(dy, self.w.compute, g, resid=resid, bnr=bnr, resid_stride=resid_stride)
+
+    def backward_lattice(self, dy, x):
+        """Strided 1x1 conv (projection shortcut): weight gradient + the input gradient on the
+        stride lattice only, as a dense [N, P, Q, C] GEMM (every other input position gets zero).
+        The caller folds it into a sibling dgrad with ``resid_stride=stride``."""
+        g = self.geom(x.shape)
+        if self.k != 1 or self.pad != 0 or self.b is not None:
+            raise ValueError("backward_lattice is for bias-free 1x1 convs")
+        G.conv_wgrad(dy, x, g, self.w.grad)
+        self.arena.grad_ready(self.w)
+        w2 = self.w.compute.view(self.cout, self.cin)
+        return G.linear_dgrad(dy.reshape(-1, self.cout), w2).view(g.N, g.P, g.Q, g.C)
 
 
 class BatchNorm:

@@ -78,6 +78,9 @@ def parse_args(argv=None):
     ap.add_argument("--seq-len", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--rendezvous-timeout", type=float, default=300.0)
+    ap.add_argument("--watchdog-timeout", type=float, default=0.0,
+                    help="exit 143 (retryable) when no step completes for this many seconds (0 = off)")
+    ap.add_argument("--trace-file", default="", help="Chrome-trace step timeline (+ roctx ranges); {rank} expands")
     # evaluator
     ap.add_argument("--eval-batches", type=int, default=4)
     ap.add_argument("--eval-timeout", type=float, default=600.0)
@@ -214,13 +217,22 @@ def run_worker(args, info, dev) -> int:
     _log({"event": "start", "rank": info.rank, "world": info.world_size, "workers": nworkers, "model": model.name,
           "params": model.arena.num_parameters(), "device": str(dev), "strategy": strat.name, "start_step": start,
           "global_batch": gb, "restart_generation": int(os.environ.get("TFK_RESTART_GENERATION", "0"))})
+    from ..utils.tracing import NULL_TRACER, Tracer
+    tracer = Tracer(rank=info.rank, device_events=dev.type == "cuda") if args.trace_file else NULL_TRACER
+    watchdog = None
+    if args.watchdog_timeout > 0:
+        from .watchdog import StepWatchdog
+        watchdog = StepWatchdog(args.watchdog_timeout, name=f"rank{info.rank}").start()
     t_last, n_last = time.perf_counter(), 0
     step = start
     while step < args.steps:
-        runner.set_batch(*batches[step % len(batches)])
-        runner.step()
+        with tracer.span("step", cat="train", step=step):
+            runner.set_batch(*batches[step % len(batches)])
+            runner.step()
         step += 1
         n_last += 1
+        if watchdog is not None:
+            watchdog.beat(step)
         if step % max(1, args.log_every) == 0 or step == args.steps:
             m = torch.tensor([runner.last_loss() or 0.0, runner.last_accuracy() or 0.0], dtype=torch.float32,
                              device=dev if strat.name == "mwms" else "cpu")
@@ -237,11 +249,16 @@ def run_worker(args, info, dev) -> int:
             t_last, n_last = now, 0
         if ckpt is not None and info.is_chief and args.checkpoint_every and step % args.checkpoint_every == 0 \
                 and step < args.steps:
-            if use_ps:
-                strat.fetch_state(opt)
-            path = ckpt.save(model.arena, opt, step)
+            with tracer.span("checkpoint", cat="io", step=step):
+                if use_ps:
+                    strat.fetch_state(opt)
+                path = ckpt.save(model.arena, opt, step)
             _log({"event": "checkpoint", "step": step, "path": path}, metrics_fh)
         maybe_fault(step, info.rank)
+    if watchdog is not None:
+        watchdog.stop()
+    if args.trace_file:
+        _log({"event": "trace", "path": tracer.dump(args.trace_file.format(rank=info.rank))})
     if ckpt is not None and info.is_chief:
         if use_ps:
             strat.fetch_state(opt)

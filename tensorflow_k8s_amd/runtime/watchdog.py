@@ -1,0 +1,105 @@
+"""Step-progress watchdog: the runtime half of failure detection.
+
+A collective whose peer died never returns: RCCL (and gloo) block inside the all-reduce until their
+own timeout, which is minutes by default, and a wedged rank keeps its GPU busy. The watchdog is a
+daemon thread that expects a heartbeat (``beat(step)``) at least every ``timeout_s`` seconds once
+training has started. When the heartbeat stops it writes the termination message, logs one JSON
+event, aborts the process group (best effort, so RCCL tears its communicators down instead of
+spinning) and exits with 143, the retryable code of the operator's ExitCode restart policy: the
+operator bumps the restart generation, every rank re-rendezvouses and training resumes from the
+latest checkpoint (runtime/train.py, runtime/checkpoint.py).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import threading
+import time
+
+EXIT_RETRY = 143
+
+
+class StepWatchdog:
+    def __init__(self, timeout_s: float, on_timeout=None, poll_s: float | None = None, name: str = "train"):
+        if timeout_s <= 0:
+            raise ValueError("watchdog timeout must be > 0")
+        self.timeout_s = float(timeout_s)
+        self.poll_s = float(poll_s) if poll_s else min(1.0, self.timeout_s / 4)
+        self.name = name
+        self.on_timeout = on_timeout or self._default_timeout
+        self.last_step = -1
+        self._last = time.monotonic()
+        self._stop = threading.Event()
+        self._fired = threading.Event()
+        self._lock = threading.Lock()
+        self._thread = None
+
+    # ------------------------------------------------------------------ control
+    def start(self) -> "StepWatchdog":
+        self._last = time.monotonic()
+        self._thread = threading.Thread(target=self._run, name=f"tfk-watchdog-{self.name}", daemon=True)
+        self._thread.start()
+        return self
+
+    def beat(self, step: int | None = None) -> None:
+        with self._lock:
+            self._last = time.monotonic()
+            if step is not None:
+                self.last_step = step
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5.0)
+
+    @property
+    def fired(self) -> bool:
+        return self._fired.is_set()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+        return False
+
+    # ------------------------------------------------------------------ loop
+    def _run(self) -> None:
+        while not self._stop.wait(self.poll_s):
+            with self._lock:
+                idle = time.monotonic() - self._last
+                step = self.last_step
+            if idle > self.timeout_s:
+                self._fired.set()
+                self.on_timeout(step, idle)
+                return
+
+    def _default_timeout(self, step: int, idle: float) -> None:
+        msg = f"watchdog: no training progress for {idle:.1f}s after step {step} (peer lost or collective hung)"
+        path = os.environ.get("TFK_TERMINATION_LOG")
+        if path:
+            try:
+                with open(path, "w") as f:
+                    f.write(msg)
+            except OSError:
+                pass
+        print(json.dumps({"event": "error", "kind": "watchdog", "step": step, "idle_s": round(idle, 2),
+                          "message": msg}, sort_keys=True), flush=True)
+        abort_process_group()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(EXIT_RETRY)
+
+
+def abort_process_group() -> None:
+    """Best-effort abort of the default process group so RCCL communicators are torn down."""
+    try:
+        import torch.distributed as dist
+        if not dist.is_available() or not dist.is_initialized():
+            return
+        abort = getattr(dist.distributed_c10d, "_abort_process_group", None)
+        if abort is not None:
+            abort()
+    except Exception:  # pragma: no cover - the process is exiting anyway
+        pass

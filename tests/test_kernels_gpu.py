@@ -192,7 +192,8 @@ def test_global_norm_clip():
 
 
 @pytest.mark.parametrize("mode", ["relu_from_y", "mask_a", "dual"])
-@pytest.mark.parametrize("cfg", [(2, 8, 8, 64, 256, 1, 1, 1, 0), (2, 9, 9, 64, 64, 3, 3, 1, 1), (2, 14, 14, 256, 512, 1, 1, 2, 0)])
+@pytest.mark.parametrize("cfg", [(2, 8, 8, 64, 256, 1, 1, 1, 0), (2, 9, 9, 64, 64, 3, 3, 1, 1), (2, 14, 14, 256, 512, 1, 1, 2, 0),
+                                 (2, 16, 16, 64, 64, 3, 3, 2, 1), (2, 15, 13, 32, 48, 3, 3, 2, 1)])
 def test_dgrad_fused_bn_reduce(cfg, mode):
     """BN-backward channel sums fused into the dgrad epilogue == the standalone reduction."""
     N, H, W, C, K, R, S, st_, pd = cfg
@@ -246,3 +247,66 @@ def test_big_tile_256(M, N, K, monkeypatch):
         out[dev] = dict(y=y, z=z, dz=dz, dx=dx, gw=gw)
     for k in out["cpu"]:
         assert rel(out[DEV][k], out["cpu"][k]) < 1e-2, k
+
+
+@pytest.mark.parametrize("M,N,K", [(70001, 256, 64), (40000, 64, 256), (33000, 200, 136)])
+def test_persistent_gemm_matches_one_shot(M, N, K):
+    """Far more tiles than resident blocks -> persistent grid (next tile prefetched during the
+    epilogue). Must equal the one-shot grid bitwise (same per-tile math) and the fp32 reference."""
+    L = lib()
+    x, w = bf(M, K, seed=1), bf(N, K, scale=0.05, seed=2)
+    xd, wd = x.to(DEV), w.to(DEV)
+    res = {}
+    try:
+        for flag in (0, 1):
+            L.gemm_set_persist(flag)
+            y = G.linear_fwd(xd, wd, act="relu")
+            dx = G.linear_dgrad(y, wd) if N % 8 == 0 else None
+            res[flag] = (y, dx)
+    finally:
+        L.gemm_set_persist(1)
+    assert torch.equal(res[0][0], res[1][0])
+    if res[1][1] is not None:
+        assert torch.equal(res[0][1], res[1][1])
+    assert rel(res[1][0], G.linear_fwd(x, w, act="relu")) < 1e-2
+
+
+def test_persistent_conv_stats():
+    """Pointwise conv fwd on a persistent grid: output and fused BN batch statistics."""
+    g = G.ConvGeom(64, 32, 32, 64, 256, 1, 1)
+    x = bf(64, 32, 32, 64, seed=3)
+    w = bf(256, 1, 1, 64, scale=0.05, seed=4)
+    st_ref = torch.zeros(2 * 256)
+    y_ref = G.conv_fwd(x, w, g, st_ref, 1)
+    st = torch.zeros(32 * 2 * 256, device=DEV)
+    y = G.conv_fwd(x.to(DEV), w.to(DEV), g, st, 32)
+    assert rel(y, y_ref) < 1e-2
+    s = st.view(32, 2, 256).sum(0).cpu()
+    assert rel(s[0], st_ref.view(2, 256)[0]) < 1e-3
+    assert rel(s[1], st_ref.view(2, 256)[1]) < 1e-3
+
+
+@pytest.mark.parametrize("mode", ["mask_a", "dual"])
+def test_dgrad_lattice_resid(mode):
+    """Pointwise dgrad + a stride-2 sub-sampled residual (the strided projection shortcut's
+    lattice gradient) with the fused BN reduction, against the CPU reference."""
+    N, H, W, C, K = 2, 14, 13, 64, 128
+    g = G.ConvGeom(N, H, W, C, K, 1, 1)
+    w = bf(K, 1, 1, C, scale=0.05, seed=2)
+    dy = bf(N, H, W, K, seed=3)
+    t = bf(N, (H + 1) // 2, (W + 1) // 2, C, seed=4)
+    y, y2, a = bf(N, H, W, C, seed=5), bf(N, H, W, C, seed=6), bf(N, H, W, C, seed=7)
+    gen = torch.Generator().manual_seed(8)
+    vals = [(torch.randn(C, generator=gen) * 0.1, torch.rand(C, generator=gen) + 0.5) for _ in range(2)]
+    res = {}
+    for dev in ("cpu", DEV):
+        st, st2 = BN.BNState(C, dev), BN.BNState(C, dev)
+        for s_, (mu, inv) in zip((st, st2), vals):
+            s_.mean.copy_(mu); s_.invstd.copy_(inv)
+        spec = BN.BNReduce(y.to(dev), st, a=a.to(dev), y2=y2.to(dev) if mode == "dual" else None,
+                           st2=st2 if mode == "dual" else None)
+        dx = G.conv_dgrad(dy.to(dev), w.to(dev), g, resid=t.to(dev), bnr=spec, resid_stride=2)
+        res[dev] = (dx, st.sums.view(st.shards, 3, C).sum(0).cpu())
+    assert rel(res[DEV][0], res["cpu"][0]) < 1e-2
+    for k in range(3 if mode == "dual" else 2):
+        assert rel(res[DEV][1][k], res["cpu"][1][k]) < 2e-2, k

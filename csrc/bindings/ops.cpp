@@ -134,7 +134,10 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
     need_numel(C, bC + (long long)(M - 1) * ldc + N, "C");
   } else {
     TORCH_CHECK(ns == 1 || batch == 1, "split-K with batch>1 unsupported");
-    need_numel(C, bC + (long long)(ns - 1) * split_stride + (long long)(M - 1) * ldc + N, "C");
+    // split_stride == -1: atomic split-K, every split accumulates into the one [M][ldc] C
+    TORCH_CHECK(split_stride >= -1, "split_stride must be >= 0, or -1 for atomic split-K");
+    TORCH_CHECK(split_stride >= 0 || (batch == 1 && beta == 0.0), "atomic split-K needs batch 1 and beta 0");
+    need_numel(C, bC + (long long)(ns - 1) * std::max<int64_t>(split_stride, 0) + (long long)(M - 1) * ldc + N, "C");
   }
   if (bias.has_value() && bias->defined()) { need_f32(*bias, "bias"); need_numel(*bias, N, "bias"); }
   const bool resid_sub = rowmap.size() == 14 && rowmap[12] > 0;  // checked with the row maps below

@@ -57,7 +57,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   const int wm = wid / WN, wn = wid % WN;
   const int ml = lane & 15, nl = (lane >> 4) * 4;
   if constexpr (EPI == EPI_F32) {
-    float* C = (float*)p.C + bz * p.sC + (long long)blockIdx.z * p.split_stride;
+    // split_stride < 0: every split adds its partial straight into C with hardware f32 atomics
+    // (global_atomic_add_f32, -munsafe-fp-atomics) -- no slab workspace, no reduce pass.
+    const bool atomic = p.split_stride < 0;
+    float* C = (float*)p.C + bz * p.sC + (atomic ? 0LL : (long long)blockIdx.z * p.split_stride);
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = m0 + wm * TM + i * 16 + ml;
@@ -67,7 +70,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         const int n = n0 + wn * TN + j * 16 + nl;
         float* dst = C + (long long)m * p.ldc + n;
         f32x4 v = acc[i][j] * p.alpha;
-        if (n + 3 < p.N && (p.ldc & 3) == 0) {
+        if (atomic) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) atomicAdd(dst + r, v[r]);
+        } else if (n + 3 < p.N && (p.ldc & 3) == 0) {
           if (p.beta != 0.f) v += p.beta * *(f32x4*)dst;
           *(f32x4*)dst = v;
         } else {

@@ -310,3 +310,26 @@ def test_dgrad_lattice_resid(mode):
     assert rel(res[DEV][0], res["cpu"][0]) < 1e-2
     for k in range(3 if mode == "dual" else 2):
         assert rel(res[DEV][1][k], res["cpu"][1][k]) < 2e-2, k
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 256, 200704), (256, 1152, 50176), (100, 72, 30000)])
+def test_splitk_atomic_matches_slab(M, N, K):
+    """Weight-gradient-shaped GEMMs (tiny M x N, huge K -> hundreds of split-K slices): the atomic
+    epilogue (splits add into the output) must agree with the slab + reduce path and fp32."""
+    dy, x = bf(K, M, seed=3), bf(K, N, seed=4)
+    ref = dy.float().t() @ x.float()
+    got = {}
+    try:
+        for mode in (True, False):
+            G.SPLITK_ATOMIC = mode
+            gw = torch.full((M, N), 7.0, device=DEV)
+            G.linear_wgrad(dy.to(DEV), x.to(DEV), gw)
+            acc = torch.ones(M, N, device=DEV)
+            G.linear_wgrad(dy.to(DEV), x.to(DEV), acc, accumulate=True)
+            got[mode] = (gw.cpu(), acc.cpu())
+    finally:
+        G.SPLITK_ATOMIC = True
+    for mode in (True, False):
+        assert rel(got[mode][0], ref) < 1e-3, mode
+        assert rel(got[mode][1], ref + 1.0) < 1e-3, mode
+    assert rel(got[True][0], got[False][0]) < 1e-5

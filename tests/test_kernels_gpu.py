@@ -318,7 +318,7 @@ def test_splitk_atomic_matches_slab(M, N, K):
     epilogue (splits add into the output) must agree with the slab + reduce path and fp32."""
     dy, x = bf(K, M, seed=3), bf(K, N, seed=4)
     ref = dy.float().t() @ x.float()
-    got = {}
+    got, saved = {}, G.SPLITK_ATOMIC
     try:
         for mode in (True, False):
             G.SPLITK_ATOMIC = mode
@@ -328,7 +328,7 @@ def test_splitk_atomic_matches_slab(M, N, K):
             G.linear_wgrad(dy.to(DEV), x.to(DEV), acc, accumulate=True)
             got[mode] = (gw.cpu(), acc.cpu())
     finally:
-        G.SPLITK_ATOMIC = True
+        G.SPLITK_ATOMIC = saved
     for mode in (True, False):
         assert rel(got[mode][0], ref) < 1e-3, mode
         assert rel(got[mode][1], ref + 1.0) < 1e-3, mode

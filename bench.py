@@ -109,9 +109,11 @@ def main():
                        "optimizer": opt_name, "hipgraph": use_graph},
             "loss": loss}), flush=True)
     elif rank == 0:
-        base = _baseline(world)
+        is_r50 = args.model == "resnet50"
+        base = _baseline(world) if is_r50 else None
         print(json.dumps({
-            "metric": "images/sec (whole node) ResNet-50 TFJob at 1/2/4/8 MI355X workers",
+            "metric": ("images/sec (whole node) ResNet-50 TFJob at 1/2/4/8 MI355X workers" if is_r50
+                       else f"{args.model} images/sec (whole node)"),
             "value": round(value, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / base, 4) if base else None, "dtype": "bf16",

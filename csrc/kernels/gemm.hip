@@ -452,6 +452,9 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
   TFK_GEMM_TILES3(A_CONV_DGRAD, B_KIN, EPI_BF16)
   TFK_GEMM_TILES3(A_CONV_DGRAD, B_KOUT, EPI_BF16)
   TFK_GEMM_TILES(A_KOUT, B_CONV_WGRAD, EPI_F32)
+  // Cout=64 conv weight gradients (stem 7x7, stage-1 3x3): a 64x256 tile gives each wave a 32x128
+  // sub-tile (2x8 MFMA fragments per LDS fragment load instead of 64x64's 2x2)
+  TFK_GEMM_CASE(64, 256, A_KOUT, B_CONV_WGRAD, EPI_F32)
   // transformer epilogue extras: fwd (aux/dropout) and dgrad (activation backward)
   TFK_GEMM_TILES_BIG(A_KIN, B_KIN, EPI_BF16_EXT)
   TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_BF16_EXT)

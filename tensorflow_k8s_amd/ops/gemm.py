@@ -31,7 +31,8 @@ def act_ref(y: torch.Tensor, act) -> torch.Tensor:
         return torch.tanh(y)
     return y
 NO_CONV = [0] * 15
-TARGET_BLOCKS = 1024  # ~4 blocks per CU on 256 CUs
+TARGET_BLOCKS = int(os.environ.get("TFK_TARGET_BLOCKS", 1024))  # split-K fill target: ~4 blocks per CU on 256 CUs
+SPLIT_MIN_KTILES = int(os.environ.get("TFK_SPLIT_MIN_KTILES", 4))  # min 64-deep K tiles per split
 # Split-K for f32 outputs (weight gradients): "slab" (default) = per-split workspace slabs +
 # splitk_reduce (two passes, bitwise deterministic); "atomic" = splits accumulate into the output
 # with f32 atomics from the GEMM epilogue (one pass). Measured on MI355X, ResNet-50 bs256 step:
@@ -78,21 +79,30 @@ class ConvGeom:
 
 # (bm, bn): (concurrent blocks on the chip, relative MFMA efficiency measured by tools/gemm_bench.py)
 _TILES = {(256, 256): (256, 0.76), (128, 128): (512, 0.62), (256, 64): (512, 0.60), (128, 64): (768, 0.45),
-          (64, 64): (1024, 0.30)}
+          (64, 64): (1024, 0.30), (64, 256): (512, 0.55)}
+# 64x256 tile for Cout<=64 conv weight gradients whose B gather changes (r,s) every chunk (C <= 16,
+# i.e. the 7x7 stem on C padded to 8). Measured on MI355X (ResNet-50 bs256, rocprofv3): stem wgrad
+# 673 -> 644 us; the stage-1 3x3 (C=64) got slower on it (236 -> 249 us), so it keeps 64x64.
+WIDE_WGRAD = os.environ.get("TFK_WIDE_WGRAD", "1") == "1"
+WIDE_WGRAD_MAX_C = 16
 BIG_TILE_MIN_K = 2048  # one 8-wave block per CU: its prologue/epilogue is exposed, so it needs a long K loop
 
 
-def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: int = 0, mid_ok: bool = True):
+def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: int = 0, mid_ok: bool = True,
+              wide_ok: bool = False):
     """Tile with the lowest modelled time: rounds of concurrent blocks x per-block work / efficiency
     (a 256x256 tile runs one 8-wave block per CU; smaller tiles 2-4 blocks/CU at lower efficiency).
     big_ok: operand modes that have the 256x256 instantiation (dense, non-gather); K: reduction
     length (the big tile is only used without split-K and for K >= BIG_TILE_MIN_K). mid_ok: the
-    mode has the 256x64 tile (every mode except the conv fwd/dgrad gathers)."""
+    mode has the 256x64 tile (every mode except the conv fwd/dgrad gathers). wide_ok: the mode has
+    the 64x256 tile (conv weight gradient gather), only worth it for M <= 64."""
     best, best_cost = None, None
     for (bm, bn), (slots, eff) in _TILES.items():
         if (bm, bn) == (256, 256) and (not big_ok or splits_ok or M < 256 or N < 256 or K < BIG_TILE_MIN_K):
             continue
         if (bm, bn) == (256, 64) and (not mid_ok or M < 256):
+            continue
+        if (bm, bn) == (64, 256) and (not wide_ok or M > 64 or N <= 128):
             continue
         if bn > 64 and N <= 64:
             continue
@@ -106,7 +116,8 @@ def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: 
     return best
 
 
-def pick_splits(tiles: int, K: int, min_ktiles: int = 4) -> int:
+def pick_splits(tiles: int, K: int, min_ktiles: int | None = None) -> int:
+    min_ktiles = SPLIT_MIN_KTILES if min_ktiles is None else min_ktiles
     nkt = (K + 63) // 64
     if tiles >= TARGET_BLOCKS // 2:
         return 1
@@ -406,7 +417,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
         v = gw.view(g.K, Nn)
         v.add_(gwt) if accumulate else v.copy_(gwt)
         return
-    tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp)
+    tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp, wide_ok=WIDE_WGRAD and not g.pointwise and g.C <= WIDE_WGRAD_MAX_C)
     tiles = ((g.K + tile[0] - 1) // tile[0]) * ((Nn + tile[1] - 1) // tile[1])
 
     def run(C, sp, stride, beta):

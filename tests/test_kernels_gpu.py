@@ -39,6 +39,9 @@ CONVS = [
     (2, 32, 32, 8, 64, 7, 7, 2, 3),
     (3, 7, 7, 24, 40, 3, 3, 1, 1),
     (1, 5, 6, 16, 200, 3, 3, 2, 1),
+    # Cout <= 64 non-pointwise weight gradients take the 64x256 tile (stem 7x7 on C padded to 8, ragged M/N)
+    (1, 20, 20, 8, 64, 7, 7, 2, 3),
+    (1, 10, 10, 16, 48, 3, 3, 1, 1),
 ]
 
 
@@ -70,6 +73,23 @@ def test_conv_fwd_dgrad_wgrad(cfg):
     # accumulate path
     G.conv_wgrad(dy.to(DEV), x.to(DEV), g, gw, accumulate=True)
     assert rel(gw, 2 * gw_ref) < 5e-3
+
+
+@pytest.mark.parametrize("cfg", [(2, 9, 9, 64, 64, 3, 3, 1, 1), (1, 20, 20, 8, 64, 7, 7, 2, 3),
+                                 (1, 10, 10, 16, 48, 3, 3, 1, 1), (2, 12, 12, 32, 64, 3, 3, 2, 1)])
+def test_conv_wgrad_wide_tile(cfg, monkeypatch):
+    """The 64x256 weight-gradient tile (forced; the picker only takes it at ResNet-scale K)."""
+    N, H, W, C, K, R, S, st, pd = cfg
+    g = G.ConvGeom(N, H, W, C, K, R, S, st, st, pd, pd)
+    x = bf(N, H, W, C, seed=1)
+    dy = bf(N, g.P, g.Q, K, seed=3)
+    gw_ref = torch.zeros(K, R, S, C)
+    G.conv_wgrad(dy, x, g, gw_ref)
+    monkeypatch.setattr(G, "pick_tile", lambda *a, **k: (64, 256))
+    for splits in (1, 3):
+        gw = torch.zeros(K, R, S, C, device=DEV)
+        G.conv_wgrad(dy.to(DEV), x.to(DEV), g, gw, splits=splits)
+        assert rel(gw, gw_ref) < 5e-3, splits
 
 
 @pytest.mark.parametrize("M,K,N", [(37, 64, 200), (256, 2048, 1000), (512, 768, 3072), (128, 3072, 768), (8, 16, 24)])

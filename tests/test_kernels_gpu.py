@@ -117,6 +117,19 @@ def test_linear(M, K, N):
     assert rel(gb, gb_ref) < 1e-3
 
 
+@pytest.mark.parametrize("M,N,ld", [(8192, 768, 768), (8192, 3072, 3072), (100, 520, 520), (33, 24, 40), (70, 13, 13)])
+def test_bias_grad_colsum(M, N, ld):
+    """Column sums: 16-B vector path (N, ld multiples of 8) and the scalar fallback; write + accumulate."""
+    full = bf(M, ld, seed=11)
+    dy = full[:, :N].contiguous()
+    ref = dy.float().sum(0)
+    gb = torch.zeros(N, device=DEV)
+    lib().colsum(full.to(DEV), M, N, ld, gb)  # strided rows: only the first N of each ld are summed
+    assert rel(gb, ref) < 1e-4
+    G.bias_grad(dy.to(DEV), gb, accumulate=True)
+    assert rel(gb, 2 * ref) < 1e-4
+
+
 def test_gemm_asymmetric_identity():
     """A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)."""
     n = 64

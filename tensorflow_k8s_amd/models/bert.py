@@ -44,6 +44,9 @@ class BertConfig:
     seq_len: int = 128
     max_predictions: int = 20
     fp8: bool = False  # forward GEMMs in MX-fp8 (e4m3 + e8m0 block scales); backward bf16
+    # split-K fill target for the encoder weight gradients (None = ops.gemm.TARGET_BLOCKS). Measured
+    # on MI355X, base bs64x128: 512 -> 15.44 ms/step vs 16.17 at 1024 (profiles/splitk_sweep_*).
+    wgrad_split_target: int | None = 512
 
     @classmethod
     def base(cls):
@@ -79,6 +82,8 @@ class BertLayer:
         self.ff1 = Linear(arena, f"{pre}/intermediate/dense", W, cfg.intermediate, init="trunc_normal", std=std)
         self.ff2 = Linear(arena, f"{pre}/output/dense", cfg.intermediate, W, init="trunc_normal", std=std)
         self.ln2 = LayerNorm(arena, f"{pre}/output/LayerNorm", W, cfg.ln_eps)
+        for lin in (self.qkv, self.ao, self.ff1, self.ff2):
+            lin.split_target = cfg.wgrad_split_target
         self.saved = None
 
     def forward(self, h, B, S, kv_len, seed: int, training: bool):

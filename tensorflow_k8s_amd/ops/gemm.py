@@ -89,7 +89,7 @@ BIG_TILE_MIN_K = 2048  # one 8-wave block per CU: its prologue/epilogue is expos
 
 
 def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: int = 0, mid_ok: bool = True,
-              wide_ok: bool = False):
+              wide_ok: bool = False, split_target: int | None = None):
     """Tile with the lowest modelled time: rounds of concurrent blocks x per-block work / efficiency
     (a 256x256 tile runs one 8-wave block per CU; smaller tiles 2-4 blocks/CU at lower efficiency).
     big_ok: operand modes that have the 256x256 instantiation (dense, non-gather); K: reduction
@@ -107,7 +107,7 @@ def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: 
         if bn > 64 and N <= 64:
             continue
         tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
-        s = pick_splits(tiles, K) if (splits_ok and K) else 1
+        s = pick_splits(tiles, K, target=split_target) if (splits_ok and K) else 1
         kfrac = 1.0 / s
         rounds = -(-tiles * s // slots)
         cost = rounds * (slots / 256) * bm * bn * kfrac / eff
@@ -116,8 +116,10 @@ def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: 
     return best
 
 
-def pick_splits(tiles: int, K: int, min_ktiles: int | None = None) -> int:
+def pick_splits(tiles: int, K: int, min_ktiles: int | None = None, target: int | None = None) -> int:
+    """Split-K count filling ~`target` blocks (default TARGET_BLOCKS) with >= min_ktiles K-tiles each."""
     min_ktiles = SPLIT_MIN_KTILES if min_ktiles is None else min_ktiles
+    TARGET_BLOCKS = target or globals()["TARGET_BLOCKS"]
     nkt = (K + 63) // 64
     if tiles >= TARGET_BLOCKS // 2:
         return 1
@@ -136,9 +138,9 @@ def _gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile, *, alpha=1.0
 
 
 def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, accumulate: bool, device,
-                    force_splits: int | None = None):
+                    force_splits: int | None = None, split_target: int | None = None):
     """Run an f32-epilogue GEMM with split-K into a workspace, then reduce into `out` ([M][N] f32)."""
-    splits = force_splits if force_splits is not None else pick_splits(tiles, K)
+    splits = force_splits if force_splits is not None else pick_splits(tiles, K, target=split_target)
     ns = int(lib().gemm_splits(K, splits))
     if ns == 1:
         run(out, 1, 0, 1.0 if accumulate else 0.0)
@@ -225,8 +227,9 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
     return dx
 
 
-def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate: bool = False) -> None:
-    """gw[N,K] (f32) (+)= dy[M,N]^T @ x[M,K]."""
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate: bool = False,
+                 split_target: int | None = None) -> None:
+    """gw[N,K] (f32) (+)= dy[M,N]^T @ x[M,K]. split_target: split-K fill target override (blocks)."""
     N = dy.shape[-1]
     K = x.shape[-1]
     dy2, x2 = dy.reshape(-1, N), x.reshape(-1, K)
@@ -238,13 +241,13 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
         else:
             gw.view(N, K).copy_(g)
         return
-    tile = pick_tile(N, K, splits_ok=True, big_ok=True, K=M)
+    tile = pick_tile(N, K, splits_ok=True, big_ok=True, K=M, split_target=split_target)
     tiles = ((N + tile[0] - 1) // tile[0]) * ((K + tile[1] - 1) // tile[1])
 
     def run(C, splits, stride, beta):
         _gemm(dy2, x2, C, N, K, M, N, K, K, A_KOUT, B_KOUT, EPI_F32, tile, beta=beta, splits=splits,
               split_stride=stride)
-    _f32_out_splitk(run, N, K, M, tiles, gw.view(-1), accumulate, dy.device)
+    _f32_out_splitk(run, N, K, M, tiles, gw.view(-1), accumulate, dy.device, split_target=split_target)
 
 
 def bias_grad(dy: torch.Tensor, gb: torch.Tensor, accumulate: bool = False) -> None:

@@ -150,6 +150,7 @@ class Linear:
         self.b = arena.add(ParamSpec(f"{name}/bias", (fout,), init="zeros", decay=False)) if bias else None
         self.arena = arena
         self.fp8 = False  # forward GEMM in MX-fp8 (ops.fp8); backward stays bf16
+        self.split_target = None  # weight-gradient split-K fill target override (ops.gemm.pick_splits)
 
     def forward(self, x, act=None, resid=None, aux=None, drop_p: float = 0.0, drop_seed: int = 0):
         return linear_forward(x, self.w.compute, self.b.master if self.b else None, self.fp8, act=act, resid=resid,
@@ -158,7 +159,7 @@ class Linear:
     def backward(self, dy, x, need_dx: bool = True, resid=None, accumulate: bool = False, dact_src=None,
                  dact=None):
         """dy: gradient of this layer's (pre-dropout, post-activation-backward) output."""
-        G.linear_wgrad(dy, x, self.w.grad, accumulate=accumulate)
+        G.linear_wgrad(dy, x, self.w.grad, accumulate=accumulate, split_target=self.split_target)
         if self.b is not None:
             G.bias_grad(dy, self.b.grad, accumulate=accumulate)
             self.arena.grad_ready(self.w, self.b)
@@ -212,7 +213,7 @@ class FusedLinear:
 
     def backward(self, dy, x, need_dx: bool = True, resid=None):
         w, gw, _, gb = self.views()
-        G.linear_wgrad(dy, x, gw)
+        G.linear_wgrad(dy, x, gw, split_target=getattr(self, "split_target", None))
         if gb is not None:
             G.bias_grad(dy, gb)
         self.arena.grad_ready(*[p.w for p in self.parts], *[p.b for p in self.parts if p.b is not None])

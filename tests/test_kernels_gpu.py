@@ -262,9 +262,9 @@ def test_big_tile_256(M, N, K, monkeypatch):
     """The 8-wave 256x256 tile (dense operand modes) on interior and ragged shapes: fwd (bias+gelu
     with aux) and dgrad (K-outer B, fused GELU backward); wgrad (split-K) stays on 128 tiles."""
     real = G.pick_tile
-    monkeypatch.setattr(G, "pick_tile", lambda m, n, splits_ok=False, big_ok=False, K=0:
+    monkeypatch.setattr(G, "pick_tile", lambda m, n, splits_ok=False, big_ok=False, K=0, **kw:
                         (256, 256) if big_ok and not splits_ok and m >= 256 and n >= 256
-                        else real(m, n, splits_ok, big_ok, K))
+                        else real(m, n, splits_ok, big_ok, K, **kw))
     x, w = bf(M, K, seed=1), bf(N, K, seed=2, scale=0.05)
     b = torch.randn(N) * 0.1
     dy = bf(M, N, seed=3)

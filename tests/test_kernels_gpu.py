@@ -216,6 +216,21 @@ def test_optimizers():
     assert rel(wg, wc) < 1e-6 and rel(vg, vc) < 1e-6
 
 
+@pytest.mark.parametrize("n,off", [(10007, 0), (1 << 20, 0), (4099, 1), (3, 0)])
+def test_adamw_vector_and_tail(n, off):
+    """AdamW: 4-wide vector kernel + scalar tail (n % 4), the misaligned fallback (off=1), bf16 shadow."""
+    w = torch.randn(n + off); g = torch.randn(n + off); m = torch.randn(n + off) * 0.1; v = torch.rand(n + off) * 0.1
+    wc, mc, vc = w[off:].clone(), m[off:].clone(), v[off:].clone()
+    O.adamw_(wc, None, g[off:], mc, vc, 1e-3, 0.9, 0.98, 1e-9, 0.01, 7)
+    wg, mg, vg, gg = w.to(DEV), m.to(DEV), v.to(DEV), g.to(DEV)
+    wb = torch.empty(n + off, dtype=torch.bfloat16, device=DEV)
+    O.adamw_(wg[off:], wb[off:], gg[off:], mg[off:], vg[off:], 1e-3, 0.9, 0.98, 1e-9, 0.01, 7)
+    assert rel(wg[off:], wc) < 1e-6 and rel(mg[off:], mc) < 1e-6 and rel(vg[off:], vc) < 1e-6
+    assert rel(wb[off:], wc) < 1e-2
+    if off:
+        assert float(wg[0].cpu()) == float(w[0])  # element before the slice untouched
+
+
 def test_global_norm_clip():
     g = torch.randn(100000) * 3
     ss, coef, nrm = (torch.zeros(1, device=DEV) for _ in range(3))

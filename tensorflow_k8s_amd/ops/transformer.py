@@ -38,6 +38,17 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
     return y, mean, rstd
 
 
+def _zero_pair(a: torch.Tensor, b: torch.Tensor) -> None:
+    """Zero two 1-D f32 gradient views with one fill when b directly follows a in the same storage
+    (gamma/beta of one LayerNorm are consecutive in the flat arena): saves a launch per LayerNorm."""
+    if (a.is_contiguous() and b.is_contiguous() and a.dtype == b.dtype and a.device == b.device
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+            and b.storage_offset() == a.storage_offset() + a.numel()):
+        a.as_strided((a.numel() + b.numel(),), (1,), a.storage_offset()).zero_()
+    else:
+        a.zero_(); b.zero_()
+
+
 def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate: bool = False):
     """dx (+ dres) bf16; dgamma/dbeta (f32, written or accumulated)."""
     W = x.shape[-1]
@@ -56,7 +67,7 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate
             dgamma.copy_(dg); dbeta.copy_(db)
         return dx.to(torch.bfloat16).reshape(dy.shape)
     if not accumulate:
-        dgamma.zero_(); dbeta.zero_()
+        _zero_pair(dgamma, dbeta)
     dx = torch.empty_like(dy)
     lib().layernorm_bwd(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W)
     return dx

@@ -231,6 +231,24 @@ def test_adamw_vector_and_tail(n, off):
         assert float(wg[0].cpu()) == float(w[0])  # element before the slice untouched
 
 
+@pytest.mark.parametrize("B,V,ld,smooth", [(24, 33708, 33712, 0.1), (8, 8195, 8200, 0.0), (16, 32000, 32000, 0.1),
+                                          (4, 40960, 40960, 0.0)])
+def test_softmax_xent_padded_vocab(B, V, ld, smooth):
+    """Register-resident xent kernel: vocab padded to ld (the Transformer-big 33708 -> 33712 layout),
+    padding columns excluded from the softmax and given a zero gradient; argmax ties / ignore_index."""
+    x = bf(B, ld, scale=3.0, seed=15)
+    x[1, 5] = x[1, 9] = 40.0  # tie: smallest index wins
+    lab = torch.randint(0, V, (B,), dtype=torch.int32)
+    lab[0] = -100
+    lab[1] = 5
+    l_ref, d_ref, c_ref = LS.softmax_xent(x, lab, smooth, scale=1.0 / B, want_correct=True, V=V)
+    l, d, c = LS.softmax_xent(x.to(DEV), lab.to(DEV), smooth, scale=1.0 / B, want_correct=True, V=V)
+    assert rel(l, l_ref) < 1e-3
+    assert rel(d[:, :V], d_ref[:, :V]) < 1e-2
+    assert float(d[:, V:].float().abs().sum().cpu()) == 0.0
+    assert torch.equal(c.cpu(), c_ref)
+
+
 def test_global_norm_clip():
     g = torch.randn(100000) * 3
     ss, coef, nrm = (torch.zeros(1, device=DEV) for _ in range(3))

@@ -34,6 +34,7 @@ int tfk_maxpool_bwd(const void*, const uint8_t*, void*, int, int, int, int, int,
 int tfk_avgpool_fwd(const void*, void*, int, int, int, hipStream_t);
 int tfk_avgpool_bwd(const void*, void*, int, int, int, hipStream_t);
 int tfk_softmax_xent(const void*, const int*, int, int, long long, float, int, float, float*, void*, float*, hipStream_t);
+int tfk_xent_full_row(int, long long);
 int tfk_sgd(float*, void*, const float*, float*, long long, float, float, float, int, float, const float*, hipStream_t);
 int tfk_adamw(float*, void*, const float*, float*, float*, long long, float, float, float, float, float, float, float, float,
               const float*, hipStream_t);
@@ -568,6 +569,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("softmax_xent", &softmax_xent);
+  m.def("xent_full_row", [](int V, int64_t ld) { return tfk_xent_full_row(V, ld) != 0; });
   m.def("sgd", &sgd);
   m.def("adamw", &adamw);
   m.def("lamb", &lamb);

@@ -151,9 +151,11 @@ __global__ __launch_bounds__(NT) void xent_reg_kernel(const bf16* __restrict__ l
   if (!dlogits) return;
   bf16* d = dlogits + (long long)row * ld;
   const float inv_se = 1.f / se, off = smoothing / V, sc = valid ? scale : 0.f;
+  const int nw = (int)(ld >> 3);  // every chunk of the padded row is written (padding -> 0)
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     const int i = threadIdx.x + c * NT;
+    if (i >= nch && i < nw) *(bf16x8*)(d + i * 8) = bf16x8{};
     if (i < nch) {
       bf16x8 o;
 #pragma unroll
@@ -175,9 +177,15 @@ static bool xent_reg_on() {
 }
 }  // namespace
 
+// 1 when the launcher takes the register kernel, which writes every column of the padded dlogits row
+// (callers can then skip zero-filling the padding).
+extern "C" int tfk_xent_full_row(int V, long long ld) {
+  return (ld % 8 == 0 && ld >= V && ld / 8 <= XENT_REG_CH * NT && xent_reg_on()) ? 1 : 0;
+}
+
 extern "C" int tfk_softmax_xent(const bf16* logits, const int* labels, int B, int V, long long ld, float smoothing,
                                 int ignore_index, float scale, float* loss, bf16* dlogits, float* correct, hipStream_t s) {
-  if (ld % 8 == 0 && ld >= V && (V + 7) / 8 <= XENT_REG_CH * NT && xent_reg_on()) {
+  if (tfk_xent_full_row(V, ld)) {
     hipLaunchKernelGGL(xent_reg_kernel<XENT_REG_CH>, dim3(B), dim3(NT), 0, s, logits, labels, V, ld, smoothing,
                        ignore_index, scale, loss, dlogits, correct);
     return hipGetLastError() == hipSuccess ? 0 : -1;

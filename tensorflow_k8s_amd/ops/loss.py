@@ -37,7 +37,9 @@ def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 
         corr = ((x.argmax(1) == lab) & valid).float() if want_correct else None
         return loss, d, corr
     loss = torch.empty(B, dtype=torch.float32, device=logits.device)
-    d = (torch.empty_like(logits) if V == ld else torch.zeros_like(logits)) if want_grad else None
+    # the register kernel writes the padding columns itself; only the streaming kernel needs a zeroed buffer
+    full = V == ld or bool(lib().xent_full_row(V, ld))
+    d = (torch.empty_like(logits) if full else torch.zeros_like(logits)) if want_grad else None
     corr = torch.empty(B, dtype=torch.float32, device=logits.device) if want_correct else None
     lib().softmax_xent(logits, labels, B, V, ld, smoothing, ignore_index, scale, loss, d, corr)
     return loss, d, corr

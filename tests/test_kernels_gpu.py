@@ -231,7 +231,7 @@ def test_adamw_vector_and_tail(n, off):
         assert float(wg[0].cpu()) == float(w[0])  # element before the slice untouched
 
 
-@pytest.mark.parametrize("B,V,ld,smooth", [(24, 33708, 33712, 0.1), (8, 8195, 8200, 0.0), (16, 32000, 32000, 0.1),
+@pytest.mark.parametrize("B,V,ld,smooth", [(24, 33708, 33712, 0.1), (8, 33708, 33728, 0.1), (8, 8195, 8200, 0.0), (16, 32000, 32000, 0.1),
                                           (4, 40960, 40960, 0.0)])
 def test_softmax_xent_padded_vocab(B, V, ld, smooth):
     """Register-resident xent kernel: vocab padded to ld (the Transformer-big 33708 -> 33712 layout),

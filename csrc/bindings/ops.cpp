@@ -14,6 +14,7 @@ extern "C" {
 int tfk_gemm_launch(tfk::GemmParams p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits, hipStream_t s);
 int tfk_gemm_splits(int K, int splits);
 void tfk_gemm_set_persist(int on);
+void tfk_gemm_set_engine(int e);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_probe(const int*, const int*, const int*, const int*, float*, hipStream_t);
 int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, hipStream_t s);
@@ -199,8 +200,10 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
   p.drop_seed = (unsigned long long)drop_seed;
   const bool dense_a = amode == A_KIN || amode == A_KOUT;
+  // the conv-fwd-gather 256x256 tile exists on the LDS-DMA engine (gemm_g4.hip) only; the launcher
+  // falls back to 128x128 where that engine declines the shape
   TORCH_CHECK((bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64) ||
-                  (bm == 256 && bn == 256 && dense_a && (bmode == B_KIN || bmode == B_KOUT)) ||
+                  (bm == 256 && bn == 256 && (dense_a || amode == A_CONV_FWD) && (bmode == B_KIN || bmode == B_KOUT)) ||
                   (bm == 256 && bn == 64 && dense_a && !(amode == A_KOUT && bmode == B_KOUT && epi == 0)) ||
                   (bm == 64 && bn == 256 && amode == A_KOUT && bmode == B_CONV_WGRAD && epi == 1),
               "unsupported tile ", bm, "x", bn, " for operand modes ", amode, "/", bmode);
@@ -237,6 +240,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
 int64_t gemm_splits(int K, int splits) { return tfk_gemm_splits(K, splits); }
 // A/B switch for the persistent GEMM grid (tools/op_profile.py); default on.
 void gemm_set_persist(int on) { tfk_gemm_set_persist(on); }
+void gemm_set_engine(int e) { tfk_gemm_set_engine(e); }
 
 void mx_probe(torch::Tensor X, torch::Tensor Y, torch::Tensor sx, torch::Tensor sy, torch::Tensor D) {
   for (auto* t : {&X, &Y}) { need(*t, at::kInt, "probe operand"); need_numel(*t, 64 * 8, "probe operand"); }
@@ -555,6 +559,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm);
   m.def("gemm_splits", &gemm_splits);
   m.def("gemm_set_persist", &gemm_set_persist);
+  m.def("gemm_set_engine", &gemm_set_engine);
   m.def("mx_quant", &mx_quant);
   m.def("mx_probe", &mx_probe);
   m.def("gemm_mxfp8", &gemm_mxfp8);

@@ -429,19 +429,28 @@ static int launch_gemm(const GemmParams& p, int tiles, int batch, int splits, hi
 #define TFK_GEMM_TILES(AM_, BM2_, EPI_) TFK_GEMM_TILES3(AM_, BM2_, EPI_) TFK_GEMM_CASE(256, 64, AM_, BM2_, EPI_)
 #define TFK_GEMM_TILES_BIG(AM_, BM2_, EPI_) TFK_GEMM_TILES(AM_, BM2_, EPI_) TFK_GEMM_CASE(256, 256, AM_, BM2_, EPI_)
 
+extern "C" int tfk_g4_ok(const GemmParams& p, int amode, int bmode);
+extern "C" int tfk_g4_launch(const GemmParams& p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits,
+                             hipStream_t stream);
+// Engine for the tiles the LDS-DMA kernel serves: 1 = g4 (gemm_g4.hip: 64x64 wave tiles,
+// 128x128 / 256x256 blocks, dense + conv-fwd gather), 0 = this file's register-staged engine
+// (TFK_GEMM_ENGINE=reg, for A/B).
+static int g_pp = -1;
+static int engine() {
+  if (g_pp < 0) {
+    const char* e = getenv("TFK_GEMM_ENGINE");
+    g_pp = (e && e[0] == 'r') ? 0 : 1;
+  }
+  return g_pp;
+}
+extern "C" void tfk_gemm_set_engine(int e) { g_pp = e; }
+
 // Host launcher. Grid: x = tiles (M x N), y = batch, z = split-K. Returns 0 on success.
-extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits,
-                               hipStream_t stream) {
+// Register-staged engine: every instantiated (tile, operand modes, epilogue). -1 if absent.
+static int launch_reg(GemmParams p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits,
+                      hipStream_t stream) {
   const int tiles_m = (p.M + bm - 1) / bm, tiles_n = (p.N + bn - 1) / bn;
-  const int nkt = (p.K + BK - 1) / BK;
-  if (splits < 1) splits = 1;
-  if (splits > nkt) splits = nkt > 0 ? nkt : 1;
-  p.kt_per_split = (nkt + splits - 1) / splits;
-  splits = nkt > 0 ? (nkt + p.kt_per_split - 1) / p.kt_per_split : 1;
   p.tiles_n = tiles_n;
-  if (p.stats_shards < 1) p.stats_shards = 1;
-  if (epi == EPI_BF16 && p.bn_sums) epi = EPI_BF16_BNR;
-  if (epi == EPI_BF16 && (p.aux || p.dact_src || p.drop_p > 0.f)) epi = EPI_BF16_EXT;
   TFK_GEMM_TILES_BIG(A_KIN, B_KIN, EPI_BF16)
   TFK_GEMM_TILES_BIG(A_KIN, B_KIN, EPI_F32)
   TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_BF16)
@@ -463,6 +472,31 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
   TFK_GEMM_TILES3(A_CONV_DGRAD, B_KIN, EPI_BF16_BNR)
   TFK_GEMM_TILES3(A_CONV_DGRAD, B_KOUT, EPI_BF16_BNR)
   return -1;  // unsupported combination
+}
+
+// Host launcher. Grid: x = tiles (M x N), y = batch, z = split-K. Returns 0 on success.
+// The LDS-DMA engine (g4) takes the tiles/modes it serves; the rest, and any tile it declines
+// (ineligible shape/alignment), runs on the register-staged engine.
+extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits,
+                               hipStream_t stream) {
+  const int nkt = (p.K + BK - 1) / BK;
+  if (splits < 1) splits = 1;
+  if (splits > nkt) splits = nkt > 0 ? nkt : 1;
+  p.kt_per_split = (nkt + splits - 1) / splits;
+  splits = nkt > 0 ? (nkt + p.kt_per_split - 1) / p.kt_per_split : 1;
+  p.tiles_n = (p.N + bn - 1) / bn;
+  if (p.stats_shards < 1) p.stats_shards = 1;
+  if (epi == EPI_BF16 && p.bn_sums) epi = EPI_BF16_BNR;
+  if (epi == EPI_BF16 && (p.aux || p.dact_src || p.drop_p > 0.f)) epi = EPI_BF16_EXT;
+  if (p.om_hp == 0 && p.rs_sh == 0) {
+    if (engine() == 1 && tfk_g4_ok(p, amode, bmode)) {
+      const int r = tfk_g4_launch(p, bm, bn, amode, bmode, epi, batch, splits, stream);
+      if (r != -1) return r;
+    }
+  }
+  const int r = launch_reg(p, bm, bn, amode, bmode, epi, batch, splits, stream);
+  if (r != -1 || (bm == 128 && bn == 128)) return r;
+  return launch_reg(p, 128, 128, amode, bmode, epi, batch, splits, stream);
 }
 
 // Number of split-K slabs the launcher will actually use (for workspace sizing).

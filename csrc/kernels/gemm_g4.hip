@@ -1,0 +1,290 @@
+// tfk "g4" GEMM engine for gfx950: 4 waves per block (one per SIMD), each wave owning a large
+// (BM/2 x BN/2) output tile so that LDS fragment reads per MFMA are halved against 8-wave tiles
+// (rocprofv3 on 8192^3: the 8-wave ping-pong kernel issued 1.8x the LDS instructions of
+// hipBLASLt's MT256x256x64 4-wave kernel and spent 3.2e8 quad-cycles waiting at barriers;
+// profiles/gemm_engine_r2.md). The accumulators live in the AGPR half of the 512-entry register file.
+//
+// Pipeline per K-tile t (BK = 64, stage s = t & 1, two LDS stages):
+//   issue the LDS-DMA of K-tile t+1 into stage s^1        (lands during the whole of tile t)
+//   read the k-half-1 fragments of tile t from stage s    (overlaps the k-half-0 MFMAs)
+//   MFMAs k-half 0, then k-half 1
+//   s_waitcnt vmcnt(0) lgkmcnt(0); barrier               (tile t+1 landed; every read of s retired)
+//   read the k-half-0 fragments of tile t+1 from stage s^1
+// so HBM/L2 latency hides under one K-tile of MFMAs and each K-tile costs one barrier.
+//
+// Operand images (cdna_hip_programming.md §2 T2 / T10; one __shared__ array):
+//   K-inner [rows][64 k] bf16, 128-B rows, chunk c of row r at r*128 + ((c ^ (r>>1 & 7)) << 4)
+//     -> conflict-free ds_read_b128 row fragments.
+//   K-outer blocks of 64 rows: [64 k][64 rows] bf16, chunk c of k-row k at k*128 + ((c ^ swz(k)) << 4),
+//     swz(k) = 2*((k>>1 & 1) | (k>>3 & 1)<<1) -> conflict-free ds_read_b64_tr_b16 column fragments.
+// LDS-DMA writes 1 KiB lane-linear per wave instruction (8 image rows / 8 k-rows, full 128-B
+// global lines), so the swizzle goes on the per-lane SOURCE address (rule 21). Out-of-range
+// rows/k read zeros: the buffer descriptor range check returns 0 for offsets past num_records.
+//
+// Operand modes: A_KIN / A_KOUT / A_CONV_FWD (implicit-GEMM gather, Cin % 64 == 0: a K-tile is one
+// (r,s) tap and 64 channels) x B_KIN / B_KOUT. Epilogues: gemm_epilogue.h (LDS-staged).
+#include "common.h"
+#include "gemm_params.h"
+#include "gemm_epilogue.h"
+
+namespace tfk {
+namespace g4 {
+
+constexpr int BK = 64;
+constexpr unsigned OOB = 0x80000000u;
+constexpr int NREC = 0x7FFFFFF0;
+
+enum { KIN = 0, KOUT = 1, CONV_FWD = 2 };
+
+__device__ __forceinline__ int swz64(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
+
+// Fragment (16 image rows from rb, K-half kk) of an operand image with ROWS rows.
+template <bool KO>
+__device__ __forceinline__ bf16x8 frag(const char* img, int rb, int kk) {
+  const int l = threadIdx.x & 63;
+  if constexpr (!KO) {
+    const int row = rb + (l & 15);
+    const int c = kk * 4 + (l >> 4);
+    return *(const bf16x8*)(img + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+  } else {
+    const char* b = img + (rb >> 6) * 8192;
+    const int g = l >> 4, i = l & 15, q = i >> 2, pc = i & 3;
+    const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;
+    const int ch = ((rb & 63) >> 3) + (pc >> 1);
+    const int o0 = k0 * 128 + ((ch ^ swz64(k0)) << 4) + (pc & 1) * 8;
+    const int o1 = k1 * 128 + ((ch ^ swz64(k1)) << 4) + (pc & 1) * 8;
+    bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)(b + o0));
+    bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)(b + o1));
+    bf16x8 r;
+    r.lo = lo;
+    r.hi = hi;
+    return r;
+  }
+}
+
+// Per-thread DMA plan of one operand: ROWS/32 instructions per K-tile. Instruction j (of ROWS/8,
+// wave w takes j = 4i + w) fills image bytes [j*1024, j*1024+1024).
+template <int ROWS, int MODE, int NW>
+struct Loader {
+  static constexpr int NI = ROWS / 8 / NW;  // DMA instructions per thread per K-tile
+  // dense: byte offset from the tile origin at K-tile 0; conv: image index n of the lane's pixel
+  unsigned off[NI];
+  // conv gather: input-space origin (p*sh - ph, q*sw - pw) of the lane's output pixel
+  int ch[NI], cw[NI];
+
+  // row (K-inner) / column (K-outer) of instruction i's lane inside the tile, and its k in a K-tile
+  __device__ __forceinline__ static int row_of(int i, int w, int lane) {
+    const int j = NW * i + w;
+    if constexpr (MODE == KOUT) return (j >> 3) * 64 + 8 * ((lane & 7) ^ swz64((j & 7) * 8 + (lane >> 3)));
+    else return 8 * j + (lane >> 3);
+  }
+  __device__ __forceinline__ static int k_of(int i, int w, int lane) {
+    const int j = NW * i + w;
+    if constexpr (MODE == KOUT) return (j & 7) * 8 + (lane >> 3);
+    else return 8 * ((lane & 7) ^ (((8 * j + (lane >> 3)) >> 1) & 7));
+  }
+
+  __device__ __forceinline__ void init(const GemmParams& p, int lane, int w, long long ld, int row0, int rows) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int r = row_of(i, w, lane), kl = k_of(i, w, lane);
+      if constexpr (MODE == KIN) {
+        off[i] = (unsigned)(((long long)r * ld + kl) * 2);
+      } else if constexpr (MODE == KOUT) {
+        off[i] = (unsigned)(((long long)kl * ld + r) * 2);
+      } else {
+        const int m = min(row0 + r, rows - 1);
+        const int PQ = p.P * p.Q;
+        const int n = m / PQ, rem = m - n * PQ, pp = rem / p.Q, qq = rem - pp * p.Q;
+        ch[i] = pp * p.sh - p.ph;
+        cw[i] = qq * p.sw - p.pw;
+        off[i] = (unsigned)n;
+      }
+    }
+  }
+
+  // Issue this thread's DMA instructions of K-tile kt into image `img`. base = tile origin;
+  // lim = rows left from the tile origin. Interior tiles with a full K-tile skip every edge test.
+  __device__ __forceinline__ void issue(const GemmParams& p, const char* base, long long step, int kt, int lim,
+                                        char* img, int w, int lane) const {
+    const int krem = p.K - kt * BK;
+    const bool inner = lim >= ROWS && krem >= BK;  // block-uniform
+    if constexpr (MODE == CONV_FWD) {
+      // K-tile kt covers tap (r, s) = divmod(kt*64 / Cin, S) and channels c0..c0+63 (Cin % 64 == 0)
+      const int k0 = kt * BK, rs = k0 / p.Cin, c0 = k0 - rs * p.Cin;
+      const int r = rs / p.S, s = rs - r * p.S;
+      __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, NREC, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int h = ch[i] + r * p.dh, wq = cw[i] + s * p.dw;
+        const bool ok = (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
+        const long long pix = ((long long)off[i] * p.H + h) * p.W + wq;
+        const unsigned vo = ok ? (unsigned)((pix * p.Cin + c0 + k_of(i, w, lane)) * 2) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
+      }
+    } else {
+      __amdgpu_buffer_rsrc_t rsrc =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(base + kt * step), (short)0, NREC, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        unsigned vo = off[i];
+        if (!inner) vo = (row_of(i, w, lane) < lim && k_of(i, w, lane) < krem) ? vo : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
+      }
+    }
+  }
+};
+
+// Block = (BM/64) x (BN/64) waves, each owning a 64x64 output tile (4x4 16x16 fragments): the
+// 128x128 tile runs 4 waves at two blocks per CU, 256x128 runs 8 and 256x256 runs 16 waves (one
+// block per CU, 128 KiB of stages) -- occupancy from co-resident waves, not one big wave per SIMD
+// (measured: 1-wave/SIMD 128x128 wave tiles spill AGPR accumulators under hipcc 7.2).
+template <int BM, int BN>
+constexpr int nwaves() { return (BM / 64) * (BN / 64); }
+
+template <int BM, int BN, int AM, int BMD, int EPI>
+__global__ __launch_bounds__((nwaves<BM, BN>() * 64), ((BM * BN <= 128 * 128) ? 2 : 1)) void g4_kernel(GemmParams p) {
+  constexpr int NW = nwaves<BM, BN>(), NTH = NW * 64, WGM = BM / 64, WGN = BN / 64;
+  constexpr bool AKO = (AM == KOUT), BKO = (BMD == KOUT);
+  constexpr int WTM = 64, WTN = 64, FM = 4, FN = 4;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int MAIN = 2 * STAGE, EPIB = epi_lds_bytes<BM, BN, WGM>();
+  __shared__ __attribute__((aligned(16))) char smem[MAIN > EPIB ? MAIN : EPIB];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WGN, wn = w % WGN;
+  const int bz = blockIdx.y;
+
+  // tile order: XCD remap, then GROUP_M = 4 inside each XCD's contiguous range
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 4;
+  const int grp = tile / (GM * p.tiles_n), first_m = grp * GM;
+  const int gm = min(GM, tiles_m - first_m), inr = tile - grp * GM * p.tiles_n;
+  const int m0 = (first_m + inr % gm) * BM, n0 = (inr / gm) * BN;
+
+  const int nkt = (p.K + BK - 1) / BK;
+  const int kt0 = blockIdx.z * p.kt_per_split;
+  const int kt1 = min(nkt, kt0 + p.kt_per_split);
+
+  const char* Ab;
+  if constexpr (AM == CONV_FWD) Ab = (const char*)p.A + (long long)bz * p.sA * 2;
+  else Ab = (const char*)p.A + (long long)bz * p.sA * 2 + (AKO ? (long long)m0 * 2 : (long long)m0 * p.lda * 2);
+  const char* Bb = (const char*)p.B + (long long)bz * p.sB * 2 + (BKO ? (long long)n0 * 2 : (long long)n0 * p.ldb * 2);
+  const long long a_step = AKO ? (long long)BK * p.lda * 2 : BK * 2;
+  const long long b_step = BKO ? (long long)BK * p.ldb * 2 : BK * 2;
+  const int lim_a = p.M - m0, lim_b = p.N - n0;
+
+  Loader<BM, AM, NW> la;
+  Loader<BN, BMD, NW> lb;
+  la.init(p, lane, w, p.lda, m0, p.M);
+  lb.init(p, lane, w, p.ldb, n0, p.N);
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage_ptr = [&](int s) { return smem + s * STAGE; };
+
+  la.issue(p, Ab, a_step, kt0, lim_a, stage_ptr(0), w, lane);
+  lb.issue(p, Bb, b_step, kt0, lim_b, stage_ptr(0) + A_BYTES, w, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // B fragments of a K-half are held for the whole half (FN x 4 VGPRs); A fragments stream, one
+  // 16-row fragment at a time (read one ahead of its FN MFMAs), so the double-buffered operand
+  // registers stay at 2*FN*4 + ~3*4 next to the AGPR accumulators.
+  bf16x8 b0[FN], b1[FN];
+  const int ar = wm * WTM, bc = wn * WTN;
+  {
+    const char* As = stage_ptr(0);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) b0[j] = frag<BKO>(As + A_BYTES, bc + j * 16, 0);
+  }
+
+#pragma unroll 1
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int s = (kt - kt0) & 1;
+    const char* As = stage_ptr(s);
+    const char* Bs = As + A_BYTES;
+    const bool more = kt + 1 < kt1;
+    if (more) {
+      char* nx = stage_ptr(s ^ 1);
+      la.issue(p, Ab, a_step, kt + 1, lim_a, nx, w, lane);
+      lb.issue(p, Bb, b_step, kt + 1, lim_b, nx + A_BYTES, w, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) b1[j] = frag<BKO>(Bs, bc + j * 16, 1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const bf16x8 a = frag<AKO>(As, ar + i * 16, 0);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a, acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const bf16x8 a = frag<AKO>(As, ar + i * 16, 1);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a, acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const char* Bn = stage_ptr(s ^ 1) + A_BYTES;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b0[j] = frag<BKO>(Bn, bc + j * 16, 0);
+    }
+  }
+  __syncthreads();
+  gemm_epilogue<BM, BN, NTH, WGM, EPI>(p, acc, smem, m0, n0, bz);
+}
+
+}  // namespace g4
+}  // namespace tfk
+
+using namespace tfk;
+
+// Eligibility: 16-B aligned operand rows, K % 8 == 0 (a chunk never straddles K), K-outer row
+// counts % 8 == 0; conv gather: Cin % 64 == 0 (a K-tile = one tap x 64 channels).
+extern "C" int tfk_g4_ok(const GemmParams& p, int amode, int bmode) {
+  if (!(amode == 0 || amode == 1 || amode == 2) || bmode > 1) return 0;
+  if ((p.K & 7) || (p.ldb & 7)) return 0;
+  if (amode != 2 && (p.lda & 7)) return 0;
+  if (((uintptr_t)p.A & 15) || ((uintptr_t)p.B & 15)) return 0;
+  if ((p.sA & 7) || (p.sB & 7)) return 0;
+  if (amode == 1 && (p.M & 7)) return 0;
+  if (bmode == 1 && (p.N & 7)) return 0;
+  if (amode == 2 && ((p.Cin & 63) || (long long)p.Nimg * p.H * p.W * p.Cin >= (1LL << 30))) return 0;
+  return 1;
+}
+
+#define TFK_G4_CASE(BM_, BN_, AM_, BM2_, EPI_)                                                      \
+  if (bm == BM_ && bn == BN_ && amode == AM_ && bmode == BM2_ && epi == EPI_) {                     \
+    hipLaunchKernelGGL((g4::g4_kernel<BM_, BN_, AM_, BM2_, EPI_>), dim3(tiles, batch, splits),                \
+                       dim3(g4::nwaves<BM_, BN_>() * 64), 0,                                           \
+                       stream, p);                                                                  \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                                \
+  }
+#define TFK_G4_TILES(AM_, BM2_, EPI_) TFK_G4_CASE(256, 256, AM_, BM2_, EPI_) TFK_G4_CASE(128, 128, AM_, BM2_, EPI_)
+
+// p.tiles_n / p.kt_per_split set by the caller (tfk_gemm_launch). Returns -1 if not instantiated.
+extern "C" int tfk_g4_launch(const GemmParams& p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits,
+                             hipStream_t stream) {
+  const int tiles = ((p.M + bm - 1) / bm) * p.tiles_n;
+  TFK_G4_TILES(0, 0, EPI_BF16)
+  TFK_G4_TILES(0, 0, EPI_F32)
+  TFK_G4_TILES(0, 0, EPI_BF16_EXT)
+  TFK_G4_TILES(0, 1, EPI_BF16)
+  TFK_G4_TILES(0, 1, EPI_F32)
+  TFK_G4_TILES(0, 1, EPI_BF16_EXT)
+  TFK_G4_TILES(0, 1, EPI_BF16_BNR)
+  TFK_G4_TILES(1, 1, EPI_F32)
+  TFK_G4_TILES(1, 1, EPI_BF16)
+  TFK_G4_TILES(2, 0, EPI_BF16)
+  return -1;
+}

@@ -77,28 +77,40 @@ class ConvGeom:
         return 2 * self.N * self.P * self.Q * self.K * self.R * self.S * self.C
 
 
-# (bm, bn): (concurrent blocks on the chip, relative MFMA efficiency measured by tools/gemm_bench.py)
+# (bm, bn): (concurrent blocks on the chip, relative MFMA efficiency) of the register-staged engine
+# (gemm.hip), measured by tools/gemm_bench.py in round 1.
 _TILES = {(256, 256): (256, 0.76), (128, 128): (512, 0.62), (256, 64): (512, 0.60), (128, 64): (768, 0.45),
           (64, 64): (1024, 0.30), (64, 256): (512, 0.55)}
+# The LDS-DMA engine (gemm_g4.hip) on the same scale, for the modes it serves (dense operands and the
+# Cin % 64 == 0 conv-forward gather): tools/engine_bench.py on MI355X -- 256x256 (16 waves) ~1.0-1.3
+# PF/s, 128x128 (4 waves, 2 blocks/CU) ~0.7-1.1 PF/s vs the register engine's 0.6-0.9.
+_G4_TILES = {(256, 256): (256, 0.95), (128, 128): (512, 0.80)}
+G4_BIG_MIN_K = 512  # one 16-wave block per CU: shorter K cannot amortise its prologue/epilogue
 # 64x256 tile for Cout<=64 conv weight gradients whose B gather changes (r,s) every chunk (C <= 16,
 # i.e. the 7x7 stem on C padded to 8). Measured on MI355X (ResNet-50 bs256, rocprofv3): stem wgrad
 # 673 -> 644 us; the stage-1 3x3 (C=64) got slower on it (236 -> 249 us), so it keeps 64x64.
 WIDE_WGRAD = os.environ.get("TFK_WIDE_WGRAD", "1") == "1"
 WIDE_WGRAD_MAX_C = 16
-BIG_TILE_MIN_K = 2048  # one 8-wave block per CU: its prologue/epilogue is exposed, so it needs a long K loop
+BIG_TILE_MIN_K = 2048  # register engine: one 8-wave block per CU, needs a long K loop
+G4_ENABLED = os.environ.get("TFK_GEMM_ENGINE", "g4") != "reg"
 
 
 def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: int = 0, mid_ok: bool = True,
-              wide_ok: bool = False, split_target: int | None = None):
+              wide_ok: bool = False, split_target: int | None = None, g4: bool = False):
     """Tile with the lowest modelled time: rounds of concurrent blocks x per-block work / efficiency
-    (a 256x256 tile runs one 8-wave block per CU; smaller tiles 2-4 blocks/CU at lower efficiency).
+    (a 256x256 tile runs one block per CU; smaller tiles 2-4 blocks/CU at lower efficiency).
     big_ok: operand modes that have the 256x256 instantiation (dense, non-gather); K: reduction
-    length (the big tile is only used without split-K and for K >= BIG_TILE_MIN_K). mid_ok: the
-    mode has the 256x64 tile (every mode except the conv fwd/dgrad gathers). wide_ok: the mode has
-    the 64x256 tile (conv weight gradient gather), only worth it for M <= 64."""
+    length. mid_ok: the mode has the 256x64 tile (every mode except the conv fwd/dgrad gathers).
+    wide_ok: the mode has the 64x256 tile (conv weight gradient gather), only worth it for M <= 64.
+    g4: the mode runs on the LDS-DMA engine (its 128x128 / 256x256 tiles; 256x256 also with split-K)."""
+    g4 = g4 and G4_ENABLED
     best, best_cost = None, None
     for (bm, bn), (slots, eff) in _TILES.items():
-        if (bm, bn) == (256, 256) and (not big_ok or splits_ok or M < 256 or N < 256 or K < BIG_TILE_MIN_K):
+        if g4 and (bm, bn) in _G4_TILES:
+            slots, eff = _G4_TILES[(bm, bn)]
+            if (bm, bn) == (256, 256) and (M < 256 or N < 256 or K < G4_BIG_MIN_K):
+                continue
+        elif (bm, bn) == (256, 256) and (not big_ok or splits_ok or M < 256 or N < 256 or K < BIG_TILE_MIN_K):
             continue
         if (bm, bn) == (256, 64) and (not mid_ok or M < 256):
             continue
@@ -108,9 +120,13 @@ def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: 
             continue
         tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
         s = pick_splits(tiles, K, target=split_target) if (splits_ok and K) else 1
-        kfrac = 1.0 / s
         rounds = -(-tiles * s // slots)
-        cost = rounds * (slots / 256) * bm * bn * kfrac / eff
+        # seconds: MFMA work per round at eff x (2.3 PF / 256 CUs), a fixed prologue/epilogue
+        # latency per round, and the f32 split-K slabs (written, then read by splitk_reduce)
+        kb = max(K, 64) / s
+        cost = rounds * ((slots / 256) * 2.0 * bm * bn * kb / (eff * 9.0e12) + 1.5e-6)
+        if s > 1:
+            cost += 2.0 * s * M * N * 4 / 4.0e12
         if best_cost is None or cost < best_cost * 0.98:
             best, best_cost = (bm, bn), cost
     return best
@@ -186,7 +202,7 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
     x2 = x.reshape(-1, K)
     M = x2.shape[0]
     y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-    _gemm(x2, w, y, M, N, K, K, K, N, A_KIN, B_KIN, EPI_BF16, pick_tile(M, N, big_ok=True, K=K), bias=bias, act=ACT[act],
+    _gemm(x2, w, y, M, N, K, K, K, N, A_KIN, B_KIN, EPI_BF16, pick_tile(M, N, big_ok=True, K=K, g4=True), bias=bias, act=ACT[act],
           resid=resid.reshape(-1, N) if resid is not None else None, aux=aux, drop_p=drop_p, drop_seed=drop_seed)
     return y
 
@@ -220,7 +236,7 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
             dx = (dx.float() + resid.reshape(-1, K).float()).to(torch.bfloat16)
         return dx
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
-    _gemm(dy2, w, dx, M, K, N, N, K, K, A_KIN, B_KOUT, EPI_BF16, pick_tile(M, K, big_ok=True, K=N),
+    _gemm(dy2, w, dx, M, K, N, N, K, K, A_KIN, B_KOUT, EPI_BF16, pick_tile(M, K, big_ok=True, K=N, g4=K % 8 == 0),
           resid=resid.reshape(-1, K) if resid is not None else None,
           dact_src=dact_src.reshape(-1, K) if dact_src is not None else None,
           dact=ACT[dact] if dact_src is not None else 0)
@@ -241,7 +257,7 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
         else:
             gw.view(N, K).copy_(g)
         return
-    tile = pick_tile(N, K, splits_ok=True, big_ok=True, K=M, split_target=split_target)
+    tile = pick_tile(N, K, splits_ok=True, big_ok=True, K=M, split_target=split_target, g4=N % 8 == 0 and K % 8 == 0)
     tiles = ((N + tile[0] - 1) // tile[0]) * ((K + tile[1] - 1) // tile[1])
 
     def run(C, splits, stride, beta):
@@ -270,7 +286,7 @@ def matmul_tn(a: torch.Tensor, b: torch.Tensor, out_f32: torch.Tensor | None = N
     if not on_gpu(a):
         out.copy_(a.float().t() @ b.float())
         return out
-    tile = pick_tile(M, N, splits_ok=True, big_ok=True, K=K)
+    tile = pick_tile(M, N, splits_ok=True, big_ok=True, K=K, g4=M % 8 == 0 and N % 8 == 0)
     tiles = ((M + tile[0] - 1) // tile[0]) * ((N + tile[1] - 1) // tile[1])
 
     def run(C, splits, stride, beta):
@@ -303,7 +319,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
         return y.to(torch.bfloat16).contiguous()
     M = g.N * g.P * g.Q
     y = torch.empty(g.N, g.P, g.Q, g.K, dtype=torch.bfloat16, device=x.device)
-    tile = pick_tile(M, g.K, big_ok=g.pointwise, K=g.C, mid_ok=g.pointwise)
+    tile = pick_tile(M, g.K, big_ok=g.pointwise, K=g.R * g.S * g.C, mid_ok=g.pointwise,
+                     g4=g.pointwise or g.C % 64 == 0)
     if g.pointwise:
         _gemm(x, w, y, M, g.K, g.C, g.C, g.C, g.K, A_KIN, B_KIN, EPI_BF16, tile, stats=stats, shards=shards,
               bias=bias, act=ACT[act])
@@ -372,7 +389,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
         return dx
     M = g.N * g.H * g.W
     dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
-    tile = pick_tile(M, g.C, big_ok=g.pointwise, K=g.K, mid_ok=g.pointwise)
+    tile = pick_tile(M, g.C, big_ok=g.pointwise, K=g.K, mid_ok=g.pointwise, g4=g.pointwise and g.C % 8 == 0)
     if resid_stride > 1:
         if not g.pointwise or bnr is None or resid is None:
             raise ValueError("resid_stride needs a pointwise conv, a resid and the fused BN reduction")
@@ -420,7 +437,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
         v = gw.view(g.K, Nn)
         v.add_(gwt) if accumulate else v.copy_(gwt)
         return
-    tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp, wide_ok=WIDE_WGRAD and not g.pointwise and g.C <= WIDE_WGRAD_MAX_C)
+    tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp,
+                     wide_ok=WIDE_WGRAD and not g.pointwise and g.C <= WIDE_WGRAD_MAX_C,
+                     g4=g.pointwise and g.K % 8 == 0 and g.C % 8 == 0)
     tiles = ((g.K + tile[0] - 1) // tile[0]) * ((Nn + tile[1] - 1) // tile[1])
 
     def run(C, sp, stride, beta):

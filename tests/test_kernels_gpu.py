@@ -399,3 +399,70 @@ def test_splitk_atomic_matches_slab(M, N, K):
         assert rel(got[mode][0], ref) < 1e-3, mode
         assert rel(got[mode][1], ref + 1.0) < 1e-3, mode
     assert rel(got[True][0], got[False][0]) < 1e-5
+
+
+G4_SHAPES = [(256, 256, 64), (512, 768, 1024), (300, 264, 200), (1000, 520, 72), (2048, 1024, 136),
+             (4200, 4104, 200)]  # last: 289 tiles > 256 resident blocks -> persistent multi-item walk
+
+
+@pytest.mark.parametrize("tile", [(256, 256), (128, 128)])
+@pytest.mark.parametrize("M,N,K", G4_SHAPES)
+def test_lds_dma_gemm_modes(M, N, K, tile):
+    """The LDS-DMA GEMM engine (gemm_g4.hip: 64x64 wave tiles; 256x256 = 16 waves, 128x128 = 4) in
+    every dense mode it serves: NT bf16 (bias+relu), NN bf16 (residual), TN f32 (beta accumulate;
+    split-K slabs), on interior and ragged M/N/K (zero-filled out-of-range DMA), against the fp32
+    reference AND the register-staged engine (TFK_GEMM_ENGINE=reg)."""
+    L = lib()
+    x, w = bf(M, K, seed=1), bf(N, K, seed=2, scale=0.05)
+    dy, r = bf(M, N, seed=3), bf(M, K, seed=4)
+    b = torch.randn(N) * 0.1
+    gw0 = torch.randn(N, K)
+    xd, wd, dyd, rd, bd = x.to(DEV), w.to(DEV), dy.to(DEV), r.to(DEV), b.to(DEV)
+    t = tile
+    engines = (1, 0)
+    res = {}
+    try:
+        for eng in engines:
+            L.gemm_set_engine(eng)
+            y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            G._gemm(xd, wd, y, M, N, K, K, K, N, G.A_KIN, G.B_KIN, G.EPI_BF16, t, bias=bd, act=1)
+            dx = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
+            G._gemm(dyd, wd, dx, M, K, N, N, K, K, G.A_KIN, G.B_KOUT, G.EPI_BF16, t, resid=rd)
+            gw = gw0.clone().to(DEV)
+            G._gemm(dyd, xd, gw, N, K, M, N, K, K, G.A_KOUT, G.B_KOUT, G.EPI_F32, t, beta=1.0)
+            ns = int(L.gemm_splits(M, 3))
+            stride = ((N * K + 3) // 4) * 4
+            ws = torch.full((ns * stride,), float("nan"), device=DEV)
+            G._gemm(dyd, xd, ws, N, K, M, N, K, K, G.A_KOUT, G.B_KOUT, G.EPI_F32, t, splits=3, split_stride=stride)
+            gws = ws.view(ns, stride)[:, :N * K].sum(0).view(N, K)
+            torch.cuda.synchronize()
+            res[eng] = dict(y=y, dx=dx, gw=gw, gws=gws)
+    finally:
+        L.gemm_set_engine(1)
+    ref = dict(y=torch.relu(x.float() @ w.float().t() + b),
+               dx=(dy.float() @ w.float()).to(torch.bfloat16).float() + r.float(),
+               gw=gw0 + dy.float().t() @ x.float(), gws=dy.float().t() @ x.float())
+    for k, v in ref.items():
+        for eng in engines[:-1]:
+            assert rel(res[eng][k], v) < 1e-2, (eng, k, rel(res[eng][k], v))
+            assert rel(res[eng][k], res[0][k]) < 1e-2, (eng, k)
+
+
+@pytest.mark.parametrize("cfg", [(2, 14, 14, 64, 128, 3, 3, 1, 1), (3, 9, 11, 128, 200, 3, 3, 2, 1),
+                                 (2, 8, 8, 64, 64, 1, 1, 2, 0), (1, 30, 30, 64, 136, 5, 5, 1, 2)])
+@pytest.mark.parametrize("tile", [(256, 256), (128, 128)])
+def test_g4_conv_fwd_gather(cfg, tile):
+    """g4's implicit-GEMM conv-forward gather (Cin % 64 == 0: a K-tile is one tap x 64 channels,
+    zero padding from out-of-range DMA) against the fp32 reference, with BN statistics."""
+    N, H, W, C, K, R, S, st, pd = cfg
+    g = G.ConvGeom(N, H, W, C, K, R, S, st, st, pd, pd)
+    x, w = bf(N, H, W, C, seed=7), bf(K, R, S, C, scale=0.05, seed=8)
+    M = N * g.P * g.Q
+    Kd = R * S * C
+    y = torch.empty(N, g.P, g.Q, K, dtype=torch.bfloat16, device=DEV)
+    st_ = torch.zeros(2, K, device=DEV)
+    G._gemm(x.to(DEV), w.to(DEV), y, M, K, Kd, 0, Kd, K, G.A_CONV_FWD, G.B_KIN, G.EPI_BF16, tile, stats=st_,
+            shards=1, conv=g.vec())
+    ref = G._ref_conv(x, w, g)
+    assert rel(y, ref) < 1e-2
+    assert rel(st_[0], ref.reshape(-1, K).sum(0)) < 1e-2

@@ -546,6 +546,7 @@ void Store::gc_dependents_locked(const std::string& owner_uid, const std::string
       int64_t rv = rv_++;
       next["metadata"]["resourceVersion"] = std::to_string(rv);
       it->second = Obj{next, rv};
+      wal_locked("put", v.first, next);  // the terminating state must survive a WAL replay
       emit_locked(v.first, "MODIFIED", next, rv);
       continue;
     }

@@ -124,24 +124,38 @@ void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
   env["TFK_TERMINATION_LOG"] = c.term_path;
   if (opts_.local_dns) env["TFK_LOCAL_DNS"] = "1";
   std::string wd = spec->at("workingDir").str();
+  // Everything the child needs is built BEFORE fork(): the kubelet is multithreaded (informer,
+  // HTTP and watch threads), so between fork and exec the child may only make async-signal-safe
+  // calls -- a malloc there can deadlock on a lock another thread held at fork time.
+  std::vector<std::string> envs;
+  for (auto& kv : env) envs.push_back(kv.first + "=" + kv.second);
+  std::vector<char*> ev, av;
+  for (auto& s : envs) ev.push_back((char*)s.c_str());
+  ev.push_back(nullptr);
+  for (auto& s : argv) av.push_back((char*)s.c_str());
+  av.push_back(nullptr);
+  // execvp's PATH search is not async-signal-safe: resolve the program here, execve in the child
+  std::string prog = av[0] ? av[0] : "";
+  if (prog.find('/') == std::string::npos) {
+    for (const std::string& dir : split(env.count("PATH") ? env["PATH"] : std::string(getenv("PATH") ? getenv("PATH") : "/usr/bin:/bin"), ':')) {
+      std::string cand = (dir.empty() ? std::string(".") : dir) + "/" + prog;
+      if (access(cand.c_str(), X_OK) == 0) { prog = cand; break; }
+    }
+  }
+  const char* log_path = c.log_path.c_str();
+  const char* wd_c = wd.empty() ? nullptr : wd.c_str();
+  static const char kExecFail[] = "tfk-kubelet: exec failed\n";
   pid_t pid = fork();
   if (pid == 0) {
     setsid();
-    int fd = open(c.log_path.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
+    int fd = open(log_path, O_WRONLY | O_CREAT | O_APPEND, 0644);
     if (fd >= 0) { dup2(fd, 1); dup2(fd, 2); close(fd); }
     int nul = open("/dev/null", O_RDONLY);
     if (nul >= 0) { dup2(nul, 0); close(nul); }
-    if (!wd.empty() && chdir(wd.c_str()) != 0) { perror("chdir"); _exit(127); }
-    std::vector<std::string> envs;
-    for (auto& kv : env) envs.push_back(kv.first + "=" + kv.second);
-    std::vector<char*> ev, av;
-    for (auto& s : envs) ev.push_back((char*)s.c_str());
-    ev.push_back(nullptr);
-    for (auto& s : argv) av.push_back((char*)s.c_str());
-    av.push_back(nullptr);
-    environ = ev.data();
-    execvp(av[0], av.data());
-    fprintf(stderr, "exec %s failed: %s\n", av[0], strerror(errno));
+    if (wd_c && chdir(wd_c) != 0) _exit(127);
+    execve(prog.c_str(), av.data(), ev.data());
+    ssize_t wr = write(2, kExecFail, sizeof(kExecFail) - 1);
+    (void)wr;
     _exit(127);
   }
   if (pid < 0) {

@@ -252,6 +252,35 @@ TEST(store_finalizers_and_gc) {
   CHECK_EQ(s->get("pods", "default", "child", &out).code, 404);
 }
 
+// a dependent that cascade GC marks terminating (it has finalizers) must keep that
+// state across an apiserver restart (WAL replay).
+TEST(store_gc_terminating_dependent_survives_wal_replay) {
+  char tmpl[] = "/tmp/tfk-wal-XXXXXX";
+  int fd = mkstemp(tmpl);
+  CHECK(fd >= 0);
+  close(fd);
+  std::string path = tmpl;
+  {
+    Store s(path);
+    install_tfjob_crd(s);
+    Json owner, out;
+    CHECK(s.create("tfjobs", "default", J(R"({"apiVersion":"kubeflow.org/v1","kind":"TFJob","metadata":{"name":"o"},
+        "spec":{"tfReplicaSpecs":{}}})"), &owner).ok());
+    Json pod = J(R"({"metadata":{"name":"child","finalizers":["tfk.io/keep"],"ownerReferences":[{"apiVersion":
+        "kubeflow.org/v1","kind":"TFJob","name":"o","controller":true}]}})");
+    pod["metadata"]["ownerReferences"][(size_t)0]["uid"] = owner.path("metadata.uid");
+    CHECK(s.create("pods", "default", pod, &out).ok());
+    CHECK(s.remove("tfjobs", "default", "o", "Background", &out).ok());
+    CHECK(s.get("pods", "default", "child", &out).ok());
+    CHECK(!out.path("metadata.deletionTimestamp").is_null());
+  }
+  Store s2(path);  // restart: replay the WAL
+  Json out;
+  CHECK(s2.get("pods", "default", "child", &out).ok());
+  CHECK(!out.path("metadata.deletionTimestamp").is_null());
+  unlink(path.c_str());
+}
+
 TEST(store_watch_replay_and_gone) {
   auto s = std::make_shared<Store>("", 4);  // tiny history window
   Json out;

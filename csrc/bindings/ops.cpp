@@ -36,11 +36,13 @@ int tfk_avgpool_fwd(const void*, void*, int, int, int, hipStream_t);
 int tfk_avgpool_bwd(const void*, void*, int, int, int, hipStream_t);
 int tfk_softmax_xent(const void*, const int*, int, int, long long, float, int, float, float*, void*, float*, hipStream_t);
 int tfk_xent_full_row(int, long long);
-int tfk_sgd(float*, void*, const float*, float*, long long, float, float, float, int, float, const float*, hipStream_t);
+int tfk_sgd(float*, void*, const float*, float*, long long, float, float, float, int, float, const float*, const float*,
+            hipStream_t);
 int tfk_adamw(float*, void*, const float*, float*, float*, long long, float, float, float, float, float, float, float, float,
-              const float*, hipStream_t);
+              const float*, const float*, hipStream_t);
 int tfk_lamb(float*, void*, const float*, float*, float*, float*, const long long*, const int*, const int*, int, float*,
-             float, float, float, float, float, float, float, float, const float*, hipStream_t);
+             float, float, float, float, float, float, float, float, const float*, const float*, hipStream_t);
+int tfk_opt_hyper(int*, const float*, int, int, float, float, float*, hipStream_t);
 int tfk_sumsq(const float*, long long, float*, hipStream_t);
 int tfk_clip_coef(const float*, float, float*, float*, hipStream_t);
 int tfk_splitk_reduce(const float*, int, long long, long long, float*, void*, int, float, hipStream_t);
@@ -429,33 +431,41 @@ void softmax_xent(torch::Tensor logits, torch::Tensor labels, int B, int V, int6
            "softmax_xent");
 }
 
+// hp (optional): device f32[3] {lr, bc1, bc2} from opt_hyper -- overrides the host lr / bias corrections
+static const float* hp_ptr(const c10::optional<torch::Tensor>& hp) {
+  if (!hp.has_value() || !hp->defined()) return nullptr;
+  need_f32(*hp, "hp");
+  need_numel(*hp, 3, "hp");
+  return hp->data_ptr<float>();
+}
 void sgd(torch::Tensor w, c10::optional<torch::Tensor> wb, torch::Tensor g, torch::Tensor m, double lr, double mu,
-         double wd, bool nesterov, double gs, c10::optional<torch::Tensor> gs_dev) {
+         double wd, bool nesterov, double gs, c10::optional<torch::Tensor> gs_dev, c10::optional<torch::Tensor> hp) {
   need_f32(w, "w"); need_f32(g, "g"); need_f32(m, "m");
   long long n = w.numel();
   need_numel(g, n, "g"); need_numel(m, n, "m");
   need_aligned(w, 16, "w"); need_aligned(g, 16, "g"); need_aligned(m, 16, "m");
   if (wb.has_value() && wb->defined()) { need_bf16(*wb, "wb"); need_numel(*wb, n, "wb"); need_aligned(*wb, 8, "wb"); }
   check_rc(tfk_sgd(w.data_ptr<float>(), opt_ptr<void>(wb), g.data_ptr<float>(), m.data_ptr<float>(), n, (float)lr,
-                   (float)mu, (float)wd, nesterov ? 1 : 0, (float)gs, opt_ptr<const float>(gs_dev), cur_stream()),
+                   (float)mu, (float)wd, nesterov ? 1 : 0, (float)gs, opt_ptr<const float>(gs_dev), hp_ptr(hp),
+                   cur_stream()),
            "sgd");
 }
 void adamw(torch::Tensor w, c10::optional<torch::Tensor> wb, torch::Tensor g, torch::Tensor m, torch::Tensor v, double lr,
            double b1, double b2, double eps, double wd, double bc1, double bc2, double gs,
-           c10::optional<torch::Tensor> gs_dev) {
+           c10::optional<torch::Tensor> gs_dev, c10::optional<torch::Tensor> hp) {
   need_f32(w, "w"); need_f32(g, "g"); need_f32(m, "m"); need_f32(v, "v");
   long long n = w.numel();
   need_numel(g, n, "g"); need_numel(m, n, "m"); need_numel(v, n, "v");
   if (wb.has_value() && wb->defined()) { need_bf16(*wb, "wb"); need_numel(*wb, n, "wb"); }
   check_rc(tfk_adamw(w.data_ptr<float>(), opt_ptr<void>(wb), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                      n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, (float)gs,
-                     opt_ptr<const float>(gs_dev), cur_stream()),
+                     opt_ptr<const float>(gs_dev), hp_ptr(hp), cur_stream()),
            "adamw");
 }
 void lamb(torch::Tensor w, c10::optional<torch::Tensor> wb, torch::Tensor g, torch::Tensor m, torch::Tensor v,
           torch::Tensor u, torch::Tensor cstart, torch::Tensor clen, torch::Tensor cseg, torch::Tensor seg_norms, double lr,
           double b1, double b2, double eps, double wd, double bc1, double bc2, double gs,
-          c10::optional<torch::Tensor> gs_dev) {
+          c10::optional<torch::Tensor> gs_dev, c10::optional<torch::Tensor> hp) {
   need_f32(w, "w"); need_f32(g, "g"); need_f32(m, "m"); need_f32(v, "v"); need_f32(u, "u");
   need(cstart, at::kLong, "cstart"); need(clen, at::kInt, "clen"); need(cseg, at::kInt, "cseg");
   need_f32(seg_norms, "seg_norms");
@@ -467,8 +477,17 @@ void lamb(torch::Tensor w, c10::optional<torch::Tensor> wb, torch::Tensor g, tor
                     u.data_ptr<float>(), cstart.data_ptr<int64_t>() ? (const long long*)cstart.data_ptr<int64_t>() : nullptr,
                     clen.data_ptr<int>(), cseg.data_ptr<int>(), nch, seg_norms.data_ptr<float>(), (float)lr, (float)b1,
                     (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, (float)gs, opt_ptr<const float>(gs_dev),
-                    cur_stream()),
+                    hp_ptr(hp), cur_stream()),
            "lamb");
+}
+// Advance the device optimizer step and write hp = {lr_table[step-1+off], 1-b1^step, 1-b2^step}.
+void opt_hyper(torch::Tensor step, torch::Tensor lr_table, int64_t lr_offset, double b1, double b2, torch::Tensor hp) {
+  need(step, at::kInt, "step"); need_numel(step, 1, "step");
+  need_f32(lr_table, "lr_table"); TORCH_CHECK(lr_table.numel() >= 1, "lr_table");
+  need_f32(hp, "hp"); need_numel(hp, 3, "hp");
+  check_rc(tfk_opt_hyper(step.data_ptr<int>(), lr_table.data_ptr<float>(), (int)lr_table.numel(), (int)lr_offset,
+                         (float)b1, (float)b2, hp.data_ptr<float>(), cur_stream()),
+           "opt_hyper");
 }
 void sumsq(torch::Tensor x, torch::Tensor out) {
   need_f32(x, "x"); need_f32(out, "out");
@@ -578,6 +597,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sgd", &sgd);
   m.def("adamw", &adamw);
   m.def("lamb", &lamb);
+  m.def("opt_hyper", &opt_hyper);
   m.def("sumsq", &sumsq);
   m.def("clip_coef", &clip_coef);
   m.def("splitk_reduce", &splitk_reduce);

@@ -8,10 +8,15 @@ namespace {
 constexpr int NT = 256;
 
 __device__ __forceinline__ float gscale_of(float host, const float* dev) { return dev ? host * dev[0] : host; }
+// Device hyper-parameters (hipGraph-safe schedules): hp = {lr, bc1, bc2} written on device each
+// step by opt_hyper_kernel; a null hp means the host values passed at launch.
+__device__ __forceinline__ float hp_or(const float* hp, int i, float host) { return hp ? hp[i] : host; }
 
 __global__ void sgd_kernel(float* __restrict__ w, bf16* __restrict__ wb, const float* __restrict__ g, float* __restrict__ m,
-                           long long n, float lr, float mu, float wd, int nesterov, float gs_host, const float* gs_dev) {
+                           long long n, float lr_h, float mu, float wd, int nesterov, float gs_host, const float* gs_dev,
+                           const float* hp) {
   const float gs = gscale_of(gs_host, gs_dev);
+  const float lr = hp_or(hp, 0, lr_h);
   for (long long i = ((long long)blockIdx.x * NT + threadIdx.x) * 4; i < n; i += (long long)gridDim.x * NT * 4) {
     if (i + 3 < n) {
       f32x4 wv = *(f32x4*)(w + i), gv = *(const f32x4*)(g + i), mv = *(f32x4*)(m + i);
@@ -39,10 +44,11 @@ __global__ void sgd_kernel(float* __restrict__ w, bf16* __restrict__ wb, const f
 }
 
 __global__ void adamw_kernel(float* __restrict__ w, bf16* __restrict__ wb, const float* __restrict__ g, float* __restrict__ m,
-                             float* __restrict__ v, long long n, float lr, float b1, float b2, float eps, float wd,
-                             float bc1, float bc2, float gs_host, const float* gs_dev) {
+                             float* __restrict__ v, long long n, float lr_h, float b1, float b2, float eps, float wd,
+                             float bc1, float bc2, float gs_host, const float* gs_dev, const float* hp) {
   const float gs = gscale_of(gs_host, gs_dev);
-  const float ibc1 = 1.f / bc1, ibc2 = 1.f / bc2;
+  const float lr = hp_or(hp, 0, lr_h);
+  const float ibc1 = 1.f / hp_or(hp, 1, bc1), ibc2 = 1.f / hp_or(hp, 2, bc2);
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
     float gr = g[i] * gs;
     float mm = b1 * m[i] + (1.f - b1) * gr;
@@ -60,10 +66,12 @@ __global__ void adamw_kernel(float* __restrict__ w, bf16* __restrict__ wb, const
 // the update is HBM-bound (~30 B/param), so the wide accesses are what sets its speed.
 // Requires w, g, m, v 16-B aligned and wb 8-B aligned; n4 = n / 4 (the tail runs the scalar kernel).
 __global__ void adamw4_kernel(float* __restrict__ w, bf16* __restrict__ wb, const float* __restrict__ g,
-                              float* __restrict__ m, float* __restrict__ v, long long n4, float lr, float b1, float b2,
-                              float eps, float wd, float bc1, float bc2, float gs_host, const float* gs_dev) {
+                              float* __restrict__ m, float* __restrict__ v, long long n4, float lr_h, float b1, float b2,
+                              float eps, float wd, float bc1, float bc2, float gs_host, const float* gs_dev,
+                              const float* hp) {
   const float gs = gscale_of(gs_host, gs_dev);
-  const float ibc1 = 1.f / bc1, ibc2 = 1.f / bc2;
+  const float lr = hp_or(hp, 0, lr_h);
+  const float ibc1 = 1.f / hp_or(hp, 1, bc1), ibc2 = 1.f / hp_or(hp, 2, bc2);
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long long)gridDim.x * NT) {
     const float4 gr4 = ((const float4*)g)[i];
     float4 m4 = ((float4*)m)[i], v4 = ((float4*)v)[i], w4 = ((float4*)w)[i];
@@ -91,10 +99,11 @@ __global__ void adamw4_kernel(float* __restrict__ w, bf16* __restrict__ wb, cons
 __global__ void lamb_stage1_kernel(const float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
                                    float* __restrict__ v, float* __restrict__ u, const long long* __restrict__ chunk_start,
                                    const int* __restrict__ chunk_len, const int* __restrict__ chunk_seg, int nchunks,
-                                   float b1, float b2, float eps, float wd, float bc1, float bc2,
-                                   float* __restrict__ seg_norms, float gs_host, const float* gs_dev) {
+                                   float b1, float b2, float eps, float wd, float bc1_h, float bc2_h,
+                                   float* __restrict__ seg_norms, float gs_host, const float* gs_dev, const float* hp) {
   __shared__ float red[NT / 64];
   const float gs = gscale_of(gs_host, gs_dev);
+  const float bc1 = hp_or(hp, 1, bc1_h), bc2 = hp_or(hp, 2, bc2_h);
   for (int c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const long long s0 = chunk_start[c];
     const int len = chunk_len[c];
@@ -123,7 +132,8 @@ __global__ void lamb_stage1_kernel(const float* __restrict__ w, const float* __r
 __global__ void lamb_stage2_kernel(float* __restrict__ w, bf16* __restrict__ wb, const float* __restrict__ u,
                                    const long long* __restrict__ chunk_start, const int* __restrict__ chunk_len,
                                    const int* __restrict__ chunk_seg, int nchunks, const float* __restrict__ seg_norms,
-                                   float lr) {
+                                   float lr_h, const float* hp) {
+  const float lr = hp_or(hp, 0, lr_h);
   for (int c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const int sg = chunk_seg[c];
     const float wn = sqrtf(seg_norms[2 * sg]), un = sqrtf(seg_norms[2 * sg + 1]);
@@ -137,6 +147,17 @@ __global__ void lamb_stage2_kernel(float* __restrict__ w, bf16* __restrict__ wb,
       if (wb) wb[i] = f2bf(ww);
     }
   }
+}
+
+// One step of the device schedule: step += 1 (the count of updates applied, TF global_step
+// semantics); lr = table[min(step - 1 + lr_offset, T - 1)]; Adam bias corrections 1 - b^step.
+__global__ void opt_hyper_kernel(int* step, const float* lr_table, int T, int lr_offset, float b1, float b2, float* hp) {
+  const int s = step[0] + 1;
+  step[0] = s;
+  const int i = min(max(s - 1 + lr_offset, 0), T - 1);
+  hp[0] = lr_table[i];
+  hp[1] = 1.f - powf(b1, (float)s);
+  hp[2] = 1.f - powf(b2, (float)s);
 }
 
 // out[0] += sum(x^2) (global grad norm)
@@ -165,34 +186,40 @@ int grid_for(long long work, int cap = 4096) {
 
 extern "C" {
 int tfk_sgd(float* w, bf16* wb, const float* g, float* m, long long n, float lr, float mu, float wd, int nesterov,
-            float gs, const float* gs_dev, hipStream_t s) {
-  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4 + 1)), dim3(NT), 0, s, w, wb, g, m, n, lr, mu, wd, nesterov, gs, gs_dev);
+            float gs, const float* gs_dev, const float* hp, hipStream_t s) {
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4 + 1)), dim3(NT), 0, s, w, wb, g, m, n, lr, mu, wd, nesterov, gs, gs_dev,
+                     hp);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_adamw(float* w, bf16* wb, const float* g, float* m, float* v, long long n, float lr, float b1, float b2, float eps,
-              float wd, float bc1, float bc2, float gs, const float* gs_dev, hipStream_t s) {
+              float wd, float bc1, float bc2, float gs, const float* gs_dev, const float* hp, hipStream_t s) {
   const bool vec = (((uintptr_t)w | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 && (((uintptr_t)wb) & 7) == 0;
   if (vec && n >= 4) {
     const long long n4 = n / 4, done = n4 * 4;
     hipLaunchKernelGGL(adamw4_kernel, dim3(grid_for(n4)), dim3(NT), 0, s, w, wb, g, m, v, n4, lr, b1, b2, eps, wd, bc1,
-                       bc2, gs, gs_dev);
+                       bc2, gs, gs_dev, hp);
     if (done < n)
       hipLaunchKernelGGL(adamw_kernel, dim3(1), dim3(NT), 0, s, w + done, wb ? wb + done : nullptr, g + done, m + done,
-                         v + done, n - done, lr, b1, b2, eps, wd, bc1, bc2, gs, gs_dev);
+                         v + done, n - done, lr, b1, b2, eps, wd, bc1, bc2, gs, gs_dev, hp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(NT), 0, s, w, wb, g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2, gs,
-                     gs_dev);
+                     gs_dev, hp);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_lamb(float* w, bf16* wb, const float* g, float* m, float* v, float* u, const long long* cstart, const int* clen,
              const int* cseg, int nchunks, float* seg_norms, float lr, float b1, float b2, float eps, float wd, float bc1,
-             float bc2, float gs, const float* gs_dev, hipStream_t s) {
+             float bc2, float gs, const float* gs_dev, const float* hp, hipStream_t s) {
   int grid = nchunks < 4096 ? nchunks : 4096;
   if (grid < 1) return 0;
   hipLaunchKernelGGL(lamb_stage1_kernel, dim3(grid), dim3(NT), 0, s, w, g, m, v, u, cstart, clen, cseg, nchunks, b1, b2, eps,
-                     wd, bc1, bc2, seg_norms, gs, gs_dev);
-  hipLaunchKernelGGL(lamb_stage2_kernel, dim3(grid), dim3(NT), 0, s, w, wb, u, cstart, clen, cseg, nchunks, seg_norms, lr);
+                     wd, bc1, bc2, seg_norms, gs, gs_dev, hp);
+  hipLaunchKernelGGL(lamb_stage2_kernel, dim3(grid), dim3(NT), 0, s, w, wb, u, cstart, clen, cseg, nchunks, seg_norms, lr,
+                     hp);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_opt_hyper(int* step, const float* lr_table, int T, int lr_offset, float b1, float b2, float* hp, hipStream_t s) {
+  hipLaunchKernelGGL(opt_hyper_kernel, dim3(1), dim3(1), 0, s, step, lr_table, T, lr_offset, b1, b2, hp);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_sumsq(const float* x, long long n, float* out, hipStream_t s) {

@@ -6,8 +6,31 @@ import torch
 from ._lib import lib, on_gpu
 
 
-def sgd_(w, wb, g, m, lr, momentum=0.9, wd=0.0, nesterov=False, grad_scale=1.0, grad_scale_dev=None):
+def opt_hyper(step: torch.Tensor, lr_table: torch.Tensor, lr_offset: int, b1: float, b2: float,
+              hp: torch.Tensor) -> None:
+    """Device schedule step (hipGraph-safe): step += 1; hp = {lr_table[min(step-1+off, T-1)],
+    1 - b1^step, 1 - b2^step}. The optimizer kernels read hp instead of host scalars."""
+    if not on_gpu(hp):
+        s = int(step[0]) + 1
+        step[0] = s
+        i = min(max(s - 1 + lr_offset, 0), lr_table.numel() - 1)
+        hp[0] = lr_table[i]
+        hp[1] = 1 - b1 ** s
+        hp[2] = 1 - b2 ** s
+        return
+    lib().opt_hyper(step, lr_table, lr_offset, b1, b2, hp)
+
+
+def _hp(hp, lr, bc1=None, bc2=None):
+    """Host view of the (lr, bc1, bc2) a kernel would use (CPU reference path)."""
+    if hp is None:
+        return lr, bc1, bc2
+    return float(hp[0]), float(hp[1]), float(hp[2])
+
+
+def sgd_(w, wb, g, m, lr, momentum=0.9, wd=0.0, nesterov=False, grad_scale=1.0, grad_scale_dev=None, hp=None):
     if not on_gpu(w):
+        lr = _hp(hp, lr)[0]
         gs = grad_scale * (float(grad_scale_dev[0]) if grad_scale_dev is not None else 1.0)
         d = g * gs + wd * w
         m.mul_(momentum).add_(d)
@@ -15,12 +38,13 @@ def sgd_(w, wb, g, m, lr, momentum=0.9, wd=0.0, nesterov=False, grad_scale=1.0, 
         if wb is not None:
             wb.copy_(w)
         return
-    lib().sgd(w, wb, g, m, lr, momentum, wd, nesterov, grad_scale, grad_scale_dev)
+    lib().sgd(w, wb, g, m, lr, momentum, wd, nesterov, grad_scale, grad_scale_dev, hp)
 
 
-def adamw_(w, wb, g, m, v, lr, b1, b2, eps, wd, step, grad_scale=1.0, grad_scale_dev=None):
+def adamw_(w, wb, g, m, v, lr, b1, b2, eps, wd, step, grad_scale=1.0, grad_scale_dev=None, hp=None):
     bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
     if not on_gpu(w):
+        lr, bc1, bc2 = _hp(hp, lr, bc1, bc2)
         gs = grad_scale * (float(grad_scale_dev[0]) if grad_scale_dev is not None else 1.0)
         gr = g * gs
         m.mul_(b1).add_((1 - b1) * gr)
@@ -29,14 +53,15 @@ def adamw_(w, wb, g, m, v, lr, b1, b2, eps, wd, step, grad_scale=1.0, grad_scale
         if wb is not None:
             wb.copy_(w)
         return
-    lib().adamw(w, wb, g, m, v, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, grad_scale_dev)
+    lib().adamw(w, wb, g, m, v, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, grad_scale_dev, hp)
 
 
-def lamb_(w, wb, g, m, v, u, chunks, seg_norms, lr, b1, b2, eps, wd, step, grad_scale=1.0, grad_scale_dev=None):
+def lamb_(w, wb, g, m, v, u, chunks, seg_norms, lr, b1, b2, eps, wd, step, grad_scale=1.0, grad_scale_dev=None, hp=None):
     """chunks: (start int64[n], len int32[n], seg int32[n]) over the flat arena."""
     bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
     cstart, clen, cseg = chunks
     if not on_gpu(w):
+        lr, bc1, bc2 = _hp(hp, lr, bc1, bc2)
         gs = grad_scale * (float(grad_scale_dev[0]) if grad_scale_dev is not None else 1.0)
         gr = g * gs
         m.mul_(b1).add_((1 - b1) * gr)
@@ -55,7 +80,7 @@ def lamb_(w, wb, g, m, v, u, chunks, seg_norms, lr, b1, b2, eps, wd, step, grad_
         return
     seg_norms.zero_()
     lib().lamb(w, wb, g, m, v, u, cstart, clen, cseg, seg_norms, lr, b1, b2, eps, wd, bc1, bc2, grad_scale,
-               grad_scale_dev)
+               grad_scale_dev, hp)
 
 
 def global_norm_clip_coef(g: torch.Tensor, max_norm: float, ss: torch.Tensor, coef: torch.Tensor,

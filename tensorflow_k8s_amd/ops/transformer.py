@@ -39,14 +39,18 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
 
 
 def _zero_pair(a: torch.Tensor, b: torch.Tensor) -> None:
-    """Zero two 1-D f32 gradient views with one fill when b directly follows a in the same storage
-    (gamma/beta of one LayerNorm are consecutive in the flat arena): saves a launch per LayerNorm."""
+    """Zero two 1-D f32 gradient views with one fill when they are adjacent in the same storage, in
+    either order (gamma/beta of one LayerNorm are consecutive in the flat arena; ParamArena places
+    parameters in reverse registration order, so beta precedes gamma): saves a launch per LN."""
     if (a.is_contiguous() and b.is_contiguous() and a.dtype == b.dtype and a.device == b.device
-            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
-            and b.storage_offset() == a.storage_offset() + a.numel()):
-        a.as_strided((a.numel() + b.numel(),), (1,), a.storage_offset()).zero_()
-    else:
-        a.zero_(); b.zero_()
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()):
+        if b.storage_offset() == a.storage_offset() + a.numel():
+            a.as_strided((a.numel() + b.numel(),), (1,), a.storage_offset()).zero_()
+            return
+        if a.storage_offset() == b.storage_offset() + b.numel():
+            b.as_strided((a.numel() + b.numel(),), (1,), b.storage_offset()).zero_()
+            return
+    a.zero_(); b.zero_()
 
 
 def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate: bool = False):

@@ -37,16 +37,45 @@ from ..runtime.arena import ALIGN, ParamArena
 PUSH, DONE, FETCH, LOAD, PULL = 1, 2, 3, 4, 5
 
 
-def shard_bounds(numel: int, nshards: int) -> list[tuple[int, int]]:
-    """Contiguous ALIGN-aligned shards of [0, numel) with near-equal sizes."""
-    units = (numel + ALIGN - 1) // ALIGN
+def shard_bounds(numel: int, nshards: int, param_spans: list[tuple[int, int]] | None = None) -> list[tuple[int, int]]:
+    """Contiguous shards of [0, numel) with near-equal sizes. With param_spans (each parameter's
+    [offset, offset+numel) in the arena) every cut falls on a parameter boundary, so no tensor is
+    split across two parameter servers: LAMB's per-tensor trust ratio ||w||/||u|| then sees the
+    whole tensor on one PS, exactly as in single-process and MWMS training. Without
+    spans: ALIGN-aligned cuts."""
+    if not param_spans:
+        units = (numel + ALIGN - 1) // ALIGN
+        out, lo = [], 0
+        for s in range(nshards):
+            n = units // nshards + (1 if s < units % nshards else 0)
+            hi = min(numel, lo + n * ALIGN)
+            out.append((lo, hi))
+            lo = hi
+        return out
+    # candidate cut points = parameter ends (sorted, de-duplicated); greedy toward equal byte shares
+    ends = sorted({e for _, e in param_spans if 0 < e < numel})
     out, lo = [], 0
     for s in range(nshards):
-        n = units // nshards + (1 if s < units % nshards else 0)
-        hi = min(numel, lo + n * ALIGN)
+        if s == nshards - 1:
+            out.append((lo, numel))
+            break
+        target = lo + (numel - lo) / (nshards - s)
+        best = None
+        for e in ends:
+            if e <= lo:
+                continue
+            if best is None or abs(e - target) < abs(best - target):
+                best = e
+            if e > target:
+                break
+        hi = best if best is not None else numel
         out.append((lo, hi))
         lo = hi
     return out
+
+
+def _param_spans(arena) -> list[tuple[int, int]]:
+    return [(p.offset, p.offset + p.numel) for p in arena.params]
 
 
 def _hdr(cmd: int, step: int = 0, rank: int = 0) -> torch.Tensor:
@@ -68,7 +97,7 @@ class ParameterServerStrategy:
         self.arena, self.ps_ranks, self.worker_ranks, self.mode, self.group = arena, list(ps_ranks), list(worker_ranks), mode, group
         self.transport = transport
         self.rank = dist.get_rank()
-        self.shards = shard_bounds(arena.numel, len(self.ps_ranks))
+        self.shards = shard_bounds(arena.numel, len(self.ps_ranks), _param_spans(arena))
         if transport == "gloo":
             pin = arena.grad.is_cuda
             self._g = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
@@ -196,7 +225,7 @@ class ParameterServer:
         self.arena, self.opt, self.mode, self.group = arena, opt, mode, group
         self.worker_ranks = list(worker_ranks)
         self.ps_ranks = list(ps_ranks)
-        self.shards = shard_bounds(arena.numel, len(ps_ranks))
+        self.shards = shard_bounds(arena.numel, len(ps_ranks), _param_spans(arena))
         self.lo, self.hi = self.shards[shard]
         opt.region = (self.lo, self.hi)
         if mode == "sync":

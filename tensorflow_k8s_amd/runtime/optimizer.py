@@ -44,8 +44,40 @@ class Optimizer:
         self.grad_scale = 1.0          # e.g. 1/world for gradient averaging
         self.grad_scale_dev = None     # device scalar (global-norm clipping)
         self.region = None             # (start, end) restrict to a shard (parameter-server)
+        self._dev = None               # device schedule state (hipGraph capture), see enable_device_schedule
         for s in self.slot_names:
             arena.slot(s)
+
+    # Adam-family bias-correction bases (SGD has none)
+    _betas = (0.0, 0.0)
+
+    def enable_device_schedule(self, max_steps: int = 200_000) -> None:
+        """Move the per-step host scalars -- learning rate, step counter and Adam bias corrections --
+        onto the device, so a hipGraph-captured step replays a correct update every time (a captured
+        host scalar would freeze at its capture-time value). The LR schedule is tabulated on device
+        for steps [0, T): T covers warmup + decay of an LRSchedule, else max_steps."""
+        dev = self.arena.device
+        if isinstance(self.lr, LRSchedule):
+            T = max(1, (self.lr.total if self.lr.kind != "constant" else 0), self.lr.warmup) + 1
+        else:
+            T = max_steps
+        table = torch.tensor([self.lr(i) for i in range(T)], dtype=torch.float32, device=dev)
+        self._dev = {"step": torch.tensor([self.step_count], dtype=torch.int32, device=dev),
+                     "lr": table, "hp": torch.zeros(3, dtype=torch.float32, device=dev)}
+
+    def _device_hp(self):
+        """Advance the device schedule (inside the step, hence inside a captured graph)."""
+        if self._dev is None:
+            return None
+        b1, b2 = self._betas
+        O.opt_hyper(self._dev["step"], self._dev["lr"], 0, b1, b2, self._dev["hp"])
+        return self._dev["hp"]
+
+    def sync_step(self) -> int:
+        """Host step counter (reads the device counter when the schedule lives on device)."""
+        if self._dev is not None:
+            self.step_count = int(self._dev["step"][0].item())
+        return self.step_count
 
     def _regions(self):
         lo, hi = self.region if self.region is not None else (0, self.arena.numel)
@@ -61,10 +93,12 @@ class Optimizer:
         return out
 
     def state_dict(self):
-        return {"step": self.step_count}
+        return {"step": self.sync_step()}
 
     def load_state_dict(self, d):
         self.step_count = int(d.get("step", 0))
+        if self._dev is not None:
+            self._dev["step"].fill_(self.step_count)
 
 
 class SGD(Optimizer):
@@ -77,10 +111,11 @@ class SGD(Optimizer):
     def step(self):
         a = self.arena
         lr = self.lr(self.step_count)
+        hp = self._device_hp()
         m = a.slot("Momentum")
         for lo, hi, wd in self._regions():
             O.sgd_(a.master[lo:hi], a.compute[lo:hi], a.grad[lo:hi], m[lo:hi], lr, self.momentum, wd, self.nesterov,
-                   self.grad_scale, self.grad_scale_dev)
+                   self.grad_scale, self.grad_scale_dev, hp=hp)
         self.step_count += 1
 
 
@@ -90,15 +125,17 @@ class AdamW(Optimizer):
     def __init__(self, arena, lr, b1=0.9, b2=0.999, eps=1e-6, weight_decay=0.01):
         super().__init__(arena, lr, weight_decay)
         self.b1, self.b2, self.eps = b1, b2, eps
+        self._betas = (b1, b2)
 
     def step(self):
         a = self.arena
         self.step_count += 1
         lr = self.lr(self.step_count - 1)
+        hp = self._device_hp()
         m, v = a.slot("Adam"), a.slot("Adam_1")
         for lo, hi, wd in self._regions():
             O.adamw_(a.master[lo:hi], a.compute[lo:hi], a.grad[lo:hi], m[lo:hi], v[lo:hi], lr, self.b1, self.b2,
-                     self.eps, wd, self.step_count, self.grad_scale, self.grad_scale_dev)
+                     self.eps, wd, self.step_count, self.grad_scale, self.grad_scale_dev, hp=hp)
 
 
 class LAMB(Optimizer):
@@ -109,6 +146,7 @@ class LAMB(Optimizer):
     def __init__(self, arena, lr, b1=0.9, b2=0.999, eps=1e-6, weight_decay=0.01):
         super().__init__(arena, lr, weight_decay)
         self.b1, self.b2, self.eps = b1, b2, eps
+        self._betas = (b1, b2)
         self._tables = {}
         self._u = torch.zeros(arena.numel, dtype=torch.float32, device=arena.device)
         self._norms = torch.zeros(2 * len(arena.params), dtype=torch.float32, device=arena.device)
@@ -131,8 +169,9 @@ class LAMB(Optimizer):
         a = self.arena
         self.step_count += 1
         lr = self.lr(self.step_count - 1)
+        hp = self._device_hp()
         m, v = a.slot("Adam"), a.slot("Adam_1")
         for lo, hi, wd in self._regions():
             O.lamb_(a.master[lo:hi], a.compute[lo:hi], a.grad[lo:hi], m[lo:hi], v[lo:hi], self._u[lo:hi],
                     self._chunks(lo, hi), self._norms, lr, self.b1, self.b2, self.eps, wd, self.step_count,
-                    self.grad_scale, self.grad_scale_dev)
+                    self.grad_scale, self.grad_scale_dev, hp=hp)

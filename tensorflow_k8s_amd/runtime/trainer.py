@@ -5,10 +5,29 @@ hipGraph (``torch.cuda.CUDAGraph`` on ROCm) removes the ~600 host launches of a 
 after two eager warm-up steps (which also size every workspace) the whole step is captured once
 and replayed. Capture is used for single-GPU runs; multi-GPU runs stay eager so RCCL buckets can
 be issued as soon as backward produces them.
+
+Everything a replay must see change per step lives on the device: the optimizer's learning-rate
+schedule, step counter and Adam bias corrections (Optimizer.enable_device_schedule). Host-side
+per-step values that would freeze inside a graph -- dropout seeds drawn on the host -- make
+capture refuse (GraphUnsafe) instead of silently training wrong.
 """
 from __future__ import annotations
 
 import torch
+
+
+class GraphUnsafe(RuntimeError):
+    """The step has host-side per-step state a captured graph would freeze."""
+
+
+def graph_hazards(model) -> list[str]:
+    """Reasons a model's step cannot be replayed from a hipGraph (empty = safe)."""
+    out = []
+    cfg = getattr(model, "cfg", None)
+    for k in ("dropout", "hidden_dropout", "attn_dropout", "relu_dropout"):
+        if cfg is not None and float(getattr(cfg, k, 0.0) or 0.0) > 0.0 and getattr(model, "training", True):
+            out.append(f"{type(model).__name__}.cfg.{k}={getattr(cfg, k)} (dropout seeds are drawn on the host per step)")
+    return out
 
 
 class StepRunner:
@@ -17,6 +36,12 @@ class StepRunner:
         self.batch = batch
         self.use_graph = (use_graph and torch.cuda.is_available() and batch[0].is_cuda
                           and not hasattr(strategy, "apply_gradients"))
+        if self.use_graph:
+            bad = graph_hazards(model)
+            if bad:
+                raise GraphUnsafe("hipGraph capture refused: " + "; ".join(bad))
+            if opt is not None and hasattr(opt, "enable_device_schedule"):
+                opt.enable_device_schedule()
         self.warmup_eager = warmup_eager
         self.graph = None
         self.n = 0

@@ -55,18 +55,28 @@ def test_graph_capture_replays_schedule_gpu():
     dev = torch.device("cuda", 0)
     sched = LRSchedule(2e-3, warmup=4, total=20, kind="cosine", end_lr=1e-4)
     finals = []
-    for graph in (False, True):
+    for graph, frozen in ((False, False), (True, False), (False, True)):
         torch.manual_seed(0)
         m = build_model("lenet").to(dev)
-        opt = AdamW(m.arena, sched)
+        w0 = m.arena.master.clone()
+        # frozen: what a graph with captured host scalars would replay (lr/bias corrections of step 3)
+        opt = AdamW(m.arena, (lambda s: sched(2)) if frozen else sched)
         batch = synthetic_batch(m, 64, dev, seed=3)
         r = StepRunner(m, opt, None, batch, use_graph=graph)
+        if not graph:
+            opt.enable_device_schedule()  # same on-device lr / bias-correction arithmetic as the graph
         for _ in range(12):
             r.step()
         torch.cuda.synchronize()
-        finals.append((m.arena.master.clone(), opt.sync_step(), r.last_loss()))
+        finals.append((m.arena.master - w0, opt.sync_step(), r.last_loss()))
     assert finals[1][1] == 12  # the device counter advanced on every replay
-    assert torch.allclose(finals[0][0], finals[1][0], rtol=1e-4, atol=1e-6)
+    # Adam amplifies f32 reduction-order noise on near-zero gradients, so compare whole updates:
+    # the replayed schedule tracks eager closely, a frozen schedule does not
+    d_eager, d_graph, d_frozen = (f[0] for f in finals)
+    err = float((d_graph - d_eager).norm() / d_eager.norm())
+    err_frozen = float((d_frozen - d_eager).norm() / d_eager.norm())
+    assert err < 2e-2, err
+    assert err_frozen > 5 * err, (err, err_frozen)
 
 
 @pytest.mark.gpu

@@ -30,6 +30,22 @@ bool ApiServer::start(const std::string& host, int port, std::string* err) {
   return true;
 }
 
+bool ApiServer::load_token_file(const std::string& path, std::string* err) {
+  std::ifstream f(path);
+  if (!f) { *err = "cannot read token file " + path; return false; }
+  std::string line;
+  size_t n0 = tokens_.size();
+  while (std::getline(f, line)) {
+    line = trim(line);
+    if (line.empty() || line[0] == '#') continue;
+    auto cols = split(line, ',');
+    if (cols.size() < 2) { *err = "token file " + path + ": want token,user,uid"; return false; }
+    tokens_[trim(cols[0])] = trim(cols[1]);
+  }
+  if (tokens_.size() == n0) { *err = "token file " + path + " has no tokens"; return false; }
+  return true;
+}
+
 static void reply(ResponseWriter& w, const ApiStatus& st, const Json& body) {
   w.respond(st.code, st.ok() ? body.dump() : st.to_json().dump());
 }
@@ -37,6 +53,14 @@ static void reply(ResponseWriter& w, const ApiStatus& st, const Json& body) {
 void ApiServer::handle(const HttpRequest& req, ResponseWriter& w) {
   const std::string& p = req.path;
   if (p == "/healthz" || p == "/readyz" || p == "/livez") { w.respond(200, "ok", "text/plain"); return; }
+  if (!tokens_.empty()) {
+    auto it = req.headers.find("authorization");
+    std::string tok = it == req.headers.end() ? "" : it->second;
+    if (!starts_with(tok, "Bearer ") || !tokens_.count(trim(tok.substr(7)))) {
+      w.respond(401, ApiStatus::Err(401, "Unauthorized", "Unauthorized").to_json().dump());
+      return;
+    }
+  }
   if (p == "/version") {
     w.respond(200, R"({"major":"1","minor":"9","gitVersion":"v1.9.0-tfk","platform":"linux/amd64"})");
     return;
@@ -247,7 +271,7 @@ void ApiServer::do_watch(const HttpRequest& req, ResponseWriter& w, const std::s
   if (!w.start_stream(200)) { watcher->close(); return; }
   int64_t deadline = mono_ms() + timeout_s * 1000;
   int64_t last_write = mono_ms();
-  while (mono_ms() < deadline) {
+  while (mono_ms() < deadline && w.alive()) {
     WatchEvent ev;
     if (watcher->next(&ev, 500)) {
       Json j = Json::object();

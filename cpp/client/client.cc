@@ -1,5 +1,7 @@
 #include "client.h"
 
+#include <fstream>
+#include <sstream>
 #include <thread>
 
 #include "../api/types.h"
@@ -42,14 +44,46 @@ static void group_version(const std::string& plural, const std::string& tfjob_ve
   else { *group = ""; *version = "v1"; }
 }
 
-RestClient::RestClient(const RestConfig& cfg) : cfg_(cfg), http_("127.0.0.1", 8080, cfg.timeout_ms) {
-  std::string host;
-  int port;
-  if (!parse_url(cfg.host, &host, &port)) throw std::runtime_error("bad apiserver url " + cfg.host);
-  http_ = HttpClient(host, port, cfg.timeout_ms);
+RestClient::RestClient(const RestConfig& cfg) : cfg_(cfg) {
+  Endpoint ep;
+  if (!parse_endpoint(cfg.host, &ep)) throw std::runtime_error("bad apiserver url " + cfg.host);
+  std::shared_ptr<TlsContext> tls;
+  if (ep.https) {
+    std::string err;
+    TlsOptions o = cfg.tls;
+    o.enabled = true;
+    tls = TlsContext::client(o, &err);
+    if (!tls) throw std::runtime_error("TLS config for " + cfg.host + ": " + err);
+  }
+  http_.reset(new HttpClient(ep, tls, cfg.timeout_ms));
+  http_->set_keepalive(cfg.keepalive);
   // NewForConfig: install a token bucket only when QPS > 0 (images/tf4.PNG:L4-L5)
   if (cfg.qps > 0) limiter_ = std::make_shared<TokenBucket>(cfg.qps, std::max(1, cfg.burst));
   if (cfg_.user_agent.empty()) cfg_.user_agent = "tfk-client/v0.1 (linux/amd64)";  // DefaultKubernetesUserAgent
+  token_ = cfg_.bearer_token;
+}
+
+std::map<std::string, std::string> RestClient::auth_headers() {
+  std::map<std::string, std::string> h{{"User-Agent", cfg_.user_agent}, {"Accept", "application/json"}};
+  std::string tok;
+  {
+    // projected service-account tokens rotate: re-read the file at most once a minute (client-go)
+    std::lock_guard<std::mutex> g(tok_mu_);
+    if (!cfg_.bearer_token_file.empty() && mono_ms() - token_read_ms_ > 60000) {
+      std::ifstream f(cfg_.bearer_token_file);
+      std::stringstream ss;
+      if (f) {
+        ss << f.rdbuf();
+        std::string t = trim(ss.str());
+        if (!t.empty()) token_ = t;
+      }
+      token_read_ms_ = mono_ms();
+    }
+    tok = token_;
+  }
+  if (!tok.empty()) h["Authorization"] = "Bearer " + tok;
+  else if (!cfg_.username.empty()) h["Authorization"] = "Basic " + base64_encode(cfg_.username + ":" + cfg_.password);
+  return h;
 }
 
 std::string RestClient::path(const std::string& plural, const std::string& ns, const std::string& name,
@@ -65,10 +99,13 @@ std::string RestClient::path(const std::string& plural, const std::string& ns, c
   return p;
 }
 
-ApiStatus RestClient::call(const std::string& method, const std::string& path, const std::string& body, Json* out) {
+ApiStatus RestClient::call(const std::string& method, const std::string& path, const std::string& body, Json* out,
+                           const char* content_type) {
   if (limiter_) limiter_->accept();
   requests++;
-  HttpResponse r = http_.request(method, path, body, {{"User-Agent", cfg_.user_agent}});
+  auto hdrs = auth_headers();
+  if (!body.empty()) hdrs["Content-Type"] = content_type ? content_type : "application/json";
+  HttpResponse r = http_->request(method, path, body, hdrs);
   if (r.status == 0) return ApiStatus::Err(503, "ServiceUnavailable", r.error);
   Json j;
   try { j = r.body.empty() ? Json() : Json::parse(r.body); } catch (...) { j = Json(r.body); }
@@ -105,7 +142,8 @@ ApiStatus RestClient::update_status(const std::string& plural, const std::string
 }
 ApiStatus RestClient::patch(const std::string& plural, const std::string& ns, const std::string& name, const Json& p,
                             Json* out) {
-  return call("PATCH", path(plural, ns, name), p.dump(), out);
+  // JSON merge patch (RFC 7386): the content type a kube-apiserver requires for this body
+  return call("PATCH", path(plural, ns, name), p.dump(), out, "application/merge-patch+json");
 }
 ApiStatus RestClient::remove(const std::string& plural, const std::string& ns, const std::string& name,
                              const std::string& propagation) {
@@ -116,7 +154,8 @@ namespace {
 // Background thread reading the HTTP watch stream into a queue.
 class RestWatch : public WatchStream {
  public:
-  RestWatch(HttpClient http, std::string path) : http_(std::move(http)), path_(std::move(path)) {
+  RestWatch(HttpClient http, std::string path, std::map<std::string, std::string> hdrs)
+      : http_(std::move(http)), path_(std::move(path)), hdrs_(std::move(hdrs)) {
     thr_ = std::thread([this] { run(); });
   }
   ~RestWatch() override {
@@ -156,7 +195,7 @@ class RestWatch : public WatchStream {
       }
       cv_.notify_all();
       return !stop_.load();
-    }, &stop_, &err);
+    }, &stop_, &err, hdrs_);
     {
       std::lock_guard<std::mutex> g(mu_);
       done_ = true;
@@ -165,6 +204,7 @@ class RestWatch : public WatchStream {
   }
   HttpClient http_;
   std::string path_;
+  std::map<std::string, std::string> hdrs_;
   std::thread thr_;
   mutable std::mutex mu_;
   std::condition_variable cv_;
@@ -190,12 +230,12 @@ std::unique_ptr<WatchStream> RestClient::watch(const std::string& plural, const 
                                                const std::string& ls, const std::string& fs, ApiStatus* st) {
   if (limiter_) limiter_->accept();
   requests++;
-  std::string q = "watch=1&resourceVersion=" + std::to_string(rv);
+  std::string q = "watch=true&resourceVersion=" + std::to_string(rv) + "&allowWatchBookmarks=false";
   if (!ls.empty()) q += "&labelSelector=" + url_encode(ls);
   if (!fs.empty()) q += "&fieldSelector=" + url_encode(fs);
-  HttpClient h(http_.host(), http_.port(), cfg_.timeout_ms);
   *st = ApiStatus::Ok();
-  return std::unique_ptr<WatchStream>(new RestWatch(h, path(plural, ns) + "?" + q));
+  // copies of the HttpClient share its TLS context; the stream dials its own connection
+  return std::unique_ptr<WatchStream>(new RestWatch(*http_, path(plural, ns) + "?" + q, auth_headers()));
 }
 
 // ------------------------------------------------------------------------------ fake

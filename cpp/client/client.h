@@ -1,12 +1,15 @@
 // Clientset for the tfk control plane (reference: pkg/client/clientset/versioned/*, images/tf3.PNG:L18-L40;
 // NewForConfig + token-bucket RateLimiter images/tf4.PNG:L2-L20; setConfigDefaults images/tf6.PNG).
 // One untyped resource interface (CRUD + List + Watch keyed by plural) with two backends:
-//   RestClient - HTTP/1.1 to tfk-apiserver, QPS/Burst token bucket, UserAgent, GroupVersion table.
+//   RestClient - HTTP/1.1 (or HTTPS) to tfk-apiserver or a real kube-apiserver: QPS/Burst token
+//                bucket, UserAgent, GroupVersion table, bearer-token / basic / client-cert auth,
+//                keep-alive connection reuse (config.h builds the RestConfig).
 //   FakeClient - in-process Store (the generated "fake clientset": no server, records Actions()).
 #pragma once
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -15,6 +18,7 @@
 
 #include "../apiserver/store.h"
 #include "../common/http.h"
+#include "config.h"
 
 namespace tfk {
 
@@ -33,15 +37,6 @@ class TokenBucket {
   int burst_;
   double tokens_;
   int64_t last_;
-};
-
-struct RestConfig {
-  std::string host = "http://127.0.0.1:8080";
-  double qps = 5;    // client-go defaults
-  int burst = 10;
-  std::string user_agent;
-  std::string tfjob_version = "v1";  // GroupVersion for TFJobs (v1 | v1alpha1)
-  int timeout_ms = 30000;
 };
 
 class WatchStream {
@@ -94,13 +89,18 @@ class RestClient : public Client {
   std::string path(const std::string& plural, const std::string& ns, const std::string& name = "",
                    const std::string& sub = "") const;
   const RestConfig& config() const { return cfg_; }
-  HttpClient& http() { return http_; }
+  HttpClient& http() { return *http_; }
 
  private:
-  ApiStatus call(const std::string& method, const std::string& path, const std::string& body, Json* out);
+  ApiStatus call(const std::string& method, const std::string& path, const std::string& body, Json* out,
+                 const char* content_type = nullptr);
+  std::map<std::string, std::string> auth_headers();
   RestConfig cfg_;
-  HttpClient http_;
+  std::unique_ptr<HttpClient> http_;
   std::shared_ptr<TokenBucket> limiter_;
+  std::mutex tok_mu_;
+  std::string token_;
+  int64_t token_read_ms_ = 0;
 };
 
 // Fake clientset: talks to an in-process Store; records (verb, plural, name) actions.

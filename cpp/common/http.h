@@ -1,5 +1,9 @@
-// Minimal HTTP/1.1 server + client over POSIX sockets for the tfk control plane
-// (REST + chunked watch streams, like the Kubernetes API). No external dependencies.
+// HTTP/1.1 server + client over POSIX sockets for the tfk control plane (REST + chunked watch
+// streams, like the Kubernetes API), with optional TLS (OpenSSL) on both ends:
+//   * client: http:// and https:// URLs, CA bundle (file or PEM data), insecure-skip-verify,
+//     client certificate auth, bearer tokens (set by the REST layer), keep-alive connection pool
+//     shared by copies of one HttpClient (client-go's transport reuses connections the same way);
+//   * server: plain or TLS listener, keep-alive, thread per connection.
 #pragma once
 #include <atomic>
 #include <functional>
@@ -12,13 +16,62 @@
 
 #include "util.h"
 
+typedef struct ssl_st SSL;
+typedef struct ssl_ctx_st SSL_CTX;
+
 namespace tfk {
+
+// TLS material. Empty ca = system default verify paths (unless insecure).
+struct TlsOptions {
+  bool enabled = false;
+  std::string ca_file, ca_data;           // PEM (file path or inline data)
+  std::string cert_file, cert_data;       // client cert (client) / serving cert (server)
+  std::string key_file, key_data;
+  std::string server_name;                // SNI + hostname check (client); default: URL host
+  bool insecure_skip_verify = false;
+};
+
+// OpenSSL context (client or server role), shared by all connections of an endpoint.
+class TlsContext {
+ public:
+  static std::shared_ptr<TlsContext> client(const TlsOptions& o, std::string* err);
+  static std::shared_ptr<TlsContext> server(const TlsOptions& o, std::string* err);
+  ~TlsContext();
+  SSL_CTX* ctx() const { return ctx_; }
+  const TlsOptions& options() const { return opt_; }
+
+ private:
+  SSL_CTX* ctx_ = nullptr;
+  TlsOptions opt_;
+};
+
+// One stream connection: a socket, optionally wrapped in TLS. Owns (and closes) the fd.
+class Conn {
+ public:
+  Conn(int fd, SSL* ssl) : fd_(fd), ssl_(ssl) {}
+  ~Conn();
+  Conn(const Conn&) = delete;
+  Conn& operator=(const Conn&) = delete;
+  // Waits up to poll_ms for data; >0 bytes read, 0 = timeout (no data yet), -1 = EOF / error.
+  int read_some(char* buf, int cap, int poll_ms);
+  bool send_all(const std::string& s);
+  void shutdown();
+  int fd() const { return fd_; }
+  bool tls() const { return ssl_ != nullptr; }
+  bool peer_closed() const;  // orderly shutdown / reset seen on the socket (non-blocking probe)
+
+ private:
+  int fd_;
+  SSL* ssl_;
+  std::mutex wmu_;
+};
 
 struct HttpRequest {
   std::string method, path, query_string, body;
   std::map<std::string, std::string> query;    // decoded
   std::map<std::string, std::string> headers;  // lower-case keys
   std::string peer;
+  bool tls = false;
 };
 
 struct HttpResponse {
@@ -31,7 +84,11 @@ struct HttpResponse {
 
 class ResponseWriter {
  public:
-  explicit ResponseWriter(int fd) : fd_(fd) {}
+  explicit ResponseWriter(Conn* c, const std::atomic<bool>* server_stopping = nullptr)
+      : c_(c), stopping_(server_stopping) {}
+  // False once the server is stopping or the peer has closed its end: long-running handlers
+  // (watch streams) poll this so HttpServer::stop() can join every connection thread.
+  bool alive() const;
   void respond(int status, const std::string& body, const std::string& content_type = "application/json");
   bool start_stream(int status, const std::string& content_type = "application/json");
   bool write_chunk(const std::string& data);  // false once the peer is gone
@@ -40,8 +97,8 @@ class ResponseWriter {
   bool streaming() const { return streaming_; }
 
  private:
-  bool write_all(const std::string& s);
-  int fd_;
+  Conn* c_;
+  const std::atomic<bool>* stopping_;
   bool responded_ = false, streaming_ = false;
 };
 
@@ -51,11 +108,15 @@ class HttpServer {
  public:
   HttpServer() = default;
   ~HttpServer();
+  // Serve TLS on this listener (call before listen()). Returns false if the cert/key do not load.
+  bool enable_tls(const TlsOptions& o, std::string* err);
   // host "127.0.0.1", port 0 = ephemeral. Returns false on bind failure (err filled: e.g. port in use).
   bool listen(const std::string& host, int port, std::string* err);
   int port() const { return port_; }
+  bool tls() const { return tls_ != nullptr; }
   void serve(HttpHandler h);  // spawns the accept thread
   void stop();
+  long long connections_accepted() const { return accepted_.load(); }
 
  private:
   void accept_loop();
@@ -64,33 +125,61 @@ class HttpServer {
   int port_ = 0;
   std::atomic<bool> stopping_{false};
   std::atomic<int> active_{0};
+  std::atomic<long long> accepted_{0};
   HttpHandler handler_;
   std::thread accept_thr_;
+  std::shared_ptr<TlsContext> tls_;
 };
 
 std::string http_status_text(int code);
 
+// Parsed endpoint URL: scheme://host[:port]
+struct Endpoint {
+  bool https = false;
+  std::string host;
+  int port = 80;
+};
+bool parse_endpoint(const std::string& url, Endpoint* ep);
+// "http://host:port" -> (host, port) (scheme optional)
+bool parse_url(const std::string& url, std::string* host, int* port);
+
 class HttpClient {
  public:
-  HttpClient(std::string host, int port, int timeout_ms = 30000)
-      : host_(std::move(host)), port_(port), timeout_ms_(timeout_ms) {}
+  HttpClient(std::string host, int port, int timeout_ms = 30000);
+  // Full endpoint (https:// uses tls options; `tls` may be null for plain http).
+  HttpClient(const Endpoint& ep, std::shared_ptr<TlsContext> tls, int timeout_ms = 30000);
   HttpResponse request(const std::string& method, const std::string& path, const std::string& body = "",
                        const std::map<std::string, std::string>& headers = {});
-  // Streams a chunked (or close-delimited) body line by line. Returns the status code, or 0 on a
-  // transport error. on_line returns false to stop. `stop` (optional) aborts from another thread.
+  // Streams a chunked (or close-delimited) body line by line on a dedicated connection. Returns
+  // the status code, or 0 on a transport error. on_line returns false to stop. `stop` (optional)
+  // aborts from another thread.
   int stream_lines(const std::string& path, const std::function<bool(const std::string&)>& on_line,
-                   std::atomic<bool>* stop = nullptr, std::string* err = nullptr);
+                   std::atomic<bool>* stop = nullptr, std::string* err = nullptr,
+                   const std::map<std::string, std::string>& headers = {});
   const std::string& host() const { return host_; }
   int port() const { return port_; }
+  bool https() const { return tls_ != nullptr; }
+  // Connection reuse statistics (shared by copies of this client).
+  long long connects() const { return pool_->connects.load(); }
+  long long reuses() const { return pool_->reuses.load(); }
+  void set_keepalive(bool on) { keepalive_ = on; }
 
  private:
-  int connect_fd(std::string* err);
+  struct Pool {
+    std::mutex mu;
+    std::vector<std::unique_ptr<Conn>> idle;
+    std::atomic<long long> connects{0}, reuses{0};
+  };
+  std::unique_ptr<Conn> dial(std::string* err);
+  std::unique_ptr<Conn> take_idle();
+  void put_idle(std::unique_ptr<Conn> c);
+  HttpResponse round_trip(Conn& c, const std::string& wire, bool* reusable, bool* nothing_read);
   std::string host_;
   int port_;
   int timeout_ms_;
+  bool keepalive_ = true;
+  std::shared_ptr<TlsContext> tls_;
+  std::shared_ptr<Pool> pool_;
 };
-
-// "http://host:port" -> (host, port)
-bool parse_url(const std::string& url, std::string* host, int* port);
 
 }  // namespace tfk

@@ -1,5 +1,7 @@
 #include "trainer.h"
 
+#include "../client/tfjob_client.h"
+
 #include <algorithm>
 #include <set>
 
@@ -191,10 +193,9 @@ Trainer::PodState Trainer::pod_state(const Json& pod) {
 
 // ------------------------------------------------------------------------------ reconcile
 ApiStatus Trainer::write_status(api::TFJob& job, const Json& orig) {
-  Json obj = api::to_json(job);
-  obj["metadata"]["resourceVersion"] = orig.path("metadata.resourceVersion");
-  Json out;
-  return client_->update_status(api::kPlural, job.ns(), obj, &out);
+  // typed TFJob client (typed/tensorflow/<version>/tfjob.go UpdateStatus) in the job's own version
+  job.metadata["resourceVersion"] = orig.path("metadata.resourceVersion");
+  return TFJobInterface(client_, job.ns(), job.api_version).UpdateStatus(job);
 }
 
 void Trainer::ensure_podgroup(const api::TFJob& job) {

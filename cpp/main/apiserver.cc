@@ -6,7 +6,7 @@
 
 int main(int argc, char** argv) {
   using namespace tfk;
-  std::string host = "127.0.0.1", wal, log_root, level = "info", port_file;
+  std::string host = "127.0.0.1", wal, log_root, level = "info", port_file, tls_cert, tls_key, token_file;
   long long port = 8080, history = 10000;
   bool json = false;
   FlagSet fs("tfk-apiserver");
@@ -17,6 +17,9 @@ int main(int argc, char** argv) {
   fs.add_string("port-file", &port_file, "write the bound port here");
   fs.add_bool("json-log-format", &json, "JSON logs");
   fs.add_string("log-level", &level, "log level");
+  fs.add_string("tls-cert-file", &tls_cert, "serve HTTPS with this PEM certificate (chain)");
+  fs.add_string("tls-private-key-file", &tls_key, "PEM private key for --tls-cert-file");
+  fs.add_string("token-auth-file", &token_file, "CSV token,user,uid: require bearer-token authentication");
   std::string err;
   if (!fs.parse(argc, argv, &err)) { fprintf(stderr, "%s\n%s", err.c_str(), fs.usage().c_str()); return 2; }
   if (fs.help_requested()) { printf("%s", fs.usage().c_str()); return 0; }
@@ -26,13 +29,22 @@ int main(int argc, char** argv) {
   auto store = std::make_shared<Store>(wal, (size_t)history);
   install_tfjob_crd(*store);
   ApiServer srv(store);
+  if (!tls_cert.empty()) {
+    TlsOptions o;
+    o.enabled = true;
+    o.cert_file = tls_cert;
+    o.key_file = tls_key;
+    if (!srv.enable_tls(o, &err)) { TFK_LOG(Error, "tls: " + err); return 1; }
+  }
+  if (!token_file.empty() && !srv.load_token_file(token_file, &err)) { TFK_LOG(Error, err); return 1; }
   if (!srv.start(host, (int)port, &err)) { TFK_LOG(Error, "cannot start: " + err); return 1; }
-  TFK_LOG(Info, "serving", Json(Json::object_t{{"url", Json("http://" + host + ":" + std::to_string(srv.port()))}}));
+  const std::string scheme = srv.tls() ? "https://" : "http://";
+  TFK_LOG(Info, "serving", Json(Json::object_t{{"url", Json(scheme + host + ":" + std::to_string(srv.port()))}}));
   if (!port_file.empty()) {
     FILE* f = fopen(port_file.c_str(), "w");
     if (f) { fprintf(f, "%d\n", srv.port()); fclose(f); }
   }
-  printf("listening on http://%s:%d\n", host.c_str(), srv.port());
+  printf("listening on %s%s:%d\n", scheme.c_str(), host.c_str(), srv.port());
   fflush(stdout);
   while (!stop.wait_for(1000)) {
   }

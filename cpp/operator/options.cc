@@ -3,19 +3,22 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <cstdlib>
 #include <fstream>
 #include <random>
 #include <sstream>
 #include <thread>
 
+#include "../client/config.h"
 #include "../controller/controller.h"
 #include "../leaderelection/leaderelection.h"
 
 namespace tfk {
 
 void ServerOption::AddFlags(FlagSet& fs) {
-  fs.add_string("apiserver", &apiserver, "tfk-apiserver URL");
-  fs.add_string("kubeconfig", &kubeconfig, "path to a JSON kubeconfig {server, qps, burst}");
+  fs.add_string("apiserver", &apiserver, "API server URL (http[s]://host:port); overrides the kubeconfig server");
+  fs.add_string("master", &apiserver, "alias of --apiserver (client-go --master)");
+  fs.add_string("kubeconfig", &kubeconfig, "kubeconfig (YAML/JSON); default: in-cluster service account, else tfk-apiserver on 127.0.0.1:8080");
   fs.add_string("controller-config-file", &controller_config_file, "JSON controller config (accelerators)");
   fs.add_string("namespace", &ns, "namespace to watch (default all)");
   fs.add_int("threadiness", &threadiness, "number of reconcile workers");
@@ -62,6 +65,8 @@ void HandleSignals(StopToken& stop) {
 }
 
 static std::string default_identity() {
+  const char* pod = getenv("MY_POD_NAME");  // set from the downward API in deploy/operator.yaml
+  if (pod && *pod) return pod;
   char host[256] = {0};
   gethostname(host, sizeof host - 1);
   return std::string(host) + "_" + std::to_string(getpid());
@@ -69,20 +74,25 @@ static std::string default_identity() {
 
 int RunServer(const ServerOption& opt_in, StopToken& stop) {
   ServerOption opt = opt_in;
+  // clientcmd.BuildConfigFromFlags(master, kubeconfig) (k8s-operator.md:92-101); with neither flag an
+  // operator pod uses its service account (rest.InClusterConfig), a dev box the local tfk-apiserver
   RestConfig rc;
-  rc.host = opt.apiserver;
+  std::string cerr;
+  if (!opt.kubeconfig.empty() || !opt.apiserver.empty() || getenv("KUBERNETES_SERVICE_HOST")) {
+    if (!build_config_from_flags(opt.apiserver, opt.kubeconfig, &rc, &cerr)) {
+      TFK_LOG(Error, "client config: " + cerr);
+      return 1;
+    }
+  } else {
+    rc.host = "http://127.0.0.1:8080";
+  }
   rc.qps = opt.qps;
   rc.burst = (int)opt.burst;
   rc.user_agent = "tf-operator/v0.1 (tfk)";
-  if (!opt.kubeconfig.empty()) {
-    std::ifstream f(opt.kubeconfig);
-    std::stringstream ss;
-    ss << f.rdbuf();
-    Json k = Json::parse(ss.str());
-    if (k.has("server")) rc.host = k.at("server").str();
-    if (k.has("qps")) rc.qps = k.at("qps").as_double();
-    if (k.has("burst")) rc.burst = (int)k.at("burst").as_int();
-  }
+  TFK_LOG(Info, "api server", Json(Json::object_t{{"host", Json(rc.host)},
+                                                 {"auth", Json(!rc.bearer_token.empty() ? "bearer-token"
+                                                               : !rc.tls.cert_file.empty() || !rc.tls.cert_data.empty()
+                                                                   ? "client-certificate" : "none")}}));
   auto client = new_for_config(rc);
   ControllerOptions co;
   co.threadiness = (int)opt.threadiness;

@@ -9,8 +9,8 @@
 namespace tfk {
 
 struct ServerOption {
-  std::string apiserver = "http://127.0.0.1:8080";
-  std::string kubeconfig;              // JSON {"server": "http://host:port", "qps":.., "burst":..}
+  std::string apiserver;                // "" = from kubeconfig / in-cluster / http://127.0.0.1:8080
+  std::string kubeconfig;              // kubeconfig YAML/JSON (client/config.h)
   std::string controller_config_file;  // JSON ControllerConfig (accelerators, grpcServerFilePath)
   std::string ns;                      // watch namespace ("" = all)
   long long threadiness = 2;

@@ -33,11 +33,18 @@ class ApiError(RuntimeError):
 
 
 class TfkClient:
-    def __init__(self, server: str | None = None, tfjob_version: str = "v1", timeout: float = 30.0):
+    def __init__(self, server: str | None = None, tfjob_version: str = "v1", timeout: float = 30.0,
+                 token: str | None = None, ca: str | None = None):
+        """token: bearer token (tfk-apiserver --token-auth-file / a service account); ca: PEM bundle
+        that signs an https:// server's certificate."""
         self.server = (server or os.environ.get("TFK_APISERVER", "http://127.0.0.1:8080")).rstrip("/")
         self.tfjob_version = tfjob_version
         self.timeout = timeout
         self.s = requests.Session()
+        token = token or os.environ.get("TFK_TOKEN")
+        if token:
+            self.s.headers["Authorization"] = f"Bearer {token}"
+        self.ca = ca
 
     def path(self, plural: str, ns: str | None = None, name: str | None = None, sub: str | None = None,
              version: str | None = None) -> str:
@@ -61,7 +68,8 @@ class TfkClient:
 
     def _do(self, method, url, body=None, params=None, raw=False):
         r = self.s.request(method, url, data=json.dumps(body) if body is not None else None, params=params,
-                           timeout=self.timeout, headers={"Content-Type": "application/json"})
+                           timeout=self.timeout, headers={"Content-Type": "application/json"},
+                           **({"verify": self.ca} if self.ca else {}))  # explicit: REQUESTS_CA_BUNDLE would win
         if raw:
             if r.status_code >= 300:
                 raise ApiError(r.status_code, r.text)
@@ -123,7 +131,8 @@ class TfkClient:
 
     def healthy(self) -> bool:
         try:
-            return self.s.get(self.server + "/healthz", timeout=2).status_code == 200
+            return self.s.get(self.server + "/healthz", timeout=2,
+                              **({"verify": self.ca} if self.ca else {})).status_code == 200
         except requests.RequestException:
             return False
 

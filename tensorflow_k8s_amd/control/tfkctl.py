@@ -95,6 +95,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser(prog="tfkctl")
     ap.add_argument("--server", default=os.environ.get("TFK_APISERVER", "http://127.0.0.1:8080"))
     ap.add_argument("-n", "--namespace", default="default")
+    ap.add_argument("--token", default=None, help="bearer token (kubectl --token)")
+    ap.add_argument("--certificate-authority", default=None, help="CA bundle for an https:// server")
     sub = ap.add_subparsers(dest="cmd", required=True)
     p = sub.add_parser("apply"); p.add_argument("-f", "--filename", required=True)
     p = sub.add_parser("create"); p.add_argument("-f", "--filename", required=True)
@@ -109,7 +111,7 @@ def main(argv=None):
     p = sub.add_parser("cluster"); p.add_argument("--gpus", type=int, default=-1); p.add_argument("--port", type=int, default=8080)
     p.add_argument("--root-dir", default="/tmp/tfk-kubelet")
     a = ap.parse_args(argv)
-    c = TfkClient(a.server)
+    c = TfkClient(a.server, token=a.token, ca=a.certificate_authority)
     try:
         if a.cmd in ("apply", "create"):
             for d in _load_docs(a.filename):

@@ -46,7 +46,7 @@ int tfk_opt_hyper(int*, const float*, int, int, float, float, float*, hipStream_
 int tfk_sumsq(const float*, long long, float*, hipStream_t);
 int tfk_clip_coef(const float*, float, float*, float*, hipStream_t);
 int tfk_splitk_reduce(const float*, int, long long, long long, float*, void*, int, float, hipStream_t);
-int tfk_transpose_arb(const void*, void*, int, int, int, hipStream_t);
+int tfk_transpose_arb(const void*, void*, int, int, int, int, hipStream_t);
 int tfk_transpose_f32(const float*, float*, int, int, hipStream_t);
 int tfk_cast_f32_bf16(const float*, void*, long long, hipStream_t);
 int tfk_cast_bf16_f32(const void*, float*, long long, hipStream_t);
@@ -202,10 +202,11 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
   p.drop_seed = (unsigned long long)drop_seed;
   const bool dense_a = amode == A_KIN || amode == A_KOUT;
-  // the conv-fwd-gather 256x256 tile exists on the LDS-DMA engine (gemm_g4.hip) only; the launcher
-  // falls back to 128x128 where that engine declines the shape
-  TORCH_CHECK((bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64) ||
+  // the conv-fwd-gather / wgrad-gather 256x256 tiles and the 64x128 tile exist on the LDS-DMA engine
+  // (gemm_g4.hip) only; the launcher falls back to 128x128 where that engine declines the shape
+  TORCH_CHECK((bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64) || (bm == 64 && bn == 128) ||
                   (bm == 256 && bn == 256 && (dense_a || amode == A_CONV_FWD) && (bmode == B_KIN || bmode == B_KOUT)) ||
+                  (bm == 256 && bn == 256 && amode == A_KOUT && bmode == B_CONV_WGRAD) ||
                   (bm == 256 && bn == 64 && dense_a && !(amode == A_KOUT && bmode == B_KOUT && epi == 0)) ||
                   (bm == 64 && bn == 256 && amode == A_KOUT && bmode == B_CONV_WGRAD && epi == 1),
               "unsupported tile ", bm, "x", bn, " for operand modes ", amode, "/", bmode);
@@ -511,10 +512,10 @@ void splitk_reduce(torch::Tensor slabs, int S, int64_t stride, int64_t n, c10::o
                              accumulate ? 1 : 0, (float)alpha, cur_stream()),
            "splitk_reduce");
 }
-void transpose_arb(torch::Tensor in, torch::Tensor out, int A, int R, int B) {
+void transpose_arb(torch::Tensor in, torch::Tensor out, int A, int R, int B, int flip) {
   need_bf16(in, "in"); need_bf16(out, "out");
   need_numel(in, (long long)A * R * B, "in"); need_numel(out, (long long)A * R * B, "out");
-  check_rc(tfk_transpose_arb(in.data_ptr(), out.data_ptr(), A, R, B, cur_stream()), "transpose_arb");
+  check_rc(tfk_transpose_arb(in.data_ptr(), out.data_ptr(), A, R, B, flip, cur_stream()), "transpose_arb");
 }
 void transpose_f32(torch::Tensor in, torch::Tensor out, int rows, int cols) {
   need_f32(in, "in"); need_f32(out, "out");
@@ -601,7 +602,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sumsq", &sumsq);
   m.def("clip_coef", &clip_coef);
   m.def("splitk_reduce", &splitk_reduce);
-  m.def("transpose_arb", &transpose_arb);
+  m.def("transpose_arb", &transpose_arb, py::arg("in"), py::arg("out"), py::arg("A"), py::arg("R"), py::arg("B"),
+        py::arg("flip") = 0);
   m.def("transpose_f32", &transpose_f32);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("cast_bf16_f32", &cast_bf16_f32);

@@ -22,7 +22,10 @@
 // rows/k read zeros: the buffer descriptor range check returns 0 for offsets past num_records.
 //
 // Operand modes: A_KIN / A_KOUT / A_CONV_FWD (implicit-GEMM gather, Cin % 64 == 0: a K-tile is one
-// (r,s) tap and 64 channels) x B_KIN / B_KOUT. Epilogues: gemm_epilogue.h (LDS-staged).
+// (r,s) tap and 64 channels) x B_KIN / B_KOUT / B_CONV_WGRAD (im2col of X as the K-outer operand of
+// a weight gradient: GEMM k = output pixel (n,p,q), column = (r,s,c); each lane's 16-B chunk is 8
+// channels of one tap, so C % 8 == 0; the pixel of a K-tile row is found with magic-number
+// division). Epilogues: gemm_epilogue.h (LDS-staged).
 #include "common.h"
 #include "gemm_params.h"
 #include "gemm_epilogue.h"
@@ -34,7 +37,9 @@ constexpr int BK = 64;
 constexpr unsigned OOB = 0x80000000u;
 constexpr int NREC = 0x7FFFFFF0;
 
-enum { KIN = 0, KOUT = 1, CONV_FWD = 2 };
+enum { KIN = 0, KOUT = 1, CONV_FWD = 2, CONV_WGRAD = 3 };
+
+__device__ __forceinline__ unsigned fdiv(unsigned x, unsigned mul, int shift) { return (__umulhi(x, mul) + x) >> shift; }
 
 __device__ __forceinline__ int swz64(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
 
@@ -75,12 +80,12 @@ struct Loader {
   // row (K-inner) / column (K-outer) of instruction i's lane inside the tile, and its k in a K-tile
   __device__ __forceinline__ static int row_of(int i, int w, int lane) {
     const int j = NW * i + w;
-    if constexpr (MODE == KOUT) return (j >> 3) * 64 + 8 * ((lane & 7) ^ swz64((j & 7) * 8 + (lane >> 3)));
+    if constexpr (MODE == KOUT || MODE == CONV_WGRAD) return (j >> 3) * 64 + 8 * ((lane & 7) ^ swz64((j & 7) * 8 + (lane >> 3)));
     else return 8 * j + (lane >> 3);
   }
   __device__ __forceinline__ static int k_of(int i, int w, int lane) {
     const int j = NW * i + w;
-    if constexpr (MODE == KOUT) return (j & 7) * 8 + (lane >> 3);
+    if constexpr (MODE == KOUT || MODE == CONV_WGRAD) return (j & 7) * 8 + (lane >> 3);
     else return 8 * ((lane & 7) ^ (((8 * j + (lane >> 3)) >> 1) & 7));
   }
 
@@ -92,6 +97,15 @@ struct Loader {
         off[i] = (unsigned)(((long long)r * ld + kl) * 2);
       } else if constexpr (MODE == KOUT) {
         off[i] = (unsigned)(((long long)kl * ld + r) * 2);
+      } else if constexpr (MODE == CONV_WGRAD) {
+        // column (r, s, c) of the im2col operand is fixed for the kernel: keep the tap's input
+        // offset and the channel; columns past N are flagged invalid (top bit of off)
+        const int col = row0 + r;
+        const int cc = min(col, rows - 1);
+        const int rs = cc / p.Cin, c = cc - rs * p.Cin, rr = rs / p.S, ss = rs - rr * p.S;
+        ch[i] = rr * p.dh - p.ph;
+        cw[i] = ss * p.dw - p.pw;
+        off[i] = (unsigned)c | (col < rows ? 0u : OOB);
       } else {
         const int m = min(row0 + r, rows - 1);
         const int PQ = p.P * p.Q;
@@ -109,7 +123,20 @@ struct Loader {
                                         char* img, int w, int lane) const {
     const int krem = p.K - kt * BK;
     const bool inner = lim >= ROWS && krem >= BK;  // block-uniform
-    if constexpr (MODE == CONV_FWD) {
+    if constexpr (MODE == CONV_WGRAD) {
+      __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, NREC, 0x00020000);
+      const unsigned PQ = (unsigned)(p.P * p.Q);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const unsigned pix = (unsigned)(kt * BK + k_of(i, w, lane));
+        const unsigned n = fdiv(pix, p.fd_pq_mul, p.fd_pq_shift), rem = pix - n * PQ;
+        const unsigned pp = fdiv(rem, p.fd_q_mul, p.fd_q_shift), qq = rem - pp * (unsigned)p.Q;
+        const int h = (int)pp * p.sh + ch[i], wq = (int)qq * p.sw + cw[i];
+        const bool ok = !(off[i] & OOB) && (int)pix < p.K && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
+        const unsigned vo = ok ? (unsigned)(((((long long)n * p.H + h) * p.W + wq) * p.Cin + off[i]) * 2) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
+      }
+    } else if constexpr (MODE == CONV_FWD) {
       // K-tile kt covers tap (r, s) = divmod(kt*64 / Cin, S) and channels c0..c0+63 (Cin % 64 == 0)
       const int k0 = kt * BK, rs = k0 / p.Cin, c0 = k0 - rs * p.Cin;
       const int r = rs / p.S, s = rs - r * p.S;
@@ -145,7 +172,8 @@ constexpr int nwaves() { return (BM / 64) * (BN / 64); }
 template <int BM, int BN, int AM, int BMD, int EPI>
 __global__ __launch_bounds__((nwaves<BM, BN>() * 64), ((BM * BN <= 128 * 128) ? 2 : 1)) void g4_kernel(GemmParams p) {
   constexpr int NW = nwaves<BM, BN>(), NTH = NW * 64, WGM = BM / 64, WGN = BN / 64;
-  constexpr bool AKO = (AM == KOUT), BKO = (BMD == KOUT);
+  constexpr int LBM = BMD == 2 ? CONV_WGRAD : BMD;  // B_CONV_WGRAD (= 2 in the B-mode numbering)
+  constexpr bool AKO = (AM == KOUT), BKO = (LBM == KOUT || LBM == CONV_WGRAD);
   constexpr int WTM = 64, WTN = 64, FM = 4, FN = 4;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int MAIN = 2 * STAGE, EPIB = epi_lds_bytes<BM, BN, WGM>();
@@ -171,13 +199,14 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), ((BM * BN <= 128 * 128) ? 
   const char* Ab;
   if constexpr (AM == CONV_FWD) Ab = (const char*)p.A + (long long)bz * p.sA * 2;
   else Ab = (const char*)p.A + (long long)bz * p.sA * 2 + (AKO ? (long long)m0 * 2 : (long long)m0 * p.lda * 2);
-  const char* Bb = (const char*)p.B + (long long)bz * p.sB * 2 + (BKO ? (long long)n0 * 2 : (long long)n0 * p.ldb * 2);
+  const char* Bb = (const char*)p.B + (long long)bz * p.sB * 2 +
+                   (LBM == CONV_WGRAD ? 0LL : BKO ? (long long)n0 * 2 : (long long)n0 * p.ldb * 2);
   const long long a_step = AKO ? (long long)BK * p.lda * 2 : BK * 2;
   const long long b_step = BKO ? (long long)BK * p.ldb * 2 : BK * 2;
   const int lim_a = p.M - m0, lim_b = p.N - n0;
 
   Loader<BM, AM, NW> la;
-  Loader<BN, BMD, NW> lb;
+  Loader<BN, LBM, NW> lb;
   la.init(p, lane, w, p.lda, m0, p.M);
   lb.init(p, lane, w, p.ldb, n0, p.N);
 
@@ -252,13 +281,15 @@ using namespace tfk;
 // Eligibility: 16-B aligned operand rows, K % 8 == 0 (a chunk never straddles K), K-outer row
 // counts % 8 == 0; conv gather: Cin % 64 == 0 (a K-tile = one tap x 64 channels).
 extern "C" int tfk_g4_ok(const GemmParams& p, int amode, int bmode) {
-  if (!(amode == 0 || amode == 1 || amode == 2) || bmode > 1) return 0;
+  if (!(amode == 0 || amode == 1 || amode == 2) || bmode > 2) return 0;
+  if (bmode == 2 && ((p.Cin & 7) || amode != 1 || (long long)p.Nimg * p.H * p.W * p.Cin >= (1LL << 30) ||
+                     (long long)p.Nimg * p.P * p.Q >= (1LL << 31) - 64)) return 0;
   if ((p.K & 7) || (p.ldb & 7)) return 0;
   if (amode != 2 && (p.lda & 7)) return 0;
   if (((uintptr_t)p.A & 15) || ((uintptr_t)p.B & 15)) return 0;
   if ((p.sA & 7) || (p.sB & 7)) return 0;
   if (amode == 1 && (p.M & 7)) return 0;
-  if (bmode == 1 && (p.N & 7)) return 0;
+  if (bmode >= 1 && (p.N & 7)) return 0;
   if (amode == 2 && ((p.Cin & 63) || (long long)p.Nimg * p.H * p.W * p.Cin >= (1LL << 30))) return 0;
   return 1;
 }
@@ -271,11 +302,26 @@ extern "C" int tfk_g4_ok(const GemmParams& p, int amode, int bmode) {
     return hipGetLastError() == hipSuccess ? 0 : -2;                                                \
   }
 #define TFK_G4_TILES(AM_, BM2_, EPI_) TFK_G4_CASE(256, 256, AM_, BM2_, EPI_) TFK_G4_CASE(128, 128, AM_, BM2_, EPI_)
+// 2-wave tiles for 64-wide operands (Cout = 64 weight gradients, 64-channel dgrads)
+#define TFK_G4_NARROW(AM_, BM2_, EPI_) TFK_G4_CASE(128, 64, AM_, BM2_, EPI_) TFK_G4_CASE(64, 128, AM_, BM2_, EPI_)
+
+static void fast_div(unsigned d, unsigned* mul, int* shift) {
+  int s = 0;
+  while ((1ull << s) < d) ++s;
+  *shift = s;
+  *mul = (unsigned)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+}
 
 // p.tiles_n / p.kt_per_split set by the caller (tfk_gemm_launch). Returns -1 if not instantiated.
-extern "C" int tfk_g4_launch(const GemmParams& p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits,
-                             hipStream_t stream) {
+extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, int bmode, int epi, int batch,
+                             int splits, hipStream_t stream) {
+  GemmParams p = p_in;
+  p.tiles_n = (p.N + bn - 1) / bn;
   const int tiles = ((p.M + bm - 1) / bm) * p.tiles_n;
+  if (bmode == 2) {
+    fast_div((unsigned)p.Q, &p.fd_q_mul, &p.fd_q_shift);
+    fast_div((unsigned)(p.P * p.Q), &p.fd_pq_mul, &p.fd_pq_shift);
+  }
   TFK_G4_TILES(0, 0, EPI_BF16)
   TFK_G4_TILES(0, 0, EPI_F32)
   TFK_G4_TILES(0, 0, EPI_BF16_EXT)
@@ -286,5 +332,18 @@ extern "C" int tfk_g4_launch(const GemmParams& p, int bm, int bn, int amode, int
   TFK_G4_TILES(1, 1, EPI_F32)
   TFK_G4_TILES(1, 1, EPI_BF16)
   TFK_G4_TILES(2, 0, EPI_BF16)
+  // stride-1 conv dgrad run as a forward conv over dY with flipped weights (ops/gemm.py), carrying
+  // the fused BN-backward reduction of the layer that produced x
+  TFK_G4_TILES(2, 0, EPI_BF16_BNR)
+  // conv weight gradients: dY (K-outer) x im2col(X) gather, f32 split-K slabs
+  TFK_G4_TILES(1, 2, EPI_F32)
+  TFK_G4_NARROW(1, 2, EPI_F32)
+  TFK_G4_NARROW(2, 0, EPI_BF16_BNR)
+  TFK_G4_NARROW(2, 0, EPI_BF16)
+  TFK_G4_NARROW(0, 1, EPI_BF16_BNR)
+  TFK_G4_NARROW(0, 1, EPI_F32)
+  TFK_G4_NARROW(1, 1, EPI_F32)
+  TFK_G4_NARROW(0, 0, EPI_BF16)
+  TFK_G4_NARROW(0, 1, EPI_BF16)
   return -1;
 }

@@ -54,5 +54,9 @@ struct GemmParams {
   //    (n, h/rs_sh, w/rs_sw) of [rs_p][rs_q] on the stride lattice and no resid elsewhere.
   int om_hp, om_wp, om_h, om_w, om_sh, om_sw, om_a, om_b;
   int rs_h, rs_w, rs_p, rs_q, rs_sh, rs_sw;
+  // LDS-DMA conv weight-gradient gather (gemm_g4.hip): magic-number division of a pixel index by
+  // Q and P*Q ((umulhi(x, mul) + x) >> shift, x < 2^31), filled by the g4 host launcher
+  unsigned fd_q_mul, fd_pq_mul;
+  int fd_q_shift, fd_pq_shift;
 };
 }  // namespace tfk

@@ -55,7 +55,10 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slabs, int S, lon
 }
 
 // in [A][R][B] -> out [B][R][A] (bf16), 32x32 LDS tiles; grid (ceil(B/32), ceil(A/32), R).
-__global__ void transpose_arb_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int A, int R, int B) {
+// flip: write middle index R-1-r (a conv weight's (r,s) taps reversed: the stride-1 dgrad as a
+// forward conv over dY, ops/gemm.py conv_dgrad).
+__global__ void transpose_arb_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int A, int R, int B,
+                                     int flip) {
   __shared__ bf16 tile[32][33];
   const int b0 = blockIdx.x * 32, a0 = blockIdx.y * 32, r = blockIdx.z;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads -> 8 rows per pass
@@ -66,7 +69,7 @@ __global__ void transpose_arb_kernel(const bf16* __restrict__ in, bf16* __restri
   __syncthreads();
   for (int i = ty; i < 32; i += 8) {
     int b = b0 + i, a = a0 + tx;
-    if (a < A && b < B) out[((long long)b * R + r) * A + a] = tile[tx][i];
+    if (a < A && b < B) out[((long long)b * R + (flip ? R - 1 - r : r)) * A + a] = tile[tx][i];
   }
 }
 
@@ -207,9 +210,9 @@ int tfk_splitk_reduce(const float* slabs, int S, long long stride, long long n, 
                      S - SG, stride, n, out, outb, 1, alpha, 1);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int tfk_transpose_arb(const bf16* in, bf16* out, int A, int R, int B, hipStream_t s) {
+int tfk_transpose_arb(const bf16* in, bf16* out, int A, int R, int B, int flip, hipStream_t s) {
   dim3 grid((B + 31) / 32, (A + 31) / 32, R);
-  hipLaunchKernelGGL(transpose_arb_kernel, grid, dim3(NT), 0, s, in, out, A, R, B);
+  hipLaunchKernelGGL(transpose_arb_kernel, grid, dim3(NT), 0, s, in, out, A, R, B, flip);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_transpose_f32(const float* in, float* out, int rows, int cols, hipStream_t s) {

@@ -84,7 +84,7 @@ _TILES = {(256, 256): (256, 0.76), (128, 128): (512, 0.62), (256, 64): (512, 0.6
 # The LDS-DMA engine (gemm_g4.hip) on the same scale, for the modes it serves (dense operands and the
 # Cin % 64 == 0 conv-forward gather): tools/engine_bench.py on MI355X -- 256x256 (16 waves) ~1.0-1.3
 # PF/s, 128x128 (4 waves, 2 blocks/CU) ~0.7-1.1 PF/s vs the register engine's 0.6-0.9.
-_G4_TILES = {(256, 256): (256, 0.95), (128, 128): (512, 0.80)}
+_G4_TILES = {(256, 256): (256, 0.95), (128, 128): (512, 0.80), (128, 64): (768, 0.62), (64, 128): (768, 0.62)}
 G4_BIG_MIN_K = 512  # one 16-wave block per CU: shorter K cannot amortise its prologue/epilogue
 # 64x256 tile for Cout<=64 conv weight gradients whose B gather changes (r,s) every chunk (C <= 16,
 # i.e. the 7x7 stem on C padded to 8). Measured on MI355X (ResNet-50 bs256, rocprofv3): stem wgrad
@@ -96,17 +96,22 @@ G4_ENABLED = os.environ.get("TFK_GEMM_ENGINE", "g4") != "reg"
 
 
 def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: int = 0, mid_ok: bool = True,
-              wide_ok: bool = False, split_target: int | None = None, g4: bool = False):
+              wide_ok: bool = False, split_target: int | None = None, g4: bool = False, narrow_ok: bool = False):
     """Tile with the lowest modelled time: rounds of concurrent blocks x per-block work / efficiency
     (a 256x256 tile runs one block per CU; smaller tiles 2-4 blocks/CU at lower efficiency).
     big_ok: operand modes that have the 256x256 instantiation (dense, non-gather); K: reduction
     length. mid_ok: the mode has the 256x64 tile (every mode except the conv fwd/dgrad gathers).
     wide_ok: the mode has the 64x256 tile (conv weight gradient gather), only worth it for M <= 64.
-    g4: the mode runs on the LDS-DMA engine (its 128x128 / 256x256 tiles; 256x256 also with split-K)."""
+    g4: the mode runs on the LDS-DMA engine (its 128x128 / 256x256 tiles; 256x256 also with split-K).
+    narrow_ok: also its 2-wave 128x64 / 64x128 tiles (measured faster than the register engine
+    for the im2col weight-gradient gather only; dense and BN-epilogue shapes keep the latter)."""
     g4 = g4 and G4_ENABLED
     best, best_cost = None, None
-    for (bm, bn), (slots, eff) in _TILES.items():
-        if g4 and (bm, bn) in _G4_TILES:
+    cands = dict(_TILES)
+    if g4:
+        cands.update({t: v for t, v in _G4_TILES.items() if narrow_ok or t[0] == t[1]})
+    for (bm, bn), (slots, eff) in cands.items():
+        if g4 and (bm, bn) in _G4_TILES and (narrow_ok or bm == bn):
             slots, eff = _G4_TILES[(bm, bn)]
             if (bm, bn) == (256, 256) and (M < 256 or N < 256 or K < G4_BIG_MIN_K):
                 continue
@@ -331,13 +336,37 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
     return y
 
 
-def conv_weight_t(w: torch.Tensor, g: ConvGeom, out: torch.Tensor | None = None) -> torch.Tensor:
-    """OHWI [K][R][S][C] -> [C][R][S][K] (dgrad B operand)."""
+def conv_weight_t(w: torch.Tensor, g: ConvGeom, out: torch.Tensor | None = None, flip: bool = False) -> torch.Tensor:
+    """OHWI [K][R][S][C] -> [C][R][S][K] (dgrad B operand); flip: taps reversed,
+    out[c][r][s][k] = w[k][R-1-r][S-1-s][c] (the stride-1 dgrad as a forward conv)."""
     if not on_gpu(w):
-        return w.permute(3, 1, 2, 0).contiguous()
+        t = w.flip(1, 2) if flip else w
+        return t.permute(3, 1, 2, 0).contiguous()
     out = out if out is not None else torch.empty(g.C, g.R, g.S, g.K, dtype=torch.bfloat16, device=w.device)
-    lib().transpose_arb(w, out, g.K, g.R * g.S, g.C)
+    lib().transpose_arb(w, out, g.K, g.R * g.S, g.C, int(flip))
     return out
+
+
+def dgrad_as_fwd_geom(g: ConvGeom) -> ConvGeom | None:
+    """A stride-1, undilated conv's input gradient is a forward conv of dY with the flipped,
+    transposed kernel: dx[n,h,w,c] = sum_{r,s,k} dy[n, h - (R-1-ph) + r', w - (S-1-pw) + s', k]
+    * w[k][R-1-r'][S-1-s'][c]. Returns that forward conv's geometry (input dY [N,P,Q,K], Cout = C,
+    pad R-1-ph), or None when the conv is not of that kind or the output size would differ."""
+    if g.sh != 1 or g.sw != 1 or g.dh != 1 or g.dw != 1 or g.pointwise:
+        return None
+    if g.R - 1 - g.ph < 0 or g.S - 1 - g.pw < 0:
+        return None
+    f = ConvGeom(g.N, g.P, g.Q, g.K, g.C, g.R, g.S, 1, 1, g.R - 1 - g.ph, g.S - 1 - g.pw)
+    return f if (f.P == g.H and f.Q == g.W) else None
+
+
+# Stride-1 dgrads go through the LDS-DMA engine's conv-forward gather (its Cin = the conv's Cout
+# must be a multiple of 64) for outputs of >= 128 channels. TFK_DGRAD_AS_FWD=0 restores the
+# register-engine gather (measured ResNet-50 step: 31.13 -> 30.81 ms with it on).
+DGRAD_AS_FWD = os.environ.get("TFK_DGRAD_AS_FWD", "1") == "1"
+DGRAD_AS_FWD_MIN_C = 128  # 64-channel dx: the 2-wave 128x64 BN epilogue measured slower (0.28 vs 0.22 ms)
+# Non-pointwise weight gradients on the LDS-DMA engine's im2col gather (B_CONV_WGRAD, C % 8 == 0).
+G4_WGRAD = os.environ.get("TFK_G4_WGRAD", "1") == "1"
 
 
 def _phases(g: ConvGeom):
@@ -401,6 +430,14 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
     if g.pointwise:
         _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid, bnr=bnr)
         return dx
+    f = dgrad_as_fwd_geom(g) if (DGRAD_AS_FWD and G4_ENABLED and g.K % 64 == 0 and g.C >= DGRAD_AS_FWD_MIN_C
+                                 and g.C % 8 == 0) else None
+    if f is not None:
+        wf = conv_weight_t(w, g, flip=True)  # [C][R][S][K]: the forward conv's OHWI weight
+        Kd = g.R * g.S * g.K
+        _gemm(dy, wf, dx, M, g.C, Kd, 0, Kd, g.C, A_CONV_FWD, B_KIN, EPI_BF16,
+              pick_tile(M, g.C, K=Kd, mid_ok=False, g4=True), resid=resid, conv=f.vec(), bnr=bnr)
+        return dx
     phases = _phases(g) if (bnr is not None and (g.sh > 1 or g.sw > 1)) else None
     if phases is not None:
         wt = wt if wt is not None else conv_weight_t(w, g)
@@ -439,7 +476,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
         return
     tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp,
                      wide_ok=WIDE_WGRAD and not g.pointwise and g.C <= WIDE_WGRAD_MAX_C,
-                     g4=g.pointwise and g.K % 8 == 0 and g.C % 8 == 0)
+                     g4=(G4_WGRAD or g.pointwise) and g.K % 8 == 0 and g.C % 8 == 0,
+                     narrow_ok=G4_WGRAD and not g.pointwise)
     tiles = ((g.K + tile[0] - 1) // tile[0]) * ((Nn + tile[1] - 1) // tile[1])
 
     def run(C, sp, stride, beta):

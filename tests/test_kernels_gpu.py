@@ -42,6 +42,11 @@ CONVS = [
     # Cout <= 64 non-pointwise weight gradients take the 64x256 tile (stem 7x7 on C padded to 8, ragged M/N)
     (1, 20, 20, 8, 64, 7, 7, 2, 3),
     (1, 10, 10, 16, 48, 3, 3, 1, 1),
+    # stride-1 dgrads with >= 128 input channels run as a forward conv over dY (flipped weights, g4)
+    (2, 9, 9, 128, 64, 3, 3, 1, 1),
+    (1, 12, 12, 128, 64, 5, 5, 1, 2),
+    (2, 10, 10, 256, 128, 3, 3, 1, 1),
+    (1, 9, 11, 128, 64, 3, 3, 1, 0),
 ]
 
 
@@ -259,7 +264,8 @@ def test_global_norm_clip():
 
 @pytest.mark.parametrize("mode", ["relu_from_y", "mask_a", "dual"])
 @pytest.mark.parametrize("cfg", [(2, 8, 8, 64, 256, 1, 1, 1, 0), (2, 9, 9, 64, 64, 3, 3, 1, 1), (2, 14, 14, 256, 512, 1, 1, 2, 0),
-                                 (2, 16, 16, 64, 64, 3, 3, 2, 1), (2, 15, 13, 32, 48, 3, 3, 2, 1)])
+                                 (2, 16, 16, 64, 64, 3, 3, 2, 1), (2, 15, 13, 32, 48, 3, 3, 2, 1),
+                                 (2, 9, 9, 128, 64, 3, 3, 1, 1), (3, 20, 20, 256, 256, 3, 3, 1, 1)])
 def test_dgrad_fused_bn_reduce(cfg, mode):
     """BN-backward channel sums fused into the dgrad epilogue == the standalone reduction."""
     N, H, W, C, K, R, S, st_, pd = cfg

@@ -124,6 +124,7 @@ TFJob from_json(const Json& j) {
     job.status.completion_time = st.at("completionTime").str();
     job.status.last_reconcile_time = st.at("lastReconcileTime").str();
     job.status.restart_count = (int)st.at("restartCount").as_int(0);
+    job.status.resize_count = (int)st.at("resizeCount").as_int(0);
     for (auto& c : st.at("conditions").items()) {
       JobCondition jc;
       jc.type = c.at("type").str(); jc.status = c.at("status").str(); jc.reason = c.at("reason").str();
@@ -241,6 +242,7 @@ Json to_json(const TFJob& job) {
   if (!job.status.completion_time.empty()) st["completionTime"] = job.status.completion_time;
   if (!job.status.last_reconcile_time.empty()) st["lastReconcileTime"] = job.status.last_reconcile_time;
   if (job.status.restart_count) st["restartCount"] = job.status.restart_count;
+  if (job.status.resize_count) st["resizeCount"] = job.status.resize_count;
   j["spec"] = spec;
   if (st.size()) j["status"] = st;
   return j;

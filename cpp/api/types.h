@@ -72,7 +72,8 @@ struct TFJobStatus {
   std::vector<JobCondition> conditions;
   std::map<RType, ReplicaStatus> replica_statuses;
   std::string start_time, completion_time, last_reconcile_time;
-  int restart_count = 0;
+  int restart_count = 0;  // gang restarts after retryable failures (counted against backoffLimit)
+  int resize_count = 0;   // coordinated restarts after a replica-count change (not counted)
 };
 
 struct TFJob {

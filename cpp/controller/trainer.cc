@@ -106,6 +106,18 @@ Json Trainer::make_service(const api::TFJob& job, RType t, int index) const {
   return s;
 }
 
+// The training world a pod's TF_CONFIG describes: replica counts of every cluster member type
+// (the Evaluator is outside the cluster spec). Pods carry it as an annotation so a replica-count
+// change (scale up or down) is detected against the pods that are running.
+static std::string world_signature(const api::TFJob& job) {
+  std::map<std::string, int> m;
+  for (auto& r : job.replicas)
+    if (r.type != RType::Evaluator) m[api::rtype_title(r.type)] = r.replicas;
+  std::string s;
+  for (auto& kv : m) s += (s.empty() ? "" : ",") + kv.first + "=" + std::to_string(kv.second);
+  return s;
+}
+
 Json Trainer::make_pod(const api::TFJob& job, RType t, int index, int generation) const {
   const api::ReplicaSpec* rs = job.replica(t);
   Json tmpl = rs && rs->template_.is_object() ? rs->template_.clone() : Json::object();
@@ -124,6 +136,7 @@ Json Trainer::make_pod(const api::TFJob& job, RType t, int index, int generation
   md["annotations"]["scheduling.tfk.io/group-name"] = job.name();
   md["annotations"]["scheduling.tfk.io/min-available"] = std::to_string(min_avail);
   md["annotations"]["tfk.io/restart-generation"] = std::to_string(generation);
+  md["annotations"]["tfk.io/world"] = world_signature(job);
   md["ownerReferences"] = Json(Json::array_t{api::as_owner(job)});
   pod["metadata"] = md;
   Json spec = tmpl.at("spec").is_object() ? tmpl.at("spec").clone() : Json::object();
@@ -379,8 +392,16 @@ ReconcileResult Trainer::reconcile(const Json& orig, const std::vector<Json>& po
   // ---------------------------------------------------------------- index existing pods
   std::map<std::pair<RType, int>, Json> slot;
   std::vector<Json> extra;
+  // Pods of an older generation were already acted upon (a gang restart or a resize deleted
+  // them); a stale cache or a late kubelet status must not restart the job a second time.
+  const int cur_gen = job.status.restart_count + job.status.resize_count;
   for (auto& p : pods_in) {
     if (p.path("metadata.deletionTimestamp").is_string()) continue;
+    const Json& ga = p.path("metadata.annotations").at("tfk.io/restart-generation");
+    if (ga.is_string() && atoi(ga.str().c_str()) < cur_gen) {
+      if (client_->remove("pods", job.ns(), p.path("metadata.name").str(), "Background").ok()) res.pods_deleted++;
+      continue;
+    }
     const Json& l = p.path("metadata.labels");
     RType t = api::rtype_from(l.at("tf-replica-type").str());
     int idx = atoi(l.at("tf-replica-index").str("-1").c_str());
@@ -390,7 +411,43 @@ ReconcileResult Trainer::reconcile(const Json& orig, const std::vector<Json>& po
     if (!slot.count(key) || slot[key].path("metadata.creationTimestamp").str() < p.path("metadata.creationTimestamp").str())
       slot[key] = p;
   }
-  // scale-down (elastic resize of a replica set): remove pods beyond the new count
+  // ---------------------------------------------------------------- coordinated resize (扩容/缩容)
+  // A replica-count change alters the cluster every rank's TF_CONFIG lists, and collective
+  // training (RCCL rings, PS shard maps) cannot admit or drop a rank in place: every pod built for
+  // the old world is replaced together under a new generation, and the new gang resumes from the
+  // chief's latest checkpoint at the new world size. Not counted against backoffLimit.
+  const std::string world = world_signature(job);
+  std::vector<Json> stale;
+  for (auto& kv : slot) {
+    const Json& w = kv.second.path("metadata.annotations").at("tfk.io/world");
+    if (w.is_string() && w.str() != world && kv.first.first != RType::Evaluator) stale.push_back(kv.second);
+  }
+  if (!stale.empty()) {
+    for (auto& p : extra) stale.push_back(p);
+    for (auto& kv : slot)
+      if (kv.first.first != RType::Evaluator) stale.push_back(kv.second);
+    std::set<std::string> gone;
+    for (auto& p : stale) {
+      const std::string n = p.path("metadata.name").str();
+      if (!gone.insert(n).second) continue;
+      if (client_->remove("pods", job.ns(), n, "Background").ok()) {
+        res.pods_deleted++;
+        if (metrics_) metrics_->pods_deleted++;
+      }
+    }
+    job.status.resize_count++;
+    const std::string msg = "TFJob " + job.name() + " is resizing to " + world + " (generation " +
+                            std::to_string(job.status.restart_count + job.status.resize_count) + ")";
+    api::set_condition(job.status, "Restarting", "TFJobResized", msg, now);
+    if (job.is_v1alpha1()) job.status.phase = "Running";
+    rec_->event(orig, "Normal", "TFJobResized", msg);
+    ApiStatus st = write_status(job, orig);
+    res.status_changed = true;
+    res.requeue = true;
+    if (!st.ok()) res.error = st.message;
+    return res;
+  }
+  // replicas beyond the count of a pre-annotation pod set (no world recorded): remove them
   for (auto& p : extra)
     if (client_->remove("pods", job.ns(), p.path("metadata.name").str(), "Background").ok()) {
       res.pods_deleted++;
@@ -398,7 +455,8 @@ ReconcileResult Trainer::reconcile(const Json& orig, const std::vector<Json>& po
     }
   std::set<std::string> have_svc;
   for (auto& s : services) have_svc.insert(s.path("metadata.name").str());
-  int generation = job.status.restart_count;
+  // pod generation: gang restarts + coordinated resizes (TFK_RESTART_GENERATION in the pod)
+  int generation = job.status.restart_count + job.status.resize_count;
 
   // ---------------------------------------------------------------- services + pods
   std::vector<std::string> permanent_failures;

@@ -145,8 +145,17 @@ void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
   const char* log_path = c.log_path.c_str();
   const char* wd_c = wd.empty() ? nullptr : wd.c_str();
   static const char kExecFail[] = "tfk-kubelet: exec failed\n";
+  // The kubelet blocks SIGINT/SIGTERM for its sigwait thread (HandleSignals) and ignores SIGPIPE;
+  // both survive exec, so the container would ignore the SIGTERM of a graceful stop and only die
+  // at the SIGKILL deadline. The child restores an empty mask and default dispositions.
+  sigset_t none;
+  sigemptyset(&none);
   pid_t pid = fork();
   if (pid == 0) {
+    sigprocmask(SIG_SETMASK, &none, nullptr);
+    signal(SIGPIPE, SIG_DFL);
+    signal(SIGTERM, SIG_DFL);
+    signal(SIGINT, SIG_DFL);
     setsid();
     int fd = open(log_path, O_WRONLY | O_CREAT | O_APPEND, 0644);
     if (fd >= 0) { dup2(fd, 1); dup2(fd, 2); close(fd); }
@@ -293,6 +302,15 @@ void Kubelet::sync_once() {
     if (it == pods_.end()) {
       std::string phase = p.path("status.phase").str();
       if (phase == "Succeeded" || phase == "Failed") continue;  // already terminal (kubelet restart)
+      // A replacement pod with the name of one still terminating (gang restart / resize) waits
+      // until the old containers have exited, as the API's graceful deletion guarantees on a real
+      // cluster: two incarnations of one rank would fight over its port and checkpoint.
+      bool predecessor = false;
+      for (auto& kv : pods_)
+        if (kv.first != uid && kv.second.name == p.path("metadata.name").str() &&
+            kv.second.ns == p.path("metadata.namespace").str())
+          for (auto& c : kv.second.containers) predecessor |= c.pid > 0;
+      if (predecessor) continue;
       PodRun pr;
       pr.uid = uid;
       pr.ns = p.path("metadata.namespace").str();

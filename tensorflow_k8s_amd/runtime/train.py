@@ -77,6 +77,7 @@ def parse_args(argv=None):
     ap.add_argument("--num-classes", type=int, default=0)
     ap.add_argument("--seq-len", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--step-sleep", type=float, default=0.0, help="seconds to pause after each step (paces demo/test jobs)")
     ap.add_argument("--rendezvous-timeout", type=float, default=300.0)
     ap.add_argument("--watchdog-timeout", type=float, default=0.0,
                     help="exit 143 (retryable) when no step completes for this many seconds (0 = off)")
@@ -255,6 +256,8 @@ def run_worker(args, info, dev) -> int:
                 path = ckpt.save(model.arena, opt, step)
             _log({"event": "checkpoint", "step": step, "path": path}, metrics_fh)
         maybe_fault(step, info.rank)
+        if args.step_sleep > 0:
+            time.sleep(args.step_sleep)
     if watchdog is not None:
         watchdog.stop()
     if args.trace_file:

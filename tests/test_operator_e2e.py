@@ -115,3 +115,41 @@ def test_deploy_examples_are_accepted(cluster):
     for n in names:
         c.delete("tfjobs", n)
     assert not pending, pending
+
+
+def test_scale_up_restarts_gang_with_new_world(cluster, tmp_path):
+    """Coordinated scale-up (扩容, k8s-operator.md:1): raising Worker replicas on a running job
+    replaces every pod of the old world under a new generation; the new gang's TF_CONFIG lists the
+    larger cluster and training resumes from the chief's checkpoint instead of starting over."""
+    import time
+    c = cluster.client
+    ck = str(tmp_path / "ck")
+    args = _args(ck, steps=40) + ["--step-sleep", "0.1"]
+    c.create(_job("elastic", {"Chief": _rs(1, args), "Worker": _rs(1, args)}))
+    dl = time.time() + 120
+    while time.time() < dl:
+        try:
+            if any(e["event"] == "checkpoint" for e in _events(c.logs("elastic-chief-0"))):
+                break
+        except Exception:
+            pass
+        time.sleep(0.2)
+    else:
+        raise AssertionError("chief never checkpointed")
+    c.patch("tfjobs", "elastic", {"spec": {"tfReplicaSpecs": {"Worker": {"replicas": 2}}}})
+    j = c.wait_tfjob("elastic", timeout=300)
+    st = j["status"]
+    assert tfjob_condition(j) == "Succeeded", st
+    assert st.get("resizeCount") == 1 and not st.get("restartCount"), st
+    assert any(cd["type"] == "Restarting" and cd["reason"] == "TFJobResized" for cd in st["conditions"]), st
+    pod = c.get("pods", "elastic-worker-1")
+    assert pod["metadata"]["annotations"]["tfk.io/world"] == "Chief=1,Worker=2"
+    env = {e["name"]: e.get("value") for e in pod["spec"]["containers"][0]["env"]}
+    assert len(json.loads(env["TF_CONFIG"])["cluster"]["worker"]) == 2
+    assert env.get("TFK_RESTART_GENERATION") == "1"
+    ev = _events(c.logs("elastic-chief-0"))
+    restored = [e for e in ev if e["event"] == "restored"]
+    start = [e for e in ev if e["event"] == "start"][-1]
+    assert restored and restored[-1]["step"] >= 4, ev[:5]
+    assert start["workers"] == 3 and start["start_step"] == restored[-1]["step"]
+    assert [e for e in ev if e["event"] == "done"][-1]["step"] == 40

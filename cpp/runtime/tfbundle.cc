@@ -5,6 +5,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -334,9 +336,14 @@ static bool write_file_atomic(const std::string& path, const std::string& data, 
   std::string tmp = path + ".tmp" + rand_string(6);
   int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
   if (fd < 0) { *err = "open " + tmp + ": " + strerror(errno); return false; }
+  // Fault injection (k8s-operator.md:5 "disk failure"): TFK_FAULT_CKPT_ENOSPC=<substring> makes
+  // writes of matching files fail as a full disk would, half-way through the file.
+  const char* fault = getenv("TFK_FAULT_CKPT_ENOSPC");
+  const bool inject = fault && *fault && path.find(fault) != std::string::npos;
   size_t off = 0;
   while (off < data.size()) {
-    ssize_t n = write(fd, data.data() + off, data.size() - off);
+    ssize_t n = (inject && off >= data.size() / 2) ? (errno = ENOSPC, -1)
+                                                   : write(fd, data.data() + off, inject ? data.size() / 2 - off : data.size() - off);
     if (n < 0) {
       *err = "write " + tmp + ": " + strerror(errno) + (errno == ENOSPC ? " (disk full)" : "");
       close(fd);

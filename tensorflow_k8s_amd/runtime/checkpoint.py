@@ -23,6 +23,11 @@ from ..ops._lib import lib
 SLOT_SUFFIX = {"Momentum": "Momentum", "Adam": "Adam", "Adam_1": "Adam_1"}
 
 
+class CheckpointWriteError(RuntimeError):
+    """A checkpoint could not be written (e.g. the disk is full). The previous checkpoint and the
+    `checkpoint` state file are untouched (tmp + rename), so a restart resumes from it."""
+
+
 def _to_tf(p, arr: np.ndarray) -> np.ndarray:
     return p.spec.to_tf(arr) if p.spec.to_tf is not None else arr
 
@@ -80,7 +85,7 @@ class CheckpointManager:
                     for f in glob.glob(os.path.join(self.dir, old + ".*")):
                         os.remove(f)
             except Exception as e:  # surfaced by wait()
-                self.error = e
+                self.error = CheckpointWriteError(f"checkpoint {name} not written: {e}")
 
         if blocking:
             work()

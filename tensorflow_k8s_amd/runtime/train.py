@@ -283,6 +283,7 @@ def run_worker(args, info, dev) -> int:
 def main(argv=None) -> int:
     args = parse_args(argv)
     from ..parallel import cluster
+    from .checkpoint import CheckpointWriteError
     info = cluster.resolve()
     if info.is_evaluator:
         from .evaluator import run_evaluator
@@ -296,6 +297,7 @@ def main(argv=None) -> int:
             use_ps = args.strategy == "ps" or (args.strategy == "auto" and info.ps_ranks)
             backend = "nccl" if (dev.type == "cuda" and (not use_ps or args.ps_transport == "rccl")) else "gloo"
             cluster.init_process_group(info, backend, timeout_s=args.rendezvous_timeout,
+                                       retries=int(os.environ.get("TFK_RENDEZVOUS_RETRIES", "5")),
                                        device_id=dev if backend == "nccl" else None)
         if info.is_ps:
             return run_ps(args, info, dev)
@@ -304,6 +306,11 @@ def main(argv=None) -> int:
         _termination_message("OOMKilled")
         _log({"event": "error", "kind": "oom", "message": str(e)[:500]})
         return EXIT_OOM
+    except CheckpointWriteError as e:
+        # permanent (a restart would hit the same full disk); the previous checkpoint is intact
+        _termination_message(f"CheckpointWriteFailed: {e}"[:2000])
+        _log({"event": "error", "kind": "checkpoint", "message": str(e)[:500]})
+        return EXIT_USER
     except cluster.RendezvousError as e:
         _termination_message(str(e))
         _log({"event": "error", "kind": "rendezvous", "message": str(e)[:500]})

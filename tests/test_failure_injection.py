@@ -1,0 +1,57 @@
+"""Failure modes named by the reference (k8s-operator.md:5: OOM, port already in use, disk
+failure), injected at the runtime boundary (the operator-side handling is in test_operator_e2e.py).
+
+Port in use: the chief's rendezvous port (tfPort, TF_CONFIG) is held by another process -- in
+practice the previous restart generation still shutting down. init_process_group retries, then
+raises RendezvousError, and the replica exits 143 (retryable: the operator restarts the gang)
+with the reason in its termination log.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from tensorflow_k8s_amd.parallel import cluster
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _held_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    s.listen(1)
+    return s, s.getsockname()[1]
+
+
+def test_rendezvous_port_in_use_raises_retryable():
+    s, port = _held_port()
+    try:
+        info = cluster.ClusterInfo(task_type="chief", task_index=0, rank=0, world_size=2, master_addr="127.0.0.1",
+                                   master_port=port, worker_ranks=[0, 1], source="tf_config")
+        with pytest.raises(cluster.RendezvousError) as e:
+            cluster.init_process_group(info, "gloo", timeout_s=5, retries=2)
+        assert "port already in use" in str(e.value)
+        assert cluster.RendezvousError.exit_code == 143
+    finally:
+        s.close()
+
+
+def test_chief_replica_exits_143_on_port_in_use(tmp_path):
+    s, port = _held_port()
+    try:
+        tf = {"cluster": {"chief": [f"127.0.0.1:{port}"], "worker": ["127.0.0.1:1"]},
+              "task": {"type": "chief", "index": 0}, "environment": "cloud"}
+        env = dict(os.environ, TF_CONFIG=json.dumps(tf), TFK_TERMINATION_LOG=str(tmp_path / "term"),
+                   PYTHONPATH=ROOT, TFK_RENDEZVOUS_RETRIES="1")
+        r = subprocess.run([sys.executable, "-m", "tensorflow_k8s_amd.runtime.train", "--model", "lenet", "--steps", "2",
+                            "--device", "cpu", "--rendezvous-timeout", "5"], env=env, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 143, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+        assert "port already in use" in (tmp_path / "term").read_text()
+        ev = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+        assert ev[-1]["kind"] == "rendezvous"
+    finally:
+        s.close()

@@ -153,3 +153,25 @@ def test_scale_up_restarts_gang_with_new_world(cluster, tmp_path):
     assert restored and restored[-1]["step"] >= 4, ev[:5]
     assert start["workers"] == 3 and start["start_step"] == restored[-1]["step"]
     assert [e for e in ev if e["event"] == "done"][-1]["step"] == 40
+
+
+def test_checkpoint_disk_full_fails_clearly_keeps_previous(cluster, tmp_path):
+    """Disk failure (k8s-operator.md:5): the step-8 checkpoint write hits ENOSPC (injected in the
+    native bundle writer); the job fails with a clear CheckpointWriteFailed message, no partial
+    files are left, and the `checkpoint` state still names the intact step-4 checkpoint."""
+    import glob
+    c = cluster.client
+    ck = str(tmp_path / "ck")
+    c.create(_job("diskfull", {"Chief": _rs(1, _args(ck, steps=12), [("TFK_FAULT_CKPT_ENOSPC", "model.ckpt-8")])}))
+    j = c.wait_tfjob("diskfull", timeout=180)
+    assert tfjob_condition(j) == "Failed", j["status"]
+    ev = _events(c.logs("diskfull-chief-0"))
+    err = [e for e in ev if e["event"] == "error"]
+    assert err and err[-1]["kind"] == "checkpoint" and "disk full" in err[-1]["message"], ev[-3:]
+    state = open(os.path.join(ck, "checkpoint")).read()
+    assert 'model_checkpoint_path: "model.ckpt-4"' in state, state
+    assert os.path.exists(os.path.join(ck, "model.ckpt-4.index"))
+    assert not glob.glob(os.path.join(ck, "model.ckpt-8*")) and not glob.glob(os.path.join(ck, "*.tmp*"))
+    pod = c.get("pods", "diskfull-chief-0")
+    term = pod["status"]["containerStatuses"][0]["state"]["terminated"]
+    assert term["exitCode"] == 1 and "CheckpointWriteFailed" in term.get("message", ""), term

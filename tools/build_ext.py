@@ -62,9 +62,18 @@ def ext_path() -> str:
 
 
 def build_kernels(jobs: int | None = None, verbose: bool = False) -> str:
+    headers = glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.h"))
+    srcs = (glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")) + glob.glob(os.path.join(ROOT, "csrc", "bindings", "*.cpp"))
+            + headers + glob.glob(os.path.join(ROOT, "cpp", "*", "*.h"))
+            + [os.path.join(ROOT, r) for r in ("cpp/runtime/tfbundle.cc", "cpp/common/util.cc", "cpp/common/json.cc")])
+    so = ext_path()
+    if os.path.exists(so) and not _stale(so, srcs):
+        # up to date -- also the case on a GPU box, whose snapshot carries the .so but not build/obj
+        if verbose:
+            print(f"[tfk build] {so} is up to date")
+        return so
     os.makedirs(OBJ, exist_ok=True)
     inc, libs = _torch_paths()
-    headers = glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.h"))
     jobs = jobs or min(16, os.cpu_count() or 4)
     tasks = []
     objs = []

@@ -62,9 +62,12 @@ TFJob from_json(const Json& j) {
   job.metadata = j.at("metadata").is_object() ? j.at("metadata").clone() : Json::object();
   const Json& spec = j.at("spec");
   if (!spec.is_object()) throw std::runtime_error("TFJob.spec missing");
+  // v1alpha1-only spec fields ride in annotations while the object is stored in the v1 shape, so
+  // a v1alpha1 -> v1 -> v1alpha1 round trip is lossless (runtimeId names every replica's pods)
+  const Json& ann = job.metadata.at("annotations");
   if (job.is_v1alpha1()) {
-    job.runtime_id = spec.at("runtimeId").str();
-    job.tf_image = spec.at("tfImage").str();
+    job.runtime_id = spec.at("runtimeId").str(ann.at(kAnnRuntimeId).str());
+    job.tf_image = spec.at("tfImage").str(ann.at(kAnnTfImage).str());
     job.scheduler_name = spec.at("schedulerName").str();
     if (spec.at("terminationPolicy").is_object()) {
       job.has_termination_policy = true;
@@ -113,6 +116,13 @@ TFJob from_json(const Json& j) {
     job.run_policy.scheduling.priority_class = sp.at("priorityClass").str();
     job.success_policy = spec.at("successPolicy").str();
     job.scheduler_name = rp.path("schedulingPolicy.schedulerName").str(spec.at("schedulerName").str());
+    job.runtime_id = ann.at(kAnnRuntimeId).str();
+    job.tf_image = ann.at(kAnnTfImage).str();
+    if (ann.at(kAnnChief).is_string()) {
+      auto parts = split(ann.at(kAnnChief).str(), ':');
+      job.has_termination_policy = parts.size() == 2;
+      if (job.has_termination_policy) { job.chief_name = parts[0]; job.chief_index = atoi(parts[1].c_str()); }
+    }
   }
   // status (both shapes tolerated)
   const Json& st = j.at("status");
@@ -161,6 +171,10 @@ Json to_json(const TFJob& job) {
   Json spec = Json::object();
   Json st = Json::object();
   if (job.is_v1alpha1()) {
+    if (j["metadata"].at("annotations").is_object()) {
+      for (const char* k : {kAnnRuntimeId, kAnnTfImage, kAnnChief}) j["metadata"]["annotations"].erase(k);
+      if (j["metadata"]["annotations"].size() == 0) j["metadata"].erase("annotations");
+    }
     if (!job.runtime_id.empty()) spec["runtimeId"] = job.runtime_id;
     if (!job.tf_image.empty()) spec["tfImage"] = job.tf_image;
     if (!job.scheduler_name.empty()) spec["schedulerName"] = job.scheduler_name;
@@ -194,6 +208,10 @@ Json to_json(const TFJob& job) {
     }
     if (rs.size()) st["replicaStatuses"] = rs;
   } else {
+    if (!job.runtime_id.empty()) j["metadata"]["annotations"][kAnnRuntimeId] = job.runtime_id;
+    if (!job.tf_image.empty()) j["metadata"]["annotations"][kAnnTfImage] = job.tf_image;
+    if (job.has_termination_policy)
+      j["metadata"]["annotations"][kAnnChief] = job.chief_name + ":" + std::to_string(job.chief_index);
     Json m = Json::object();
     for (auto& r : job.replicas) {
       Json o = Json::object();

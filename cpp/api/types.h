@@ -25,6 +25,10 @@ constexpr const char* kPortName = "tfjob-port";
 constexpr int kDefaultPort = 2222;
 constexpr const char* kFinalizer = "tfjob.kubeflow.org/cleanup";
 constexpr const char* kGPUResource = "amd.com/gpu";
+// v1alpha1-only spec fields carried as annotations by the v1 storage shape
+constexpr const char* kAnnRuntimeId = "tensorflow.org/v1alpha1-runtime-id";
+constexpr const char* kAnnTfImage = "tensorflow.org/v1alpha1-tf-image";
+constexpr const char* kAnnChief = "tensorflow.org/v1alpha1-termination-chief";
 
 // Canonical (upper-case) replica types. v1alpha1 uses them verbatim; v1 uses Title case.
 enum class RType { Master, Chief, PS, Worker, Evaluator, Unknown };

@@ -132,6 +132,20 @@ TEST(version_conversion_roundtrip) {
   CHECK_EQ(back.path("spec.tfReplicaSpecs.PS.replicas").as_int(), 1LL);
 }
 
+TEST(v1alpha1_only_fields_survive_v1_storage) {
+  Json a = J(R"({"apiVersion":"kubeflow.org/v1alpha1","kind":"TFJob","metadata":{"name":"x","namespace":"default"},
+      "spec":{"runtimeId":"ab12","tfImage":"tf:1.5","terminationPolicy":{"chief":{"replicaName":"WORKER","replicaIndex":1}},
+              "replicaSpecs":[{"replicas":2,"tfReplicaType":"WORKER","template":{"spec":{"containers":[{"name":"tensorflow"}]}}}]}})");
+  Json v1 = api::convert(a, "kubeflow.org/v1");
+  CHECK_EQ(v1.path("metadata.annotations").at(api::kAnnRuntimeId).str(), std::string("ab12"));
+  Json back = api::convert(v1, "kubeflow.org/v1alpha1");
+  CHECK_EQ(back.path("spec.runtimeId").str(), std::string("ab12"));
+  CHECK_EQ(back.path("spec.tfImage").str(), std::string("tf:1.5"));
+  CHECK_EQ(back.path("spec.terminationPolicy.chief.replicaName").str(), std::string("WORKER"));
+  CHECK_EQ(back.path("spec.terminationPolicy.chief.replicaIndex").as_int(), 1LL);
+  CHECK(!back.path("metadata.annotations").is_object() || !back.path("metadata.annotations").has(api::kAnnRuntimeId));
+}
+
 TEST(gen_name_and_tf_config) {
   api::TFJob job = api::from_json(v1_job(std::string(50, 'x'), 2, 1));
   api::set_defaults(job);

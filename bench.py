@@ -32,20 +32,34 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--graph", type=int, default=-1, help="capture step in a hipGraph (default: on for 1 GPU)")
     ap.add_argument("--fp8", type=int, default=0, help="transformer models: MX-fp8 forward GEMMs")
+    ap.add_argument("--via-operator", action="store_true",
+                    help="measure through a TFJob: tfk-cluster gang-schedules one pod per GPU (TF_CONFIG rendezvous)")
+    ap.add_argument("--tfjob-worker", action="store_true", help=argparse.SUPPRESS)  # a pod of --via-operator
     args = ap.parse_args()
+    if args.via_operator:
+        return run_via_operator(args)
     if not args.batch:
         args.batch = 256 if args.model.startswith("resnet") else (64 if args.model.startswith("bert") else 32)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    info = None
+    if args.tfjob_worker:
+        # one pod per GPU (HIP_VISIBLE_DEVICES pinned by the kubelet): the world comes from TF_CONFIG
+        from tensorflow_k8s_amd.parallel import cluster
+        info = cluster.resolve()
+        world, rank, local = info.world_size, info.rank, 0
     if args.gpus > 1 and world == 1:
         sys.exit("for --gpus > 1 launch with: python -m torch.distributed.run --nproc-per-node N "
                  "--master-addr 127.0.0.1 bench.py --gpus N")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     import torch.distributed as dist
-    if world > 1:
+    if world > 1 and info is not None:
+        from tensorflow_k8s_amd.parallel import cluster
+        cluster.init_process_group(info, "nccl", timeout_s=300, device_id=dev)
+    elif world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
@@ -79,9 +93,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-step device timestamps (no host sync inside the timed loop) for the median / p90
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         runner.step()
+        evs[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -92,6 +110,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     ms = dt / args.steps * 1000.0
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    dist_ms = {"median": round(step_ms[len(step_ms) // 2], 3),
+               "p90": round(step_ms[min(len(step_ms) - 1, int(0.9 * len(step_ms)))], 3),
+               "min": round(step_ms[0], 3), "max": round(step_ms[-1], 3)}
+    per_rank = [ms]
+    if world > 1:
+        g = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(g, torch.tensor([dt / args.steps * 1000.0], dtype=torch.float64, device=dev))
+        per_rank = [round(float(x.item()), 3) for x in g]
     gb = args.batch * world
     value = gb / (ms / 1000.0)
     loss = runner.last_loss()
@@ -101,8 +128,10 @@ def main():
         print(json.dumps({
             "metric": f"{args.model} training throughput (whole node)", "value": round(toks / (ms / 1000.0), 1),
             "unit": "tokens/sec", "sequences_per_sec": round(value, 2), "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16+mxfp8-fwd" if args.fp8 else "bf16",
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "step_ms": dist_ms, "per_rank_ms": per_rank,
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": _token_baseline(args.model, toks / (ms / 1000.0), world),
+            "dtype": "bf16+mxfp8-fwd" if args.fp8 else "bf16",
             "data": "synthetic token ids, random-init weights",
             "config": {"model": args.model, "global_batch": gb, "seq_len": seq, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (RCCL all-reduce)",
@@ -115,7 +144,8 @@ def main():
             "metric": ("images/sec (whole node) ResNet-50 TFJob at 1/2/4/8 MI355X workers" if is_r50
                        else f"{args.model} images/sec (whole node)"),
             "value": round(value, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "step_ms": dist_ms, "per_rank_ms": per_rank,
+            "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / base, 4) if base else None, "dtype": "bf16",
             "data": "synthetic (on-device ImageNet-shaped 224x224x3 bf16 batch, random-init weights)",
             "config": {"model": args.model, "global_batch": gb, "seq_len": None, "per_gpu_batch": args.batch,
@@ -125,6 +155,54 @@ def main():
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_via_operator(args) -> int:
+    """The headline metric measured the way BASELINE.json names it -- as a TFJob: start the native
+    control plane (tfk-cluster: apiserver + operator + gang scheduler + kubelet), submit a TFJob of
+    N one-GPU pods (Chief + N-1 Workers, amd.com/gpu: 1 each), and report the chief's JSON line.
+    This process never initialises HIP; every GPU process is a kubelet-spawned pod."""
+    import tempfile
+
+    from tensorflow_k8s_amd.control.client import LocalCluster, tfjob_condition
+    n = max(1, args.gpus)
+    root = os.path.dirname(os.path.abspath(__file__))
+    cmd = ["python3", os.path.join(root, "bench.py"), "--tfjob-worker", "--gpus", str(n), "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--model", args.model, "--bucket-mb", str(args.bucket_mb), "--graph",
+           str(args.graph), "--fp8", str(args.fp8)] + (["--batch", str(args.batch)] if args.batch else [])
+
+    def rs(k):
+        return {"replicas": k, "restartPolicy": "Never", "template": {"spec": {"containers": [{
+            "name": "tensorflow", "image": "tfk/runtime", "command": cmd,
+            "env": [{"name": "PYTHONPATH", "value": root}],
+            "resources": {"limits": {"amd.com/gpu": 1}}}]}}}
+    specs = {"Chief": rs(1)}
+    if n > 1:
+        specs["Worker"] = rs(n - 1)
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": f"bench-{args.model}", "namespace": "default"},
+           "spec": {"tfReplicaSpecs": specs, "runPolicy": {"backoffLimit": 0, "cleanPodPolicy": "None"}}}
+    with LocalCluster(gpus=n, root_dir=tempfile.mkdtemp(prefix="tfk-bench-")) as c:
+        c.client.create(job)
+        j = c.client.wait_tfjob(job["metadata"]["name"], timeout=1800)
+        log = c.client.logs(f"bench-{args.model}-chief-0")
+        if tfjob_condition(j) != "Succeeded":
+            sys.stderr.write(log[-4000:] + "\n")
+            raise SystemExit(f"bench TFJob ended {tfjob_condition(j)}: {j.get('status')}")
+    line = [l for l in log.splitlines() if l.startswith("{") and '"metric"' in l][-1]
+    out = json.loads(line)
+    out["config"]["launcher"] = "TFJob via tfk-cluster (operator + gang scheduler + kubelet), one pod per GPU"
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+def _token_baseline(model: str, value: float, world: int):
+    """value / the stock PyTorch comparator (tools/stock_transformer.py, profiles/comparators.json)."""
+    try:
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "comparators.json")) as f:
+            v = json.load(f).get(f"{model.replace('-', '_')}_bf16_stock_pytorch_1gpu_tok_s")
+        return round(value / (v * world), 4) if v else None
+    except Exception:
+        return None
 
 
 def _baseline(world: int):
@@ -140,4 +218,4 @@ def _baseline(world: int):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -56,19 +56,29 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--compile", type=int, default=0)
+    ap.add_argument("--precision", default="autocast", choices=["autocast", "bf16"],
+                    help="autocast: f32 weights under bf16 autocast; bf16: bf16 weights + activations")
+    ap.add_argument("--fused", type=int, default=1, help="fused (single-kernel) SGD")
     a = ap.parse_args()
     dev = torch.device("cuda")
     m = ResNet50().to(dev).to(memory_format=torch.channels_last)
-    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+    if a.precision == "bf16":
+        m = m.to(torch.bfloat16)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5, **({"fused": True} if a.fused else {}))
     crit = nn.CrossEntropyLoss(label_smoothing=0.1)
     x = torch.randn(a.batch, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
+    if a.precision == "bf16":
+        x = x.to(torch.bfloat16)
     y = torch.randint(0, 1000, (a.batch,), device=dev)
     fwd = torch.compile(m) if a.compile else m
 
     def step():
         opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            loss = crit(fwd(x), y)
+        if a.precision == "autocast":
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = crit(fwd(x), y)
+        else:
+            loss = crit(fwd(x).float(), y)
         loss.backward()
         opt.step()
         return loss
@@ -81,7 +91,8 @@ def main():
         loss = step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
-    print(json.dumps({"comparator": "stock_pytorch_eager" + ("_compile" if a.compile else ""), "batch": a.batch,
+    print(json.dumps({"comparator": f"stock_pytorch_{a.precision}" + ("_fusedsgd" if a.fused else "") +
+                      ("_compile" if a.compile else ""), "batch": a.batch,
                       "ms_per_step": round(dt * 1000, 3), "img_s": round(a.batch / dt, 2),
                       "loss": float(loss)}))
 

@@ -30,7 +30,11 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: 256 ResNet, 64 BERT, 32 Transformer)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--comm-dtype", default="bf16", choices=["bf16", "f32"],
+                    help="gradient all-reduce wire dtype (bf16: half the xGMI bytes; f32 master update either way)")
     ap.add_argument("--graph", type=int, default=-1, help="capture step in a hipGraph (default: on for 1 GPU)")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="1 GPU: still run the RCCL gradient all-reduce (world-size-1 process group)")
     ap.add_argument("--fp8", type=int, default=0, help="transformer models: MX-fp8 forward GEMMs")
     ap.add_argument("--via-operator", action="store_true",
                     help="measure through a TFJob: tfk-cluster gang-schedules one pod per GPU (TF_CONFIG rendezvous)")
@@ -56,7 +60,13 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     import torch.distributed as dist
-    if world > 1 and info is not None:
+
+    from tensorflow_k8s_amd.parallel import comm
+    if world > 1 or args.force_comm:
+        comm.enable_transport_log()
+    if args.force_comm and world == 1:
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29541", rank=0, world_size=1, device_id=dev)
+    elif world > 1 and info is not None:
         from tensorflow_k8s_amd.parallel import cluster
         cluster.init_process_group(info, "nccl", timeout_s=300, device_id=dev)
     elif world > 1:
@@ -79,7 +89,8 @@ def main():
     else:
         opt = AdamW(model.arena, lr=1e-4, b2=0.98, eps=1e-9, weight_decay=0.0)
         opt_name = "Adam (fused HIP)"
-    strat = MultiWorkerMirroredStrategy(model.arena, bucket_mb=args.bucket_mb)
+    strat = MultiWorkerMirroredStrategy(model.arena, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype,
+                                        force=args.force_comm)
     strat.configure_optimizer(opt)
     strat.broadcast_parameters()
     batch = synthetic_batch(model, args.batch, dev, seed=1000 + rank)
@@ -121,6 +132,10 @@ def main():
         per_rank = [round(float(x.item()), 3) for x in g]
     gb = args.batch * world
     value = gb / (ms / 1000.0)
+    comm_cfg = {"comm_dtype": args.comm_dtype, "bucket_mb": args.bucket_mb, "buckets": len(strat.buckets),
+                "wire_mb_per_step": round(strat.wire_bytes() / 2**20, 1) if strat.enabled else 0.0}
+    if strat.enabled:
+        comm_cfg["rccl_transport"] = comm.transport_summary()
     loss = runner.last_loss()
     if rank == 0 and not is_cnn:
         seq = model.cfg.seq_len if args.model.startswith("bert") else model.cfg.tgt_len
@@ -135,7 +150,7 @@ def main():
             "data": "synthetic token ids, random-init weights",
             "config": {"model": args.model, "global_batch": gb, "seq_len": seq, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (RCCL all-reduce)",
-                       "optimizer": opt_name, "hipgraph": use_graph},
+                       "optimizer": opt_name, "hipgraph": use_graph, "comm": comm_cfg},
             "loss": loss}), flush=True)
     elif rank == 0:
         is_r50 = args.model == "resnet50"
@@ -150,10 +165,10 @@ def main():
             "data": "synthetic (on-device ImageNet-shaped 224x224x3 bf16 batch, random-init weights)",
             "config": {"model": args.model, "global_batch": gb, "seq_len": None, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (RCCL all-reduce)",
-                       "optimizer": opt_name, "hipgraph": use_graph},
+                       "optimizer": opt_name, "hipgraph": use_graph, "comm": comm_cfg},
             "loss": loss,
         }), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -168,7 +183,7 @@ def run_via_operator(args) -> int:
     n = max(1, args.gpus)
     root = os.path.dirname(os.path.abspath(__file__))
     cmd = ["python3", os.path.join(root, "bench.py"), "--tfjob-worker", "--gpus", str(n), "--steps", str(args.steps),
-           "--warmup", str(args.warmup), "--model", args.model, "--bucket-mb", str(args.bucket_mb), "--graph",
+           "--warmup", str(args.warmup), "--model", args.model, "--bucket-mb", str(args.bucket_mb), "--comm-dtype", args.comm_dtype, "--graph",
            str(args.graph), "--fp8", str(args.fp8)] + (["--batch", str(args.batch)] if args.batch else [])
 
     def rs(k):

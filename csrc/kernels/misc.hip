@@ -89,11 +89,31 @@ __global__ void transpose_f32_kernel(const float* __restrict__ in, float* __rest
   }
 }
 
+// Casts (master refresh, MWMS bf16 wire buckets): 4 elements per lane (16-B f32 / 8-B bf16
+// accesses) when both pointers are aligned for it; the launcher runs the scalar form otherwise.
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n) {
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) y[i] = f2bf(x[i]);
 }
 __global__ void cast_bf16_f32_kernel(const bf16* __restrict__ x, float* __restrict__ y, long long n) {
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) y[i] = bf2f(x[i]);
+}
+__global__ void cast4_f32_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n4) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long long)gridDim.x * NT) {
+    const f32x4 v = ((const f32x4*)x)[i];
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+    ((bf16x4*)y)[i] = o;
+  }
+}
+__global__ void cast4_bf16_f32_kernel(const bf16* __restrict__ x, float* __restrict__ y, long long n4) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long long)gridDim.x * NT) {
+    const bf16x4 v = ((const bf16x4*)x)[i];
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = bf2f(v[e]);
+    ((f32x4*)y)[i] = o;
+  }
 }
 
 // Uniform [lo, hi) bf16 with channel padding: tensor [rows][Cpad], channels >= Creal are zero.
@@ -221,11 +241,23 @@ int tfk_transpose_f32(const float* in, float* out, int rows, int cols, hipStream
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t s) {
-  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n);
+  long long done = 0;
+  if ((((uintptr_t)x & 15) | ((uintptr_t)y & 7)) == 0 && n >= 4) {
+    done = n / 4 * 4;
+    hipLaunchKernelGGL(cast4_f32_bf16_kernel, dim3(grid_for(n / 4)), dim3(NT), 0, s, x, y, n / 4);
+  }
+  if (done < n)
+    hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n - done)), dim3(NT), 0, s, x + done, y + done, n - done);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_cast_bf16_f32(const bf16* x, float* y, long long n, hipStream_t s) {
-  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n);
+  long long done = 0;
+  if ((((uintptr_t)x & 7) | ((uintptr_t)y & 15)) == 0 && n >= 4) {
+    done = n / 4 * 4;
+    hipLaunchKernelGGL(cast4_bf16_f32_kernel, dim3(grid_for(n / 4)), dim3(NT), 0, s, x, y, n / 4);
+  }
+  if (done < n)
+    hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n - done)), dim3(NT), 0, s, x + done, y + done, n - done);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_synth_uniform(bf16* y, long long rows, int Creal, int Cpad, float lo, float hi, unsigned long long seed,

@@ -102,3 +102,10 @@ def cast_f32_bf16(x: torch.Tensor, y: torch.Tensor) -> None:
         y.copy_(x)
         return
     lib().cast_f32_bf16(x, y)
+
+
+def cast_bf16_f32(x: torch.Tensor, y: torch.Tensor) -> None:
+    if not on_gpu(x):
+        y.copy_(x)
+        return
+    lib().cast_bf16_f32(x, y)

@@ -6,8 +6,19 @@ so a bucket is a contiguous slice -> one ``all_reduce`` per bucket with no flatt
 are launched the moment the backward pass has written their last gradient (executor readiness
 callbacks), so ring all-reduce over xGMI overlaps the remaining backward compute; RCCL runs on its
 own internal stream and the compute stream only waits on it right before the optimizer.
-Bucket size default 32 MiB: large enough to amortise RCCL launch/latency on the 7x153 GB/s xGMI
-mesh, small enough that the last bucket's exposed tail is short.
+
+* Launch order is the bucket order on every rank (a bucket that completes early waits for its
+  predecessors), so all ranks issue the same collective sequence whatever the readiness callbacks
+  do -- a mismatched order would pair different buckets in the ring and hang or corrupt.
+* ``comm_dtype=torch.bfloat16`` puts bf16 on the wire: the bucket is packed f32->bf16 by a HIP
+  cast kernel on the compute stream (the RCCL stream waits on it), all-reduced in bf16 (half the
+  xGMI bytes of f32: 51 MB instead of 102 MB per ResNet-50 step) and unpacked into the f32 arena
+  right after the wait; the 1/world mean stays in the fused optimizer's grad_scale.
+* Bucket size default 32 MiB of f32 gradient: large enough to amortise RCCL launch/latency on the
+  7x153 GB/s point-to-point xGMI mesh, small enough that the last bucket's exposed tail is short.
+* ``force=True`` runs the collectives even with world size 1 (exercises the RCCL path -- and its
+  hipGraph capture -- on a single-GPU box).
+* Everything here is hipGraph-capturable: no host synchronisation, all buffers pre-allocated.
 """
 from __future__ import annotations
 
@@ -15,6 +26,20 @@ import torch
 import torch.distributed as dist
 
 from ..runtime.arena import ParamArena
+
+_COMM_DTYPES = {"f32": torch.float32, "fp32": torch.float32, "float32": torch.float32,
+                "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+
+
+def comm_dtype_of(x) -> torch.dtype:
+    if isinstance(x, torch.dtype):
+        if x not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"MWMS comm_dtype must be float32 or bfloat16, got {x}")
+        return x
+    try:
+        return _COMM_DTYPES[str(x).lower()]
+    except KeyError:
+        raise ValueError(f"MWMS comm_dtype must be f32|bf16, got {x!r}") from None
 
 
 class Bucket:
@@ -30,22 +55,27 @@ class Bucket:
 class MultiWorkerMirroredStrategy:
     name = "mwms"
 
-    def __init__(self, arena: ParamArena, group=None, bucket_mb: float = 32.0, comm_dtype: torch.dtype = torch.float32):
+    def __init__(self, arena: ParamArena, group=None, bucket_mb: float = 32.0, comm_dtype=torch.float32,
+                 force: bool = False):
         self.arena = arena
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if self.world > 1 else 0
-        self.comm_dtype = comm_dtype
+        inited = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if inited else 1
+        self.rank = dist.get_rank(group) if inited else 0
+        self.comm_dtype = comm_dtype_of(comm_dtype)
         self.buckets: list[Bucket] = []
         self.bucket_of: dict[int, Bucket] = {}
         self._build(int(bucket_mb * (1 << 20)) // 4)
-        self.enabled = self.world > 1
+        self.enabled = self.world > 1 or (force and inited)
+        self._next = 0  # index of the next bucket to launch (in-order launch)
+        self.wire = None
+        if self.enabled and self.comm_dtype != torch.float32:
+            self.wire = torch.empty(arena.numel, dtype=self.comm_dtype, device=arena.grad.device)
         if self.enabled:
             arena.on_grad_ready(self._on_ready)
 
     def _build(self, elems_per_bucket: int):
         params = sorted(self.arena.params, key=lambda p: p.offset)
-        cur, start, n = [], None, 0
         regions = [self.arena.decay_region(), self.arena.nodecay_region()]
         for lo, hi in regions:
             grp = [p for p in params if lo <= p.offset < hi]
@@ -69,48 +99,74 @@ class MultiWorkerMirroredStrategy:
         for p in params:
             self.bucket_of[p.index] = b
 
+    def wire_bytes(self) -> int:
+        """Bytes one rank contributes to the gradient all-reduce per step."""
+        return sum(b.end - b.start for b in self.buckets) * (2 if self.comm_dtype == torch.bfloat16 else 4)
+
     # ------------------------------------------------------------------ per step
     def begin_step(self):
         for b in self.buckets:
             b.pending, b.work, b.launched = b.nparams, None, False
+        self._next = 0
 
     def _on_ready(self, p):
         b = self.bucket_of.get(p.index)
         if b is None:
             return
         b.pending -= 1
-        if b.pending == 0 and not b.launched:
-            self._launch(b)
+        # launch every leading bucket whose gradients are complete, in bucket order
+        while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
+            self._launch(self.buckets[self._next])
+            self._next += 1
 
     def _launch(self, b: Bucket):
         b.launched = True
         view = self.arena.grad[b.start:b.end]
+        if self.wire is not None:
+            from ..ops.optim import cast_f32_bf16
+            w = self.wire[b.start:b.end]
+            cast_f32_bf16(view, w)
+            view = w
         b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def finish_step(self):
-        """Launch stragglers, wait for every bucket (compute stream waits on the RCCL stream)."""
+        """Launch stragglers (in order), wait for every bucket (compute stream waits on the RCCL
+        stream), unpack bf16 wire buckets into the f32 arena."""
         if not self.enabled:
             return
-        for b in self.buckets:
-            if not b.launched:
-                self._launch(b)
+        while self._next < len(self.buckets):
+            self._launch(self.buckets[self._next])
+            self._next += 1
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
+                if self.wire is not None:
+                    from ..ops.optim import cast_bf16_f32
+                    cast_bf16_f32(self.wire[b.start:b.end], self.arena.grad[b.start:b.end])
 
     def configure_optimizer(self, opt) -> None:
         opt.grad_scale = 1.0 / self.world
 
     # ------------------------------------------------------------------ state sync
     def broadcast_parameters(self, src: int = 0):
-        if self.world <= 1:
+        """Chief's master weights + non-trainable buffers everywhere: the arena is one broadcast,
+        the buffers (BN moving statistics, ...) are coalesced into one flat tensor per dtype."""
+        if not self.enabled:
             return
         dist.broadcast(self.arena.master, src, group=self.group)
+        by_dtype: dict = {}
         for b in self.arena.buffers:
-            dist.broadcast(b.tensor, src, group=self.group)
+            by_dtype.setdefault((b.tensor.dtype, b.tensor.device), []).append(b.tensor)
+        for ts in by_dtype.values():
+            flat = torch.cat([t.reshape(-1) for t in ts])
+            dist.broadcast(flat, src, group=self.group)
+            o = 0
+            for t in ts:
+                t.copy_(flat[o:o + t.numel()].view_as(t))
+                o += t.numel()
         self.arena.refresh_compute()
 
     def all_reduce_metrics(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
+        if self.enabled:
             dist.all_reduce(t, group=self.group)
         return t

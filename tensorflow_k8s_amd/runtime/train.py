@@ -65,6 +65,7 @@ def parse_args(argv=None):
     ap.add_argument("--ps-transport", default="gloo", choices=["gloo", "rccl"],
                     help="gloo: ps tasks on CPU (sync/async); rccl: ps tasks own a GPU, RCCL reduce/broadcast (sync)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--comm-dtype", default="f32", choices=["f32", "bf16"], help="MWMS gradient all-reduce wire dtype")
     ap.add_argument("--device", default="auto", choices=["auto", "cpu", "cuda"])
     ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph (1 GPU, MWMS)")
     ap.add_argument("--checkpoint-dir", default="")
@@ -193,7 +194,7 @@ def run_worker(args, info, dev) -> int:
         strat.configure_optimizer(opt)
     else:
         from ..parallel.mwms import MultiWorkerMirroredStrategy
-        strat = MultiWorkerMirroredStrategy(model.arena, bucket_mb=args.bucket_mb)
+        strat = MultiWorkerMirroredStrategy(model.arena, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype)
         strat.configure_optimizer(opt)
     nworkers = max(1, len(info.worker_ranks))
     wrank = info.worker_ranks.index(info.rank) if info.rank in info.worker_ranks else 0

@@ -15,6 +15,7 @@ int tfk_gemm_launch(tfk::GemmParams p, int bm, int bn, int amode, int bmode, int
 int tfk_gemm_splits(int K, int splits);
 void tfk_gemm_set_persist(int on);
 void tfk_gemm_set_engine(int e);
+void tfk_g4_set_shortk(int on);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_probe(const int*, const int*, const int*, const int*, float*, hipStream_t);
 int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, hipStream_t s);
@@ -244,6 +245,7 @@ int64_t gemm_splits(int K, int splits) { return tfk_gemm_splits(K, splits); }
 // A/B switch for the persistent GEMM grid (tools/op_profile.py); default on.
 void gemm_set_persist(int on) { tfk_gemm_set_persist(on); }
 void gemm_set_engine(int e) { tfk_gemm_set_engine(e); }
+void gemm_set_shortk(int on) { tfk_g4_set_shortk(on); }
 
 void mx_probe(torch::Tensor X, torch::Tensor Y, torch::Tensor sx, torch::Tensor sy, torch::Tensor D) {
   for (auto* t : {&X, &Y}) { need(*t, at::kInt, "probe operand"); need_numel(*t, 64 * 8, "probe operand"); }
@@ -580,6 +582,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_splits", &gemm_splits);
   m.def("gemm_set_persist", &gemm_set_persist);
   m.def("gemm_set_engine", &gemm_set_engine);
+  m.def("gemm_set_shortk", &gemm_set_shortk);
   m.def("mx_quant", &mx_quant);
   m.def("mx_probe", &mx_probe);
   m.def("gemm_mxfp8", &gemm_mxfp8);

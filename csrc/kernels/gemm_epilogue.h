@@ -47,7 +47,7 @@ __device__ __forceinline__ long long resid_row(const GemmParams& p, long long mo
   return (n * p.rs_p + h / p.rs_sh) * p.rs_q + w / p.rs_sw;
 }
 
-template <int BM, int BN, int NT, int WM, int EPI>
+template <int BM, int BN, int NT, int WM, int EPI, int BNRG = 0>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[BM / WM / 16][BN / (NT / 64 / WM) / 16],
                                               char* smem, int m0, int n0, int bz) {
   constexpr int NW = NT / 64, WN = NW / WM;
@@ -168,7 +168,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     // always-valid addresses (absent tensors alias y / C) so no per-element branch splits them.
     const bool tile_fast = (m0 + BM <= p.M) && (n0 + BN <= p.N) && ((p.ldc & 7) == 0);
     constexpr int NIT = TOT / NT;
-    constexpr int G = bnr ? 1 : (EPI == EPI_BF16_EXT ? (NIT < 2 ? NIT : 2) : (NIT < 4 ? NIT : 4));
+    // BNR groups: 1 chunk in flight (BNRG template override); G=2 on <= 128x128 tiles compiled
+    // spill-free (137 VGPRs) but a ResNet-50 step then faulted -- not yet root-caused, kept off
+    constexpr int GB = BNRG > 0 ? BNRG : 1;
+    constexpr int G = bnr ? (NIT < GB ? NIT : GB) : (EPI == EPI_BF16_EXT ? (NIT < 2 ? NIT : 2) : (NIT < 4 ? NIT : 4));
     if (tile_fast) {
       const bf16* resid_b = p.resid ? (const bf16*)p.resid : (const bf16*)p.C;
       const bf16* dsrc_b = (EPI == EPI_BF16_EXT && p.dact_src) ? (const bf16*)p.dact_src : (const bf16*)p.C;
@@ -192,7 +195,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           rok[g] = p.resid && mr >= 0;
           mlog[g] = m; nlog[g] = n;
           cv[g] = *(const bf16x8*)(Cs + row * LDC_S + cc * 8);
-          rr[g] = *(const bf16x8*)(resid_b + (rok[g] ? bz * p.sC + mr * p.ldc + n : off[g]));
+          // off the residual's sub-sampling lattice the (unused) load reads C itself: resid is the
+          // smaller lattice tensor there, so resid + off[g] could run past its allocation
+          rr[g] = *(const bf16x8*)(rok[g] ? resid_b + bz * p.sC + mr * p.ldc + n : (const bf16*)p.C + off[g]);
           if constexpr (EPI == EPI_BF16_EXT) zv[g] = *(const bf16x8*)(dsrc_b + off[g]);
           if constexpr (bnr) {
             yv[g] = *(const bf16x8*)(y_b + off[g]);

@@ -169,14 +169,22 @@ struct Loader {
 template <int BM, int BN>
 constexpr int nwaves() { return (BM / 64) * (BN / 64); }
 
-template <int BM, int BN, int AM, int BMD, int EPI>
-__global__ __launch_bounds__((nwaves<BM, BN>() * 64), ((BM * BN <= 128 * 128) ? 2 : 1)) void g4_kernel(GemmParams p) {
+// OCC = 4: short-K variant for blocks that own exactly ONE K-tile (K <= 64 per split: the 1x1
+// convs of ResNet stage 2, M=802816 x N=256 x K=64). Such a block is load -> 32 MFMAs -> epilogue
+// with nothing to pipeline, so latency is hidden by co-resident blocks instead: one LDS stage
+// (36 KiB with the epilogue image) and <= 128 VGPRs put 4 blocks (16 waves) on a CU instead of 2.
+template <int BM, int BN>
+constexpr int occ_default() { return (BM * BN <= 128 * 128) ? 2 : 1; }
+
+template <int BM, int BN, int AM, int BMD, int EPI, int OCC = occ_default<BM, BN>()>
+__global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmParams p) {
   constexpr int NW = nwaves<BM, BN>(), NTH = NW * 64, WGM = BM / 64, WGN = BN / 64;
   constexpr int LBM = BMD == 2 ? CONV_WGRAD : BMD;  // B_CONV_WGRAD (= 2 in the B-mode numbering)
   constexpr bool AKO = (AM == KOUT), BKO = (LBM == KOUT || LBM == CONV_WGRAD);
   constexpr int WTM = 64, WTN = 64, FM = 4, FN = 4;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int MAIN = 2 * STAGE, EPIB = epi_lds_bytes<BM, BN, WGM>();
+  constexpr bool SHORTK = OCC > occ_default<BM, BN>();  // host guarantees kt_per_split == 1
+  constexpr int MAIN = (SHORTK ? 1 : 2) * STAGE, EPIB = epi_lds_bytes<BM, BN, WGM>();
   __shared__ __attribute__((aligned(16))) char smem[MAIN > EPIB ? MAIN : EPIB];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -270,7 +278,7 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), ((BM * BN <= 128 * 128) ? 
     }
   }
   __syncthreads();
-  gemm_epilogue<BM, BN, NTH, WGM, EPI>(p, acc, smem, m0, n0, bz);
+  gemm_epilogue<BM, BN, NTH, WGM, EPI, (SHORTK ? 1 : 0)>(p, acc, smem, m0, n0, bz);
 }
 
 }  // namespace g4
@@ -305,6 +313,23 @@ extern "C" int tfk_g4_ok(const GemmParams& p, int amode, int bmode) {
 // 2-wave tiles for 64-wide operands (Cout = 64 weight gradients, 64-channel dgrads)
 #define TFK_G4_NARROW(AM_, BM2_, EPI_) TFK_G4_CASE(128, 64, AM_, BM2_, EPI_) TFK_G4_CASE(64, 128, AM_, BM2_, EPI_)
 
+#define TFK_G4_SHORTK(AM_, BM2_, EPI_)                                                               \
+  if (amode == AM_ && bmode == BM2_ && epi == EPI_) {                                               \
+    hipLaunchKernelGGL((g4::g4_kernel<128, 128, AM_, BM2_, EPI_, 4>), dim3(tiles, batch, splits),    \
+                       dim3(g4::nwaves<128, 128>() * 64), 0, stream, p);                            \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                                \
+  }
+
+static int g_shortk = -1;
+static bool shortk_on() {
+  if (g_shortk < 0) {
+    const char* e = getenv("TFK_G4_SHORTK");
+    g_shortk = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_shortk == 1;
+}
+extern "C" void tfk_g4_set_shortk(int on) { g_shortk = on ? 1 : 0; }
+
 static void fast_div(unsigned d, unsigned* mul, int* shift) {
   int s = 0;
   while ((1ull << s) < d) ++s;
@@ -321,6 +346,14 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
   if (bmode == 2) {
     fast_div((unsigned)p.Q, &p.fd_q_mul, &p.fd_q_shift);
     fast_div((unsigned)(p.P * p.Q), &p.fd_pq_mul, &p.fd_pq_shift);
+  }
+  // one K-tile per block: the 4-blocks-per-CU single-stage instantiations (TFK_G4_SHORTK=1: on)
+  if (p.kt_per_split == 1 && bm == 128 && bn == 128 && shortk_on()) {
+    TFK_G4_SHORTK(0, 0, EPI_BF16)
+    TFK_G4_SHORTK(0, 1, EPI_BF16)
+    TFK_G4_SHORTK(0, 1, EPI_BF16_BNR)
+    TFK_G4_SHORTK(2, 0, EPI_BF16)
+    TFK_G4_SHORTK(2, 0, EPI_BF16_BNR)
   }
   TFK_G4_TILES(0, 0, EPI_BF16)
   TFK_G4_TILES(0, 0, EPI_F32)

@@ -22,9 +22,19 @@ Two transports:
   -> reply shard f32; DONE=2; FETCH=3 (reply master + slots, for checkpoints); LOAD=4 (payload
   master + slots, restore); PULL=5 (reply master shard).
 * ``transport="rccl"`` (ps tasks own a GPU, e.g. BASELINE's PS=2/worker=6 on one 8xMI355X node;
-  sync only): per step and shard one RCCL ``reduce`` of the gradient shard onto its owner over
-  xGMI, the owner's fused HIP optimizer update, one ``broadcast`` of the updated shard back. The
-  schedule is identical on every rank (steps and checkpoint steps are known), so no control
+  sync only), bucketed and overlapped (``CollectivePlan``):
+  - each shard is cut into parameter-aligned buckets (<= bucket_mb); every shard s has two RCCL
+    communicators over {its owner} + workers -- one for gradient ``reduce``, one for parameter
+    ``broadcast`` -- so a bucket's broadcast does not queue behind later buckets' reduces, and no
+    other ps task contributes zeros to s's traffic;
+  - workers launch the ``reduce`` of a bucket the moment backward has produced its last gradient
+    (arena readiness callbacks, in bucket order -- the same order on every rank), overlapping the
+    rest of backward, exactly like MWMS buckets;
+  - the owner zeroes ONLY its own shard's gradient, posts its buckets' reduces, and per bucket:
+    stream-waits for that reduce, runs the fused HIP optimizer on the bucket, posts its broadcast;
+    so early buckets are updated and shipped back while later ones are still being reduced;
+  - workers stream-wait for the broadcasts and refresh the bf16 compute copy.
+  The schedule is identical on every rank (steps and checkpoint steps are known), so no control
   messages are needed; for a checkpoint the owners ``send`` master + slots to the chief.
 """
 from __future__ import annotations
@@ -87,7 +97,7 @@ class ParameterServerStrategy:
     name = "ps"
 
     def __init__(self, arena: ParamArena, ps_ranks: list[int], worker_ranks: list[int], mode: str = "sync",
-                 group=None, transport: str = "gloo"):
+                 group=None, transport: str = "gloo", bucket_mb: float = 32.0):
         if mode not in ("sync", "async"):
             raise ValueError(f"ps mode must be sync|async, got {mode}")
         if transport not in ("gloo", "rccl"):
@@ -98,21 +108,43 @@ class ParameterServerStrategy:
         self.transport = transport
         self.rank = dist.get_rank()
         self.shards = shard_bounds(arena.numel, len(self.ps_ranks), _param_spans(arena))
+        self.plan = None
         if transport == "gloo":
             pin = arena.grad.is_cuda
             self._g = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
             self._p = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
+        else:
+            self.plan = CollectivePlan(arena, self.shards, self.ps_ranks, self.worker_ranks, bucket_mb)
+            arena.on_grad_ready(self._on_ready)
         self.step_count = 0
+        self._next = 0
+        self._red = []
 
     @property
     def num_workers(self) -> int:
         return len(self.worker_ranks)
 
     def begin_step(self):
-        pass
+        if self.plan is not None:
+            self.plan.reset()
+            self._next, self._red = 0, []
+
+    def _on_ready(self, p):
+        """Backward produced p's gradient: launch every leading complete bucket's reduce."""
+        pl = self.plan
+        b = pl.bucket_of.get(p.index)
+        if b is None:
+            return
+        pl.pending[b] -= 1
+        while self._next < len(pl.buckets) and pl.pending[self._next] <= 0:
+            self._red.append(pl.reduce(self._next, self.arena.grad))
+            self._next += 1
 
     def finish_step(self):
-        pass
+        if self.plan is not None:
+            while self._next < len(self.plan.buckets):
+                self._red.append(self.plan.reduce(self._next, self.arena.grad))
+                self._next += 1
 
     def configure_optimizer(self, opt) -> None:
         """The optimizer runs on the ps tasks; the worker-side instance only provides slot names
@@ -136,7 +168,11 @@ class ParameterServerStrategy:
         """Push local gradients, pull the updated parameters (replaces optimizer.step())."""
         a = self.arena
         if self.transport == "rccl":
-            collective_exchange(a, self.shards, self.ps_ranks, self.group)
+            self.finish_step()  # (no-op when the runner already called it)
+            works = [self.plan.broadcast(i, a.master) for i in range(len(self.plan.buckets))]
+            for w in self._red + works:
+                w.wait()  # stream waits: the next forward is ordered after the pulled parameters
+            self._red = []
             a.refresh_compute()
             self.step_count += 1
             if opt is not None:
@@ -205,16 +241,66 @@ class ParameterServerStrategy:
         return t
 
 
-def collective_exchange(arena: ParamArena, shards, ps_ranks, group=None, update=None):
-    """One synchronous PS step over RCCL, executed identically by every rank: reduce each gradient
-    shard onto its owner, (owner updates), broadcast the shard back. Non-owners' buffers are
-    their local gradients (workers) or zeros (ps tasks)."""
-    for (lo, hi), ps in zip(shards, ps_ranks):
-        dist.reduce(arena.grad[lo:hi], ps, op=dist.ReduceOp.SUM, group=group)
-    if update is not None:
-        update()
-    for (lo, hi), ps in zip(shards, ps_ranks):
-        dist.broadcast(arena.master[lo:hi], ps, group=group)
+class CollectivePlan:
+    """Bucket plan + per-shard communicators of the collective PS transport (same on every rank).
+
+    Buckets are parameter-aligned slices of the arena, never crossing a shard boundary or the
+    decay/no-decay boundary (so an optimizer region per bucket is valid, LAMB's per-tensor trust
+    ratio included), listed in arena order = backward-completion order."""
+
+    def __init__(self, arena: ParamArena, shards, ps_ranks, worker_ranks, bucket_mb: float = 32.0):
+        self.arena, self.shards, self.ps_ranks = arena, list(shards), list(ps_ranks)
+        cap = max(ALIGN, int(bucket_mb * (1 << 20)) // 4)
+        cuts = sorted({lo for lo, _ in shards} | {hi for _, hi in shards} | set(arena.decay_region())
+                      | set(arena.nodecay_region()))
+        params = sorted(arena.params, key=lambda p: p.offset)
+        self.buckets: list[tuple[int, int, int]] = []  # (lo, hi, shard)
+        self.bucket_of: dict[int, int] = {}
+        self._nparams: list[int] = []
+        for lo_c, hi_c in zip(cuts, cuts[1:]):
+            if hi_c <= lo_c:
+                continue
+            shard = next(i for i, (a, b) in enumerate(shards) if a <= lo_c < b)
+            start, cur = lo_c, []
+            for p in params:
+                if not (lo_c <= p.offset < hi_c):
+                    continue
+                cur.append(p)
+                end = min(hi_c, p.offset + ((p.numel + ALIGN - 1) // ALIGN) * ALIGN)
+                if end - start >= cap:
+                    self._add(start, end, shard, cur)
+                    start, cur = end, []
+            if cur:
+                self._add(start, hi_c, shard, cur)
+        self.pending = list(self._nparams)
+        # two communicators per shard (reduce / broadcast): every rank creates every group, in order
+        self.red_groups, self.bc_groups = [], []
+        for owner in self.ps_ranks:
+            ranks = sorted({owner} | set(worker_ranks))
+            self.red_groups.append(dist.new_group(ranks))
+            self.bc_groups.append(dist.new_group(ranks))
+
+    def _add(self, lo, hi, shard, params):
+        i = len(self.buckets)
+        self.buckets.append((lo, hi, shard))
+        self._nparams.append(len(params))
+        for p in params:
+            self.bucket_of[p.index] = i
+
+    def reset(self):
+        self.pending = list(self._nparams)
+
+    def buckets_of(self, shard: int) -> list[int]:
+        return [i for i, b in enumerate(self.buckets) if b[2] == shard]
+
+    def reduce(self, i: int, grad: torch.Tensor):
+        lo, hi, s = self.buckets[i]
+        return dist.reduce(grad[lo:hi], self.ps_ranks[s], op=dist.ReduceOp.SUM, group=self.red_groups[s],
+                           async_op=True)
+
+    def broadcast(self, i: int, master: torch.Tensor):
+        lo, hi, s = self.buckets[i]
+        return dist.broadcast(master[lo:hi], self.ps_ranks[s], group=self.bc_groups[s], async_op=True)
 
 
 class ParameterServer:
@@ -297,17 +383,36 @@ class ParameterServer:
 
     # ------------------------------------------------------------------ rccl transport
     def serve_collective(self, start_step: int, total_steps: int, checkpoint_every: int = 0,
-                         chief: int = 0, final_checkpoint: bool = True) -> int:
-        """Mirror of the workers' step schedule over RCCL: initial broadcast, then per step
-        reduce -> fused optimizer on the owned shard -> broadcast; ship master + slots to the
-        chief at its checkpoint steps."""
+                         chief: int = 0, final_checkpoint: bool = True, bucket_mb: float = 32.0) -> int:
+        """Mirror of the workers' step schedule over RCCL (CollectivePlan): initial broadcast, then
+        per step: zero the own shard's gradient, post the own buckets' reduces, and per bucket
+        stream-wait -> fused optimizer on that bucket -> post its broadcast. Ships master + slots to
+        the chief at its checkpoint steps."""
         a = self.arena
-        a.grad.zero_()
+        if self.opt._dev is not None:
+            raise RuntimeError("collective PS updates per bucket with host schedules (no device schedule)")
+        # groups first: the workers create theirs in ParameterServerStrategy.__init__, before pull()
+        plan = CollectivePlan(a, self.shards, self.ps_ranks, self.worker_ranks, bucket_mb)
         for (lo, hi), ps in zip(self.shards, self.ps_ranks):
             dist.broadcast(a.master[lo:hi], ps, group=self.group)
+        me = self.ps_ranks.index(dist.get_rank())
+        mine = plan.buckets_of(me)
         for step in range(start_step + 1, total_steps + 1):
-            a.grad.zero_()  # zero contribution to every shard's reduce (reduce may scribble on non-root inputs)
-            collective_exchange(a, self.shards, self.ps_ranks, self.group, update=self.opt.step)
+            a.grad[self.lo:self.hi].zero_()  # the owner's own (zero) contribution to its reduces
+            reds = [plan.reduce(i, a.grad) for i in mine]
+            bcs = []
+            n0 = self.opt.step_count
+            for k, (i, w) in enumerate(zip(mine, reds)):
+                w.wait()
+                lo, hi, _ = plan.buckets[i]
+                self.opt.region = (lo, hi)
+                self.opt.step()
+                if k + 1 < len(mine):
+                    self.opt.step_count = n0  # one global step: advance once, after the last bucket
+                bcs.append(plan.broadcast(i, a.master))
+            for w in bcs:
+                w.wait()
+            self.opt.region = (self.lo, self.hi)
             self.updates += 1
             ckpt = (checkpoint_every and step % checkpoint_every == 0 and step < total_steps) or \
                 (final_checkpoint and step == total_steps)

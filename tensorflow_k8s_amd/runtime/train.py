@@ -167,7 +167,7 @@ def run_ps(args, info, dev) -> int:
           "transport": args.ps_transport, "device": str(dev)})
     if args.ps_transport == "rccl":
         n = server.serve_collective(start, args.steps, args.checkpoint_every if args.checkpoint_dir else 0,
-                                    chief=0, final_checkpoint=bool(args.checkpoint_dir))
+                                    chief=0, final_checkpoint=bool(args.checkpoint_dir), bucket_mb=args.bucket_mb)
     else:
         n = server.serve()
     _log({"event": "done", "role": "ps", "index": info.task_index, "updates": n})
@@ -190,7 +190,7 @@ def run_worker(args, info, dev) -> int:
         if not info.ps_ranks:
             raise SystemExit("--strategy ps needs ps tasks in TF_CONFIG")
         strat = ParameterServerStrategy(model.arena, info.ps_ranks, info.worker_ranks, args.ps_mode,
-                                        transport=args.ps_transport)
+                                        transport=args.ps_transport, bucket_mb=args.bucket_mb)
         strat.configure_optimizer(opt)
     else:
         from ..parallel.mwms import MultiWorkerMirroredStrategy

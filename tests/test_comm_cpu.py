@@ -136,3 +136,26 @@ def test_transport_summary_parses_rccl_lines(tmp_path, monkeypatch):
         "host:1:1 [0] NCCL INFO Channel 02/0 : 0[0] -> 1[1] via SHM/direct/direct\n"
         "host:1:1 [0] NCCL INFO Connected all rings\n")
     assert comm.transport_summary() == {"P2P/IPC": 2, "SHM/direct": 1}
+
+
+def test_collective_ps_plan_buckets(world1_gloo):
+    """CollectivePlan buckets cover every parameter, never cross a shard or the decay/no-decay boundary,
+    start and end on parameter boundaries, and respect the size cap."""
+    from tensorflow_k8s_amd.parallel.ps import CollectivePlan, _param_spans, shard_bounds
+    a = _arena(n_params=9, numel=3000)
+    shards = shard_bounds(a.numel, 2, _param_spans(a))
+    plan = CollectivePlan(a, shards, [0, 0], [0], bucket_mb=6000 * 4 / 2**20)
+    bs = plan.buckets
+    assert bs[0][0] == 0 and bs[-1][1] == a.numel
+    for x, y in zip(bs, bs[1:]):  # contiguous, except over arena padding that holds no parameter
+        assert x[1] == y[0] or not any(x[1] <= p.offset < y[0] for p in a.params), (x, y)
+    starts = {p.offset for p in a.params} | {a.numel}
+    nd = a.nodecay_region()[0]
+    for lo, hi, s in bs:
+        assert lo in starts or lo == nd
+        slo, shi = shards[s]
+        assert slo <= lo < hi <= shi
+        assert not (lo < nd < hi)
+        assert hi - lo <= 6000 + 3072  # cap + at most one more (aligned) parameter
+    assert sum(plan._nparams) == len(a.params)
+    assert set(plan.buckets_of(0)) | set(plan.buckets_of(1)) == set(range(len(bs)))

@@ -472,3 +472,44 @@ def test_g4_conv_fwd_gather(cfg, tile):
     ref = G._ref_conv(x, w, g)
     assert rel(y, ref) < 1e-2
     assert rel(st_[0], ref.reshape(-1, K).sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(4, 28, 28, 64, 256), (3, 17, 19, 64, 200)])
+def test_shortk_single_stage_blocks(shape):
+    """K <= 64 GEMMs (1x1 conv with 64 input channels): the single-stage 4-blocks-per-CU g4
+    instantiation must equal the two-stage kernel (same per-tile math) for conv fwd + BN stats and
+    for the BN-reduce dgrad, and match the fp32 CPU reference."""
+    L = lib()
+    N, H, W, C, K = shape
+    g = G.ConvGeom(N, H, W, C, K, 1, 1)
+    x = bf(N, H, W, C, seed=1)
+    w = bf(K, 1, 1, C, scale=0.05, seed=2)
+    dyk = bf(N, H, W, K, seed=3)            # gradient wrt the K-channel output
+    wt = bf(C, 1, 1, K, scale=0.05, seed=4)  # a K -> C conv whose dgrad has K_gemm = C = 64
+    g2 = G.ConvGeom(N, H, W, K, C, 1, 1)
+    y, a = bf(N, H, W, K, seed=5), bf(N, H, W, K, seed=6)
+    gen = torch.Generator().manual_seed(8)
+    mu, inv = torch.randn(K, generator=gen) * 0.1, torch.rand(K, generator=gen) + 0.5
+
+    def run(dev):
+        st = torch.zeros(8 * 2 * K, device=dev)
+        yf = G.conv_fwd(x.to(dev), w.to(dev), g, st, 8)
+        bst = BN.BNState(K, dev)
+        bst.mean.copy_(mu); bst.invstd.copy_(inv)
+        spec = BN.BNReduce(y.to(dev), bst, a=a.to(dev))
+        dx = G.conv_dgrad(bf(N, H, W, C, seed=7).to(dev), wt.to(dev), g2, bnr=spec)
+        return yf, st.view(8, 2, K).sum(0).cpu(), dx, bst.sums.view(bst.shards, 3, K).sum(0).cpu()
+
+    res = {}
+    try:
+        for flag in (0, 1):
+            L.gemm_set_shortk(flag)
+            res[flag] = run(DEV)
+            torch.cuda.synchronize()
+    finally:
+        L.gemm_set_shortk(1)
+    ref = run("cpu")
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][2], res[1][2])
+    for i in range(4):
+        assert rel(res[1][i], ref[i]) < 2e-2, i
+        assert rel(res[1][i], res[0][i]) < 1e-4, i

@@ -195,8 +195,9 @@ def test_checkpoint_manager_roundtrip_exact(tmp_path, native_ext):
 
 
 def test_collective_ps_transport_matches_mwms(tmp_path, native_ext):
-    """transport=rccl (reduce -> owner update -> broadcast; run here over gloo collectives) gives the
-    same trajectory as MWMS, including the chief's checkpoint fetch of the ps-held slots."""
+    """transport=rccl (bucketed reduce -> per-bucket owner update -> broadcast on per-shard
+    communicators; run here over gloo collectives) gives the same trajectory as MWMS, including the
+    chief's checkpoint fetch of the ps-held slots."""
     p = free_port()
     mw = _launch([("chief", 0), ("worker", 0)], {"chief": [f"c.svc:{p}"], "worker": ["w.svc:1"]}, BASE, str(tmp_path))
     assert all(v[0] == 0 for v in mw.values()), {k: v[2][-1500:] for k, v in mw.items()}
@@ -204,7 +205,8 @@ def test_collective_ps_transport_matches_mwms(tmp_path, native_ext):
     ck = str(tmp_path / "ck")
     out = _launch([("chief", 0), ("worker", 0), ("ps", 0), ("ps", 1)],
                   {"chief": [f"c.svc:{p}"], "worker": ["w.svc:1"], "ps": ["p0.svc:1", "p1.svc:1"]},
-                  BASE + ["--ps-transport", "rccl", "--checkpoint-dir", ck, "--checkpoint-every", "4"], str(tmp_path))
+                  BASE + ["--ps-transport", "rccl", "--checkpoint-dir", ck, "--checkpoint-every", "4",
+                          "--bucket-mb", "0.01"], str(tmp_path))  # several buckets per shard
     assert all(v[0] == 0 for v in out.values()), {k: v[2][-1500:] for k, v in out.items()}
     a, b = _final_loss(mw[("chief", 0)][1]), _final_loss(out[("chief", 0)][1])
     assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (a, b)

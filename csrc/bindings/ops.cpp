@@ -17,6 +17,7 @@ void tfk_gemm_set_persist(int on);
 void tfk_gemm_set_engine(int e);
 void tfk_g4_set_shortk(int on);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
+int tfk_mx_quant_t(const void*, void*, void*, int, int, hipStream_t);
 int tfk_mx_probe(const int*, const int*, const int*, const int*, float*, hipStream_t);
 int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, hipStream_t s);
 int tfk_bn_finalize(float*, int, int, float, const float*, const float*, float, float, float*, float*, float*, float*,
@@ -264,12 +265,27 @@ void mx_quant(torch::Tensor x, torch::Tensor q, torch::Tensor s, int64_t rows, i
   check_rc(tfk_mx_quant(x.data_ptr(), q.data_ptr(), s.data_ptr(), rows * K / 32, cur_stream()), "mx_quant");
 }
 
-// C[M][N] bf16 = epilogue(Aq[M][K] . Bq[N][K]^T) with e8m0 block scales (one per 32 K-elements).
+// MX-fp8 transposing quantizer: x bf16 [R][C] -> q uint8 [C][R], s uint8 [C][R/32]
+void mx_quant_t(torch::Tensor x, torch::Tensor q, torch::Tensor s, int64_t R, int64_t C) {
+  need_bf16(x, "x"); need(q, at::kByte, "q"); need(s, at::kByte, "s");
+  TORCH_CHECK(R % 32 == 0 && R > 0 && C > 0, "mx_quant_t needs R % 32 == 0");
+  need_numel(x, R * C, "x"); need_numel(q, R * C, "q"); need_numel(s, R * C / 32, "s");
+  need_aligned(x, 16, "x"); need_aligned(q, 16, "q");
+  check_rc(tfk_mx_quant_t(x.data_ptr(), q.data_ptr(), s.data_ptr(), (int)R, (int)C, cur_stream()), "mx_quant_t");
+}
+
+// C[M][N] = epilogue(Aq[M][K] . Bq[N][K]^T) with e8m0 block scales (one per 32 K-elements).
+// C bf16: bias / act / resid / aux / dropout / activation backward (dact_src, dact);
+// C f32: C = alpha * AB + beta * C (weight gradients).
 void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tensor Bs, torch::Tensor C, int M, int N, int K,
                 c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, int act,
-                c10::optional<torch::Tensor> aux, double drop_p, int64_t drop_seed) {
+                c10::optional<torch::Tensor> aux, double drop_p, int64_t drop_seed,
+                c10::optional<torch::Tensor> dact_src, int dact, double beta) {
   for (auto* t : {&A, &As, &B, &Bs}) need(*t, at::kByte, "mx operand");
-  need_bf16(C, "C");
+  const bool f32 = C.scalar_type() == at::kFloat;
+  if (!f32) need_bf16(C, "C");
+  TORCH_CHECK(!f32 || (!bias.has_value() && !resid.has_value() && !aux.has_value() && !dact_src.has_value() &&
+                       act == 0 && drop_p == 0.0), "gemm_mxfp8: f32 output takes no epilogue extras");
   TORCH_CHECK(M > 0 && N > 0 && K > 0 && K % 128 == 0, "gemm_mxfp8 needs K % 128 == 0, got ", K);
   need_numel(A, (long long)M * K, "A"); need_numel(B, (long long)N * K, "B");
   need_numel(As, (long long)M * K / 32, "As"); need_numel(Bs, (long long)N * K / 32, "Bs");
@@ -292,7 +308,14 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
   p.drop_p = (float)drop_p;
   p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
   p.drop_seed = (unsigned long long)drop_seed;
-  const int ext = (p.aux || drop_p > 0.0) ? 1 : 0;
+  if (dact_src.has_value() && dact_src->defined()) {
+    need_bf16(*dact_src, "dact_src"); need_numel(*dact_src, (long long)M * N, "dact_src");
+    TORCH_CHECK(dact >= 1 && dact <= 3, "dact");
+  }
+  p.dact_src = opt_ptr<const void>(dact_src);
+  p.dact = dact;
+  p.beta = (float)beta;
+  const int ext = f32 ? 2 : ((p.aux || drop_p > 0.0 || p.dact_src) ? 1 : 0);
   check_rc(tfk_gemm_mxfp8(p, ext, cur_stream()), "gemm_mxfp8");
 }
 
@@ -584,8 +607,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_engine", &gemm_set_engine);
   m.def("gemm_set_shortk", &gemm_set_shortk);
   m.def("mx_quant", &mx_quant);
+  m.def("mx_quant_t", &mx_quant_t);
   m.def("mx_probe", &mx_probe);
-  m.def("gemm_mxfp8", &gemm_mxfp8);
+  m.def("gemm_mxfp8", &gemm_mxfp8, py::arg("A"), py::arg("As"), py::arg("B"), py::arg("Bs"), py::arg("C"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("bias"), py::arg("resid"), py::arg("act"), py::arg("aux"), py::arg("drop_p"),
+        py::arg("drop_seed"), py::arg("dact_src") = py::none(), py::arg("dact") = 0, py::arg("beta") = 0.0);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);

@@ -180,6 +180,54 @@ __global__ void mx_quant_kernel(const bf16* __restrict__ x, unsigned char* __res
     s[i] = (unsigned char)(ex + 127);
   }
 }
+// Transposing quantizer for the backward GEMMs: x bf16 [R][C] (row-major) -> q e4m3 [C][R] with
+// s e8m0 [C][R/32], i.e. the MX blocks run along R (the reduction dimension of dgrad's W^T and of
+// wgrad's dY^T / X^T). Block = 256 threads = a 32-row x 256-column tile staged through LDS with
+// 16-B loads; thread t then owns column t: amax over its 32 values (LDS reads of one row by a wave
+// are 128 contiguous bytes: conflict-free), one exponent, 32 e4m3 bytes written as two 16-B stores.
+// R % 32 == 0 (host-checked); ragged C is masked.
+__global__ void mx_quant_t_kernel(const bf16* __restrict__ x, unsigned char* __restrict__ q,
+                                  unsigned char* __restrict__ s, int R, int C) {
+  __shared__ bf16 tile[32][256 + 8];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 256, t = threadIdx.x;
+  const bool vec = (C & 7) == 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // 32 rows x 32 chunks of 8 columns = 1024 chunks / 256 threads
+    const int idx = t + i * 256, row = idx >> 5, ch = (idx & 31) * 8;
+    const int c = c0 + ch;
+    const bf16* src = x + (long long)(r0 + row) * C + c;
+    if (vec && c + 8 <= C) {
+      *(bf16x8*)&tile[row][ch] = *(const bf16x8*)src;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) tile[row][ch + e] = c + e < C ? src[e] : f2bf(0.f);
+    }
+  }
+  __syncthreads();
+  const int c = c0 + t;
+  if (c >= C) return;
+  float v[32];
+  float amax = 0.f;
+#pragma unroll
+  for (int r = 0; r < 32; ++r) { v[r] = bf2f(tile[r][t]); amax = fmaxf(amax, fabsf(v[r])); }
+  int ex = amax > 0.f ? (int)ceilf(log2f(amax * (1.f / 448.f))) : -127;
+  ex = ex < -127 ? -127 : (ex > 127 ? 127 : ex);
+  const float inv = ldexpf(1.f, -ex);
+  unsigned int w[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float a0 = fminf(fmaxf(v[4 * k] * inv, -448.f), 448.f), a1 = fminf(fmaxf(v[4 * k + 1] * inv, -448.f), 448.f);
+    float a2 = fminf(fmaxf(v[4 * k + 2] * inv, -448.f), 448.f), a3 = fminf(fmaxf(v[4 * k + 3] * inv, -448.f), 448.f);
+    int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+    pk = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, pk, true);
+    w[k] = (unsigned int)pk;
+  }
+  unsigned char* dst = q + (long long)c * R + r0;
+  *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+  *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+  s[(long long)c * (R / 32) + blockIdx.y] = (unsigned char)(ex + 127);
+}
+
 // One-wave self-test of the scaled MFMA operand maps: X/Y are [64 lanes][8] words, scales one per
 // lane, D [64 lanes][4] (lane-major) = mfma_scale(X, Y) (tests/test_fp8_gpu.py probes the layout).
 __global__ void mx_probe_kernel(const int* X, const int* Y, const int* sx, const int* sy, float* D) {
@@ -202,6 +250,12 @@ int tfk_mx_probe(const int* X, const int* Y, const int* sx, const int* sy, float
   hipLaunchKernelGGL(mx_probe_kernel, dim3(1), dim3(64), 0, st, X, Y, sx, sy, D);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+int tfk_mx_quant_t(const void* x, void* q, void* s, int R, int C, hipStream_t st) {
+  if (R % 32 || R <= 0 || C <= 0) return -1;
+  dim3 grid((unsigned)((C + 255) / 256), (unsigned)(R / 32));
+  hipLaunchKernelGGL(mx_quant_t_kernel, grid, dim3(256), 0, st, (const bf16*)x, (unsigned char*)q, (unsigned char*)s, R, C);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 int tfk_mx_quant(const void* x, void* q, void* s, long long nblocks, hipStream_t st) {
   long long g = (nblocks + 255) / 256;
   if (g > 8192) g = 8192;
@@ -210,13 +264,17 @@ int tfk_mx_quant(const void* x, void* q, void* s, long long nblocks, hipStream_t
                      (unsigned char*)s, nblocks);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-// C[M][N] bf16 = epilogue(A q[M][K] x B q[N][K]^T), scales in p.a_scale / p.b_scale.
+// C[M][N] = epilogue(A q[M][K] x B q[N][K]^T), scales in p.a_scale / p.b_scale.
+// ext: 0 bf16 (bias/act/resid), 1 bf16 EXT (aux, dropout, activation backward), 2 f32 (alpha/beta:
+// weight gradients accumulate into the f32 arena).
 int tfk_gemm_mxfp8(GemmParams p, int ext, hipStream_t st) {
   const int BM = 128, BN = 128;
   p.tiles_n = (p.N + BN - 1) / BN;
   if (p.stats_shards < 1) p.stats_shards = 1;
   dim3 grid(((p.M + BM - 1) / BM) * p.tiles_n, 1, 1);
-  if (ext)
+  if (ext == 2)
+    hipLaunchKernelGGL((mxfp8_gemm_kernel<128, 128, EPI_F32>), grid, dim3(NTF), 0, st, p);
+  else if (ext)
     hipLaunchKernelGGL((mxfp8_gemm_kernel<128, 128, EPI_BF16_EXT>), grid, dim3(NTF), 0, st, p);
   else
     hipLaunchKernelGGL((mxfp8_gemm_kernel<128, 128, EPI_BF16>), grid, dim3(NTF), 0, st, p);

@@ -43,7 +43,7 @@ class BertConfig:
     init_std: float = 0.02
     seq_len: int = 128
     max_predictions: int = 20
-    fp8: bool = False  # forward GEMMs in MX-fp8 (e4m3 + e8m0 block scales); backward bf16
+    fp8: bool = False  # all linear GEMMs (fwd, dgrad, wgrad) in MX-fp8 (e4m3 + e8m0 block scales)
     # split-K fill target for the encoder weight gradients (None = ops.gemm.TARGET_BLOCKS). Measured
     # on MI355X, base bs64x128: 512 -> 15.44 ms/step vs 16.17 at 1024 (profiles/splitk_sweep_*).
     wgrad_split_target: int | None = 512

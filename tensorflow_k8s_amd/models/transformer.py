@@ -45,7 +45,7 @@ class TransformerConfig:
     src_len: int = 256
     tgt_len: int = 256
     max_len: int = 1024
-    fp8: bool = False  # forward GEMMs in MX-fp8 (e4m3 + e8m0 block scales); backward bf16
+    fp8: bool = False  # all linear GEMMs (fwd, dgrad, wgrad) in MX-fp8 (e4m3 + e8m0 block scales)
 
     @classmethod
     def big(cls):
@@ -266,8 +266,9 @@ class Transformer:
         logits, (x, mem, st_m, y, yo, st_y) = self._forward(src, tgt_in, src_len, B, Ss, St, seed, tr)
         loss, dlogits, corr = softmax_xent(logits, tgt_out, smoothing=cfg.label_smoothing,
                                            scale=loss_scale / tgt_out.numel(), want_correct=True, V=cfg.vocab_size)
-        G.linear_wgrad(dlogits, yo, self.emb.table.grad)  # first writer of the shared table's grad
-        dyo = G.linear_dgrad(dlogits, self.emb.table.compute)
+        from ..runtime.layers import linear_dgrad, linear_wgrad
+        linear_wgrad(dlogits, yo, self.emb.table.grad, cfg.fp8)  # first writer of the shared table's grad
+        dyo = linear_dgrad(dlogits, self.emb.table.compute, cfg.fp8)
         dy = self.dec_ln.backward(dyo, y, st_y)
         dmem = torch.zeros_like(mem)
         for layer in reversed(self.dec):

@@ -2,9 +2,17 @@
 scale per 32 K-elements of each row, multiplied by gfx950's block-scaled MFMA
 (v_mfma_scale_f32_16x16x128_f8f6f4, 2x the bf16 MFMA rate).
 
-Used for the forward GEMMs of the transformer models when ``fp8=True`` (activations and weights
-are quantized on the fly; the f32 master weights, the optimizer and the backward pass stay in
-bf16/f32). The CPU path is the exact dequantized reference of the same quantization.
+Used for all three GEMMs of a linear layer of the transformer models when ``fp8=True``:
+
+* forward   y  = X  W^T : X quantized along K (rows of X), W along K (rows of W);
+* dgrad     dX = dY W   : dY quantized along N (its rows), W^T along N (``mx_quantize_t`` of W);
+* wgrad     dW = dY^T X : dY^T and X^T quantized along the token dimension (``mx_quantize_t``).
+
+MX blocks always run along the GEMM's reduction dimension, so the backward operands are produced
+by a transposing quantizer (one LDS-staged pass, csrc/kernels/fp8.hip). The f32 master weights and
+the optimizer stay f32; the weight gradient is accumulated in f32 by the GEMM epilogue. Shapes
+that do not tile (reduction dim % 128, transposed rows % 32) fall back to the bf16 GEMMs. The CPU
+path is the exact dequantized reference of the same quantization.
 """
 from __future__ import annotations
 
@@ -77,3 +85,59 @@ def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = 
     lib().gemm_mxfp8(xq, xs, wq_, ws_, y, M, N, K, bias, resid.reshape(-1, N) if resid is not None else None,
                      ACT[act], aux, drop_p, drop_seed)
     return y
+
+
+def mx_quantize_t(x: torch.Tensor):
+    """bf16 [R, C] (R % 32 == 0) -> MX of x^T: (q uint8 [C, R], s uint8 [C, R/32])."""
+    R, C = x.shape
+    if R % MX_BLOCK:
+        raise ValueError(f"transposed MX quantization needs rows % 32 == 0, got {R}")
+    if not on_gpu(x):
+        return mx_quantize(x.t().contiguous())
+    q = torch.empty(C, R, dtype=torch.uint8, device=x.device)
+    s = torch.empty(C, R // MX_BLOCK, dtype=torch.uint8, device=x.device)
+    lib().mx_quant_t(x.contiguous(), q, s, R, C)
+    return q, s
+
+
+def mx_backward_ok(M: int, N: int, K: int) -> tuple[bool, bool]:
+    """(dgrad, wgrad) eligibility of a [M tokens, K in] x [N out, K in] linear layer: the
+    reduction dims (N for dgrad, M for wgrad) must be multiples of 128 (one scaled-MFMA K-tile)."""
+    return N % 128 == 0 and K % 8 == 0, M % 128 == 0
+
+
+def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None = None,
+                    dact_src: torch.Tensor | None = None, dact: str | None = None, wt=None) -> torch.Tensor:
+    """dx[M,K] = (MX(dy) @ MX(w^T)^T) [* act'(dact_src)] (+ resid), bf16. wt: pre-quantized w^T."""
+    M, N = dy.shape
+    K = w.shape[1]
+    dq, ds = mx_quantize(dy)
+    wq_, ws_ = wt if wt is not None else mx_quantize_t(w)
+    if not on_gpu(dy):
+        from .gemm import act_grad_ref
+        y = mx_dequantize(dq, ds) @ mx_dequantize(wq_, ws_).t()
+        if dact_src is not None:
+            y = y * act_grad_ref(dact_src.float(), dact)
+        y = y.to(torch.bfloat16)
+        if resid is not None:
+            y = (y.float() + resid.float()).to(torch.bfloat16)
+        return y
+    dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
+    lib().gemm_mxfp8(dq, ds, wq_, ws_, dx, M, K, N, None, resid, 0, None, 0.0, 0,
+                     dact_src=dact_src, dact=ACT[dact] if dact_src is not None else 0)
+    return dx
+
+
+def linear_wgrad_mx(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate: bool = False) -> None:
+    """gw[N,K] (f32) (+)= MX(dy^T) @ MX(x^T)^T (reduction over the M tokens)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    aq, as_ = mx_quantize_t(dy)
+    bq, bs = mx_quantize_t(x)
+    if not on_gpu(dy):
+        g = mx_dequantize(aq, as_) @ mx_dequantize(bq, bs).t()
+        v = gw.view(N, K)
+        v.add_(g) if accumulate else v.copy_(g)
+        return
+    lib().gemm_mxfp8(aq, as_, bq, bs, gw.view(N, K), N, K, M, None, None, 0, None, 0.0, 0,
+                     beta=1.0 if accumulate else 0.0)

@@ -35,6 +35,24 @@ def linear_forward(x, w, b, fp8: bool, **kw):
     return G.linear_fwd(x, w, b, **kw)
 
 
+def linear_wgrad(dy, x, gw, fp8: bool, accumulate: bool = False, split_target=None):
+    """Weight gradient: MX-fp8 when fp8 and the token count tiles (M % 128), else bf16 split-K."""
+    if fp8:
+        from ..ops.fp8 import linear_wgrad_mx, mx_backward_ok
+        if mx_backward_ok(dy.shape[0], dy.shape[1], x.shape[1])[1]:
+            return linear_wgrad_mx(dy, x, gw, accumulate=accumulate)
+    return G.linear_wgrad(dy, x, gw, accumulate=accumulate, split_target=split_target)
+
+
+def linear_dgrad(dy, w, fp8: bool, **kw):
+    """Input gradient: MX-fp8 when fp8 and the output width tiles (N % 128), else bf16."""
+    if fp8:
+        from ..ops.fp8 import linear_dgrad_mx, mx_backward_ok
+        if mx_backward_ok(dy.shape[0], dy.shape[1], w.shape[1])[0]:
+            return linear_dgrad_mx(dy, w, **kw)
+    return G.linear_dgrad(dy, w, **kw)
+
+
 class Conv2d:
     """NHWC conv, OHWI weight. TF variable: <name>/kernel in HWIO."""
 
@@ -149,7 +167,7 @@ class Linear:
                                      from_tf=lambda a: np.ascontiguousarray(a.T), tf_shape=(fin, fout)))
         self.b = arena.add(ParamSpec(f"{name}/bias", (fout,), init="zeros", decay=False)) if bias else None
         self.arena = arena
-        self.fp8 = False  # forward GEMM in MX-fp8 (ops.fp8); backward stays bf16
+        self.fp8 = False  # forward, dgrad and wgrad GEMMs in MX-fp8 (ops.fp8)
         self.split_target = None  # weight-gradient split-K fill target override (ops.gemm.pick_splits)
 
     def forward(self, x, act=None, resid=None, aux=None, drop_p: float = 0.0, drop_seed: int = 0):
@@ -159,7 +177,7 @@ class Linear:
     def backward(self, dy, x, need_dx: bool = True, resid=None, accumulate: bool = False, dact_src=None,
                  dact=None):
         """dy: gradient of this layer's (pre-dropout, post-activation-backward) output."""
-        G.linear_wgrad(dy, x, self.w.grad, accumulate=accumulate, split_target=self.split_target)
+        linear_wgrad(dy, x, self.w.grad, self.fp8, accumulate=accumulate, split_target=self.split_target)
         if self.b is not None:
             G.bias_grad(dy, self.b.grad, accumulate=accumulate)
             self.arena.grad_ready(self.w, self.b)
@@ -167,7 +185,7 @@ class Linear:
             self.arena.grad_ready(self.w)
         if not need_dx:
             return None
-        return G.linear_dgrad(dy, self.w.compute, resid=resid, dact_src=dact_src, dact=dact)
+        return linear_dgrad(dy, self.w.compute, self.fp8, resid=resid, dact_src=dact_src, dact=dact)
 
 
 class FusedLinear:
@@ -213,13 +231,13 @@ class FusedLinear:
 
     def backward(self, dy, x, need_dx: bool = True, resid=None):
         w, gw, _, gb = self.views()
-        G.linear_wgrad(dy, x, gw, split_target=getattr(self, "split_target", None))
+        linear_wgrad(dy, x, gw, self.fp8, split_target=getattr(self, "split_target", None))
         if gb is not None:
             G.bias_grad(dy, gb)
         self.arena.grad_ready(*[p.w for p in self.parts], *[p.b for p in self.parts if p.b is not None])
         if not need_dx:
             return None
-        return G.linear_dgrad(dy, w, resid=resid)
+        return linear_dgrad(dy, w, self.fp8, resid=resid)
 
 
 class LayerNorm:

@@ -173,6 +173,8 @@ Store::Store(const std::string& wal_path, size_t history) : history_cap_(history
   register_resource({"apiextensions.k8s.io", "v1beta1", "customresourcedefinitions", "customresourcedefinition",
                      "CustomResourceDefinition", false, {"v1beta1", "v1"}, {"crd"}});
   register_resource({"scheduling.tfk.io", "v1", "podgroups", "podgroup", "PodGroup", true, {"v1"}, {"pg"}});
+  register_resource({"scheduling.k8s.io", "v1", "priorityclasses", "priorityclass", "PriorityClass", false, {"v1"},
+                     {"pc"}});
   if (!wal_path_.empty()) {
     replay_wal();
     wal_ = fopen(wal_path_.c_str(), "a");

@@ -41,6 +41,7 @@ static void group_version(const std::string& plural, const std::string& tfjob_ve
   else if (plural == "leases") { *group = "coordination.k8s.io"; *version = "v1"; }
   else if (plural == "customresourcedefinitions") { *group = "apiextensions.k8s.io"; *version = "v1beta1"; }
   else if (plural == "podgroups") { *group = "scheduling.tfk.io"; *version = "v1"; }
+  else if (plural == "priorityclasses") { *group = "scheduling.k8s.io"; *version = "v1"; }
   else { *group = ""; *version = "v1"; }
 }
 

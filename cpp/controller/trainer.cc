@@ -151,6 +151,8 @@ Json Trainer::make_pod(const api::TFJob& job, RType t, int index, int generation
   std::string rp = rs ? rs->restart_policy : "";
   if (job.is_v1alpha1()) rp = spec.at("restartPolicy").str("OnFailure");
   spec["restartPolicy"] = (rp == "ExitCode" || rp.empty()) ? "Never" : rp;
+  if (!job.run_policy.scheduling.priority_class.empty() && !spec.at("priorityClassName").is_string())
+    spec["priorityClassName"] = job.run_policy.scheduling.priority_class;
   if (!job.scheduler_name.empty()) spec["schedulerName"] = job.scheduler_name;
   else if (opts_.gang_scheduling) spec["schedulerName"] = opts_.gang_scheduler_name;
   auto ports = service_ports(job);

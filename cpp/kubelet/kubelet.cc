@@ -1,12 +1,14 @@
 #include "kubelet.h"
 
 #include <dirent.h>
+#include <sched.h>
 #include <fcntl.h>
 #include <signal.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstring>
 #include <fstream>
 #include <set>
@@ -30,6 +32,74 @@ int detect_gpus() {
   return n;
 }
 
+std::vector<int> parse_cpulist(const std::string& s) {
+  std::vector<int> out;
+  for (auto& part : split(s, ',')) {
+    std::string t = trim(part);
+    if (t.empty()) continue;
+    size_t dash = t.find('-');
+    int a = atoi(t.c_str()), b = dash == std::string::npos ? a : atoi(t.c_str() + dash + 1);
+    for (int c = a; c <= b && c - a < 65536; ++c) out.push_back(c);
+  }
+  return out;
+}
+
+static std::string read_first_line(const std::string& path) {
+  std::ifstream f(path);
+  std::string line;
+  std::getline(f, line);
+  return trim(line);
+}
+
+// KFD topology: GPU nodes (gpu_id != 0) in node-index order = HIP device order; each node's
+// properties carry the PCI location_id (bus << 8 | devfn) and domain -> the PCI device's numa_node.
+Topology detect_topology(int gpus) {
+  Topology t;
+  std::vector<std::pair<int, int>> gpu_nodes;  // (kfd node index, numa)
+  if (DIR* d = opendir("/sys/class/kfd/kfd/topology/nodes")) {
+    while (dirent* e = readdir(d)) {
+      if (e->d_name[0] == '.') continue;
+      std::string base = std::string("/sys/class/kfd/kfd/topology/nodes/") + e->d_name;
+      if (atoi(read_first_line(base + "/gpu_id").c_str()) == 0) continue;
+      long long loc = -1, dom = 0;
+      std::ifstream f(base + "/properties");
+      std::string k;
+      long long v;
+      while (f >> k >> v) {
+        if (k == "location_id") loc = v;
+        else if (k == "domain") dom = v;
+      }
+      int numa = 0;
+      if (loc >= 0) {
+        char bdf[64];
+        snprintf(bdf, sizeof bdf, "/sys/bus/pci/devices/%04llx:%02llx:%02llx.%llx/numa_node", dom, (loc >> 8) & 0xff,
+                 (loc >> 3) & 0x1f, loc & 0x7);
+        numa = std::max(0, atoi(read_first_line(bdf).c_str()));
+      }
+      gpu_nodes.push_back({atoi(e->d_name), numa});
+    }
+    closedir(d);
+  }
+  std::sort(gpu_nodes.begin(), gpu_nodes.end());
+  for (auto& g : gpu_nodes) t.gpu_numa.push_back(g.second);
+  if ((int)t.gpu_numa.size() != gpus) t.gpu_numa.assign(std::max(gpus, 0), 0);
+  for (int n = 0;; ++n) {
+    std::string cl = read_first_line("/sys/devices/system/node/node" + std::to_string(n) + "/cpulist");
+    if (cl.empty()) break;
+    t.numa_cpus.push_back(parse_cpulist(cl));
+  }
+  return t;
+}
+
+std::vector<int> cpus_for_gpus(const Topology& t, const std::vector<int>& gpu_ids) {
+  std::set<int> nodes, cpus;
+  for (int g : gpu_ids)
+    if (g >= 0 && g < (int)t.gpu_numa.size()) nodes.insert(t.gpu_numa[g]);
+  for (int n : nodes)
+    if (n >= 0 && n < (int)t.numa_cpus.size()) cpus.insert(t.numa_cpus[n].begin(), t.numa_cpus[n].end());
+  return std::vector<int>(cpus.begin(), cpus.end());
+}
+
 static void mkdirs(const std::string& p) {
   std::string cur;
   for (auto& part : split(p, '/')) {
@@ -42,6 +112,15 @@ static void mkdirs(const std::string& p) {
 Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletOptions o) : client_(std::move(c)), opts_(std::move(o)) {
   if (opts_.gpus < 0) opts_.gpus = detect_gpus();
   if (opts_.cpu_milli <= 0) opts_.cpu_milli = (long long)sysconf(_SC_NPROCESSORS_ONLN) * 1000;
+  topo_ = detect_topology(opts_.gpus);
+  if (!opts_.gpu_numa.empty()) {
+    topo_.gpu_numa.clear();
+    for (auto& x : split(opts_.gpu_numa, ',')) topo_.gpu_numa.push_back(atoi(x.c_str()));
+  }
+  if (!opts_.numa_cpus.empty()) {
+    topo_.numa_cpus.clear();
+    for (auto& x : split(opts_.numa_cpus, ';')) topo_.numa_cpus.push_back(parse_cpulist(x));
+  }
   mkdirs(opts_.root_dir + "/logs");
   mkdirs(opts_.root_dir + "/term");
   pods_inf_.reset(new SharedInformer(client_, "pods", "", 10000, "", "spec.nodeName=" + opts_.node_name));
@@ -58,6 +137,10 @@ void Kubelet::register_node(bool heartbeat) {
   n["metadata"]["name"] = opts_.node_name;
   n["metadata"]["labels"]["kubernetes.io/hostname"] = opts_.node_name;
   n["metadata"]["labels"]["amd.com/gpu.product"] = "MI355X";
+  std::string numa;
+  for (size_t i = 0; i < topo_.gpu_numa.size(); ++i) numa += (i ? "," : "") + std::to_string(topo_.gpu_numa[i]);
+  n["metadata"]["annotations"]["tfk.io/gpu-numa"] = numa;
+  n["metadata"]["annotations"]["tfk.io/numa-nodes"] = std::to_string(std::max<size_t>(1, topo_.numa_cpus.size()));
   Json cap = Json::object();
   cap["amd.com/gpu"] = opts_.gpus;
   cap["cpu"] = std::to_string(opts_.cpu_milli) + "m";
@@ -118,6 +201,21 @@ void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
   }
   std::string gpu_ids = pr.pod.path("metadata.annotations").at("tfk.io/gpu-ids").str();
   if (!gpu_ids.empty()) env["HIP_VISIBLE_DEVICES"] = gpu_ids;
+  // NUMA-local CPUs of the pod's GPUs (built here: the child only calls sched_setaffinity)
+  std::vector<int> gids;
+  for (auto& x : split(gpu_ids, ','))
+    if (!x.empty()) gids.push_back(atoi(x.c_str()));
+  std::vector<int> pin = opts_.pin_cpus ? cpus_for_gpus(topo_, gids) : std::vector<int>();
+  cpu_set_t cpuset;
+  CPU_ZERO(&cpuset);
+  std::string pin_list;
+  for (int cpu : pin)
+    if (cpu >= 0 && cpu < CPU_SETSIZE) {
+      CPU_SET(cpu, &cpuset);
+      pin_list += (pin_list.empty() ? "" : ",") + std::to_string(cpu);
+    }
+  const bool do_pin = !pin_list.empty();
+  if (do_pin) env["TFK_CPU_AFFINITY"] = pin_list;
   env["TFK_POD_NAME"] = pr.name;
   env["TFK_POD_NAMESPACE"] = pr.ns;
   env["TFK_NODE_NAME"] = opts_.node_name;
@@ -153,6 +251,7 @@ void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
   pid_t pid = fork();
   if (pid == 0) {
     sigprocmask(SIG_SETMASK, &none, nullptr);
+    if (do_pin) sched_setaffinity(0, sizeof(cpuset), &cpuset);  // best effort (cgroup may forbid)
     signal(SIGPIPE, SIG_DFL);
     signal(SIGTERM, SIG_DFL);
     signal(SIGINT, SIG_DFL);
@@ -180,7 +279,8 @@ void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
   for (size_t i = 0; i < pr.containers.size(); ++i)
     if (&pr.containers[i] == &c) pid_owner_[pid] = {pr.uid, i};
   TFK_LOG(Info, "started container", Json(Json::object_t{{"pod", Json(pr.ns + "/" + pr.name)}, {"container", Json(c.name)},
-                                                         {"pid", Json((long long)pid)}, {"gpus", Json(gpu_ids)}}));
+                                                         {"pid", Json((long long)pid)}, {"gpus", Json(gpu_ids)},
+                                                         {"cpus", Json(pin_list)}}));
 }
 
 void Kubelet::kill_pod(PodRun& pr, int sig) {

@@ -27,7 +27,19 @@ struct KubeletOptions {
   int64_t grace_ms = 5000;
   int64_t heartbeat_ms = 10000;
   bool local_dns = true;
+  // topology (two-socket 8x MI355X): GPU i's NUMA node, and each NUMA node's CPU list; detected
+  // from sysfs (KFD topology -> PCI numa_node, /sys/devices/system/node) unless given
+  std::string gpu_numa;   // e.g. "0,0,0,0,1,1,1,1"
+  std::string numa_cpus;  // e.g. "0-47,96-143;48-95,144-191" (';' separates NUMA nodes)
+  bool pin_cpus = true;   // sched_setaffinity of containers to their GPUs' NUMA CPUs
 };
+
+struct Topology {
+  std::vector<int> gpu_numa;                 // per GPU index (HIP order)
+  std::vector<std::vector<int>> numa_cpus;   // per NUMA node
+};
+Topology detect_topology(int gpus);
+std::vector<int> parse_cpulist(const std::string& s);  // "0-3,8,10-11" -> ids
 
 struct ContainerRun {
   std::string name;
@@ -57,6 +69,8 @@ struct PodRun {
 };
 
 int detect_gpus();
+// CPUs a pod with these GPU ids is pinned to (union of their NUMA nodes' CPUs; empty = no pinning)
+std::vector<int> cpus_for_gpus(const Topology& t, const std::vector<int>& gpu_ids);
 
 class Kubelet {
  public:
@@ -79,6 +93,7 @@ class Kubelet {
   std::map<std::string, PodRun> pods_;  // uid -> run
   std::map<pid_t, std::pair<std::string, size_t>> pid_owner_;
   int64_t last_heartbeat_ = 0;
+  Topology topo_;
 };
 
 }  // namespace tfk

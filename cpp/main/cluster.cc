@@ -21,6 +21,8 @@ int main(int argc, char** argv) {
   fs.add_string("wal", &wal, "apiserver WAL path");
   fs.add_string("port-file", &port_file, "write the apiserver port here");
   fs.add_int("gpus", &gpus, "node amd.com/gpu capacity (-1 = detect)");
+  fs.add_string("gpu-numa", &ko.gpu_numa, "NUMA node per GPU, e.g. 0,0,0,0,1,1,1,1 (default: sysfs)");
+  fs.add_string("numa-cpus", &ko.numa_cpus, "CPU list per NUMA node, ';'-separated (default: sysfs)");
   fs.add_string("root-dir", &ko.root_dir, "kubelet state/log dir");
   fs.add_int("restart-backoff-ms", &backoff, "kubelet restart backoff");
   fs.add_int("threadiness", &so.threadiness, "operator workers");

@@ -14,6 +14,8 @@ int main(int argc, char** argv) {
   fs.add_string("apiserver", &apiserver, "apiserver URL");
   fs.add_string("node-name", &ko.node_name, "node name");
   fs.add_int("gpus", &gpus, "amd.com/gpu capacity (-1 = detect)");
+  fs.add_string("gpu-numa", &ko.gpu_numa, "NUMA node per GPU, e.g. 0,0,0,0,1,1,1,1 (default: sysfs)");
+  fs.add_string("numa-cpus", &ko.numa_cpus, "CPU list per NUMA node, ';'-separated (default: sysfs)");
   fs.add_string("root-dir", &ko.root_dir, "state/log directory");
   fs.add_int("restart-backoff-ms", &backoff, "base container restart backoff");
   fs.add_int("grace-ms", &grace, "termination grace period");

@@ -24,6 +24,7 @@
 #include "../common/json.h"
 #include "../common/util.h"
 #include "../controller/trainer.h"
+#include "../kubelet/kubelet.h"
 #include "../leaderelection/leaderelection.h"
 #include "../runtime/tfbundle.h"
 #include "../scheduler/scheduler.h"
@@ -430,6 +431,54 @@ TEST(gang_placement_all_or_nothing) {
   CHECK_EQ(p2.size(), (size_t)2);
   for (auto& kv : p2)
     for (int g : kv.second.second) CHECK(g >= 2);
+}
+
+TEST(topology_best_fit_numa_placement) {
+  NodeInfo n;
+  n.name = "n0";
+  n.gpus = 8;
+  n.gpu_numa = parse_int_list("0,0,0,0,1,1,1,1");
+  auto v = pick_gpus(n, 4);
+  CHECK(v == std::vector<int>({0, 1, 2, 3}));
+  n.used_gpus = {0};
+  CHECK(pick_gpus(n, 4) == std::vector<int>({4, 5, 6, 7}));  // domain 0 has only 3 free
+  n.used_gpus = {0, 1, 4};
+  CHECK(pick_gpus(n, 2) == std::vector<int>({2, 3}));        // best fit: the fuller domain
+  n.used_gpus = {};
+  auto six = pick_gpus(n, 6);
+  CHECK_EQ(six.size(), (size_t)6);
+  int d0 = 0;
+  for (int g : six) d0 += g < 4;
+  CHECK(d0 == 4 || d0 == 2);  // one whole domain + 2 of the other
+  // a gang of four 1-GPU pods packs onto one socket
+  auto pod = [](const std::string& nm) {
+    Json p = J(R"({"metadata":{"name":""},"spec":{"containers":[{"name":"t","resources":{"limits":{"amd.com/gpu":1}}}]}})");
+    p["metadata"]["name"] = nm;
+    return p;
+  };
+  std::vector<NodeInfo> nodes = {n};
+  nodes[0].used_gpus = {5};
+  auto pl = GangScheduler::place_group({pod("a"), pod("b"), pod("c"), pod("d")}, nodes);
+  std::set<int> doms;
+  for (auto& kv : pl) doms.insert(n.gpu_numa[kv.second.second[0]]);
+  CHECK_EQ(doms.size(), (size_t)1);
+  CHECK_EQ(*doms.begin(), 0);  // domain 1 has a used GPU -> the whole gang fits only on domain 0
+  NodeInfo flat;  // no topology published: one domain, lowest ids
+  flat.gpus = 4;
+  flat.used_gpus = {1};
+  CHECK(pick_gpus(flat, 2) == std::vector<int>({0, 2}));
+}
+
+TEST(numa_cpu_pinning_sets) {
+  CHECK(parse_cpulist("0-3,8,10-11") == std::vector<int>({0, 1, 2, 3, 8, 10, 11}));
+  CHECK(parse_cpulist("").empty());
+  Topology t;
+  t.gpu_numa = {0, 0, 1, 1};
+  t.numa_cpus = {parse_cpulist("0-1,4-5"), parse_cpulist("2-3,6-7")};
+  CHECK(cpus_for_gpus(t, {1}) == std::vector<int>({0, 1, 4, 5}));
+  CHECK(cpus_for_gpus(t, {0, 3}) == std::vector<int>({0, 1, 2, 3, 4, 5, 6, 7}));
+  CHECK(cpus_for_gpus(t, {}).empty());
+  CHECK(cpus_for_gpus(Topology{}, {0}).empty());  // unknown topology: no pinning
 }
 
 // ----------------------------------------------------------------------------- trainer (reconcile)

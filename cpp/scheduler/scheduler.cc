@@ -1,6 +1,7 @@
 #include "scheduler.h"
 
 #include <algorithm>
+#include <climits>
 
 namespace tfk {
 
@@ -34,9 +35,60 @@ static bool terminal(const Json& pod) {
   return ph == "Succeeded" || ph == "Failed";
 }
 
+std::vector<int> parse_int_list(const std::string& s) {
+  std::vector<int> v;
+  for (auto& t : split(s, ','))
+    if (!t.empty()) v.push_back(atoi(t.c_str()));
+  return v;
+}
+
+std::vector<int> pick_gpus(const NodeInfo& n, int need, int prefer_dom, int fit_total) {
+  std::map<int, std::vector<int>> free_by_dom;  // NUMA domain -> free GPU ids (ascending)
+  for (int g = 0; g < n.gpus; ++g)
+    if (!n.used_gpus.count(g)) free_by_dom[g < (int)n.gpu_numa.size() ? n.gpu_numa[g] : 0].push_back(g);
+  std::vector<int> ids;
+  if (need <= 0) return ids;
+  // the gang already holds GPUs in prefer_dom on this node: stay there while it has room
+  auto pd = free_by_dom.find(prefer_dom);
+  if (prefer_dom >= 0 && pd != free_by_dom.end() && (int)pd->second.size() >= need)
+    return std::vector<int>(pd->second.begin(), pd->second.begin() + need);
+  // best fit: the domain with the fewest free GPUs that still holds the whole gang (fit_total),
+  // else the whole request
+  for (int want : {std::max(fit_total, need), need}) {
+    const std::vector<int>* best = nullptr;
+    for (auto& kv : free_by_dom)
+      if ((int)kv.second.size() >= want && (!best || kv.second.size() < best->size())) best = &kv.second;
+    if (best) return std::vector<int>(best->begin(), best->begin() + need);
+  }
+  // spans domains: fewest domains -> take the largest domains first
+  std::vector<const std::vector<int>*> doms;
+  for (auto& kv : free_by_dom) doms.push_back(&kv.second);
+  std::stable_sort(doms.begin(), doms.end(), [](const std::vector<int>* a, const std::vector<int>* b) {
+    return a->size() > b->size();
+  });
+  for (auto* d : doms)
+    for (int g : *d)
+      if ((int)ids.size() < need) ids.push_back(g);
+  std::sort(ids.begin(), ids.end());
+  return ids;
+}
+
 GangScheduler::GangScheduler(std::shared_ptr<Client> c, SchedulerOptions o) : client_(std::move(c)), opts_(std::move(o)) {
   pods_.reset(new SharedInformer(client_, "pods", "", 30000));
   nodes_.reset(new SharedInformer(client_, "nodes", "", 30000));
+  prio_.reset(new SharedInformer(client_, "priorityclasses", "", 30000));
+}
+
+long long GangScheduler::pod_priority(const Json& pod) const {
+  const Json& pr = pod.path("spec.priority");
+  if (pr.is_number()) return pr.as_int();
+  std::string cls = pod.path("spec.priorityClassName").str();
+  if (cls.empty()) return 0;
+  if (cls == "system-node-critical") return 2000001000LL;
+  if (cls == "system-cluster-critical") return 2000000000LL;
+  for (auto& pc : prio_->indexer().list())
+    if (pc.path("metadata.name").str() == cls) return pc.at("value").as_int();
+  return 0;
 }
 
 bool GangScheduler::mine(const Json& pod) const {
@@ -54,6 +106,7 @@ std::vector<NodeInfo> GangScheduler::node_state() const {
     const Json& g = alloc.at("amd.com/gpu");
     ni.gpus = g.is_number() ? (int)g.as_int() : atoi(g.str("0").c_str());
     ni.cpu_milli = parse_quantity_milli(alloc.at("cpu"));
+    ni.gpu_numa = parse_int_list(n.path("metadata.annotations").at("tfk.io/gpu-numa").str());
     bool ready = true;
     for (auto& c : n.path("status.conditions").items())
       if (c.at("type").str() == "Ready" && c.at("status").str() != "True") ready = false;
@@ -81,6 +134,9 @@ std::map<std::string, std::pair<std::string, std::vector<int>>> GangScheduler::p
   std::stable_sort(order.begin(), order.end(), [](const Json* a, const Json* b) {
     return pod_gpu_request(*a) > pod_gpu_request(*b);
   });
+  int remaining = 0;
+  for (auto* p : order) remaining += pod_gpu_request(*p);
+  std::map<std::string, int> gang_dom;  // node -> NUMA domain this gang packs into
   for (auto* p : order) {
     int need = pod_gpu_request(*p);
     long long cpu = pod_cpu_request_milli(*p);
@@ -89,9 +145,12 @@ std::map<std::string, std::pair<std::string, std::vector<int>>> GangScheduler::p
       int free = n.gpus - (int)n.used_gpus.size();
       if (free < need) continue;
       if (n.cpu_milli > 0 && n.used_cpu_milli + cpu > n.cpu_milli) continue;
-      std::vector<int> ids;
-      for (int g = 0; g < n.gpus && (int)ids.size() < need; ++g)
-        if (!n.used_gpus.count(g)) ids.push_back(g);
+      auto gd = gang_dom.find(n.name);
+      std::vector<int> ids = pick_gpus(n, need, gd == gang_dom.end() ? -1 : gd->second, remaining);
+      std::set<int> doms;
+      for (int g : ids) doms.insert(g < (int)n.gpu_numa.size() ? n.gpu_numa[g] : 0);
+      if (doms.size() == 1 && gd == gang_dom.end()) gang_dom[n.name] = *doms.begin();
+      remaining -= need;
       for (int g : ids) n.used_gpus.insert(g);
       n.used_cpu_milli += cpu;
       out[p->path("metadata.namespace").str() + "/" + p->path("metadata.name").str()] = {n.name, ids};
@@ -119,8 +178,26 @@ int GangScheduler::schedule_once() {
     if (!mine(p)) continue;
     groups[key].push_back(p);
   }
-  int bound = 0;
+  // placement order: priority (highest first), then the oldest member's creation time, then key
+  struct Pending { long long prio; std::string created, key; };
+  std::vector<Pending> order;
   for (auto& kv : groups) {
+    Pending pd{LLONG_MIN, "", kv.first};
+    for (auto& p : kv.second) {
+      pd.prio = std::max(pd.prio, pod_priority(p));
+      std::string c = p.path("metadata.creationTimestamp").str();
+      if (pd.created.empty() || c < pd.created) pd.created = c;
+    }
+    order.push_back(pd);
+  }
+  std::stable_sort(order.begin(), order.end(), [](const Pending& a, const Pending& b) {
+    if (a.prio != b.prio) return a.prio > b.prio;
+    if (a.created != b.created) return a.created < b.created;
+    return a.key < b.key;
+  });
+  int bound = 0;
+  for (auto& od : order) {
+    auto& kv = *groups.find(od.key);
     int need_total = min_avail.count(kv.first) ? min_avail[kv.first] : 1;
     if ((int)kv.second.size() + bound_in_group[kv.first] < need_total) continue;  // gang incomplete: wait
     auto plan = place_group(kv.second, nodes);
@@ -159,7 +236,8 @@ int GangScheduler::schedule_once() {
 void GangScheduler::run(StopToken& stop) {
   pods_->start(stop);
   nodes_->start(stop);
-  while (!stop.stopped() && !wait_for_cache_sync({pods_.get(), nodes_.get()}, 1000)) {
+  prio_->start(stop);
+  while (!stop.stopped() && !wait_for_cache_sync({pods_.get(), nodes_.get(), prio_.get()}, 1000)) {
   }
   while (!stop.stopped()) {
     try {

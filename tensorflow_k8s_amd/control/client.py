@@ -15,12 +15,13 @@ BIN = os.path.join(ROOT, "build", "bin")
 
 CORE = {"pods", "services", "events", "configmaps", "endpoints", "nodes", "namespaces"}
 GROUPS = {"tfjobs": "kubeflow.org", "leases": "coordination.k8s.io", "podgroups": "scheduling.tfk.io",
-          "customresourcedefinitions": "apiextensions.k8s.io"}
+          "customresourcedefinitions": "apiextensions.k8s.io", "priorityclasses": "scheduling.k8s.io"}
 ALIASES = {"tfjob": "tfjobs", "tfj": "tfjobs", "pod": "pods", "po": "pods", "svc": "services", "service": "services",
            "event": "events", "ev": "events", "node": "nodes", "no": "nodes", "lease": "leases", "pg": "podgroups",
-           "podgroup": "podgroups", "crd": "customresourcedefinitions", "ns": "namespaces"}
+           "podgroup": "podgroups", "crd": "customresourcedefinitions", "ns": "namespaces", "pc": "priorityclasses",
+           "priorityclass": "priorityclasses"}
 KIND_PLURAL = {"TFJob": "tfjobs", "Pod": "pods", "Service": "services", "Event": "events", "Node": "nodes",
-               "ConfigMap": "configmaps", "Lease": "leases", "PodGroup": "podgroups",
+               "ConfigMap": "configmaps", "Lease": "leases", "PodGroup": "podgroups", "PriorityClass": "priorityclasses",
                "CustomResourceDefinition": "customresourcedefinitions", "Namespace": "namespaces"}
 
 
@@ -57,7 +58,7 @@ class TfkClient:
                 raise ValueError(f"unknown resource {plural}")
             v = version or (self.tfjob_version if plural == "tfjobs" else ("v1beta1" if g == "apiextensions.k8s.io" else "v1"))
             p = f"/apis/{g}/{v}"
-        if ns and plural not in ("nodes", "namespaces", "customresourcedefinitions"):
+        if ns and plural not in ("nodes", "namespaces", "customresourcedefinitions", "priorityclasses"):
             p += f"/namespaces/{ns}"
         p += f"/{plural}"
         if name:

@@ -85,6 +85,10 @@ _TILES = {(256, 256): (256, 0.76), (128, 128): (512, 0.62), (256, 64): (512, 0.6
 # Cin % 64 == 0 conv-forward gather): tools/engine_bench.py on MI355X -- 256x256 (16 waves) ~1.0-1.3
 # PF/s, 128x128 (4 waves, 2 blocks/CU) ~0.7-1.1 PF/s vs the register engine's 0.6-0.9.
 _G4_TILES = {(256, 256): (256, 0.95), (128, 128): (512, 0.80), (128, 64): (768, 0.62), (64, 128): (768, 0.62)}
+# 4-wave 64x256 / 256x64 blocks of the g4 engine for dense weight gradients with a narrow side
+# (rect_ok): the register engine's 64x64 tile ran these at ~300 TF/s (ResNet-50 1x1 wgrads)
+_G4_RECT = {(64, 256): (512, 0.80), (256, 64): (512, 0.80)}
+G4_RECT = os.environ.get("TFK_G4_RECT", "1") == "1"
 G4_BIG_MIN_K = 512  # one 16-wave block per CU: shorter K cannot amortise its prologue/epilogue
 # 64x256 tile for Cout<=64 conv weight gradients whose B gather changes (r,s) every chunk (C <= 16,
 # i.e. the 7x7 stem on C padded to 8). Measured on MI355X (ResNet-50 bs256, rocprofv3): stem wgrad
@@ -96,7 +100,8 @@ G4_ENABLED = os.environ.get("TFK_GEMM_ENGINE", "g4") != "reg"
 
 
 def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: int = 0, mid_ok: bool = True,
-              wide_ok: bool = False, split_target: int | None = None, g4: bool = False, narrow_ok: bool = False):
+              wide_ok: bool = False, split_target: int | None = None, g4: bool = False, narrow_ok: bool = False,
+              rect_ok: bool = False):
     """Tile with the lowest modelled time: rounds of concurrent blocks x per-block work / efficiency
     (a 256x256 tile runs one block per CU; smaller tiles 2-4 blocks/CU at lower efficiency).
     big_ok: operand modes that have the 256x256 instantiation (dense, non-gather); K: reduction
@@ -110,8 +115,13 @@ def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: 
     cands = dict(_TILES)
     if g4:
         cands.update({t: v for t, v in _G4_TILES.items() if narrow_ok or t[0] == t[1]})
+    rect = g4 and rect_ok and G4_RECT
+    if rect:
+        cands.update(_G4_RECT)
     for (bm, bn), (slots, eff) in cands.items():
-        if g4 and (bm, bn) in _G4_TILES and (narrow_ok or bm == bn):
+        if rect and (bm, bn) in _G4_RECT:
+            slots, eff = _G4_RECT[(bm, bn)]
+        elif g4 and (bm, bn) in _G4_TILES and (narrow_ok or bm == bn):
             slots, eff = _G4_TILES[(bm, bn)]
             if (bm, bn) == (256, 256) and (M < 256 or N < 256 or K < G4_BIG_MIN_K):
                 continue
@@ -119,7 +129,7 @@ def pick_tile(M: int, N: int, splits_ok: bool = False, big_ok: bool = False, K: 
             continue
         if (bm, bn) == (256, 64) and (not mid_ok or M < 256):
             continue
-        if (bm, bn) == (64, 256) and (not wide_ok or M > 64 or N <= 128):
+        if (bm, bn) == (64, 256) and not (rect and N >= 256) and (not wide_ok or M > 64 or N <= 128):
             continue
         if bn > 64 and N <= 64:
             continue
@@ -477,7 +487,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
     tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp,
                      wide_ok=WIDE_WGRAD and not g.pointwise and g.C <= WIDE_WGRAD_MAX_C,
                      g4=(G4_WGRAD or g.pointwise) and g.K % 8 == 0 and g.C % 8 == 0,
-                     narrow_ok=G4_WGRAD and not g.pointwise)
+                     narrow_ok=G4_WGRAD and not g.pointwise, rect_ok=g.pointwise)
     tiles = ((g.K + tile[0] - 1) // tile[0]) * ((Nn + tile[1] - 1) // tile[1])
 
     def run(C, sp, stride, beta):

@@ -62,6 +62,12 @@ def test_per_parameter_gradient_cosine(which):
     grads = {}
     for dev in ("cpu", "cuda"):
         m = mk(dev)
+        # ResNet's zero-initialised residual-branch gammas (bn*_branch2c) block every branch
+        # gradient at step 0; give them a value so every parameter's gradient is exercised
+        for p in m.arena.params:
+            if p.name.endswith("/gamma") and float(p.master.abs().sum()) == 0.0:
+                p.master.fill_(0.5)
+        m.arena.refresh_compute()
         loss, _ = m.forward_backward(*batch(m, dev))
         grads[dev] = {p.name: p.grad.detach().float().cpu().clone() for p in m.arena.params}
     gc, gg = grads["cpu"], grads["cuda"]
@@ -76,7 +82,7 @@ def test_per_parameter_gradient_cosine(which):
         c = _cos(gg[n], gc[n])
         if c < 0.99:
             worst.append((n, round(c, 4)))
-    assert checked >= 0.5 * len(gc)
+    assert checked >= 0.9 * len(gc), (checked, len(gc))
     assert not worst, worst
 
 

@@ -12,6 +12,7 @@ from dataclasses import dataclass
 import torch
 import torch.nn.functional as F
 
+from . import tuning
 from ._lib import lib, on_gpu, workspace
 
 A_KIN, A_KOUT, A_CONV_FWD, A_CONV_DGRAD = 0, 1, 2, 3
@@ -272,13 +273,16 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
         else:
             gw.view(N, K).copy_(g)
         return
-    tile = pick_tile(N, K, splits_ok=True, big_ok=True, K=M, split_target=split_target, g4=N % 8 == 0 and K % 8 == 0)
+    tuned = tuning.wgrad_config(N, K, M) if (N % 8 == 0 and K % 8 == 0 and split_target is None) else None
+    tile = tuned[0] if tuned else pick_tile(N, K, splits_ok=True, big_ok=True, K=M, split_target=split_target,
+                                            g4=N % 8 == 0 and K % 8 == 0)
     tiles = ((N + tile[0] - 1) // tile[0]) * ((K + tile[1] - 1) // tile[1])
 
     def run(C, splits, stride, beta):
         _gemm(dy2, x2, C, N, K, M, N, K, K, A_KOUT, B_KOUT, EPI_F32, tile, beta=beta, splits=splits,
               split_stride=stride)
-    _f32_out_splitk(run, N, K, M, tiles, gw.view(-1), accumulate, dy.device, split_target=split_target)
+    _f32_out_splitk(run, N, K, M, tiles, gw.view(-1), accumulate, dy.device, split_target=split_target,
+                    force_splits=tuned[1] if tuned else None)
 
 
 def bias_grad(dy: torch.Tensor, gb: torch.Tensor, accumulate: bool = False) -> None:
@@ -484,10 +488,15 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
         v = gw.view(g.K, Nn)
         v.add_(gwt) if accumulate else v.copy_(gwt)
         return
-    tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp,
-                     wide_ok=WIDE_WGRAD and not g.pointwise and g.C <= WIDE_WGRAD_MAX_C,
-                     g4=(G4_WGRAD or g.pointwise) and g.K % 8 == 0 and g.C % 8 == 0,
-                     narrow_ok=G4_WGRAD and not g.pointwise, rect_ok=g.pointwise)
+    # measured table first (pointwise = dense GEMM shapes, tools/wgrad_sweep.py), else the model
+    tuned = tuning.wgrad_config(g.K, Nn, Kp) if (g.pointwise and g.K % 8 == 0 and g.C % 8 == 0) else None
+    if splits is None and tuned is not None:
+        tile, splits = tuned
+    else:
+        tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp,
+                         wide_ok=WIDE_WGRAD and not g.pointwise and g.C <= WIDE_WGRAD_MAX_C,
+                         g4=(G4_WGRAD or g.pointwise) and g.K % 8 == 0 and g.C % 8 == 0,
+                         narrow_ok=G4_WGRAD and not g.pointwise, rect_ok=g.pointwise)
     tiles = ((g.K + tile[0] - 1) // tile[0]) * ((Nn + tile[1] - 1) // tile[1])
 
     def run(C, sp, stride, beta):

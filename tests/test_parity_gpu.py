@@ -51,6 +51,7 @@ def _transformer(dev):
 
 MODELS = {
     "resnet50": (_resnet, lambda m, d: _resnet_batch(m, d)),
+    "resnet50-1111": (_resnet_small, lambda m, d: _resnet_batch(m, d)),
     "bert": (_bert, lambda m, d: tuple(t.to(d) for t in m.synthetic_batch(4, "cpu", seed=5))),
     "transformer": (_transformer, lambda m, d: tuple(t.to(d) for t in m.synthetic_batch(4, "cpu", seed=5))),
 }
@@ -58,16 +59,23 @@ MODELS = {
 
 @pytest.mark.parametrize("which", list(MODELS))
 def test_per_parameter_gradient_cosine(which):
+    """resnet50: real init -- the zero-initialised residual-branch gammas (bn*_branch2c) block the
+    branch gradients at step 0, so the identity/projection paths, every BN and the classifier are
+    compared. resnet50-1111 (one bottleneck per stage: stem, projection + strided shortcuts, every
+    kernel variant) un-zeroes those gammas so every parameter's gradient is exercised.
+    (At full depth with non-zero branch gammas the stem's cosine is ~0.8 GPU-vs-CPU. That is the
+    network, not the kernels: in fp32 on the CPU alone, perturbing the weights by 1e-3 relative --
+    less than bf16 rounding -- drops it to 0.49 (tools/grad_parity_diag.py --perturb 1e-3,
+    profiles/grad_sensitivity_r2.md): a 16-block random-init ResNet with active branches is chaotic.)"""
     mk, batch = MODELS[which]
     grads = {}
     for dev in ("cpu", "cuda"):
         m = mk(dev)
-        # ResNet's zero-initialised residual-branch gammas (bn*_branch2c) block every branch
-        # gradient at step 0; give them a value so every parameter's gradient is exercised
-        for p in m.arena.params:
-            if p.name.endswith("/gamma") and float(p.master.abs().sum()) == 0.0:
-                p.master.fill_(0.5)
-        m.arena.refresh_compute()
+        if which != "resnet50":
+            for p in m.arena.params:
+                if p.name.endswith("/gamma") and float(p.master.abs().sum()) == 0.0:
+                    p.master.fill_(0.5)
+            m.arena.refresh_compute()
         loss, _ = m.forward_backward(*batch(m, dev))
         grads[dev] = {p.name: p.grad.detach().float().cpu().clone() for p in m.arena.params}
     gc, gg = grads["cpu"], grads["cuda"]
@@ -82,7 +90,7 @@ def test_per_parameter_gradient_cosine(which):
         c = _cos(gg[n], gc[n])
         if c < 0.99:
             worst.append((n, round(c, 4)))
-    assert checked >= 0.9 * len(gc), (checked, len(gc))
+    assert checked >= (0.25 if which == "resnet50" else 0.9) * len(gc), (checked, len(gc))
     assert not worst, worst
 
 
@@ -108,7 +116,7 @@ def _trajectory(which, dev, steps):
     return out
 
 
-@pytest.mark.parametrize("which", list(MODELS))
+@pytest.mark.parametrize("which", ["resnet50", "bert", "transformer"])
 def test_20_step_loss_trajectory_matches_cpu(which):
     lc = _trajectory(which, "cpu", 20)
     lg = _trajectory(which, "cuda", 20)

@@ -5,6 +5,8 @@ it times each (tile, splits) candidate including the split-K slab reduce, and pr
 next to what ops.gemm.pick_tile chooses today. Interleaved rounds, median (one process).
 
     python tools/wgrad_sweep.py [--iters 20] [--rounds 3] [--out gpurun_out/wgrad_sweep.jsonl]
+                                [--table tensorflow_k8s_amd/ops/tuned_wgrad.json]
+--table writes the winners as the runtime's autotuning table (ops/tuning.py).
 """
 import argparse
 import json
@@ -44,10 +46,14 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default="")
+    ap.add_argument("--table", default="", help="write the measured winners as ops/tuning.py's table")
     args = ap.parse_args()
+    from tensorflow_k8s_amd.ops import tuning
+    tuning.ENABLED = False  # time the analytic picker's choice, not the table's
     fh = open(args.out, "w") if args.out else None
     dev = "cuda"
     ws = torch.empty(512 * 2048 * 1024 + 4096, device=dev)
+    entries = []
     for M, N, K in SHAPES:
         dy = (torch.rand(K, M, device=dev) * 2 - 1).to(torch.bfloat16)
         x = (torch.rand(K, N, device=dev) * 2 - 1).to(torch.bfloat16)
@@ -91,6 +97,11 @@ def main():
         if fh:
             fh.write(json.dumps(row) + "\n")
             fh.flush()
+        entries.append({"M": M, "N": N, "K": K, "tile": list(best[0]), "splits": best[1], "us": row["best_us"],
+                        "picker_us": row["picked_us"]})
+    if args.table:
+        with open(args.table, "w") as f:
+            json.dump({"source": "tools/wgrad_sweep.py on MI355X", "entries": entries}, f, indent=1)
 
 
 if __name__ == "__main__":

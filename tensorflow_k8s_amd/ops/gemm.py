@@ -322,6 +322,21 @@ def _ref_conv(x, w, g: ConvGeom):
     return y.permute(0, 2, 3, 1)
 
 
+# Tile selection hooks for tools/conv_sweep.py: FORCE_TILE overrides every conv fwd / dgrad GEMM
+# tile; RECORD (a list) collects (kind, geometry, flags) of every such call.
+FORCE_TILE = None
+RECORD = None
+
+
+def _conv_tile(kind: str, g: ConvGeom, default, flags=()):
+    if RECORD is not None:
+        RECORD.append((kind, tuple(g.vec()), tuple(flags)))
+    if FORCE_TILE is not None:
+        return FORCE_TILE
+    t = tuning.conv_tile(kind, tuple(g.vec()))
+    return t if t is not None else default()
+
+
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor | None = None,
              shards: int = 1, bias: torch.Tensor | None = None, act: str | None = None) -> torch.Tensor:
     """y[N,P,Q,K] = act(conv(x[N,H,W,C], w[K,R,S,C]) + bias); optionally accumulates BN batch
@@ -338,8 +353,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
         return y.to(torch.bfloat16).contiguous()
     M = g.N * g.P * g.Q
     y = torch.empty(g.N, g.P, g.Q, g.K, dtype=torch.bfloat16, device=x.device)
-    tile = pick_tile(M, g.K, big_ok=g.pointwise, K=g.R * g.S * g.C, mid_ok=g.pointwise,
-                     g4=g.pointwise or g.C % 64 == 0)
+    tile = _conv_tile("fwd", g, lambda: pick_tile(M, g.K, big_ok=g.pointwise, K=g.R * g.S * g.C, mid_ok=g.pointwise,
+                                                  g4=g.pointwise or g.C % 64 == 0),
+                      (stats is not None, bias is not None, act is not None))
     if g.pointwise:
         _gemm(x, w, y, M, g.K, g.C, g.C, g.C, g.K, A_KIN, B_KIN, EPI_BF16, tile, stats=stats, shards=shards,
               bias=bias, act=ACT[act])
@@ -432,7 +448,11 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
         return dx
     M = g.N * g.H * g.W
     dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
-    tile = pick_tile(M, g.C, big_ok=g.pointwise, K=g.K, mid_ok=g.pointwise, g4=g.pointwise and g.C % 8 == 0)
+    def _default_tile():
+        return pick_tile(M, g.C, big_ok=g.pointwise, K=g.K, mid_ok=g.pointwise, g4=g.pointwise and g.C % 8 == 0)
+    flags = (resid is not None, bnr is not None, bnr is not None and bnr.a is not None,
+             bnr is not None and bnr.y2 is not None, resid_stride)
+    tile = _conv_tile("dgrad_pw", g, _default_tile, flags) if (g.pointwise and resid_stride == 1) else _default_tile()
     if resid_stride > 1:
         if not g.pointwise or bnr is None or resid is None:
             raise ValueError("resid_stride needs a pointwise conv, a resid and the fused BN reduction")
@@ -450,7 +470,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
         wf = conv_weight_t(w, g, flip=True)  # [C][R][S][K]: the forward conv's OHWI weight
         Kd = g.R * g.S * g.K
         _gemm(dy, wf, dx, M, g.C, Kd, 0, Kd, g.C, A_CONV_FWD, B_KIN, EPI_BF16,
-              pick_tile(M, g.C, K=Kd, mid_ok=False, g4=True), resid=resid, conv=f.vec(), bnr=bnr)
+              _conv_tile("dgrad_fwd", g, lambda: pick_tile(M, g.C, K=Kd, mid_ok=False, g4=True), flags),
+              resid=resid, conv=f.vec(), bnr=bnr)
         return dx
     phases = _phases(g) if (bnr is not None and (g.sh > 1 or g.sw > 1)) else None
     if phases is not None:

@@ -1,5 +1,10 @@
-"""Measured GEMM configurations (autotuning table) for shapes whose best tile / split-K count the
+"""Measured GEMM configurations (autotuning tables) for shapes whose best tile / split-K count the
 analytic picker (ops.gemm.pick_tile) gets wrong.
+
+* ``tuned_wgrad.json`` (tools/wgrad_sweep.py): weight-gradient GEMMs, tile + split-K;
+* ``tuned_conv.json`` (tools/conv_sweep.py): the tile of every conv forward ("fwd"), pointwise
+  dgrad ("dgrad_pw") and stride-1 dgrad-as-forward ("dgrad_fwd") GEMM, keyed by the conv geometry
+  and timed with the model's own epilogue (BN statistics / fused BN-backward reduction).
 
 The table is produced ON an MI355X by ``tools/wgrad_sweep.py --table`` (every tile x split-K
 candidate timed including the split-K slab reduce, interleaved rounds, median) and shipped as
@@ -14,7 +19,9 @@ import json
 import os
 
 _PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_wgrad.json")
+_CONV_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_conv.json")
 _TABLE: dict | None = None
+_CONV: dict | None = None
 ENABLED = os.environ.get("TFK_TUNING", "1") != "0"
 
 
@@ -36,3 +43,23 @@ def wgrad_config(M: int, N: int, K: int):
     if not ENABLED:
         return None
     return _load().get((M, N, K))
+
+
+def _load_conv() -> dict:
+    global _CONV
+    if _CONV is None:
+        _CONV = {}
+        try:
+            with open(_CONV_PATH) as f:
+                for e in json.load(f)["entries"]:
+                    _CONV[(e["kind"], tuple(int(v) for v in e["geom"]))] = tuple(e["tile"])
+        except (OSError, ValueError, KeyError):
+            _CONV = {}
+    return _CONV
+
+
+def conv_tile(kind: str, geom: tuple):
+    """Measured best tile of a conv GEMM (kind: fwd | dgrad_pw | dgrad_fwd), or None."""
+    if not ENABLED:
+        return None
+    return _load_conv().get((kind, tuple(geom)))

@@ -16,6 +16,7 @@ int tfk_gemm_splits(int K, int splits);
 void tfk_gemm_set_persist(int on);
 void tfk_gemm_set_engine(int e);
 void tfk_g4_set_shortk(int on);
+extern "C" void tfk_fp8_set_engine(int e);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_quant_t(const void*, void*, void*, int, int, hipStream_t);
 int tfk_mx_probe(const int*, const int*, const int*, const int*, float*, hipStream_t);
@@ -248,6 +249,7 @@ int64_t gemm_splits(int K, int splits) { return tfk_gemm_splits(K, splits); }
 void gemm_set_persist(int on) { tfk_gemm_set_persist(on); }
 void gemm_set_engine(int e) { tfk_gemm_set_engine(e); }
 void gemm_set_shortk(int on) { tfk_g4_set_shortk(on); }
+void fp8_set_engine(int e) { tfk_fp8_set_engine(e); }
 
 void mx_probe(torch::Tensor X, torch::Tensor Y, torch::Tensor sx, torch::Tensor sy, torch::Tensor D) {
   for (auto* t : {&X, &Y}) { need(*t, at::kInt, "probe operand"); need_numel(*t, 64 * 8, "probe operand"); }
@@ -607,6 +609,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_persist", &gemm_set_persist);
   m.def("gemm_set_engine", &gemm_set_engine);
   m.def("gemm_set_shortk", &gemm_set_shortk);
+  m.def("fp8_set_engine", &fp8_set_engine);
   m.def("mx_quant", &mx_quant);
   m.def("mx_quant_t", &mx_quant_t);
   m.def("mx_probe", &mx_probe);

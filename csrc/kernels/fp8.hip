@@ -267,7 +267,18 @@ int tfk_mx_quant(const void* x, void* q, void* s, long long nblocks, hipStream_t
 // C[M][N] = epilogue(A q[M][K] x B q[N][K]^T), scales in p.a_scale / p.b_scale.
 // ext: 0 bf16 (bias/act/resid), 1 bf16 EXT (aux, dropout, activation backward), 2 f32 (alpha/beta:
 // weight gradients accumulate into the f32 arena).
+extern "C" int tfk_g4_fp8_launch(const GemmParams& p, int epi, int splits, hipStream_t stream);
+static int g_fp8_engine = -1;  // 1 = g4 LDS-DMA engine (TFK_FP8_ENGINE=g4), 0 = register-staged kernel below
+extern "C" void tfk_fp8_set_engine(int e) { g_fp8_engine = e; }
 int tfk_gemm_mxfp8(GemmParams p, int ext, hipStream_t st) {
+  if (g_fp8_engine < 0) {
+    const char* e = getenv("TFK_FP8_ENGINE");
+    g_fp8_engine = (e && e[0] == 'g') ? 1 : 0;
+  }
+  if (g_fp8_engine == 1) {
+    const int r = tfk_g4_fp8_launch(p, ext == 2 ? EPI_F32 : (ext ? EPI_BF16_EXT : EPI_BF16), 1, st);
+    if (r != -1) return r;
+  }
   const int BM = 128, BN = 128;
   p.tiles_n = (p.N + BN - 1) / BN;
   if (p.stats_shards < 1) p.stats_shards = 1;

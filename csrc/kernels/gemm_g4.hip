@@ -43,6 +43,17 @@ __device__ __forceinline__ unsigned fdiv(unsigned x, unsigned mul, int shift) { 
 
 __device__ __forceinline__ int swz64(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
 
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// Two 16-B fragment halves -> the 32-B operand of one scaled fp8 MFMA (16x16x128).
+__device__ __forceinline__ i32x8 pack8(bf16x8 lo, bf16x8 hi) {
+  const u32x4 a = __builtin_bit_cast(u32x4, lo), b = __builtin_bit_cast(u32x4, hi);
+  i32x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
 // Fragment (16 image rows from rb, K-half kk) of an operand image with ROWS rows.
 template <bool KO>
 __device__ __forceinline__ bf16x8 frag(const char* img, int rb, int kk) {
@@ -281,6 +292,124 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
   gemm_epilogue<BM, BN, NTH, WGM, EPI, (SHORTK ? 1 : 0)>(p, acc, smem, m0, n0, bz);
 }
 
+// ---------------------------------------------------------------------------------------------
+// MX-fp8 on the g4 engine: A [M][K] and B [N][K] e4m3 bytes (both K-inner), e8m0 scales [rows][K/32].
+// A K-tile is 128 fp8 bytes per row -- byte-for-byte the 128-B row image of a bf16 BK=64 tile, so
+// the LDS-DMA Loader and the XOR-swizzled image are reused unchanged (driven with bf16-equivalent
+// strides: K/2, ld/2). One v_mfma_scale_f32_16x16x128_f8f6f4 consumes a whole K-tile row pair
+// (lane (row l&15, group g = l>>4) holds 16-B chunks g and g+4 = the two K-halves of the bf16
+// fragment reader), at twice the bf16 MFMA rate. The 4 scale bytes of a row's K-tile are one u32,
+// loaded from global one tile ahead (L2-resident, 4 B per row per 128 K) into registers; lane group
+// g uses byte g. 4-wave 128x128 blocks (64x64 wave tiles), 2 LDS stages, shared epilogue.
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__((nwaves<BM, BN>() * 64), (occ_default<BM, BN>())) void g4_fp8_kernel(GemmParams p,
+                                                                                               int sld) {
+  constexpr int NW = nwaves<BM, BN>(), NTH = NW * 64, WGM = BM / 64, WGN = BN / 64;
+  constexpr int FM = 4, FN = 4;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int MAIN = 2 * STAGE, EPIB = epi_lds_bytes<BM, BN, WGM>();
+  __shared__ __attribute__((aligned(16))) char smem[MAIN > EPIB ? MAIN : EPIB];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WGN, wn = w % WGN;
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 4;
+  const int grp = tile / (GM * p.tiles_n), first_m = grp * GM;
+  const int gm = min(GM, tiles_m - first_m), inr = tile - grp * GM * p.tiles_n;
+  const int m0 = (first_m + inr % gm) * BM, n0 = (inr / gm) * BN;
+  // p.K / p.lda / p.ldb arrive in bf16-equivalent units (bytes / 2): the Loader's byte math holds
+  const int nkt = (p.K + BK - 1) / BK;
+  const int kt0 = blockIdx.z * p.kt_per_split;
+  const int kt1 = min(nkt, kt0 + p.kt_per_split);
+  const char* Ab = (const char*)p.A + (long long)m0 * p.lda * 2;
+  const char* Bb = (const char*)p.B + (long long)n0 * p.ldb * 2;
+  const int lim_a = p.M - m0, lim_b = p.N - n0;
+  Loader<BM, KIN, NW> la;
+  Loader<BN, KIN, NW> lb;
+  la.init(p, lane, w, p.lda, m0, p.M);
+  lb.init(p, lane, w, p.ldb, n0, p.N);
+
+  // scale rows of this lane's fragments (clamped: rows past M/N multiply zero-filled operands)
+  const int g = lane >> 4, li = lane & 15;
+  const unsigned* sa_row[FM];
+  const unsigned* sb_row[FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+    sa_row[i] = (const unsigned*)((const unsigned char*)p.a_scale + (long long)min(m0 + wm * 64 + i * 16 + li, p.M - 1) * sld);
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+    sb_row[j] = (const unsigned*)((const unsigned char*)p.b_scale + (long long)min(n0 + wn * 64 + j * 16 + li, p.N - 1) * sld);
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage_ptr = [&](int st) { return smem + st * STAGE; };
+  unsigned sa[FM], sb[FN];
+  if (kt0 < kt1) {
+    la.issue(p, Ab, BK * 2, kt0, lim_a, stage_ptr(0), w, lane);
+    lb.issue(p, Bb, BK * 2, kt0, lim_b, stage_ptr(0) + A_BYTES, w, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) sa[i] = sa_row[i][kt0];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) sb[j] = sb_row[j][kt0];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  const int ar = wm * 64, bc = wn * 64;
+
+#pragma unroll 1
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int st = (kt - kt0) & 1;
+    const char* As = stage_ptr(st);
+    const char* Bs = As + A_BYTES;
+    const bool more = kt + 1 < kt1;
+    unsigned sa_n[FM], sb_n[FN];
+    if (more) {
+      char* nx = stage_ptr(st ^ 1);
+      la.issue(p, Ab, BK * 2, kt + 1, lim_a, nx, w, lane);
+      lb.issue(p, Bb, BK * 2, kt + 1, lim_b, nx + A_BYTES, w, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) sa_n[i] = sa_row[i][kt + 1];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) sb_n[j] = sb_row[j][kt + 1];
+    }
+    i32x8 bfr[FN];
+    int scb[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const bf16x8 lo = frag<false>(Bs, bc + j * 16, 0), hi = frag<false>(Bs, bc + j * 16, 1);
+      bfr[j] = pack8(lo, hi);
+      scb[j] = (sb[j] >> (8 * g)) & 0xff;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const bf16x8 lo = frag<false>(As, ar + i * 16, 0), hi = frag<false>(As, ar + i * 16, 1);
+      const i32x8 a = pack8(lo, hi);
+      const int sca = (sa[i] >> (8 * g)) & 0xff;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], a, acc[i][j], 0, 0, 0, scb[j], 0, sca);
+    }
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) sa[i] = sa_n[i];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) sb[j] = sb_n[j];
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  __syncthreads();
+  gemm_epilogue<BM, BN, NTH, WGM, EPI>(p, acc, smem, m0, n0, 0);
+}
+
 }  // namespace g4
 }  // namespace tfk
 
@@ -384,4 +513,33 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
   TFK_G4_NARROW(0, 0, EPI_BF16)
   TFK_G4_NARROW(0, 1, EPI_BF16)
   return -1;
+}
+
+// MX-fp8 GEMM on the g4 engine. p in BYTES (K, lda, ldb = bytes per row); needs K % 128 == 0,
+// lda/ldb % 16 == 0 and 16-B aligned operands. Returns -1 when not eligible (caller falls back).
+extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hipStream_t stream) {
+  GemmParams p = p_in;
+  if ((p.K & 127) || (p.lda & 15) || (p.ldb & 15) || (((uintptr_t)p.A | (uintptr_t)p.B) & 15) ||
+      (((uintptr_t)p.a_scale | (uintptr_t)p.b_scale) & 3))
+    return -1;
+  const int sld = p.K / 32;
+  p.K /= 2;
+  p.lda /= 2;
+  p.ldb /= 2;
+  const int nkt = (p.K + g4::BK - 1) / g4::BK;
+  if (splits < 1) splits = 1;
+  if (splits > nkt) splits = nkt;
+  p.kt_per_split = (nkt + splits - 1) / splits;
+  splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
+  p.tiles_n = (p.N + 127) / 128;
+  const int tiles = ((p.M + 127) / 128) * p.tiles_n;
+  if (p.stats_shards < 1) p.stats_shards = 1;
+  const dim3 grid(tiles, 1, splits), block(g4::nwaves<128, 128>() * 64);
+  if (epi == EPI_F32)
+    hipLaunchKernelGGL((g4::g4_fp8_kernel<128, 128, EPI_F32>), grid, block, 0, stream, p, sld);
+  else if (epi == EPI_BF16_EXT)
+    hipLaunchKernelGGL((g4::g4_fp8_kernel<128, 128, EPI_BF16_EXT>), grid, block, 0, stream, p, sld);
+  else
+    hipLaunchKernelGGL((g4::g4_fp8_kernel<128, 128, EPI_BF16>), grid, block, 0, stream, p, sld);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }

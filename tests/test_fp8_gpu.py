@@ -125,3 +125,34 @@ def test_fp8_training_tracks_bf16_200_steps():
     assert b[-1] < 0.5 * b[0] and f[-1] < 0.5 * f[0], (b[::20], f[::20])
     mb, mf = sum(b[-20:]) / 20, sum(f[-20:]) / 20
     assert abs(mf - mb) <= 0.05 * mb + 0.02, (b[::20], f[::20])
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 1024, 1024), (300, 200, 256), (1000, 520, 384)])
+def test_g4_fp8_engine_matches_register_engine(M, N, K):
+    """The LDS-DMA (g4) MX-fp8 kernel and the register-staged one run the same quantized operands
+    through the same scaled MFMAs in the same K order: results agree to f32 rounding, for the bf16
+    (bias/relu/residual), EXT (GELU-backward) and f32 (accumulate) epilogues, incl. ragged M/N."""
+    from tensorflow_k8s_amd.ops._lib import lib
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16).cuda()
+    b = (torch.randn(N, generator=g) * 0.1).cuda()
+    r = torch.randn(M, N, generator=g).to(torch.bfloat16).cuda()
+    z = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+    dy = torch.randn(M, N, generator=g).to(torch.bfloat16).cuda()
+    out = {}
+    try:
+        for eng in (1, 0):
+            lib().fp8_set_engine(eng)
+            y = F8.linear_fwd_mx(x, w, b, act="relu", resid=r)
+            dx = F8.linear_dgrad_mx(dy, w, dact_src=z, dact="gelu") if N % 128 == 0 else None
+            gw = torch.ones(N, K, device="cuda")
+            if M % 128 == 0:
+                F8.linear_wgrad_mx(dy, x, gw, accumulate=True)
+            torch.cuda.synchronize()
+            out[eng] = (y, dx, gw)
+    finally:
+        lib().fp8_set_engine(0)
+    for a, c in zip(out[1], out[0]):
+        if a is not None:
+            assert rel(a, c) < 1e-5, rel(a, c)

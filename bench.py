@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--graph", type=int, default=-1, help="capture step in a hipGraph (default: on for 1 GPU)")
     ap.add_argument("--force-comm", action="store_true",
                     help="1 GPU: still run the RCCL gradient all-reduce (world-size-1 process group)")
-    ap.add_argument("--fp8", type=int, default=0, help="transformer models: MX-fp8 forward GEMMs")
+    ap.add_argument("--fp8", type=int, default=0, help="transformer models: MX-fp8 linear GEMMs (fwd, dgrad, wgrad)")
     ap.add_argument("--via-operator", action="store_true",
                     help="measure through a TFJob: tfk-cluster gang-schedules one pod per GPU (TF_CONFIG rendezvous)")
     ap.add_argument("--tfjob-worker", action="store_true", help=argparse.SUPPRESS)  # a pod of --via-operator
@@ -146,7 +146,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "step_ms": dist_ms, "per_rank_ms": per_rank,
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": _token_baseline(args.model, toks / (ms / 1000.0), world),
-            "dtype": "bf16+mxfp8-fwd" if args.fp8 else "bf16",
+            "dtype": "bf16+mxfp8" if args.fp8 else "bf16",
             "data": "synthetic token ids, random-init weights",
             "config": {"model": args.model, "global_batch": gb, "seq_len": seq, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (RCCL all-reduce)",

@@ -28,6 +28,8 @@ class ApiServer {
   void add_token(const std::string& token, const std::string& user) { tokens_[token] = user; }
   bool tls() const { return http_.tls(); }
   long long connections_accepted() const { return http_.connections_accepted(); }
+  long long connections_rejected() const { return http_.connections_rejected(); }
+  void set_max_connections(int n) { http_.set_max_connections(n); }
   void stop() { http_.stop(); }
   int port() const { return http_.port(); }
   Store& store() { return *store_; }

@@ -1,5 +1,9 @@
 #include "store.h"
 
+#include <unistd.h>
+
+#include <fcntl.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -158,7 +162,8 @@ void Watcher::deliver(const WatchEvent& ev) {
 }
 
 // ------------------------------------------------------------------------------ store
-Store::Store(const std::string& wal_path, size_t history) : history_cap_(history), wal_path_(wal_path) {
+Store::Store(const std::string& wal_path, size_t history, WalOptions wal_opts)
+    : history_cap_(history), wal_path_(wal_path), wal_opts_(std::move(wal_opts)) {
   auto core = [&](const char* plural, const char* singular, const char* kind, bool ns) {
     register_resource({"", "v1", plural, singular, kind, ns, {"v1"}, {}});
   };
@@ -178,11 +183,32 @@ Store::Store(const std::string& wal_path, size_t history) : history_cap_(history
   if (!wal_path_.empty()) {
     replay_wal();
     wal_ = fopen(wal_path_.c_str(), "a");
+    if (wal_opts_.sync == "interval") syncer_ = std::thread([this] { syncer_loop(); });
+  }
+}
+
+void Store::syncer_loop() {
+  while (!syncer_stop_.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(std::max<int64_t>(1, wal_opts_.sync_interval_ms)));
+    if (!wal_dirty_.exchange(false)) continue;
+    int fd = -1;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (wal_) fd = fileno(wal_);  // records are already fflush'ed under the lock
+      if (fd >= 0) ops_["wal_fsync"]++;
+    }
+    if (fd >= 0) fdatasync(fd);
   }
 }
 
 Store::~Store() {
-  if (wal_) fclose(wal_);
+  syncer_stop_ = true;
+  if (syncer_.joinable()) syncer_.join();
+  if (wal_) {
+    fflush(wal_);
+    if (wal_opts_.sync != "none") fdatasync(fileno(wal_));
+    fclose(wal_);
+  }
   std::lock_guard<std::mutex> g(mu_);
   for (auto& w : watchers_)
     if (auto s = w.lock()) s->close();
@@ -294,6 +320,61 @@ void Store::wal_locked(const std::string& op, const std::string& plural, const J
   std::string line = rec.dump() + "\n";
   fwrite(line.data(), 1, line.size(), wal_);
   fflush(wal_);
+  ++wal_records_;
+  if (wal_opts_.sync == "always") {
+    fdatasync(fileno(wal_));
+    ops_["wal_fsync"]++;
+  } else {
+    wal_dirty_ = true;
+  }
+  if (wal_opts_.compact_records > 0 && wal_records_ >= wal_opts_.compact_records) {
+    size_t live = 0;
+    for (auto& kv : data_) live += kv.second.size();
+    if (wal_records_ > 2 * live) compact_wal_locked();
+  }
+}
+
+void Store::compact_wal_locked() {
+  const std::string tmp = wal_path_ + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "w");
+  if (!f) return;
+  size_t n = 0;
+  auto put = [&](const std::string& op, const std::string& plural, const Json& obj) {
+    Json rec = Json::object();
+    rec["op"] = op;
+    rec["plural"] = plural;
+    rec["object"] = obj;
+    std::string line = rec.dump() + "\n";
+    fwrite(line.data(), 1, line.size(), f);
+    ++n;
+  };
+  // resource-version high-water mark first: deleted objects' versions must never be reissued
+  Json mark = Json::object();
+  mark["metadata"]["resourceVersion"] = std::to_string(rv_ - 1);
+  put("rv", "", mark);
+  for (auto& kv : data_)  // CRDs first so their resources are registered before their objects
+    if (kv.first == "customresourcedefinitions")
+      for (auto& o : kv.second) put("crd", kv.first, o.second.data);
+  for (auto& kv : data_)
+    if (kv.first != "customresourcedefinitions")
+      for (auto& o : kv.second) put("put", kv.first, o.second.data);
+  fflush(f);
+  const bool ok = fdatasync(fileno(f)) == 0;
+  fclose(f);
+  if (!ok || rename(tmp.c_str(), wal_path_.c_str()) != 0) {
+    unlink(tmp.c_str());
+    return;
+  }
+  std::string dir = wal_path_.substr(0, wal_path_.find_last_of('/') == std::string::npos ? 0 : wal_path_.find_last_of('/'));
+  int dfd = open(dir.empty() ? "." : dir.c_str(), O_RDONLY | O_DIRECTORY);
+  if (dfd >= 0) {
+    fsync(dfd);  // the rename itself is durable
+    ::close(dfd);
+  }
+  fclose(wal_);
+  wal_ = fopen(wal_path_.c_str(), "a");
+  wal_records_ = n;
+  ops_["wal_compactions"]++;
 }
 
 void Store::replay_wal() {
@@ -313,7 +394,9 @@ void Store::replay_wal() {
       std::string ns = obj.path("metadata.namespace").str(), name = obj.path("metadata.name").str();
       int64_t rv = std::stoll(obj.path("metadata.resourceVersion").str("0"));
       std::lock_guard<std::mutex> g(mu_);
-      if (op == "delete") data_[plural].erase(key(ns, name));
+      ++wal_records_;
+      if (op == "rv") {}  // compaction's resource-version high-water mark (applied below)
+      else if (op == "delete") data_[plural].erase(key(ns, name));
       else data_[plural][key(ns, name)] = Obj{obj, rv};
       if (op == "crd") {
         ResourceInfo ri;

@@ -7,6 +7,8 @@
 //   finalizers (delete -> deletionTimestamp, removal when the list empties), ownerReference
 //   cascading garbage collection, CRD registry + TFJob version conversion, optional JSON-lines WAL.
 #pragma once
+#include <atomic>
+#include <thread>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -86,6 +88,7 @@ class Watcher {
   void close();
   bool closed() const { return closed_; }
   void deliver(const WatchEvent& ev);  // applies ns/selector filters
+  void max_queue_for_test(size_t n) { max_queue_ = n; }
   const std::string& plural() const { return plural_; }
   std::string requested_version;       // convert objects to this version (TFJobs)
 
@@ -101,9 +104,21 @@ class Watcher {
   size_t max_queue_ = 100000;
 };
 
+// Write-ahead-log durability (etcd's WAL discipline, scaled down): every mutation is appended and
+// flushed to the page cache under the store lock; fdatasync is per record ("always"), batched by a
+// background syncer every sync_interval_ms ("interval", group commit: a crash loses at most that
+// window) or left to the kernel ("none"). The log is compacted into a snapshot of the live objects
+// (plus the resource-version high-water mark) once it holds compact_records records and more than
+// twice as many records as live objects: written to <wal>.tmp, fdatasync'ed, renamed over the WAL.
+struct WalOptions {
+  std::string sync = "interval";  // always | interval | none
+  int64_t sync_interval_ms = 100;
+  size_t compact_records = 20000;
+};
+
 class Store {
  public:
-  explicit Store(const std::string& wal_path = "", size_t history = 10000);
+  explicit Store(const std::string& wal_path = "", size_t history = 10000, WalOptions wal_opts = WalOptions());
   ~Store();
 
   void register_resource(const ResourceInfo& ri);
@@ -145,6 +160,8 @@ class Store {
   void emit_locked(const std::string& plural, const std::string& type, const Json& obj, int64_t rv);
   void wal_locked(const std::string& op, const std::string& plural, const Json& obj);
   void replay_wal();
+  void compact_wal_locked();
+  void syncer_loop();
   ApiStatus finish_delete_locked(const std::string& plural, const std::string& ns, const std::string& name,
                                  const std::string& propagation, Json* out);
   void gc_dependents_locked(const std::string& owner_uid, const std::string& ns);
@@ -161,6 +178,10 @@ class Store {
   std::string wal_path_;
   FILE* wal_ = nullptr;
   bool replaying_ = false;
+  WalOptions wal_opts_;
+  size_t wal_records_ = 0;
+  std::atomic<bool> wal_dirty_{false}, syncer_stop_{false};
+  std::thread syncer_;
   std::map<std::string, long long> ops_;
 };
 

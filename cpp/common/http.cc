@@ -346,6 +346,18 @@ void HttpServer::accept_loop() {
     char ip[64];
     inet_ntop(AF_INET, &a.sin_addr, ip, sizeof ip);
     std::string peer = std::string(ip) + ":" + std::to_string(ntohs(a.sin_port));
+    if (active_.load() >= max_conns_) {
+      // every connection owns a thread (watches are long-lived): shed load instead of exhausting
+      // threads/fds; clients retry (informers relist with backoff)
+      static const char k503[] = "HTTP/1.1 503 Service Unavailable\r\nContent-Length: 0\r\nConnection: close\r\n\r\n";
+      if (!tls_) {
+        ssize_t wr = ::send(fd, k503, sizeof(k503) - 1, MSG_NOSIGNAL);
+        (void)wr;
+      }
+      ::close(fd);
+      rejected_++;
+      continue;
+    }
     active_++;
     accepted_++;
     std::thread([this, fd, peer] {

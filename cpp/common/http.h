@@ -117,6 +117,9 @@ class HttpServer {
   void serve(HttpHandler h);  // spawns the accept thread
   void stop();
   long long connections_accepted() const { return accepted_.load(); }
+  long long connections_rejected() const { return rejected_.load(); }
+  int connections_active() const { return active_.load(); }
+  void set_max_connections(int n) { max_conns_ = n > 0 ? n : 1; }
 
  private:
   void accept_loop();
@@ -126,6 +129,8 @@ class HttpServer {
   std::atomic<bool> stopping_{false};
   std::atomic<int> active_{0};
   std::atomic<long long> accepted_{0};
+  std::atomic<long long> rejected_{0};
+  int max_conns_ = 4096;
   HttpHandler handler_;
   std::thread accept_thr_;
   std::shared_ptr<TlsContext> tls_;

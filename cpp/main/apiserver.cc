@@ -7,13 +7,18 @@
 int main(int argc, char** argv) {
   using namespace tfk;
   std::string host = "127.0.0.1", wal, log_root, level = "info", port_file, tls_cert, tls_key, token_file;
-  long long port = 8080, history = 10000;
+  long long port = 8080, history = 10000, compact = 20000, sync_ms = 100, max_conns = 4096;
+  std::string wal_sync = "interval";
   bool json = false;
   FlagSet fs("tfk-apiserver");
   fs.add_string("host", &host, "bind address");
   fs.add_int("port", &port, "port (0 = ephemeral)");
   fs.add_string("wal", &wal, "JSON-lines write-ahead log for persistence (optional)");
   fs.add_int("watch-history", &history, "events kept for watch resume (older -> 410 Gone)");
+  fs.add_string("wal-sync", &wal_sync, "WAL fdatasync: always | interval (group commit) | none");
+  fs.add_int("wal-sync-interval-ms", &sync_ms, "group-commit interval for --wal-sync=interval");
+  fs.add_int("wal-compact-records", &compact, "compact the WAL into a snapshot past this many records (0 = never)");
+  fs.add_int("max-connections", &max_conns, "concurrent connections before new ones get 503");
   fs.add_string("port-file", &port_file, "write the bound port here");
   fs.add_bool("json-log-format", &json, "JSON logs");
   fs.add_string("log-level", &level, "log level");
@@ -26,7 +31,15 @@ int main(int argc, char** argv) {
   InitLogging("tfk-apiserver", json, level);
   StopToken stop;
   HandleSignals(stop);
-  auto store = std::make_shared<Store>(wal, (size_t)history);
+  if (wal_sync != "always" && wal_sync != "interval" && wal_sync != "none") {
+    fprintf(stderr, "--wal-sync must be always|interval|none\n");
+    return 2;
+  }
+  WalOptions wo;
+  wo.sync = wal_sync;
+  wo.sync_interval_ms = sync_ms;
+  wo.compact_records = (size_t)compact;
+  auto store = std::make_shared<Store>(wal, (size_t)history, wo);
   install_tfjob_crd(*store);
   ApiServer srv(store);
   if (!tls_cert.empty()) {
@@ -37,6 +50,7 @@ int main(int argc, char** argv) {
     if (!srv.enable_tls(o, &err)) { TFK_LOG(Error, "tls: " + err); return 1; }
   }
   if (!token_file.empty() && !srv.load_token_file(token_file, &err)) { TFK_LOG(Error, err); return 1; }
+  srv.set_max_connections((int)max_conns);
   if (!srv.start(host, (int)port, &err)) { TFK_LOG(Error, "cannot start: " + err); return 1; }
   const std::string scheme = srv.tls() ? "https://" : "http://";
   TFK_LOG(Info, "serving", Json(Json::object_t{{"url", Json(scheme + host + ":" + std::to_string(srv.port()))}}));

@@ -3,6 +3,9 @@
 // replicas_test.go: images/tf3.PNG:L8-L17). Run: build/bin/tfk-unit-tests [filter]
 // Exit status 0 only if every selected test passes. Also built under TSan/ASan (make SAN=...).
 #include <unistd.h>
+#include <sys/socket.h>
+#include <netinet/in.h>
+#include <arpa/inet.h>
 
 #include <atomic>
 #include <chrono>
@@ -265,6 +268,107 @@ TEST(store_gc_terminating_dependent_survives_wal_replay) {
   CHECK(s2.get("pods", "default", "child", &out).ok());
   CHECK(!out.path("metadata.deletionTimestamp").is_null());
   unlink(path.c_str());
+}
+
+TEST(wal_compaction_snapshot_replays_identically) {
+  char tmpl[] = "/tmp/tfk-wal-XXXXXX";
+  std::string dir = mkdtemp(tmpl);
+  std::string wal = dir + "/wal.jsonl";
+  WalOptions wo;
+  wo.sync = "always";
+  wo.compact_records = 40;
+  int64_t rv_before = 0;
+  {
+    Store st(wal, 1000, wo);
+    Json out;
+    for (int i = 0; i < 5; ++i) {
+      Json cm = J(R"({"apiVersion":"v1","kind":"ConfigMap","metadata":{"name":""},"data":{"v":"0"}})");
+      cm["metadata"]["name"] = "cm" + std::to_string(i);
+      CHECK(st.create("configmaps", "default", cm, &out).ok());
+    }
+    for (int r = 0; r < 60; ++r) {  // 300 updates of 5 live objects -> several compactions
+      for (int i = 0; i < 5; ++i) {
+        Json cur;
+        CHECK(st.get("configmaps", "default", "cm" + std::to_string(i), &cur).ok());
+        cur["data"]["v"] = std::to_string(r);
+        CHECK(st.update("configmaps", "default", "cm" + std::to_string(i), cur, false, &out).ok());
+      }
+    }
+    CHECK(st.remove("configmaps", "default", "cm4", "Background", &out).ok());
+    rv_before = st.resource_version();
+    CHECK(st.counters()["wal_compactions"] > 0);
+    CHECK(st.counters()["wal_fsync"] > 300);
+  }
+  size_t lines = 0;
+  {
+    FILE* f = fopen(wal.c_str(), "r");
+    char buf[65536];
+    while (fgets(buf, sizeof buf, f)) lines++;
+    fclose(f);
+  }
+  CHECK(lines < 80);  // compacted: snapshot + the tail since the last compaction, not 306 records
+  Store st2(wal, 1000, wo);
+  Json cur;
+  CHECK(st2.get("configmaps", "default", "cm2", &cur).ok());
+  CHECK_EQ(cur.path("data.v").str(), std::string("59"));
+  CHECK(!st2.get("configmaps", "default", "cm4", &cur).ok());
+  CHECK(st2.resource_version() >= rv_before);  // deleted objects' versions are never reissued
+  unlink(wal.c_str());
+  rmdir(dir.c_str());
+}
+
+TEST(slow_watcher_is_dropped_others_unaffected) {
+  auto store = new_store();
+  ApiStatus st;
+  auto slow = store->watch("configmaps", "default", 0, LabelSelector(), FieldSelector(), &st);
+  auto fast = store->watch("configmaps", "default", 0, LabelSelector(), FieldSelector(), &st);
+  slow->max_queue_for_test(16);
+  Json out;
+  int seen = 0;
+  for (int i = 0; i < 40; ++i) {
+    Json cm = J(R"({"apiVersion":"v1","kind":"ConfigMap","metadata":{"name":""}})");
+    cm["metadata"]["name"] = "c" + std::to_string(i);
+    CHECK(store->create("configmaps", "default", cm, &out).ok());
+    WatchEvent ev;
+    while (fast->next(&ev, 0)) seen++;  // the fast consumer keeps up
+  }
+  CHECK(slow->closed());  // over its queue bound: terminated, the client relists
+  WatchEvent ev;
+  CHECK(!slow->next(&ev, 0));
+  CHECK(!fast->closed());
+  CHECK_EQ(seen, 40);
+}
+
+TEST(http_server_sheds_connections_over_the_cap) {
+  auto store = new_store();
+  ApiServer srv(store);
+  srv.set_max_connections(2);
+  std::string err;
+  CHECK(srv.start("127.0.0.1", 0, &err));
+  std::vector<int> held;
+  for (int i = 0; i < 2; ++i) {  // two idle keep-alive connections occupy the cap
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)srv.port());
+    inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+    CHECK(connect(fd, (sockaddr*)&a, sizeof a) == 0);
+    held.push_back(fd);
+  }
+  std::this_thread::sleep_for(std::chrono::milliseconds(300));
+  int fd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)srv.port());
+  inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+  CHECK(connect(fd, (sockaddr*)&a, sizeof a) == 0);
+  char buf[256] = {0};
+  ssize_t n = recv(fd, buf, sizeof buf - 1, 0);
+  CHECK(n > 0 && std::string(buf).find("503") != std::string::npos);
+  ::close(fd);
+  CHECK(srv.connections_rejected() >= 1);
+  for (int h : held) ::close(h);
+  srv.stop();
 }
 
 TEST(store_watch_replay_and_gone) {

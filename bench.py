@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--comm-dtype", default="bf16", choices=["bf16", "f32"],
                     help="gradient all-reduce wire dtype (bf16: half the xGMI bytes; f32 master update either way)")
     ap.add_argument("--graph", type=int, default=-1, help="capture step in a hipGraph (default: on for 1 GPU)")
+    ap.add_argument("--rccl-algo", default="", help="RCCL algorithm (Ring|Tree|...), see parallel/comm.py")
+    ap.add_argument("--rccl-proto", default="", help="RCCL protocol (Simple|LL|LL128)")
+    ap.add_argument("--rccl-channels", type=int, default=0, help="minimum RCCL channels (concurrent rings)")
     ap.add_argument("--force-comm", action="store_true",
                     help="1 GPU: still run the RCCL gradient all-reduce (world-size-1 process group)")
     ap.add_argument("--fp8", type=int, default=0, help="transformer models: MX-fp8 linear GEMMs (fwd, dgrad, wgrad)")
@@ -62,6 +65,7 @@ def main():
     import torch.distributed as dist
 
     from tensorflow_k8s_amd.parallel import comm
+    rccl_cfg = comm.configure_rccl(args.rccl_algo or None, args.rccl_proto or None, args.rccl_channels)
     if world > 1 or args.force_comm:
         comm.enable_transport_log()
     if args.force_comm and world == 1:
@@ -136,6 +140,7 @@ def main():
                 "wire_mb_per_step": round(strat.wire_bytes() / 2**20, 1) if strat.enabled else 0.0}
     if strat.enabled:
         comm_cfg["rccl_transport"] = comm.transport_summary()
+        comm_cfg["rccl_config"] = rccl_cfg
     loss = runner.last_loss()
     if rank == 0 and not is_cnn:
         seq = model.cfg.seq_len if args.model.startswith("bert") else model.cfg.tgt_len

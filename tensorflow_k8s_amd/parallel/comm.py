@@ -39,6 +39,35 @@ def bus_factor(op: str, world: int) -> float:
 
 _LOG_ENV = "TFK_RCCL_TRANSPORT_LOG"
 
+RCCL_ALGOS = ("Ring", "Tree", "CollNet", "NVLS")
+RCCL_PROTOS = ("Simple", "LL", "LL128")
+
+
+def configure_rccl(algo: str | None = None, proto: str | None = None, min_channels: int = 0,
+                   max_channels: int = 0) -> dict:
+    """RCCL algorithm / protocol / channel control (NCCL_ALGO, NCCL_PROTO, NCCL_MIN/MAX_NCHANNELS),
+    applied before the first communicator exists. On the fully connected 8x MI355X xGMI mesh one
+    ring uses one outbound link per GPU: more channels (concurrent rings over different links) raise
+    large-message bus bandwidth, LL/LL128 cut small-message latency. Returns the settings in force
+    (for the bench record). Values already present in the environment are left alone."""
+    want = {}
+    if algo:
+        if algo not in RCCL_ALGOS:
+            raise ValueError(f"RCCL algorithm must be one of {RCCL_ALGOS}, got {algo}")
+        want["NCCL_ALGO"] = algo
+    if proto:
+        if proto not in RCCL_PROTOS:
+            raise ValueError(f"RCCL protocol must be one of {RCCL_PROTOS}, got {proto}")
+        want["NCCL_PROTO"] = proto
+    if min_channels:
+        want["NCCL_MIN_NCHANNELS"] = str(int(min_channels))
+    if max_channels:
+        want["NCCL_MAX_NCHANNELS"] = str(int(max_channels))
+    for k, v in want.items():
+        os.environ.setdefault(k, v)
+    return {k: os.environ[k] for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS")
+            if k in os.environ}
+
 
 def enable_transport_log(directory: str | None = None) -> str | None:
     """Ask RCCL to log channel/transport setup to <dir>/rccl.<host>.<pid>.log. Must run before the
@@ -152,7 +181,11 @@ def main(argv=None) -> int:
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"])
     ap.add_argument("--transport-log", default="", help="directory for RCCL's transport log (default $TMPDIR)")
+    ap.add_argument("--rccl-algo", default="", help="|".join(RCCL_ALGOS))
+    ap.add_argument("--rccl-proto", default="", help="|".join(RCCL_PROTOS))
+    ap.add_argument("--rccl-channels", type=int, default=0, help="NCCL_MIN_NCHANNELS")
     args = ap.parse_args(argv)
+    rccl_cfg = configure_rccl(args.rccl_algo or None, args.rccl_proto or None, args.rccl_channels)
     backend = args.backend
     if backend == "auto":
         backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -179,7 +212,7 @@ def main(argv=None) -> int:
             if rank == 0:
                 print(json.dumps(r), flush=True)
     if rank == 0 and backend == "nccl":
-        print(json.dumps({"rccl_transport": transport_summary()}), flush=True)
+        print(json.dumps({"rccl_transport": transport_summary(), "rccl_config": rccl_cfg}), flush=True)
     dist.destroy_process_group()
     return 0
 

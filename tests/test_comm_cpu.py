@@ -159,3 +159,15 @@ def test_collective_ps_plan_buckets(world1_gloo):
         assert hi - lo <= 6000 + 3072  # cap + at most one more (aligned) parameter
     assert sum(plan._nparams) == len(a.params)
     assert set(plan.buckets_of(0)) | set(plan.buckets_of(1)) == set(range(len(bs)))
+
+
+def test_configure_rccl_env(monkeypatch):
+    from tensorflow_k8s_amd.parallel import comm
+    for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS"):
+        monkeypatch.delenv(k, raising=False)
+    cfg = comm.configure_rccl("Ring", "LL128", min_channels=16)
+    assert cfg == {"NCCL_ALGO": "Ring", "NCCL_PROTO": "LL128", "NCCL_MIN_NCHANNELS": "16"}
+    monkeypatch.setenv("NCCL_ALGO", "Tree")  # user settings win
+    assert comm.configure_rccl("Ring")["NCCL_ALGO"] == "Tree"
+    with pytest.raises(ValueError):
+        comm.configure_rccl("Butterfly")

@@ -193,6 +193,15 @@ class BertForPreTraining:
         return logits, nsp_logits, (rows, hm, zt, t, tl, stt, cls_rows, hc, zp, pooled)
 
     def forward_backward(self, ids, tt, mlm_pos, mlm_ids, nsp_labels, loss_scale: float = 1.0):
+        """One training step's forward + backward (see _forward_backward). The no-decay gradients
+        (biases, LayerNorm gamma/beta) are zeroed in one fill up front and accumulated by their kernels."""
+        self.arena.zero_nodecay_grads()
+        try:
+            return self._forward_backward(ids, tt, mlm_pos, mlm_ids, nsp_labels, loss_scale)
+        finally:
+            self.arena.prezeroed = False
+
+    def _forward_backward(self, ids, tt, mlm_pos, mlm_ids, nsp_labels, loss_scale: float = 1.0):
         """One pretraining step's forward + backward. Returns (loss f32 [B], mlm-correct f32 [B*P])."""
         cfg = self.cfg
         B = nsp_labels.shape[0]
@@ -209,7 +218,7 @@ class BertForPreTraining:
         nsp_loss, dnsp, _ = softmax_xent(nsp_logits, nsp_labels, scale=loss_scale / B)
         # ---- heads backward (the decoder wgrad is the first writer of the word-embedding grad)
         G.linear_wgrad(dlogits, tl, self.word.table.grad)  # first writer of the tied table's grad
-        G.bias_grad(dlogits, self.mlm_bias.grad)
+        G.bias_grad(dlogits, self.mlm_bias.grad, accumulate=self.arena.prezeroed)
         self.arena.grad_ready(self.mlm_bias)
         dtl = G.linear_dgrad(dlogits, self.word.table.compute)
         dt = self.mlm_ln.backward(dtl, t, stt)

@@ -257,6 +257,15 @@ class Transformer:
         return logits, (x, mem, st_m, y, yo, st_y)
 
     def forward_backward(self, src, tgt_in, tgt_out, src_len, loss_scale: float = 1.0):
+        """One training step's forward + backward (see _forward_backward). The no-decay gradients
+        (biases, LayerNorm gamma/beta) are zeroed in one fill up front and accumulated by their kernels."""
+        self.arena.zero_nodecay_grads()
+        try:
+            return self._forward_backward(src, tgt_in, tgt_out, src_len, loss_scale)
+        finally:
+            self.arena.prezeroed = False
+
+    def _forward_backward(self, src, tgt_in, tgt_out, src_len, loss_scale: float = 1.0):
         cfg = self.cfg
         B = src_len.shape[0]
         Ss, St = src.numel() // B, tgt_in.numel() // B

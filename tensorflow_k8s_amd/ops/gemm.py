@@ -273,6 +273,8 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
         else:
             gw.view(N, K).copy_(g)
         return
+    if RECORD is not None:
+        RECORD.append(("wgrad", (N, K, M), ()))
     tuned = tuning.wgrad_config(N, K, M) if (N % 8 == 0 and K % 8 == 0 and split_target is None) else None
     tile = tuned[0] if tuned else pick_tile(N, K, splits_ok=True, big_ok=True, K=M, split_target=split_target,
                                             g4=N % 8 == 0 and K % 8 == 0)
@@ -510,6 +512,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
         v.add_(gwt) if accumulate else v.copy_(gwt)
         return
     # measured table first (pointwise = dense GEMM shapes, tools/wgrad_sweep.py), else the model
+    if RECORD is not None and g.pointwise:
+        RECORD.append(("wgrad", (g.K, Nn, Kp), ()))
     tuned = tuning.wgrad_config(g.K, Nn, Kp) if (g.pointwise and g.K % 8 == 0 and g.C % 8 == 0) else None
     if splits is None and tuned is not None:
         tile, splits = tuned

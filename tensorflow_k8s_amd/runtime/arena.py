@@ -73,6 +73,10 @@ class ParamArena:
         self.numel = 0
         self._ready_cbs: list[Callable] = []
         self.device = None
+        # True while a step runs whose no-decay gradients (biases, LayerNorm/BN gamma+beta) were
+        # zeroed in ONE fill up front (zero_nodecay_grads): their atomic-accumulating kernels then
+        # skip their own per-tensor zero fills (BERT-base: ~80 fill launches per step -> 1)
+        self.prezeroed = False
 
     # ------------------------------------------------------------------ construction
     def add(self, spec: ParamSpec) -> Param:
@@ -137,6 +141,12 @@ class ParamArena:
         for cb in self._ready_cbs:
             for p in params:
                 cb(p)
+
+    def zero_nodecay_grads(self) -> None:
+        lo, hi = self.nodecay_region()
+        if hi > lo:
+            self.grad[lo:hi].zero_()
+        self.prezeroed = True
 
     # ------------------------------------------------------------------ regions
     def decay_region(self):

@@ -179,7 +179,7 @@ class Linear:
         """dy: gradient of this layer's (pre-dropout, post-activation-backward) output."""
         linear_wgrad(dy, x, self.w.grad, self.fp8, accumulate=accumulate, split_target=self.split_target)
         if self.b is not None:
-            G.bias_grad(dy, self.b.grad, accumulate=accumulate)
+            G.bias_grad(dy, self.b.grad, accumulate=accumulate or self.arena.prezeroed)
             self.arena.grad_ready(self.w, self.b)
         else:
             self.arena.grad_ready(self.w)
@@ -233,7 +233,7 @@ class FusedLinear:
         w, gw, _, gb = self.views()
         linear_wgrad(dy, x, gw, self.fp8, split_target=getattr(self, "split_target", None))
         if gb is not None:
-            G.bias_grad(dy, gb)
+            G.bias_grad(dy, gb, accumulate=self.arena.prezeroed)
         self.arena.grad_ready(*[p.w for p in self.parts], *[p.b for p in self.parts if p.b is not None])
         if not need_dx:
             return None
@@ -255,7 +255,8 @@ class LayerNorm:
     def backward(self, dy, x, stats, dres=None):
         """dx = LN'(x)^T dy (+ dres: gradient arriving through a residual connection)."""
         mu, rs = stats
-        dx = TR.layernorm_bwd(dy, x, self.gamma.master, mu, rs, self.gamma.grad, self.beta.grad, dres=dres)
+        dx = TR.layernorm_bwd(dy, x, self.gamma.master, mu, rs, self.gamma.grad, self.beta.grad, dres=dres,
+                              accumulate=self.arena.prezeroed)
         self.arena.grad_ready(self.gamma, self.beta)
         return dx
 

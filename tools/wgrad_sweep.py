@@ -47,14 +47,34 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default="")
     ap.add_argument("--table", default="", help="write the measured winners as ops/tuning.py's table")
+    ap.add_argument("--models", default="", help="comma list (e.g. bert-base,transformer-big): sweep the dense "
+                    "weight-gradient shapes one real step of each model issues instead of the ResNet list")
+    ap.add_argument("--merge", action="store_true", help="merge into the existing --table instead of replacing it")
     args = ap.parse_args()
+    shapes = SHAPES
+    if args.models:
+        from tensorflow_k8s_amd.models import build_model, synthetic_batch
+        seen = []
+        for name in args.models.split(","):
+            m = build_model(name).to("cuda")
+            b = synthetic_batch(m, {"bert-base": 64, "bert-large": 32}.get(name, 32), "cuda", seed=1)
+            G.RECORD = []
+            m.forward_backward(*b)
+            torch.cuda.synchronize()
+            for kind, shp, _ in G.RECORD:
+                if kind == "wgrad" and shp not in seen and shp[0] % 8 == 0 and shp[1] % 8 == 0:
+                    seen.append(shp)
+            G.RECORD = None
+            del m, b
+            torch.cuda.empty_cache()
+        shapes = seen
     from tensorflow_k8s_amd.ops import tuning
     tuning.ENABLED = False  # time the analytic picker's choice, not the table's
     fh = open(args.out, "w") if args.out else None
     dev = "cuda"
-    ws = torch.empty(512 * 2048 * 1024 + 4096, device=dev)
+    ws = torch.empty(512 * 4096 * 1024 + 4096, device=dev)
     entries = []
-    for M, N, K in SHAPES:
+    for M, N, K in shapes:
         dy = (torch.rand(K, M, device=dev) * 2 - 1).to(torch.bfloat16)
         x = (torch.rand(K, N, device=dev) * 2 - 1).to(torch.bfloat16)
         gw = torch.empty(M, N, device=dev)
@@ -100,6 +120,11 @@ def main():
         entries.append({"M": M, "N": N, "K": K, "tile": list(best[0]), "splits": best[1], "us": row["best_us"],
                         "picker_us": row["picked_us"]})
     if args.table:
+        if args.merge and os.path.exists(args.table):
+            with open(args.table) as f:
+                old = json.load(f)["entries"]
+            keys = {(e["M"], e["N"], e["K"]) for e in entries}
+            entries = [e for e in old if (e["M"], e["N"], e["K"]) not in keys] + entries
         with open(args.table, "w") as f:
             json.dump({"source": "tools/wgrad_sweep.py on MI355X", "entries": entries}, f, indent=1)
 

@@ -57,7 +57,8 @@ def main():
         seen = []
         for name in args.models.split(","):
             m = build_model(name).to("cuda")
-            b = synthetic_batch(m, {"bert-base": 64, "bert-large": 32}.get(name, 32), "cuda", seed=1)
+            bs = 256 if name.startswith("resnet") else {"bert-base": 64, "bert-large": 32}.get(name, 32)  # bench.py's
+            b = synthetic_batch(m, bs, "cuda", seed=1)
             G.RECORD = []
             m.forward_backward(*b)
             torch.cuda.synchronize()

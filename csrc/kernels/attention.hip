@@ -105,9 +105,13 @@ __device__ __forceinline__ bf16x8 pack2(const f32x4& a, const f32x4& b) {
   for (int e = 0; e < 4; ++e) { r[e] = f2bf(a[e]); r[4 + e] = f2bf(b[e]); }
   return r;
 }
-__device__ __forceinline__ bool keep_elem(const AttnParams& p, int bh, int q, int key) {
-  return u01(hash_u32(p.seed ^ ((unsigned long long)bh * 0x9E3779B97F4A7C15ull), (unsigned long long)q * p.Sk + key)) >=
-         p.p_drop;
+// keep iff the element's 24-bit uniform >= p_drop; element index q*Sk + key of head (b, h), the
+// seed folded with the head index (ops/transformer.py dropout_keep_mask is the bit-exact reference)
+__device__ __forceinline__ uint32_t head_seed(const AttnParams& p, int bh) {
+  return hash32((uint32_t)p.seed ^ (uint32_t)(p.seed >> 32) ^ ((uint32_t)bh * 0x9E3779B9u));
+}
+__device__ __forceinline__ bool keep_elem(const AttnParams& p, uint32_t hs, int q, int key) {
+  return u01(hash32(hs ^ (uint32_t)(q * p.Sk + key))) >= p.p_drop;
 }
 __device__ __forceinline__ void store_rowvec4(bf16* dst, const f32x4& v, float s) {
   bf16x4 o;
@@ -123,6 +127,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnParams p) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * TILE;
   const int bh = b * p.H + h;
+  const uint32_t hs = head_seed(p, bh);
   const bf16* Qb = p.q + b * p.q_bs + h * D;
   const bf16* Kb = p.k + b * p.k_bs + h * D;
   const bf16* Vb = p.v + b * p.v_bs + h * D;
@@ -194,7 +199,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnParams p) {
       for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          s[bb][r] = keep_elem(p, bh, qrow, k0 + arow(bb, g, r)) ? s[bb][r] * keep_scale : 0.f;
+          s[bb][r] = keep_elem(p, hs, qrow, k0 + arow(bb, g, r)) ? s[bb][r] * keep_scale : 0.f;
     }
     const bf16x8 pf0 = pack2(s[0], s[1]), pf1 = pack2(s[2], s[3]);
 #pragma unroll
@@ -238,6 +243,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AttnParams p) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * TILE;
   const int bh = b * p.H + h;
+  const uint32_t hs = head_seed(p, bh);
   const bf16* Qb = p.q + b * p.q_bs + h * D;
   const bf16* Kb = p.k + b * p.k_bs + h * D;
   const bf16* Vb = p.v + b * p.v_bs + h * D;
@@ -280,7 +286,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AttnParams p) {
         const bool valid = key < kvl && !(p.causal && key > qrow);
         const float pr = valid ? exp2f(s[r] * sl2 - lse2) : 0.f;
         float dpv = dp[r];
-        if (p.p_drop > 0.f) dpv = keep_elem(p, bh, qrow, key) ? dpv * keep_scale : 0.f;
+        if (p.p_drop > 0.f) dpv = keep_elem(p, hs, qrow, key) ? dpv * keep_scale : 0.f;
         ds[bb][r] = pr * (dpv - dlt);
       }
     }
@@ -306,6 +312,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AttnParams p) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
   const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * TILE;
   const int bh = b * p.H + h;
+  const uint32_t hs = head_seed(p, bh);
   const bf16* Qb = p.q + b * p.q_bs + h * D;
   const bf16* Kb = p.k + b * p.k_bs + h * D;
   const bf16* Vb = p.v + b * p.v_bs + h * D;
@@ -351,7 +358,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AttnParams p) {
         const float pr = valid ? exp2f(s[r] * sl2 - lse_s[qt]) : 0.f;
         float pd = pr, dpv = dp[r];
         if (p.p_drop > 0.f) {
-          const bool kp = keep_elem(p, bh, qq, krow);
+          const bool kp = keep_elem(p, hs, qq, krow);
           pd = kp ? pr * keep_scale : 0.f;
           dpv = kp ? dpv * keep_scale : 0.f;
         }

@@ -96,3 +96,10 @@ __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
   return (uint32_t)x;
 }
 __device__ __forceinline__ float u01(uint32_t h) { return (h >> 8) * (1.0f / 16777216.0f); }
+// 32-bit integer hash ("lowbias32": 2 multiplies, 3 xor-shifts, all 32-bit) for the per-element
+// attention-dropout masks, which are regenerated in every attention pass: the 64-bit hash_u32
+// above costs ~35 VALU ops per element there and was the largest cost of the dropout passes.
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}

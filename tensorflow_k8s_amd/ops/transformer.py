@@ -113,13 +113,27 @@ def embedding_bwd(ids, dy, dword, dpos=None, seq_len: int = 1, type_ids=None, dt
 
 # ----------------------------------------------------------------------------- attention
 
+def _hash32(x: torch.Tensor) -> torch.Tensor:
+    """Bit-exact torch (int64 holding uint32) copy of common.h hash32 (lowbias32)."""
+    m = 0xFFFFFFFF
+    x = x & m
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & m
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & m
+    return x ^ (x >> 16)
+
+
 def dropout_keep_mask(seed: int, B: int, H: int, Sq: int, Sk: int, p: float) -> torch.Tensor:
-    """The kernels' attention-dropout mask (bool [B,H,Sq,Sk]), bit-exact (hash_u32 in common.h)."""
-    from .elementwise import _s64, hash_u32, u01
+    """The kernels' attention-dropout mask (bool [B,H,Sq,Sk]), bit-exact (attention.hip keep_elem:
+    hash32 of the element index folded with a per-head seed hash)."""
+    s = int(seed) & 0xFFFFFFFFFFFFFFFF
+    base = (s & 0xFFFFFFFF) ^ (s >> 32)
     bh = torch.arange(B * H, dtype=torch.int64)
-    sd = torch.tensor(_s64(seed), dtype=torch.int64) ^ (bh * _s64(0x9E3779B97F4A7C15))
+    hs = _hash32(base ^ ((bh * 0x9E3779B9) & 0xFFFFFFFF))
     idx = torch.arange(Sq * Sk, dtype=torch.int64)
-    return (u01(hash_u32(sd[:, None], idx[None, :])) >= p).reshape(B, H, Sq, Sk)
+    h = _hash32(hs[:, None] ^ idx[None, :])
+    return ((h >> 8).float() * (1.0 / 16777216.0) >= p).reshape(B, H, Sq, Sk)
 
 
 def _view(buf, col, B, S, H):

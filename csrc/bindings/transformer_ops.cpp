@@ -9,6 +9,7 @@
 #include "bind_util.h"
 
 extern "C" {
+void tfk_attn_set_waves(int w);
 int tfk_layernorm_fwd(const void*, const float*, const float*, void*, float*, float*, int, int, float, hipStream_t);
 int tfk_layernorm_bwd(const void*, const void*, const float*, const float*, const float*, const void*, void*, float*,
                       float*, int, int, hipStream_t);
@@ -173,4 +174,5 @@ void register_transformer_ops(pybind11::module& m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
+  m.def("attn_set_waves", [](int w) { tfk_attn_set_waves(w); });
 }

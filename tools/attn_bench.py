@@ -33,16 +33,21 @@ def main():
         dout = torch.randn(B * S, H * D, device="cuda").to(torch.bfloat16)
         dqkv = torch.empty_like(qkv)
         row = {"shape": name, "B": B, "H": H, "S": S, "causal": causal}
-        for p in (0.0, 0.1):
+        from tensorflow_k8s_amd.ops._lib import lib
+        for p, nw in ((0.0, 4), (0.1, 4), (0.0, 8), (0.1, 8)):
+            lib().attn_set_waves(nw)
             sp = T.AttnSpec(B, H, S, Sk, (qkv, 0), (qkv, H * D), (qkv, 2 * H * D), causal=causal, p_drop=p, seed=7)
             out, lse = T.attention_fwd(sp)
+            if nw > 4:  # same result as the 4-wave kernels
+                lib().attn_set_waves(4)
+                o4, l4 = T.attention_fwd(sp)
+                lib().attn_set_waves(nw)
+                row[f"max_diff_w{nw}_p{p}"] = float((out.float() - o4.float()).abs().max())
             f = 4.0 * B * H * S * Sk * D * (0.5 if causal else 1.0)
             tf = timeit(lambda: T.attention_fwd(sp))
             tb = timeit(lambda: T.attention_bwd(sp, out, dout, lse, (dqkv, 0), (dqkv, H * D), (dqkv, 2 * H * D)))
-            row[f"fwd_us_p{p}"] = round(tf * 1e6, 1)
-            row[f"bwd_us_p{p}"] = round(tb * 1e6, 1)
-            row[f"fwd_tflops_p{p}"] = round(f / tf / 1e12, 1)
-            row[f"bwd_tflops_p{p}"] = round(2.5 * f / tb / 1e12, 1)
+            row[f"fwd_us_p{p}_w{nw}"] = round(tf * 1e6, 1)
+            row[f"bwd_us_p{p}_w{nw}"] = round(tb * 1e6, 1)
         print(json.dumps(row), flush=True)
 
 

@@ -16,6 +16,7 @@ int tfk_gemm_splits(int K, int splits);
 void tfk_gemm_set_persist(int on);
 void tfk_gemm_set_engine(int e);
 void tfk_g4_set_shortk(int on);
+void tfk_g4_set_persist(int on);
 extern "C" void tfk_fp8_set_engine(int e);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_quant_t(const void*, void*, void*, int, int, hipStream_t);
@@ -249,6 +250,7 @@ int64_t gemm_splits(int K, int splits) { return tfk_gemm_splits(K, splits); }
 void gemm_set_persist(int on) { tfk_gemm_set_persist(on); }
 void gemm_set_engine(int e) { tfk_gemm_set_engine(e); }
 void gemm_set_shortk(int on) { tfk_g4_set_shortk(on); }
+void gemm_set_g4_persist(int on) { tfk_g4_set_persist(on); }
 void fp8_set_engine(int e) { tfk_fp8_set_engine(e); }
 
 void mx_probe(torch::Tensor X, torch::Tensor Y, torch::Tensor sx, torch::Tensor sy, torch::Tensor D) {
@@ -609,6 +611,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_persist", &gemm_set_persist);
   m.def("gemm_set_engine", &gemm_set_engine);
   m.def("gemm_set_shortk", &gemm_set_shortk);
+  m.def("gemm_set_g4_persist", &gemm_set_g4_persist);
   m.def("fp8_set_engine", &fp8_set_engine);
   m.def("mx_quant", &mx_quant);
   m.def("mx_quant_t", &mx_quant_t);

@@ -47,7 +47,10 @@ __device__ __forceinline__ long long resid_row(const GemmParams& p, long long mo
   return (n * p.rs_p + h / p.rs_sh) * p.rs_q + w / p.rs_sw;
 }
 
-template <int BM, int BN, int NT, int WM, int EPI, int BNRG = 0>
+// DRAIN: the caller has LDS-DMA loads in flight (persistent g4: the next tile's prefetch), which
+// the compiler's vmcnt bookkeeping does not model -- wait for all of them before the store pass
+// issues its own global loads (residual, BN-reduce inputs), so those waits stay exact.
+template <int BM, int BN, int NT, int WM, int EPI, int BNRG = 0, bool DRAIN = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[BM / WM / 16][BN / (NT / 64 / WM) / 16],
                                               char* smem, int m0, int n0, int bz) {
   constexpr int NW = NT / 64, WN = NW / WM;
@@ -166,6 +169,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     // a store that may alias them, and every chunk paid two full memory latencies (vmcnt(0) before
     // and after its store: measured 3 TB/s on the BN-backward dgrads). Loads are unconditional from
     // always-valid addresses (absent tensors alias y / C) so no per-element branch splits them.
+    if constexpr (DRAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool tile_fast = (m0 + BM <= p.M) && (n0 + BN <= p.N) && ((p.ldc & 7) == 0);
     constexpr int NIT = TOT / NT;
     // BNR groups: 1 chunk in flight (BNRG template override); G=2 on <= 128x128 tiles compiled

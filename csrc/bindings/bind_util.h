@@ -28,4 +28,21 @@ T* opt_ptr(const c10::optional<torch::Tensor>& t) {
   return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
 }
 
+// A relu-mask operand of the BN-backward ops: either the post-activation bf16 tensor a (mask a > 0,
+// *bf16_out = a) or its packed bitmask (uint8, bit e of byte i/8 = a[i+e] > 0; returned).
+inline const uint8_t* relu_bitmask(const c10::optional<torch::Tensor>& a, long long n, const void** bf16_out) {
+  *bf16_out = nullptr;
+  if (!a.has_value() || !a->defined()) return nullptr;
+  if (a->scalar_type() == at::kByte) {
+    need(*a, at::kByte, "relu bitmask");
+    TORCH_CHECK(n % 8 == 0, "relu bitmask needs a multiple of 8 elements");
+    need_numel(*a, n / 8, "relu bitmask");
+    return a->data_ptr<uint8_t>();
+  }
+  need_bf16(*a, "a");
+  need_numel(*a, n, "a");
+  *bf16_out = a->data_ptr();
+  return nullptr;
+}
+
 }  // namespace

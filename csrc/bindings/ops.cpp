@@ -26,13 +26,13 @@ int tfk_bn_finalize(float*, int, int, float, const float*, const float*, float, 
                     float*, float*, hipStream_t);
 int tfk_bn_stats(const void*, long long, int, float*, int, hipStream_t);
 int tfk_bn_apply(const void*, const float*, const float*, const void*, const float*, const float*, int, void*, long long,
-                 int, hipStream_t);
+                 int, uint8_t*, hipStream_t);
 int tfk_bn_bwd_reduce(const void*, const void*, const void*, const float*, const float*, const void*, const float*,
-                      const float*, long long, int, float*, int, const float*, const float*, hipStream_t);
+                      const float*, long long, int, float*, int, const float*, const float*, const uint8_t*, hipStream_t);
 int tfk_bn_bwd_finalize(float*, int, int, float, const float*, const float*, const float*, const float*, const float*,
                         const float*, float*, float*, float*, float*, float*, float*, hipStream_t);
 int tfk_bn_bwd_apply(const void*, const void*, const void*, const float*, void*, const void*, const float*, void*, void*,
-                     long long, int, const float*, const float*, hipStream_t);
+                     long long, int, const float*, const float*, const uint8_t*, hipStream_t);
 int tfk_maxpool_fwd(const void*, void*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int tfk_maxpool_bwd(const void*, const uint8_t*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                     hipStream_t);
@@ -164,7 +164,9 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
     TORCH_CHECK(epi == 0 && N % 8 == 0 && ldc == N && batch == 1, "fused BN reduce needs bf16 out, N%8==0, ldc==N");
     for (int i : {0, 2, 3, 9}) TORCH_CHECK(bnr[i].has_value() && bnr[i]->defined(), "bnr missing required entry ", i);
     need_bf16(*bnr[0], "bn_y"); need_numel(*bnr[0], (long long)M * N, "bn_y");
-    if (bnr[1].has_value() && bnr[1]->defined()) { need_bf16(*bnr[1], "bn_a"); need_numel(*bnr[1], (long long)M * N, "bn_a"); }
+    const void* bn_a = nullptr;
+    p.bn_amask = relu_bitmask(bnr[1], (long long)M * N, &bn_a);
+    TORCH_CHECK(!bn_a, "fused BN reduce: pass the activation's packed relu bitmask (uint8), not the bf16 tensor");
     if (bnr[6].has_value() && bnr[6]->defined()) { need_bf16(*bnr[6], "bn_y2"); need_numel(*bnr[6], (long long)M * N, "bn_y2"); }
     for (int i : {2, 3, 4, 5, 7, 8})
       if (bnr[i].has_value() && bnr[i]->defined()) { need_f32(*bnr[i], "bn vec"); need_numel(*bnr[i], N, "bn vec"); }
@@ -172,7 +174,6 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
     TORCH_CHECK(bn_shards >= 1, "bn_shards");
     need_numel(*bnr[9], (long long)bn_shards * 3 * N, "bn_sums");
     p.bn_y = bnr[0]->data_ptr();
-    p.bn_a = opt_ptr<const void>(bnr[1]);
     p.bn_mean = bnr[2]->data_ptr<float>();
     p.bn_invstd = bnr[3]->data_ptr<float>();
     p.bn_scale = opt_ptr<const float>(bnr[4]);
@@ -183,7 +184,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
     p.bn_sums = bnr[9]->data_ptr<float>();
     p.bn_relu = bn_relu;
     p.bn_shards = bn_shards;
-    TORCH_CHECK(!(p.bn_relu && !p.bn_a && !(p.bn_scale && p.bn_shift)), "relu mask needs a or scale/shift");
+    TORCH_CHECK(!(p.bn_relu && !p.bn_amask && !(p.bn_scale && p.bn_shift)), "relu mask needs a or scale/shift");
   }
   p.bias = opt_ptr<const float>(bias);
   p.resid = opt_ptr<const void>(resid);
@@ -228,7 +229,8 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
       const long long rows = (long long)(M / (r[0] * r[1])) * r[2] * r[3];
       need_numel(C, (rows - 1) * ldc + N, "C (out-map)");
       for (int i : {0, 1, 6})
-        if (bnr[i].has_value() && bnr[i]->defined()) need_numel(*bnr[i], rows * N, "bn tensor (out-map)");
+        if (bnr[i].has_value() && bnr[i]->defined())
+          need_numel(*bnr[i], bnr[i]->scalar_type() == at::kByte ? rows * N / 8 : rows * N, "bn tensor (out-map)");
       if (resid.has_value() && resid->defined()) need_numel(*resid, (rows - 1) * ldc + N, "resid (out-map)");
     }
     if (r[12] > 0) {
@@ -344,8 +346,14 @@ void bn_stats(torch::Tensor y, int64_t M, int C, torch::Tensor stats, int shards
 
 void bn_apply(torch::Tensor y, torch::Tensor scale, torch::Tensor shift, c10::optional<torch::Tensor> r,
               c10::optional<torch::Tensor> rscale, c10::optional<torch::Tensor> rshift, bool relu, torch::Tensor out,
-              int64_t M, int C) {
+              int64_t M, int C, c10::optional<torch::Tensor> mask) {
   need_bf16(y, "y"); need_bf16(out, "out"); need_numel(y, M * C, "y"); need_numel(out, M * C, "out");
+  uint8_t* mk = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(relu && mask->scalar_type() == torch::kUInt8, "bn_apply: mask is the relu bitmask (uint8)");
+    need_numel(*mask, M * C / 8, "mask");
+    mk = mask->data_ptr<uint8_t>();
+  }
   TORCH_CHECK(C % 8 == 0, "C%8");
   need_aligned(y, 16, "y"); need_aligned(out, 16, "out");
   need_f32(scale, "scale"); need_f32(shift, "shift"); need_numel(scale, C, "scale"); need_numel(shift, C, "shift");
@@ -353,7 +361,7 @@ void bn_apply(torch::Tensor y, torch::Tensor scale, torch::Tensor shift, c10::op
   if (rscale.has_value() && rscale->defined()) { need_numel(*rscale, C, "rscale"); need_numel(*rshift, C, "rshift"); }
   check_rc(tfk_bn_apply(y.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), opt_ptr<const void>(r),
                         opt_ptr<const float>(rscale), opt_ptr<const float>(rshift), relu ? 1 : 0, out.data_ptr(), M, C,
-                        cur_stream()),
+                        mk, cur_stream()),
            "bn_apply");
 }
 
@@ -363,13 +371,14 @@ void bn_bwd_reduce(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tens
                    c10::optional<torch::Tensor> mscale, c10::optional<torch::Tensor> mshift) {
   need_bf16(da, "da"); need_bf16(y, "y"); need_numel(da, M * C, "da"); need_numel(y, M * C, "y");
   TORCH_CHECK(C % 8 == 0, "C%8");
-  if (a.has_value() && a->defined()) need_numel(*a, M * C, "a");
+  const void* ap = nullptr;
+  const uint8_t* amask = relu_bitmask(a, M * C, &ap);
   if (y2.has_value() && y2->defined()) need_numel(*y2, M * C, "y2");
   need_f32(sums, "sums"); need_numel(sums, (long long)shards * 3 * C, "sums");
-  check_rc(tfk_bn_bwd_reduce(da.data_ptr(), opt_ptr<const void>(a), y.data_ptr(), mean.data_ptr<float>(),
+  check_rc(tfk_bn_bwd_reduce(da.data_ptr(), ap, y.data_ptr(), mean.data_ptr<float>(),
                              invstd.data_ptr<float>(), opt_ptr<const void>(y2), opt_ptr<const float>(mean2),
                              opt_ptr<const float>(invstd2), M, C, sums.data_ptr<float>(), shards,
-                             opt_ptr<const float>(mscale), opt_ptr<const float>(mshift), cur_stream()),
+                             opt_ptr<const float>(mscale), opt_ptr<const float>(mshift), amask, cur_stream()),
            "bn_bwd_reduce");
 }
 
@@ -401,7 +410,8 @@ void bn_bwd_apply(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tenso
   need_bf16(da, "da"); need_bf16(y, "y"); need_bf16(dy, "dy");
   for (auto* t : {&da, &y, &dy}) need_numel(*t, M * C, "bn bwd tensor");
   need_f32(coef, "coef"); need_numel(coef, 3 * C, "coef");
-  if (a.has_value() && a->defined()) need_numel(*a, M * C, "a");
+  const void* ap = nullptr;
+  const uint8_t* amask = relu_bitmask(a, M * C, &ap);
   if (y2.has_value() && y2->defined()) {
     TORCH_CHECK(coef2.has_value() && dy2.has_value(), "bn_bwd_apply: y2 needs coef2 and dy2");
     need_numel(*y2, M * C, "y2"); need_numel(*dy2, M * C, "dy2"); need_numel(*coef2, 3 * C, "coef2");
@@ -409,10 +419,10 @@ void bn_bwd_apply(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tenso
   if (dres.has_value() && dres->defined()) need_numel(*dres, M * C, "dres");
   if (mscale.has_value() && mscale->defined()) { need_numel(*mscale, C, "mscale"); need_numel(*mshift, C, "mshift"); }
   TORCH_CHECK(C % 8 == 0, "C%8");
-  check_rc(tfk_bn_bwd_apply(da.data_ptr(), opt_ptr<const void>(a), y.data_ptr(), coef.data_ptr<float>(), dy.data_ptr(),
+  check_rc(tfk_bn_bwd_apply(da.data_ptr(), ap, y.data_ptr(), coef.data_ptr<float>(), dy.data_ptr(),
                             opt_ptr<const void>(y2), opt_ptr<const float>(coef2), opt_ptr<void>(dy2),
                             opt_ptr<void>(dres), M, C, opt_ptr<const float>(mscale), opt_ptr<const float>(mshift),
-                            cur_stream()),
+                            amask, cur_stream()),
            "bn_bwd_apply");
 }
 

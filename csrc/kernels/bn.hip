@@ -115,7 +115,7 @@ __device__ __forceinline__ void load8(const float* __restrict__ p, float (&v)[8]
 template <bool FIXED>
 __global__ void bn_apply_kernel(const bf16* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
                                 const bf16* __restrict__ r, const float* __restrict__ rscale, const float* __restrict__ rshift,
-                                int relu, bf16* __restrict__ out, long long M, int C) {
+                                int relu, bf16* __restrict__ out, long long M, int C, unsigned char* __restrict__ mask) {
   const int cpr = C >> 3;
   long long i, step;
   int c0;
@@ -159,6 +159,13 @@ __global__ void bn_apply_kernel(const bf16* __restrict__ y, const float* __restr
 #pragma unroll
     for (int e = 0; e < 8; ++e) w[e] = f2bf(relu ? fmaxf(o[e], 0.f) : o[e]);
     *(bf16x8*)(out + i) = w;
+    if (mask) {
+      // bit e of byte i/8 = (out[i+e] > 0): the backward's relu mask at 1/16 of out's bytes
+      unsigned bits = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bits |= (bf2f(w[e]) > 0.f ? 1u : 0u) << e;
+      mask[i >> 3] = (unsigned char)bits;
+    }
   }
 }
 
@@ -168,7 +175,8 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ da, const bf16* __
                                      const float* __restrict__ mean, const float* __restrict__ invstd,
                                      const bf16* __restrict__ y2, const float* __restrict__ mean2,
                                      const float* __restrict__ invstd2, long long M, int C, float* __restrict__ sums,
-                                     int shards, const float* __restrict__ mscale, const float* __restrict__ mshift) {
+                                     int shards, const float* __restrict__ mscale, const float* __restrict__ mshift,
+                                     const unsigned char* __restrict__ amask) {
   const int cpr = C >> 3;
   const int rows_par = NT / cpr > 0 ? NT / cpr : 1;
   const int t = threadIdx.x;
@@ -189,11 +197,13 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ da, const bf16* __
       bf16x8 yv = *(const bf16x8*)(y + off);
       bf16x8 av;
       if (a) av = *(const bf16x8*)(a + off);
+      const unsigned mb = amask ? amask[off >> 3] : 0xffu;
       bf16x8 y2v;
       if (y2) y2v = *(const bf16x8*)(y2 + off);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float dz = bf2f(g[e]);
+        if (!((mb >> e) & 1u)) dz = 0.f;
         if (a && !(bf2f(av[e]) > 0.f)) dz = 0.f;
         if (!a && mscale && !(bf2f(yv[e]) * msc[e] + msh[e] > 0.f)) dz = 0.f;
         s0[e] += dz;
@@ -262,7 +272,7 @@ __global__ void bn_bwd_apply_kernel(const bf16* __restrict__ da, const bf16* __r
                                     const float* __restrict__ coef, bf16* __restrict__ dy, const bf16* __restrict__ y2,
                                     const float* __restrict__ coef2, bf16* __restrict__ dy2, bf16* __restrict__ dres,
                                     long long M, int C, const float* __restrict__ mscale,
-                                    const float* __restrict__ mshift) {
+                                    const float* __restrict__ mshift, const unsigned char* __restrict__ amask) {
   const int cpr = C >> 3;
   long long i, step;
   int c0;
@@ -293,11 +303,14 @@ __global__ void bn_bwd_apply_kernel(const bf16* __restrict__ da, const bf16* __r
     bf16x8 yv = *(const bf16x8*)(y + i);
     bf16x8 av;
     if (a) av = *(const bf16x8*)(a + i);
+    const unsigned mb = amask ? amask[i >> 3] : 0xffu;
     float dz[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       dz[e] = bf2f(g[e]);
-      if (a) {
+      if (amask) {
+        if (!((mb >> e) & 1u)) dz[e] = 0.f;
+      } else if (a) {
         if (!(bf2f(av[e]) > 0.f)) dz[e] = 0.f;
       } else if (mscale) {
         if (!(bf2f(yv[e]) * ms[e] + mh[e] > 0.f)) dz[e] = 0.f;
@@ -343,23 +356,23 @@ int tfk_bn_stats(const bf16* y, long long M, int C, float* stats, int shards, hi
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_bn_apply(const bf16* y, const float* scale, const float* shift, const bf16* r, const float* rscale,
-                 const float* rshift, int relu, bf16* out, long long M, int C, hipStream_t s) {
+                 const float* rshift, int relu, bf16* out, long long M, int C, unsigned char* mask, hipStream_t s) {
   const int cpr = C / 8;
   if (NT % cpr == 0) {
     hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(grid_for(M, (NT / cpr) * 4, 8192)), dim3(NT), 0, s, y, scale, shift, r,
-                       rscale, rshift, relu, out, M, C);
+                       rscale, rshift, relu, out, M, C, mask);
   } else {
     hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(grid_for(M * cpr, NT * 4, 8192)), dim3(NT), 0, s, y, scale, shift,
-                       r, rscale, rshift, relu, out, M, C);
+                       r, rscale, rshift, relu, out, M, C, mask);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_bn_bwd_reduce(const bf16* da, const bf16* a, const bf16* y, const float* mean, const float* invstd, const bf16* y2,
                       const float* mean2, const float* invstd2, long long M, int C, float* sums, int shards,
-                      const float* mscale, const float* mshift, hipStream_t s) {
+                      const float* mscale, const float* mshift, const unsigned char* amask, hipStream_t s) {
   int cpr = C / 8, rows_par = NT / cpr > 0 ? NT / cpr : 1;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_for(M, rows_par * 16, 2048)), dim3(NT), 0, s, da, a, y, mean, invstd,
-                     y2, mean2, invstd2, M, C, sums, shards, mscale, mshift);
+                     y2, mean2, invstd2, M, C, sums, shards, mscale, mshift, amask);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_bn_bwd_finalize(float* sums, int shards, int C, float count, const float* gamma, const float* mean,
@@ -372,14 +385,14 @@ int tfk_bn_bwd_finalize(float* sums, int shards, int C, float count, const float
 }
 int tfk_bn_bwd_apply(const bf16* da, const bf16* a, const bf16* y, const float* coef, bf16* dy, const bf16* y2,
                      const float* coef2, bf16* dy2, bf16* dres, long long M, int C, const float* mscale,
-                     const float* mshift, hipStream_t s) {
+                     const float* mshift, const unsigned char* amask, hipStream_t s) {
   const int cpr = C / 8;
   if (NT % cpr == 0) {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid_for(M, (NT / cpr) * 4, 8192)), dim3(NT), 0, s, da, a, y, coef,
-                       dy, y2, coef2, dy2, dres, M, C, mscale, mshift);
+                       dy, y2, coef2, dy2, dres, M, C, mscale, mshift, amask);
   } else {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid_for(M * cpr, NT * 4, 8192)), dim3(NT), 0, s, da, a, y,
-                       coef, dy, y2, coef2, dy2, dres, M, C, mscale, mshift);
+                       coef, dy, y2, coef2, dy2, dres, M, C, mscale, mshift, amask);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -180,11 +180,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       const bf16* resid_b = p.resid ? (const bf16*)p.resid : (const bf16*)p.C;
       const bf16* dsrc_b = (EPI == EPI_BF16_EXT && p.dact_src) ? (const bf16*)p.dact_src : (const bf16*)p.C;
       const bf16* y_b = bnr ? (const bf16*)p.bn_y : nullptr;
-      const bf16* a_b = bnr ? (p.bn_a ? (const bf16*)p.bn_a : y_b) : nullptr;
       const bf16* y2_b = bnr ? (p.bn_y2 ? (const bf16*)p.bn_y2 : y_b) : nullptr;
+      const unsigned char* mk_b = bnr ? (p.bn_amask ? p.bn_amask : (const unsigned char*)y_b) : nullptr;
 #pragma unroll (bnr ? 1 : NIT)
       for (int g0 = 0; g0 < NIT; g0 += G) {
-        bf16x8 cv[G], rr[G], zv[G], yv[G], av[G], y2v[G];
+        bf16x8 cv[G], rr[G], zv[G], yv[G], y2v[G];
+        unsigned mk[G];
         long long off[G];
         bool rok[G];
         int mlog[G], nlog[G];
@@ -205,7 +206,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           if constexpr (EPI == EPI_BF16_EXT) zv[g] = *(const bf16x8*)(dsrc_b + off[g]);
           if constexpr (bnr) {
             yv[g] = *(const bf16x8*)(y_b + off[g]);
-            av[g] = *(const bf16x8*)(a_b + off[g]);
+            mk[g] = mk_b[off[g] >> 3];
             y2v[g] = *(const bf16x8*)(y2_b + off[g]);
           }
         }
@@ -242,7 +243,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float y = bf2f(yv[g][e]);
-              const bool keep = p.bn_a ? (bf2f(av[g][e]) > 0.f) : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
+              const bool keep = p.bn_amask ? ((mk[g] >> e) & 1u) != 0 : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
               const float dz = keep ? bf2f(v[e]) : 0.f;
               r0[e] += dz;
               r1[e] += dz * (y - mu[e]) * is[e];
@@ -297,13 +298,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         *(bf16x8*)dst = v;
         if constexpr (bnr) {
           bf16x8 yv = *(const bf16x8*)((const bf16*)p.bn_y + off);
-          bf16x8 av, y2v;
-          if (p.bn_a) av = *(const bf16x8*)((const bf16*)p.bn_a + off);
+          bf16x8 y2v;
           if (p.bn_y2) y2v = *(const bf16x8*)((const bf16*)p.bn_y2 + off);
+          const unsigned mk = p.bn_amask ? p.bn_amask[off >> 3] : 0xffu;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float y = bf2f(yv[e]);
-            bool keep = p.bn_a ? (bf2f(av[e]) > 0.f) : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
+            bool keep = p.bn_amask ? ((mk >> e) & 1u) != 0 : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
             const float dz = keep ? bf2f(v[e]) : 0.f;
             r0[e] += dz;
             r1[e] += dz * (y - mu[e]) * is[e];

@@ -21,10 +21,12 @@ struct GemmParams {
   long long split_stride;  // f32 elements between split-K slabs
   int tiles_n;
   // Fused BatchNorm-backward reduction over the final bf16 output dA (bf16 epilogue only, N%8==0):
-  //   dz = dA * mask,  mask = bn_a ? (a > 0) : bn_relu ? (y*scale+shift > 0) : 1
+  //   dz = dA * mask,  mask = bn_amask ? bit : bn_relu ? (y*scale+shift > 0) : 1
+  //   (bn_amask: packed relu mask of the activation, bit e of byte i/8 = a[i+e] > 0, as the
+  //   forward's bn_apply writes it -- 1 byte per 8-element chunk instead of 16)
   //   bn_sums[shard][0][n] += dz,  [1][n] += dz*(y-mean)*invstd,  [2][n] += dz*(y2-mean2)*invstd2
   const void* bn_y;
-  const void* bn_a;
+  const unsigned char* bn_amask;
   const float* bn_mean;
   const float* bn_invstd;
   const float* bn_scale;

@@ -60,34 +60,37 @@ class Bottleneck:
             ysc = self.conv_sc.forward(x, ssc if training else None)
             if training:
                 self.bn_sc.finalize(ysc.numel() // ysc.shape[-1])
-            out = BN.bn_apply(y3, s3, relu=True, r=ysc, rst=ssc)
+            out = BN.bn_apply(y3, s3, relu=True, r=ysc, rst=ssc, mask=training)
         else:
-            out = BN.bn_apply(y3, s3, relu=True, r=x)
+            out = BN.bn_apply(y3, s3, relu=True, r=x, mask=training)
         if training:
-            self.saved = (x, y1, a1, y2, a2, y3, ysc, out)
+            # the tail's relu mask is kept as a bitmask (1/16 of out's bytes): the tail BN-backward
+            # apply and the next block's fused dgrad reduction read it instead of out
+            out, mk = out
+            self.saved = (x, y1, a1, y2, a2, y3, ysc, mk)
         return out
 
     def tail_reduce(self) -> BN.BNReduce:
         """BN-backward reduction spec of this block's tail (relu(bn3(y3) + shortcut)); fused into
         the epilogue of the NEXT block's final dgrad, which produces this block's dout."""
-        x, y1, a1, y2, a2, y3, ysc, out = self.saved
-        return BN.BNReduce(y3, self.bn3.st, a=out, y2=ysc, st2=self.bn_sc.st if self.proj else None)
+        x, y1, a1, y2, a2, y3, ysc, mk = self.saved
+        return BN.BNReduce(y3, self.bn3.st, a=mk, y2=ysc, st2=self.bn_sc.st if self.proj else None)
 
     def backward(self, dout, need_dx=True, dout_reduced=False, next_bnr: BN.BNReduce | None = None):
         """dout_reduced: the producer of dout already accumulated this block's tail BN sums.
         next_bnr: reduction spec to fuse into the dgrad that produces dx (previous block's tail)."""
-        x, y1, a1, y2, a2, y3, ysc, out = self.saved
+        x, y1, a1, y2, a2, y3, ysc, mk = self.saved
         self.saved = None
         cnt3 = y3.numel() // y3.shape[-1]
         if self.proj:
-            dy3, dysc, _ = BN.bn_backward(dout, out, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
+            dy3, dysc, _ = BN.bn_backward(dout, mk, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
                                           self.bn3.beta.grad, cnt3, y2=ysc, st2=self.bn_sc.st,
                                           gamma2=self.bn_sc.gamma.master, dgamma2=self.bn_sc.gamma.grad,
                                           dbeta2=self.bn_sc.beta.grad, reduced=dout_reduced)
             dres = None
             self.arena.grad_ready(self.bn3.gamma, self.bn3.beta, self.bn_sc.gamma, self.bn_sc.beta)
         else:
-            dy3, _, dres = BN.bn_backward(dout, out, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
+            dy3, _, dres = BN.bn_backward(dout, mk, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
                                           self.bn3.beta.grad, cnt3, want_dres=True, reduced=dout_reduced)
             self.arena.grad_ready(self.bn3.gamma, self.bn3.beta)
         # bn2/bn1 have no residual input: relu mask recomputed from y, sums fused into the dgrad epilogue

@@ -58,9 +58,35 @@ def bn_stats(y: torch.Tensor, st: BNState) -> None:
     lib().bn_stats(y, y.numel() // C, C, st.stats, st.shards)
 
 
-def bn_apply(y, st: BNState, relu: bool, r=None, rst: BNState | None = None, out=None) -> torch.Tensor:
-    """a = relu?(y*scale + shift [+ r | + r*rscale + rshift])."""
+def pack_relu_mask(a: torch.Tensor) -> torch.Tensor:
+    """Relu bitmask of a (numel % 8 == 0): uint8 [numel/8], bit e of byte i = a[8i+e] > 0 -- the
+    layout bn_apply(mask=True) writes and the BN-backward kernels / GEMM epilogue read."""
+    bits = (a.reshape(-1, 8) > 0).to(torch.uint8)
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=a.device)
+    return (bits * w).sum(1, dtype=torch.uint8)
+
+
+def unpack_relu_mask(mask: torch.Tensor, shape) -> torch.Tensor:
+    """bool tensor of `shape` from a packed relu bitmask."""
+    sh = torch.arange(8, dtype=torch.uint8, device=mask.device)
+    return ((mask.reshape(-1, 1) >> sh) & 1).bool().reshape(shape)
+
+
+def _mask_of(a, shape) -> torch.Tensor:
+    """bool relu mask from a (bf16 post-activation tensor or packed bitmask)."""
+    if a.dtype == torch.uint8:
+        return unpack_relu_mask(a, shape)
+    return a.float().reshape(shape) > 0
+
+
+def bn_apply(y, st: BNState, relu: bool, r=None, rst: BNState | None = None, out=None, mask: bool = False):
+    """a = relu?(y*scale + shift [+ r | + r*rscale + rshift]).
+
+    mask=True (relu only): also return the packed relu bitmask of a (pack_relu_mask), so the
+    backward reads 1 bit per element instead of a itself: returns (a, mask)."""
     C = st.C
+    if mask and not relu:
+        raise ValueError("bn_apply: mask=True needs relu")
     if not on_gpu(y):
         o = y.float() * st.scale + st.shift
         if r is not None:
@@ -70,24 +96,28 @@ def bn_apply(y, st: BNState, relu: bool, r=None, rst: BNState | None = None, out
         o = o.to(torch.bfloat16)
         if out is not None:
             out.copy_(o)
-            return out
-        return o
+            o = out
+        return (o, pack_relu_mask(o)) if mask else o
     out = out if out is not None else torch.empty_like(y)
+    mk = torch.empty(y.numel() // 8, dtype=torch.uint8, device=y.device) if mask else None
     lib().bn_apply(y, st.scale, st.shift, r, rst.scale if rst is not None else None,
-                   rst.shift if rst is not None else None, relu, out, y.numel() // C, C)
-    return out
+                   rst.shift if rst is not None else None, relu, out, y.numel() // C, C, mk)
+    return (out, mk) if mask else out
 
 
 class BNReduce:
     """Spec for fusing a BN-backward reduction into the epilogue of the GEMM that produces dA
-    (dz = dA * mask; sums into st.sums). mask: `a > 0` if a is given, else `y*scale+shift > 0`
-    when relu, else 1. y2/st2: projection-shortcut BN sharing the same dz."""
+    (dz = dA * mask; sums into st.sums). mask: `a > 0` if a is given (a: the bf16 activation or its
+    packed relu bitmask), else `y*scale+shift > 0` when relu, else 1. y2/st2: projection-shortcut
+    BN sharing the same dz."""
 
     def __init__(self, y, st: BNState, a=None, relu: bool = True, y2=None, st2: BNState | None = None):
         self.y, self.st, self.a, self.relu, self.y2, self.st2 = y, st, a, relu, y2, st2
 
     def gemm_args(self):
         st, st2 = self.st, self.st2
+        if self.a is not None and self.a.dtype != torch.uint8:
+            self.a = pack_relu_mask(self.a)  # the epilogue reads the packed mask only
         return [self.y, self.a, st.mean, st.invstd, st.scale if (self.relu and self.a is None) else None,
                 st.shift if (self.relu and self.a is None) else None, self.y2, st2.mean if st2 else None,
                 st2.invstd if st2 else None, st.sums]
@@ -98,7 +128,7 @@ class BNReduce:
         dz = dA.float().reshape(-1, C)
         y = self.y.float().reshape(-1, C)
         if self.a is not None:
-            dz = dz * (self.a.float().reshape(-1, C) > 0)
+            dz = dz * _mask_of(self.a, (-1, C))
         elif self.relu:
             dz = dz * ((y * self.st.scale + self.st.shift) > 0)
         v = self.st.sums.view(self.st.shards, 3, C)
@@ -114,7 +144,8 @@ def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=No
                 reduced: bool = False):
     """Backward of a = relu?(bn(y) [+ bn2(y2) | + r]).
 
-    a: post-activation output used for the relu mask (None -> no relu, unless relu_from_y: the mask
+    a: post-activation output (bf16, or its packed relu bitmask) used for the relu mask (None -> no
+    relu, unless relu_from_y: the mask
     is recomputed as y*scale+shift > 0, valid when there is no residual input). reduced: the
     per-channel sums were already accumulated into st.sums by the producer's GEMM epilogue
     (BNReduce). Returns (dy, dy2, dres). Writes dgamma/dbeta (and the second BN's)."""
@@ -122,7 +153,7 @@ def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=No
     if not on_gpu(da):
         dz = da.float()
         if a is not None:
-            dz = dz * (a.float() > 0)
+            dz = dz * _mask_of(a, da.shape)
         elif relu_from_y:
             dz = dz * ((y.float() * st.scale + st.shift) > 0)
         dz2 = dz.reshape(-1, C)

@@ -182,6 +182,45 @@ def test_bn_fused_forward_backward(proj, C):
         assert rel(out[DEV][k], v) < 1e-2, k
 
 
+@pytest.mark.parametrize("proj", [False, True])
+def test_bn_relu_bitmask(proj):
+    """bn_apply(mask=True) writes the packed relu mask of its output (bit e of byte i = a[8i+e] > 0),
+    and the BN backward / fused dgrad reduction driven by that bitmask equal the bf16-a versions
+    bit for bit (the ResNet tail reads 1 bit per element instead of a)."""
+    C, N, H, W = 256, 4, 9, 7
+    M = N * H * W
+    y, r = bf(N, H, W, C, seed=21).to(DEV), bf(N, H, W, C, seed=22).to(DEV)
+    gamma, beta = (torch.rand(C) + 0.5).to(DEV), (torch.randn(C) * 0.1).to(DEV)
+    st, st2 = BN.BNState(C, DEV), BN.BNState(C, DEV)
+    for s_ in (st, st2):
+        BN.bn_stats(y if s_ is st else r, s_)
+        BN.bn_finalize(s_, M, gamma, beta, 1e-5, 0.1, None, None)
+    a, mk = BN.bn_apply(y, st, True, r=r, rst=st2 if proj else None, mask=True)
+    assert mk.dtype == torch.uint8 and mk.numel() == a.numel() // 8
+    assert torch.equal(mk, BN.pack_relu_mask(a))
+    assert torch.equal(BN.unpack_relu_mask(mk.cpu(), a.shape), a.cpu().float() > 0)
+    da = bf(N, H, W, C, seed=23).to(DEV)
+    outs = []
+    for m in (a, mk):
+        dg, db, dg2, db2 = (torch.zeros(C, device=DEV) for _ in range(4))
+        outs.append(BN.bn_backward(da, m, y, st, gamma, dg, db, M, y2=r if proj else None,
+                                   st2=st2 if proj else None, gamma2=gamma if proj else None, dgamma2=dg2,
+                                   dbeta2=db2, want_dres=not proj) + (dg, db))
+    for u, v in zip(*outs):
+        assert (u is None and v is None) or torch.equal(u, v)
+    # fused into a dgrad epilogue: packed mask vs the CPU oracle on the bf16 activation
+    g = G.ConvGeom(N, H, W, C, 64, 1, 1, 1, 1, 0, 0)
+    w, dy = bf(64, 1, 1, C, scale=0.05, seed=24).to(DEV), bf(N, H, W, 64, seed=25).to(DEV)
+    st.sums.zero_()
+    dx = G.conv_dgrad(dy, w, g, bnr=BN.BNReduce(y, st, a=mk))
+    ref = BN.BNState(C, "cpu")
+    ref.mean.copy_(st.mean.cpu()); ref.invstd.copy_(st.invstd.cpu())
+    BN.BNReduce(y.cpu(), ref, a=a.cpu()).reference_accumulate(dx.cpu())
+    got = st.sums.view(st.shards, 3, C).sum(0).cpu()
+    for k in range(2):
+        assert rel(got[k], ref.sums.view(1, 3, C)[0, k]) < 2e-2, k
+
+
 def test_pools():
     x = bf(2, 17, 17, 64, seed=11)
     y_ref, idx_ref = PL.maxpool_fwd(x)

@@ -83,3 +83,29 @@ def test_resnet_gradients_track_autograd():
     r = torch.cat([leaves[p.name].grad.reshape(-1) for p in m.arena.params])
     cos = float(F.cosine_similarity(g, r, dim=0))
     assert cos > 0.9, cos
+
+
+def test_relu_bitmask_pack_roundtrip_and_backward():
+    """Packed relu mask (bit e of byte i = a[8i+e] > 0): round trip, and the BN backward driven by
+    the bitmask equals the one driven by the bf16 activation (the ResNet tail saves the mask only)."""
+    import torch
+    from tensorflow_k8s_amd.ops import norm as BN
+    g = torch.Generator().manual_seed(0)
+    C, M = 16, 40
+    y = torch.randn(M, C, generator=g).to(torch.bfloat16)
+    r = torch.randn(M, C, generator=g).to(torch.bfloat16)
+    st = BN.BNState(C, "cpu")
+    BN.bn_stats(y, st)
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    BN.bn_finalize(st, M, gamma, beta, 1e-5, 0.1, None, None)
+    a, mk = BN.bn_apply(y, st, True, r=r, mask=True)
+    assert mk.dtype == torch.uint8 and mk.numel() == M * C // 8
+    assert torch.equal(BN.unpack_relu_mask(mk, a.shape), a.float() > 0)
+    da = torch.randn(M, C, generator=g).to(torch.bfloat16)
+    res = []
+    for m in (a, mk):
+        dg, db = torch.zeros(C), torch.zeros(C)
+        dy, _, dres = BN.bn_backward(da, m, y, st, gamma, dg, db, M, want_dres=True)
+        res.append((dy, dres, dg, db))
+    for u, v in zip(*res):
+        assert torch.equal(u, v)

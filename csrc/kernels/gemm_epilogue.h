@@ -152,15 +152,17 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     constexpr int CPR = BN / 8, TOT = BM * CPR;
     constexpr bool bnr = (EPI == EPI_BF16_BNR);
     const int ccol = tid % CPR;  // this thread's 8-column chunk (fixed: NT % CPR == 0)
-    float r0[8], r1[8], r2[8], mu[8], is[8], sc[8], sh[8], mu2[8], is2[8];
+    // BN-reduce partials: r0 = sum dz, r1 = sum dz*y, r2 = sum dz*y2 over this thread's chunks;
+    // the centring (y - mean) * invstd is applied once after the loop (r1 <- (r1 - mean*r0) *
+    // invstd), so mean/invstd need no registers inside the store pass -- those 32 VGPRs pay for a
+    // second chunk in flight on the 128-VGPR (4 waves/SIMD) instantiations.
+    float r0[8], r1[8], r2[8], sc[8], sh[8];
     if constexpr (bnr) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int n = min(n0 + ccol * 8 + e, p.N - 1);
         r0[e] = r1[e] = r2[e] = 0.f;
-        mu[e] = p.bn_mean[n]; is[e] = p.bn_invstd[n];
         sc[e] = p.bn_scale ? p.bn_scale[n] : 1.f; sh[e] = p.bn_shift ? p.bn_shift[n] : 0.f;
-        mu2[e] = p.bn_y2 ? p.bn_mean2[n] : 0.f; is2[e] = p.bn_y2 ? p.bn_invstd2[n] : 0.f;
       }
     }
     // Interior tile (block-uniform): the store pass runs in groups of G chunks whose global loads
@@ -172,8 +174,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     if constexpr (DRAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool tile_fast = (m0 + BM <= p.M) && (n0 + BN <= p.N) && ((p.ldc & 7) == 0);
     constexpr int NIT = TOT / NT;
-    // BNR groups: 1 chunk in flight (BNRG template override); G=2 on <= 128x128 tiles compiled
-    // spill-free (137 VGPRs) but a ResNet-50 step then faulted -- not yet root-caused, kept off
+    // BNR groups: BNRG chunks in flight (the caller sizes it to its VGPR budget; 0 -> 1). Every
+    // load below is from an in-bounds address: absent tensors are not loaded at all (block-uniform
+    // branches), and off the residual lattice the (unused) residual load reads C.
     constexpr int GB = BNRG > 0 ? BNRG : 1;
     constexpr int G = bnr ? (NIT < GB ? NIT : GB) : (EPI == EPI_BF16_EXT ? (NIT < 2 ? NIT : 2) : (NIT < 4 ? NIT : 4));
     if (tile_fast) {
@@ -202,12 +205,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           cv[g] = *(const bf16x8*)(Cs + row * LDC_S + cc * 8);
           // off the residual's sub-sampling lattice the (unused) load reads C itself: resid is the
           // smaller lattice tensor there, so resid + off[g] could run past its allocation
-          rr[g] = *(const bf16x8*)(rok[g] ? resid_b + bz * p.sC + mr * p.ldc + n : (const bf16*)p.C + off[g]);
-          if constexpr (EPI == EPI_BF16_EXT) zv[g] = *(const bf16x8*)(dsrc_b + off[g]);
+          if (p.resid) rr[g] = *(const bf16x8*)(rok[g] ? resid_b + bz * p.sC + mr * p.ldc + n : (const bf16*)p.C + off[g]);
+          if constexpr (EPI == EPI_BF16_EXT) {
+            if (p.dact_src) zv[g] = *(const bf16x8*)(dsrc_b + off[g]);
+          }
           if constexpr (bnr) {
             yv[g] = *(const bf16x8*)(y_b + off[g]);
-            mk[g] = mk_b[off[g] >> 3];
-            y2v[g] = *(const bf16x8*)(y2_b + off[g]);
+            if (p.bn_amask) mk[g] = mk_b[off[g] >> 3];
+            if (p.bn_y2) y2v[g] = *(const bf16x8*)(y2_b + off[g]);
           }
         }
 #pragma unroll
@@ -246,8 +251,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
               const bool keep = p.bn_amask ? ((mk[g] >> e) & 1u) != 0 : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
               const float dz = keep ? bf2f(v[e]) : 0.f;
               r0[e] += dz;
-              r1[e] += dz * (y - mu[e]) * is[e];
-              if (p.bn_y2) r2[e] += dz * (bf2f(y2v[g][e]) - mu2[e]) * is2[e];
+              r1[e] += dz * y;
+              if (p.bn_y2) r2[e] += dz * bf2f(y2v[g][e]);
             }
           }
         }
@@ -307,8 +312,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             bool keep = p.bn_amask ? ((mk >> e) & 1u) != 0 : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
             const float dz = keep ? bf2f(v[e]) : 0.f;
             r0[e] += dz;
-            r1[e] += dz * (y - mu[e]) * is[e];
-            if (p.bn_y2) r2[e] += dz * (bf2f(y2v[e]) - mu2[e]) * is2[e];
+            r1[e] += dz * y;
+            if (p.bn_y2) r2[e] += dz * bf2f(y2v[e]);
           }
         }
       } else {
@@ -330,6 +335,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     }
     }  // ragged tile
     if constexpr (bnr) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int n = min(n0 + ccol * 8 + e, p.N - 1);
+        r1[e] = (r1[e] - p.bn_mean[n] * r0[e]) * p.bn_invstd[n];
+        if (p.bn_y2) r2[e] = (r2[e] - p.bn_mean2[n] * r0[e]) * p.bn_invstd2[n];
+      }
       // lanes sharing a column chunk: tid % CPR equal -> xor over the bits above log2(CPR)
 #pragma unroll
       for (int e = 0; e < 8; ++e)

@@ -194,7 +194,9 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
   constexpr bool AKO = (AM == KOUT), BKO = (LBM == KOUT || LBM == CONV_WGRAD);
   constexpr int WTM = 64, WTN = 64, FM = 4, FN = 4;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr bool SHORTK = OCC > occ_default<BM, BN>();  // host guarantees kt_per_split == 1
+  // SHORTK: one LDS stage, no intra-block double buffering (the host launches it for blocks of
+  // <= g_shortk K-tiles); co-resident blocks hide the DMA latency instead
+  constexpr bool SHORTK = OCC > occ_default<BM, BN>();
   constexpr int MAIN = (SHORTK ? 1 : 2) * STAGE, EPIB = epi_lds_bytes<BM, BN, WGM>();
   __shared__ __attribute__((aligned(16))) char smem[MAIN > EPIB ? MAIN : EPIB];
 
@@ -256,11 +258,11 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
 
 #pragma unroll 1
   for (int kt = kt0; kt < kt1; ++kt) {
-    const int s = (kt - kt0) & 1;
+    const int s = SHORTK ? 0 : (kt - kt0) & 1;
     const char* As = stage_ptr(s);
     const char* Bs = As + A_BYTES;
     const bool more = kt + 1 < kt1;
-    if (more) {
+    if (!SHORTK && more) {
       char* nx = stage_ptr(s ^ 1);
       la.issue(p, Ab, a_step, kt + 1, lim_a, nx, w, lane);
       lb.issue(p, Bb, b_step, kt + 1, lim_b, nx + A_BYTES, w, lane);
@@ -280,16 +282,26 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
       for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a, acc[i][j], 0, 0, 0);
     }
     if (more) {
+      if constexpr (SHORTK) {
+        // every wave's reads of the single stage are done before the next K-tile overwrites it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        la.issue(p, Ab, a_step, kt + 1, lim_a, stage_ptr(0), w, lane);
+        lb.issue(p, Bb, b_step, kt + 1, lim_b, stage_ptr(0) + A_BYTES, w, lane);
+      }
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      const char* Bn = stage_ptr(s ^ 1) + A_BYTES;
+      const char* Bn = stage_ptr(SHORTK ? 0 : s ^ 1) + A_BYTES;
 #pragma unroll
       for (int j = 0; j < FN; ++j) b0[j] = frag<BKO>(Bn, bc + j * 16, 0);
     }
   }
   __syncthreads();
-  gemm_epilogue<BM, BN, NTH, WGM, EPI, (SHORTK ? 1 : 0)>(p, acc, smem, m0, n0, bz);
+  // BN-reduce chunks in flight per thread by VGPR budget: 512 / (waves per SIMD)
+  constexpr int WPS = (NW * OCC) / 4 > 0 ? (NW * OCC) / 4 : 1;
+  gemm_epilogue<BM, BN, NTH, WGM, EPI, (512 / WPS >= 256 ? 4 : 2)>(p, acc, smem, m0, n0, bz);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -618,15 +630,21 @@ static bool persist_on() {
 }
 extern "C" void tfk_g4_set_persist(int on) { g_persist = on ? 1 : 0; }
 
+#ifndef G4_SHORTK_DEFAULT_KT
+#define G4_SHORTK_DEFAULT_KT 4
+#endif
+// Max K-tiles per block for the single-stage 4-blocks-per-CU 128x128 variant (0 = off).
+// TFK_G4_SHORTK=<n> overrides the default.
 static int g_shortk = -1;
-static bool shortk_on() {
+static int shortk_max_kt() {
   if (g_shortk < 0) {
     const char* e = getenv("TFK_G4_SHORTK");
-    g_shortk = (e && e[0] == '0') ? 0 : 1;
+    g_shortk = e ? atoi(e) : G4_SHORTK_DEFAULT_KT;
   }
-  return g_shortk == 1;
+  return g_shortk;
 }
-extern "C" void tfk_g4_set_shortk(int on) { g_shortk = on ? 1 : 0; }
+// < 0: back to the environment / built-in default
+extern "C" void tfk_g4_set_shortk(int max_kt) { g_shortk = max_kt < 0 ? -1 : max_kt; }
 
 static void fast_div(unsigned d, unsigned* mul, int* shift) {
   int s = 0;
@@ -657,9 +675,9 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
     TFK_G4P_TILES(2, 0, EPI_BF16)
     TFK_G4P_TILES(2, 0, EPI_BF16_BNR)
   }
-  // one K-tile per block: the 4-blocks-per-CU single-stage instantiations (TFK_G4_SHORTK=0: off;
-  // measured ResNet-50 bs256: 30.40 -> 29.72 ms/step)
-  if (p.kt_per_split == 1 && bm == 128 && bn == 128 && shortk_on()) {
+  // few K-tiles per block: the 4-blocks-per-CU single-stage instantiations (TFK_G4_SHORTK=0: off;
+  // one K-tile measured ResNet-50 bs256: 30.40 -> 29.72 ms/step)
+  if (p.kt_per_split <= shortk_max_kt() && bm == 128 && bn == 128) {
     TFK_G4_SHORTK(0, 0, EPI_BF16)
     TFK_G4_SHORTK(0, 1, EPI_BF16)
     TFK_G4_SHORTK(0, 1, EPI_BF16_BNR)

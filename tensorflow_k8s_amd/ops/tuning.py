@@ -19,7 +19,9 @@ import json
 import os
 
 _PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_wgrad.json")
-_CONV_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_conv.json")
+# TFK_CONV_TABLE: an alternative conv tile table (A/B of a fresh tools/conv_sweep.py --table)
+_CONV_PATH = os.environ.get("TFK_CONV_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                "tuned_conv.json")
 _TABLE: dict | None = None
 _CONV: dict | None = None
 ENABLED = os.environ.get("TFK_TUNING", "1") != "0"

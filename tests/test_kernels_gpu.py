@@ -513,11 +513,13 @@ def test_g4_conv_fwd_gather(cfg, tile):
     assert rel(st_[0], ref.reshape(-1, K).sum(0)) < 1e-2
 
 
-@pytest.mark.parametrize("shape", [(4, 28, 28, 64, 256), (3, 17, 19, 64, 200)])
+@pytest.mark.parametrize("shape", [(4, 28, 28, 64, 256), (3, 17, 19, 64, 200), (4, 28, 28, 256, 128),
+                                   (3, 17, 19, 192, 200), (2, 14, 14, 512, 256)])
 def test_shortk_single_stage_blocks(shape):
-    """K <= 64 GEMMs (1x1 conv with 64 input channels): the single-stage 4-blocks-per-CU g4
-    instantiation must equal the two-stage kernel (same per-tile math) for conv fwd + BN stats and
-    for the BN-reduce dgrad, and match the fp32 CPU reference."""
+    """Few-K-tile GEMMs (1x1 convs with 64..512 input channels, 1..8 K-tiles of 64): the
+    single-stage 4-blocks-per-CU g4 instantiation (looping its K-tiles through one LDS stage) must
+    equal the two-stage kernel (same per-tile math) for conv fwd + BN stats and for the BN-reduce
+    dgrad, and match the fp32 CPU reference. 128x128 tiles forced (the variant's only tile)."""
     L = lib()
     N, H, W, C, K = shape
     g = G.ConvGeom(N, H, W, C, K, 1, 1)
@@ -541,17 +543,19 @@ def test_shortk_single_stage_blocks(shape):
 
     res = {}
     try:
-        for flag in (0, 1):
+        G.FORCE_TILE = (128, 128)
+        for flag in (0, 8):
             L.gemm_set_shortk(flag)
             res[flag] = run(DEV)
             torch.cuda.synchronize()
     finally:
-        L.gemm_set_shortk(1)
+        G.FORCE_TILE = None
+        L.gemm_set_shortk(-1)  # back to the TFK_G4_SHORTK / built-in default
     ref = run("cpu")
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][2], res[1][2])
+    assert torch.equal(res[0][0], res[8][0]) and torch.equal(res[0][2], res[8][2])
     for i in range(4):
-        assert rel(res[1][i], ref[i]) < 2e-2, i
-        assert rel(res[1][i], res[0][i]) < 1e-4, i
+        assert rel(res[8][i], ref[i]) < 2e-2, i
+        assert rel(res[8][i], res[0][i]) < 1e-4, i
 
 
 @pytest.mark.parametrize("case", ["fwd_relu", "dgrad_resid", "ext_gelu_drop", "conv_stats", "bnr_dgrad"])

@@ -94,6 +94,8 @@ def main():
     fh = open(args.out, "w") if args.out else None
     entries, saved = [], 0.0
     for (kind, geom, flags), count in sorted(calls.items(), key=lambda kv: kv[0][1]):
+        if kind not in ("fwd", "dgrad_pw", "dgrad_fwd"):
+            continue  # weight-gradient records belong to tools/wgrad_sweep.py
         pw = geom[7] == 1 and geom[8] == 1 and geom[9] == 1 and geom[10] == 1 and geom[11] == 0 and geom[12] == 0
         cands = CANDS["fwd_pw" if kind == "fwd" and pw else "fwd_gather" if kind == "fwd" else kind]
         fn = make_call(kind, geom, flags)

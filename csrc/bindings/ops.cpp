@@ -213,6 +213,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
                   (bm == 256 && bn == 256 && (dense_a || amode == A_CONV_FWD) && (bmode == B_KIN || bmode == B_KOUT)) ||
                   (bm == 256 && bn == 256 && amode == A_KOUT && bmode == B_CONV_WGRAD) ||
                   (bm == 256 && bn == 64 && dense_a && !(amode == A_KOUT && bmode == B_KOUT && epi == 0)) ||
+                  (bm == 256 && bn == 64 && amode == A_CONV_FWD && bmode == B_KIN) ||
                   (bm == 64 && bn == 256 && amode == A_KOUT && bmode == B_CONV_WGRAD && epi == 1) ||
                   (bm == 64 && bn == 256 && amode == A_KOUT && bmode == B_KOUT && epi == 1),
               "unsupported tile ", bm, "x", bn, " for operand modes ", amode, "/", bmode);

@@ -396,7 +396,8 @@ def dgrad_as_fwd_geom(g: ConvGeom) -> ConvGeom | None:
 # must be a multiple of 64) for outputs of >= 128 channels. TFK_DGRAD_AS_FWD=0 restores the
 # register-engine gather (measured ResNet-50 step: 31.13 -> 30.81 ms with it on).
 DGRAD_AS_FWD = os.environ.get("TFK_DGRAD_AS_FWD", "1") == "1"
-DGRAD_AS_FWD_MIN_C = 128  # 64-channel dx: the 2-wave 128x64 BN epilogue measured slower (0.28 vs 0.22 ms)
+# 64-channel dx: the 2-wave 128x64 BN epilogue measured slower (0.28 vs 0.22 ms); TFK_DGRAD_AS_FWD_MIN_C
+DGRAD_AS_FWD_MIN_C = int(os.environ.get("TFK_DGRAD_AS_FWD_MIN_C", 128))
 # Non-pointwise weight gradients on the LDS-DMA engine's im2col gather (B_CONV_WGRAD, C % 8 == 0).
 G4_WGRAD = os.environ.get("TFK_G4_WGRAD", "1") == "1"
 

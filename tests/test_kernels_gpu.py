@@ -335,6 +335,17 @@ def test_dgrad_fused_bn_reduce(cfg, mode):
         assert rel(res[DEV][1][k], res["cpu"][1][k]) < 2e-2, k
 
 
+@pytest.mark.parametrize("mode", ["relu_from_y", "mask_a", "dual"])
+@pytest.mark.parametrize("cfg", [(2, 9, 9, 64, 64, 3, 3, 1, 1), (3, 20, 20, 64, 128, 3, 3, 1, 1)])
+def test_dgrad_as_fwd_256x64(cfg, mode, monkeypatch):
+    """64-channel stride-1 dgrad as a forward conv on g4's 4-wave 256x64 gather tile with the fused
+    BN-backward reduction (ResNet stage-1 3x3): same checks as test_dgrad_fused_bn_reduce."""
+    monkeypatch.setattr(G, "DGRAD_AS_FWD_MIN_C", 64)
+    monkeypatch.setattr(G, "FORCE_TILE", (256, 64))
+    assert G.dgrad_as_fwd_geom(G.ConvGeom(*cfg[:7], cfg[7], cfg[7], cfg[8], cfg[8])) is not None
+    test_dgrad_fused_bn_reduce(cfg, mode)
+
+
 @pytest.mark.parametrize("M,N,K", [(512, 512, 256), (520, 300, 200), (777, 1030, 136)])
 def test_big_tile_256(M, N, K, monkeypatch):
     """The 8-wave 256x256 tile (dense operand modes) on interior and ragged shapes: fwd (bias+gelu
@@ -495,7 +506,7 @@ def test_lds_dma_gemm_modes(M, N, K, tile):
 
 @pytest.mark.parametrize("cfg", [(2, 14, 14, 64, 128, 3, 3, 1, 1), (3, 9, 11, 128, 200, 3, 3, 2, 1),
                                  (2, 8, 8, 64, 64, 1, 1, 2, 0), (1, 30, 30, 64, 136, 5, 5, 1, 2)])
-@pytest.mark.parametrize("tile", [(256, 256), (128, 128)])
+@pytest.mark.parametrize("tile", [(256, 256), (128, 128), (256, 64)])
 def test_g4_conv_fwd_gather(cfg, tile):
     """g4's implicit-GEMM conv-forward gather (Cin % 64 == 0: a K-tile is one tap x 64 channels,
     zero padding from out-of-range DMA) against the fp32 reference, with BN statistics."""

@@ -26,9 +26,9 @@ from tensorflow_k8s_amd.ops import tuning  # noqa: E402
 
 CANDS = {
     "fwd_pw": [(128, 128), (256, 256), (128, 64), (64, 128), (256, 64), (64, 64)],
-    "fwd_gather": [(128, 128), (256, 256), (128, 64), (64, 128), (64, 64)],
+    "fwd_gather": [(128, 128), (256, 256), (128, 64), (64, 128), (64, 64), (256, 64)],
     "dgrad_pw": [(128, 128), (256, 256), (128, 64), (64, 128), (256, 64), (64, 64)],
-    "dgrad_fwd": [(128, 128), (256, 256), (128, 64), (64, 128), (64, 64)],
+    "dgrad_fwd": [(128, 128), (256, 256), (128, 64), (64, 128), (64, 64), (256, 64)],
 }
 
 

@@ -488,7 +488,9 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
   if (p.stats_shards < 1) p.stats_shards = 1;
   if (epi == EPI_BF16 && p.bn_sums) epi = EPI_BF16_BNR;
   if (epi == EPI_BF16 && (p.aux || p.dact_src || p.drop_p > 0.f)) epi = EPI_BF16_EXT;
-  if (p.om_hp == 0 && p.rs_sh == 0) {
+  // row maps (strided-conv dgrad phases, lattice residual) live in the BN-reduce epilogue, which
+  // both engines share
+  if ((p.om_hp == 0 && p.rs_sh == 0) || epi == EPI_BF16_BNR) {
     if (engine() == 1 && tfk_g4_ok(p, amode, bmode)) {
       const int r = tfk_g4_launch(p, bm, bn, amode, bmode, epi, batch, splits, stream);
       if (r != -1) return r;

@@ -398,6 +398,9 @@ def dgrad_as_fwd_geom(g: ConvGeom) -> ConvGeom | None:
 DGRAD_AS_FWD = os.environ.get("TFK_DGRAD_AS_FWD", "1") == "1"
 # 64-channel dx: the 2-wave 128x64 BN epilogue measured slower (0.28 vs 0.22 ms); TFK_DGRAD_AS_FWD_MIN_C
 DGRAD_AS_FWD_MIN_C = int(os.environ.get("TFK_DGRAD_AS_FWD_MIN_C", 128))
+# Strided-conv dgrad phases (BN-reduce epilogue with the phase out-map) as forward convs over dY on
+# the LDS-DMA gather (needs the conv's Cout % 64 == 0); TFK_PHASES_AS_FWD=0: register-engine gather.
+PHASES_AS_FWD = os.environ.get("TFK_PHASES_AS_FWD", "1") == "1"
 # Non-pointwise weight gradients on the LDS-DMA engine's im2col gather (B_CONV_WGRAD, C % 8 == 0).
 G4_WGRAD = os.environ.get("TFK_G4_WGRAD", "1") == "1"
 
@@ -479,13 +482,21 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
     phases = _phases(g) if (bnr is not None and (g.sh > 1 or g.sw > 1)) else None
     if phases is not None:
         wt = wt if wt is not None else conv_weight_t(w, g)
+        as_fwd = PHASES_AS_FWD and G4_ENABLED and g.K % 64 == 0
         for a, b, Ha, Wb, r0, s0, Rp, Sp, php, pwp in phases:
-            wp = wt[:, r0::g.sh, s0::g.sw, :].contiguous()  # [C][Rp][Sp][K] sub-kernel (weights only)
+            wp = wt[:, r0::g.sh, s0::g.sw, :]  # [C][Rp][Sp][K] sub-kernel (weights only)
             Mp, Kd = g.N * Ha * Wb, Rp * Sp * g.K
-            conv = [g.N, Ha, Wb, g.C, g.P, g.Q, g.K, Rp, Sp, 1, 1, php, pwp, 1, 1]
             rmap = [Ha, Wb, g.H, g.W, g.sh, g.sw, a, b] + [0] * 6
-            _gemm(dy, wp, dx, Mp, g.C, Kd, 0, Kd, g.C, A_CONV_DGRAD, B_KIN, EPI_BF16,
-                  pick_tile(Mp, g.C, K=Kd, mid_ok=False), resid=resid, conv=conv, bnr=bnr, rowmap=rmap)
+            if as_fwd:
+                # the phase's stride-1 dgrad as a forward conv over dY (flipped taps, pad Rp-1-php)
+                # on the LDS-DMA gather; GEMM rows walk the phase grid, the out-map scatters them
+                conv = [g.N, g.P, g.Q, g.K, Ha, Wb, g.C, Rp, Sp, 1, 1, Rp - 1 - php, Sp - 1 - pwp, 1, 1]
+                _gemm(dy, wp.flip(1, 2).contiguous(), dx, Mp, g.C, Kd, 0, Kd, g.C, A_CONV_FWD, B_KIN, EPI_BF16,
+                      pick_tile(Mp, g.C, K=Kd, mid_ok=False, g4=True), resid=resid, conv=conv, bnr=bnr, rowmap=rmap)
+            else:
+                conv = [g.N, Ha, Wb, g.C, g.P, g.Q, g.K, Rp, Sp, 1, 1, php, pwp, 1, 1]
+                _gemm(dy, wp.contiguous(), dx, Mp, g.C, Kd, 0, Kd, g.C, A_CONV_DGRAD, B_KIN, EPI_BF16,
+                      pick_tile(Mp, g.C, K=Kd, mid_ok=False), resid=resid, conv=conv, bnr=bnr, rowmap=rmap)
         return dx
     if g.R == 1 and g.S == 1:
         # strided 1x1: B(n=c, k=co) = W[co][c] is K-outer with ldb = C; gather handles the stride

@@ -304,7 +304,9 @@ def test_global_norm_clip():
 @pytest.mark.parametrize("mode", ["relu_from_y", "mask_a", "dual"])
 @pytest.mark.parametrize("cfg", [(2, 8, 8, 64, 256, 1, 1, 1, 0), (2, 9, 9, 64, 64, 3, 3, 1, 1), (2, 14, 14, 256, 512, 1, 1, 2, 0),
                                  (2, 16, 16, 64, 64, 3, 3, 2, 1), (2, 15, 13, 32, 48, 3, 3, 2, 1),
-                                 (2, 9, 9, 128, 64, 3, 3, 1, 1), (3, 20, 20, 256, 256, 3, 3, 1, 1)])
+                                 (2, 9, 9, 128, 64, 3, 3, 1, 1), (3, 20, 20, 256, 256, 3, 3, 1, 1),
+                                 (2, 14, 14, 64, 128, 3, 3, 2, 1), (2, 15, 13, 64, 128, 3, 3, 2, 1),
+                                 (2, 12, 12, 32, 64, 5, 5, 2, 2)])
 def test_dgrad_fused_bn_reduce(cfg, mode):
     """BN-backward channel sums fused into the dgrad epilogue == the standalone reduction."""
     N, H, W, C, K, R, S, st_, pd = cfg

@@ -22,7 +22,7 @@
 // rows/k read zeros: the buffer descriptor range check returns 0 for offsets past num_records.
 //
 // Operand modes: A_KIN / A_KOUT / A_CONV_FWD (implicit-GEMM gather, Cin % 64 == 0: a K-tile is one
-// (r,s) tap and 64 channels) x B_KIN / B_KOUT / B_CONV_WGRAD (im2col of X as the K-outer operand of
+// (r,s) tap and 64 channels; Cin % 8 == 0 below 64: 64/Cin taps per K-tile) x B_KIN / B_KOUT / B_CONV_WGRAD (im2col of X as the K-outer operand of
 // a weight gradient: GEMM k = output pixel (n,p,q), column = (r,s,c); each lane's 16-B chunk is 8
 // channels of one tap, so C % 8 == 0; the pixel of a K-tile row is found with magic-number
 // division). Epilogues: gemm_epilogue.h (LDS-staged).
@@ -80,7 +80,9 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int rb, int kk) {
 
 // Per-thread DMA plan of one operand: ROWS/32 instructions per K-tile. Instruction j (of ROWS/8,
 // wave w takes j = 4i + w) fills image bytes [j*1024, j*1024+1024).
-template <int ROWS, int MODE, int NW>
+// SMALLC: also compile the Cin < 64 conv-forward gather (off in the 128-VGPR single-stage kernels,
+// which the host never gives such a conv)
+template <int ROWS, int MODE, int NW, bool SMALLC = true>
 struct Loader {
   static constexpr int NI = ROWS / 8 / NW;  // DMA instructions per thread per K-tile
   // dense: byte offset from the tile origin at K-tile 0; conv: image index n of the lane's pixel
@@ -148,17 +150,35 @@ struct Loader {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
       }
     } else if constexpr (MODE == CONV_FWD) {
-      // K-tile kt covers tap (r, s) = divmod(kt*64 / Cin, S) and channels c0..c0+63 (Cin % 64 == 0)
-      const int k0 = kt * BK, rs = k0 / p.Cin, c0 = k0 - rs * p.Cin;
-      const int r = rs / p.S, s = rs - r * p.S;
       __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, NREC, 0x00020000);
+      if (!SMALLC || p.Cin >= BK) {
+        // K-tile kt covers tap (r, s) = divmod(kt*64 / Cin, S) and channels c0..c0+63 (Cin % 64 == 0)
+        const int k0 = kt * BK, rs = k0 / p.Cin, c0 = k0 - rs * p.Cin;
+        const int r = rs / p.S, s = rs - r * p.S;
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int h = ch[i] + r * p.dh, wq = cw[i] + s * p.dw;
-        const bool ok = (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
-        const long long pix = ((long long)off[i] * p.H + h) * p.W + wq;
-        const unsigned vo = ok ? (unsigned)((pix * p.Cin + c0 + k_of(i, w, lane)) * 2) : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
+        for (int i = 0; i < NI; ++i) {
+          const int h = ch[i] + r * p.dh, wq = cw[i] + s * p.dw;
+          const bool ok = (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
+          const long long pix = ((long long)off[i] * p.H + h) * p.W + wq;
+          const unsigned vo = ok ? (unsigned)((pix * p.Cin + c0 + k_of(i, w, lane)) * 2) : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
+        }
+      } else {
+        // Cin % 8 == 0, Cin < 64 (the stem's 3 channels padded to 8): a K-tile spans 64/Cin taps and
+        // each lane's 16-B chunk is 8 channels of ONE tap -- per-lane (tap, c) by magic-number
+        // division (host: fd_pq = Cin, fd_q = S); k >= K (the ragged last K-tile) reads zeros
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const unsigned k = (unsigned)(kt * BK + k_of(i, w, lane));
+          const unsigned rs = fdiv(k, p.fd_pq_mul, p.fd_pq_shift), c = k - rs * (unsigned)p.Cin;
+          const unsigned r = fdiv(rs, p.fd_q_mul, p.fd_q_shift), sx = rs - r * (unsigned)p.S;
+          const int h = ch[i] + (int)r * p.dh, wq = cw[i] + (int)sx * p.dw;
+          const bool ok = (int)k < p.K && (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H &&
+                          (unsigned)wq < (unsigned)p.W;
+          const long long pix = ((long long)off[i] * p.H + h) * p.W + wq;
+          const unsigned vo = ok ? (unsigned)((pix * p.Cin + c) * 2) : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
+        }
       }
     } else {
       __amdgpu_buffer_rsrc_t rsrc =
@@ -226,7 +246,7 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
   const long long b_step = BKO ? (long long)BK * p.ldb * 2 : BK * 2;
   const int lim_a = p.M - m0, lim_b = p.N - n0;
 
-  Loader<BM, AM, NW> la;
+  Loader<BM, AM, NW, !SHORTK> la;
   Loader<BN, LBM, NW> lb;
   la.init(p, lane, w, p.lda, m0, p.M);
   lb.init(p, lane, w, p.ldb, n0, p.N);
@@ -569,7 +589,9 @@ extern "C" int tfk_g4_ok(const GemmParams& p, int amode, int bmode) {
   if ((p.sA & 7) || (p.sB & 7)) return 0;
   if (amode == 1 && (p.M & 7)) return 0;
   if (bmode >= 1 && (p.N & 7)) return 0;
-  if (amode == 2 && ((p.Cin & 63) || (long long)p.Nimg * p.H * p.W * p.Cin >= (1LL << 30))) return 0;
+  // conv-fwd gather: Cin % 64 == 0 (one tap per K-tile) or Cin % 8 == 0 below 64 (taps per K-tile)
+  if (amode == 2 && (((p.Cin & 63) && ((p.Cin & 7) || p.Cin > 64)) || (long long)p.Nimg * p.H * p.W * p.Cin >= (1LL << 30)))
+    return 0;
   return 1;
 }
 
@@ -663,6 +685,10 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
     fast_div((unsigned)p.Q, &p.fd_q_mul, &p.fd_q_shift);
     fast_div((unsigned)(p.P * p.Q), &p.fd_pq_mul, &p.fd_pq_shift);
   }
+  if (amode == 2 && p.Cin < 64) {
+    fast_div((unsigned)p.S, &p.fd_q_mul, &p.fd_q_shift);
+    fast_div((unsigned)p.Cin, &p.fd_pq_mul, &p.fd_pq_shift);
+  }
   // many tiles: the persistent kernel on a resident grid (opt-in TFK_G4_PERSIST=1; measured slower
   // than the one-shot grid: sq4096 fwd 814 vs 854 TF, tfm_ffn1 772 vs 840, ResNet-50 29.01 vs
   // 28.81 ms -- its 165-200 VGPRs and the drain before the epilogue's loads eat the overlap)
@@ -677,7 +703,7 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
   }
   // few K-tiles per block: the 4-blocks-per-CU single-stage instantiations (TFK_G4_SHORTK=0: off;
   // one K-tile measured ResNet-50 bs256: 30.40 -> 29.72 ms/step)
-  if (p.kt_per_split <= shortk_max_kt() && bm == 128 && bn == 128) {
+  if (p.kt_per_split <= shortk_max_kt() && bm == 128 && bn == 128 && !(amode == 2 && p.Cin < 64)) {
     TFK_G4_SHORTK(0, 0, EPI_BF16)
     TFK_G4_SHORTK(0, 1, EPI_BF16)
     TFK_G4_SHORTK(0, 1, EPI_BF16_BNR)

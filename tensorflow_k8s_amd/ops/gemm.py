@@ -356,7 +356,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
     M = g.N * g.P * g.Q
     y = torch.empty(g.N, g.P, g.Q, g.K, dtype=torch.bfloat16, device=x.device)
     tile = _conv_tile("fwd", g, lambda: pick_tile(M, g.K, big_ok=g.pointwise, K=g.R * g.S * g.C, mid_ok=g.pointwise,
-                                                  g4=g.pointwise or g.C % 64 == 0),
+                                                  g4=g.pointwise or g.C % 64 == 0 or (g.C % 8 == 0 and g.C < 64)),
                       (stats is not None, bias is not None, act is not None))
     if g.pointwise:
         _gemm(x, w, y, M, g.K, g.C, g.C, g.C, g.K, A_KIN, B_KIN, EPI_BF16, tile, stats=stats, shards=shards,

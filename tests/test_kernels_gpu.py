@@ -507,11 +507,15 @@ def test_lds_dma_gemm_modes(M, N, K, tile):
 
 
 @pytest.mark.parametrize("cfg", [(2, 14, 14, 64, 128, 3, 3, 1, 1), (3, 9, 11, 128, 200, 3, 3, 2, 1),
-                                 (2, 8, 8, 64, 64, 1, 1, 2, 0), (1, 30, 30, 64, 136, 5, 5, 1, 2)])
+                                 (2, 8, 8, 64, 64, 1, 1, 2, 0), (1, 30, 30, 64, 136, 5, 5, 1, 2),
+                                 # Cin < 64: several taps per K-tile (stem 7x7/2 on 8 channels, ragged K)
+                                 (2, 20, 20, 8, 64, 7, 7, 2, 3), (1, 15, 17, 16, 72, 3, 3, 1, 1),
+                                 (2, 9, 9, 32, 64, 5, 5, 2, 2)])
 @pytest.mark.parametrize("tile", [(256, 256), (128, 128), (256, 64)])
 def test_g4_conv_fwd_gather(cfg, tile):
-    """g4's implicit-GEMM conv-forward gather (Cin % 64 == 0: a K-tile is one tap x 64 channels,
-    zero padding from out-of-range DMA) against the fp32 reference, with BN statistics."""
+    """g4's implicit-GEMM conv-forward gather (Cin % 64 == 0: a K-tile is one tap x 64 channels;
+    Cin % 8 == 0 below 64: 64/Cin taps per K-tile; zero padding from out-of-range DMA) against the
+    fp32 reference, with BN statistics."""
     N, H, W, C, K, R, S, st, pd = cfg
     g = G.ConvGeom(N, H, W, C, K, R, S, st, st, pd, pd)
     x, w = bf(N, H, W, C, seed=7), bf(K, R, S, C, scale=0.05, seed=8)

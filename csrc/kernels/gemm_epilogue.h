@@ -174,7 +174,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     if constexpr (DRAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool tile_fast = (m0 + BM <= p.M) && (n0 + BN <= p.N) && ((p.ldc & 7) == 0);
     constexpr int NIT = TOT / NT;
-    // BNR groups: BNRG chunks in flight (the caller sizes it to its VGPR budget; 0 -> 1). Every
+    // BNR groups: BNRG chunks in flight (the caller sizes it to its VGPR budget; 0 -> 1). Measured
+    // on the 128-VGPR single-stage 128x128 kernels (ResNet-50 bs256 step): 1 -> 26.47 ms, 2 -> 26.32,
+    // 4 -> 29.52 (208 B/lane of spills). Every
     // load below is from an in-bounds address: absent tensors are not loaded at all (block-uniform
     // branches), and off the residual lattice the (unused) residual load reads C.
     constexpr int GB = BNRG > 0 ? BNRG : 1;

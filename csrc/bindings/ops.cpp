@@ -35,6 +35,7 @@ int tfk_bn_bwd_apply(const void*, const void*, const void*, const float*, void*,
                      long long, int, const float*, const float*, const uint8_t*, hipStream_t);
 int tfk_maxpool_fwd(const void*, void*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int tfk_maxpool_bwd(const void*, const uint8_t*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                    const void*, const float*, const float*, const float*, const float*, const uint8_t*, float*, int,
                     hipStream_t);
 int tfk_avgpool_fwd(const void*, void*, int, int, int, hipStream_t);
 int tfk_avgpool_bwd(const void*, void*, int, int, int, hipStream_t);
@@ -440,13 +441,45 @@ void maxpool_fwd(torch::Tensor x, torch::Tensor y, torch::Tensor idx, std::vecto
                            g[7], g[8], g[9], g[10], g[11], cur_stream()),
            "maxpool_fwd");
 }
-void maxpool_bwd(torch::Tensor dy, torch::Tensor idx, torch::Tensor dx, std::vector<int64_t> g) {
+// bnr (optional, the gemm's 10-entry BN-reduce spec without y2): also accumulate the BN-backward
+// channel sums of the layer that produced the pooled input from the final dx
+void maxpool_bwd(torch::Tensor dy, torch::Tensor idx, torch::Tensor dx, std::vector<int64_t> g,
+                 std::vector<c10::optional<torch::Tensor>> bnr, int bn_shards) {
   TORCH_CHECK(g.size() == 12, "geom");
   need_bf16(dy, "dy"); need_bf16(dx, "dx"); need(idx, at::kByte, "idx");
-  need_numel(dx, g[0] * g[1] * g[2] * g[3], "dx");
+  const long long nx = g[0] * g[1] * g[2] * g[3];
+  need_numel(dx, nx, "dx");
   need_numel(dy, g[0] * g[4] * g[5] * g[3], "dy");
+  need_numel(idx, g[0] * g[4] * g[5] * g[3], "idx");
+  const void* y = nullptr;
+  const float *mean = nullptr, *invstd = nullptr, *msc = nullptr, *msh = nullptr;
+  const uint8_t* amask = nullptr;
+  float* sums = nullptr;
+  if (!bnr.empty()) {
+    TORCH_CHECK(bnr.size() == 10, "bnr needs 10 entries");
+    for (int i : {0, 2, 3, 9}) TORCH_CHECK(bnr[i].has_value() && bnr[i]->defined(), "bnr missing required entry ", i);
+    TORCH_CHECK(!(bnr[6].has_value() && bnr[6]->defined()), "maxpool_bwd BN reduce: no second BN");
+    TORCH_CHECK(256 % (g[3] / 8) == 0 && g[3] % 8 == 0, "maxpool_bwd BN reduce needs (C/8) | 256");
+    need_bf16(*bnr[0], "bn_y"); need_numel(*bnr[0], nx, "bn_y");
+    const void* bn_a = nullptr;
+    amask = relu_bitmask(bnr[1], nx, &bn_a);
+    TORCH_CHECK(!bn_a, "maxpool_bwd BN reduce: pass the packed relu bitmask");
+    for (int i : {2, 3, 4, 5})
+      if (bnr[i].has_value() && bnr[i]->defined()) { need_f32(*bnr[i], "bn vec"); need_numel(*bnr[i], g[3], "bn vec"); }
+    need_f32(*bnr[9], "bn_sums");
+    TORCH_CHECK(bn_shards >= 1, "bn_shards");
+    need_numel(*bnr[9], (long long)bn_shards * 3 * g[3], "bn_sums");
+    y = bnr[0]->data_ptr();
+    mean = bnr[2]->data_ptr<float>();
+    invstd = bnr[3]->data_ptr<float>();
+    msc = opt_ptr<const float>(bnr[4]);
+    msh = opt_ptr<const float>(bnr[5]);
+    TORCH_CHECK((msc == nullptr) == (msh == nullptr), "scale and shift go together");
+    sums = bnr[9]->data_ptr<float>();
+  }
   check_rc(tfk_maxpool_bwd(dy.data_ptr(), idx.data_ptr<uint8_t>(), dx.data_ptr(), g[0], g[1], g[2], g[3], g[4], g[5], g[6],
-                           g[7], g[8], g[9], g[10], g[11], cur_stream()),
+                           g[7], g[8], g[9], g[10], g[11], y, mean, invstd, msc, msh, amask, sums, bn_shards,
+                           cur_stream()),
            "maxpool_bwd");
 }
 void avgpool_fwd(torch::Tensor x, torch::Tensor y, int N, int HW, int C) {

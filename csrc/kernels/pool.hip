@@ -45,10 +45,30 @@ __global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict_
   }
 }
 
+// BNR: also accumulate the BN-backward channel sums of the layer that produced the pooled input
+// (the ResNet stem), dz = dx * relu-mask: sums[shard][0][c] += dz, [1][c] += dz*(y-mean)*invstd --
+// the standalone bn_bwd_reduce pass would re-read dx and y (846 MB at bs256). Mask: amask bit if
+// given, else y*mscale+mshift > 0 if mscale is given, else 1. Needs NT % (C/8) == 0 (a thread's
+// channel chunk is fixed across the grid-stride loop).
+template <bool BNR>
 __global__ void maxpool_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* __restrict__ idx, bf16* __restrict__ dx, int N,
-                                   int H, int W, int C, int P, int Q, int KH, int KW, int sh, int sw, int ph, int pw) {
+                                   int H, int W, int C, int P, int Q, int KH, int KW, int sh, int sw, int ph, int pw,
+                                   const bf16* __restrict__ y, const float* __restrict__ mean,
+                                   const float* __restrict__ invstd, const float* __restrict__ mscale,
+                                   const float* __restrict__ mshift, const unsigned char* __restrict__ amask,
+                                   float* __restrict__ sums, int shards) {
   const int cpr = C >> 3;
   const long long total = (long long)N * H * W * cpr;
+  float s0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mu[8], is[8], ms[8], mh[8];
+  const int c0 = (threadIdx.x % cpr) * 8;
+  if constexpr (BNR) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e];
+      ms[e] = mscale ? mscale[c0 + e] : 1.f; mh[e] = mshift ? mshift[c0 + e] : 0.f;
+    }
+  }
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
     int cc = (int)(i % cpr);
     long long pix = i / cpr;
@@ -82,6 +102,39 @@ __global__ void maxpool_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* _
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
     *(bf16x8*)(dx + i * 8) = o;
+    if constexpr (BNR) {
+      const bf16x8 yv = *(const bf16x8*)(y + i * 8);
+      const unsigned mb = amask ? amask[i] : 0xffu;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float yf = bf2f(yv[e]);
+        float dz = bf2f(o[e]);  // the stored (bf16-rounded) gradient, as the standalone pass reads it
+        if (!((mb >> e) & 1u)) dz = 0.f;
+        if (!amask && mscale && !(yf * ms[e] + mh[e] > 0.f)) dz = 0.f;
+        s0[e] += dz;
+        s1[e] += dz * (yf - mu[e]) * is[e];
+      }
+    }
+  }
+  if constexpr (BNR) {
+    __shared__ float red[2][NT * 8];
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[0][t * 8 + e] = s0[e]; red[1][t * 8 + e] = s1[e]; }
+    __syncthreads();
+    if (t < cpr) {
+      float* st = sums + (long long)(blockIdx.x % shards) * 3 * C;
+      for (int pass = 0; pass < 2; ++pass) {
+        float a8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a8[e] = 0.f;
+        for (int rr = t; rr < NT; rr += cpr)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a8[e] += red[pass][rr * 8 + e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) atomicAdd(st + pass * C + c0 + e, a8[e]);
+      }
+    }
   }
 }
 
@@ -136,10 +189,18 @@ int tfk_maxpool_fwd(const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, i
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_maxpool_bwd(const bf16* dy, const uint8_t* idx, bf16* dx, int N, int H, int W, int C, int P, int Q, int KH, int KW,
-                    int sh, int sw, int ph, int pw, hipStream_t s) {
+                    int sh, int sw, int ph, int pw, const bf16* y, const float* mean, const float* invstd,
+                    const float* mscale, const float* mshift, const unsigned char* amask, float* sums, int shards,
+                    hipStream_t s) {
   long long total = (long long)N * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, dy, idx, dx, N, H, W, C, P, Q, KH, KW, sh,
-                     sw, ph, pw);
+  if (sums) {
+    if (NT % (C / 8) != 0 || shards < 1) return -1;
+    hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(grid_for(total)), dim3(NT), 0, s, dy, idx, dx, N, H, W, C, P, Q, KH,
+                       KW, sh, sw, ph, pw, y, mean, invstd, mscale, mshift, amask, sums, shards);
+  } else {
+    hipLaunchKernelGGL(maxpool_bwd_kernel<false>, dim3(grid_for(total)), dim3(NT), 0, s, dy, idx, dx, N, H, W, C, P, Q, KH,
+                       KW, sh, sw, ph, pw, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_avgpool_fwd(const bf16* x, bf16* y, int N, int HW, int C, hipStream_t s) {

@@ -8,6 +8,8 @@ fc1000) so checkpoints line up with TF-era tooling.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops import norm as BN
@@ -16,6 +18,10 @@ from ..ops.loss import softmax_xent
 from ..runtime.arena import ParamArena
 from ..runtime.layers import BatchNorm, Conv2d, Linear
 
+# stem BN's backward channel sums inside the max-pool backward (opt-in TFK_FUSE_POOL_BNR=1): measured
+# neutral on MI355X (ResNet-50 bs256, same box: fused 26.71/26.76 ms vs standalone reduce 26.67/26.69) --
+# the gather-form pool backward is latency-bound and absorbs the saved pass in its own time
+FUSE_POOL_BNR = os.environ.get("TFK_FUSE_POOL_BNR", "0") == "1"
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
 
@@ -204,9 +210,11 @@ class ResNet:
         for i in range(nb - 1, -1, -1):
             nxt = self.blocks[i - 1].tail_reduce() if i > 0 else None
             dh = self.blocks[i].backward(dh, dout_reduced=i < nb - 1, next_bnr=nxt)
-        da0 = PL.maxpool_bwd(dh, idx, a0.shape, 3, 2, 1)
+        # the stem BN's backward channel sums accumulate inside the max-pool backward
+        fuse = FUSE_POOL_BNR and y0.shape[-1] % 8 == 0 and 256 % (y0.shape[-1] // 8) == 0
+        da0 = PL.maxpool_bwd(dh, idx, a0.shape, 3, 2, 1, bnr=BN.BNReduce(y0, self.bn1.st) if fuse else None)
         dy0, _, _ = BN.bn_backward(da0, None, y0, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
-                                   self.bn1.beta.grad, y0.numel() // y0.shape[-1], relu_from_y=True)
+                                   self.bn1.beta.grad, y0.numel() // y0.shape[-1], relu_from_y=True, reduced=fuse)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
         self.conv1.backward(dy0, x0, need_dx=False)
         return loss, corr

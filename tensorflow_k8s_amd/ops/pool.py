@@ -24,17 +24,28 @@ def maxpool_fwd(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1):
     return y, idx
 
 
-def maxpool_bwd(dy: torch.Tensor, idx, x_shape, k: int = 3, s: int = 2, p: int = 1) -> torch.Tensor:
+def maxpool_bwd(dy: torch.Tensor, idx, x_shape, k: int = 3, s: int = 2, p: int = 1, bnr=None) -> torch.Tensor:
+    """dx of a max pool (gradients of overlapping windows accumulate). bnr (ops.norm.BNReduce, no
+    second BN): also accumulate the BN-backward channel sums of the layer that produced x from the
+    final dx (the ResNet stem: saves the standalone reduction's re-read of dx and y)."""
     N, H, W, C = x_shape
+    if bnr is not None and bnr.y2 is not None:
+        raise ValueError("maxpool_bwd BN reduce supports one BN")
     if not on_gpu(dy):
         # overlapping windows: gradients of windows sharing an argmax must ACCUMULATE
         ind, nshape = idx
         g = dy.float().permute(0, 3, 1, 2).reshape(N, C, -1)
         dx = torch.zeros(N, C, H * W).scatter_add_(2, ind.reshape(N, C, -1), g)
-        return dx.reshape(N, C, H, W).permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+        dx = dx.reshape(N, C, H, W).permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+        if bnr is not None:
+            bnr.reference_accumulate(dx)
+        return dx
     P, Q = dy.shape[1], dy.shape[2]
     dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
-    lib().maxpool_bwd(dy, idx, dx, [N, H, W, C, P, Q, k, k, s, s, p, p])
+    if bnr is not None and 256 % (C // 8) != 0:
+        raise ValueError("maxpool_bwd BN reduce needs (C/8) | 256")
+    lib().maxpool_bwd(dy, idx, dx, [N, H, W, C, P, Q, k, k, s, s, p, p],
+                      bnr.gemm_args() if bnr is not None else [], bnr.st.shards if bnr is not None else 1)
     return dx
 
 

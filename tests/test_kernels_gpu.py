@@ -221,6 +221,33 @@ def test_bn_relu_bitmask(proj):
         assert rel(got[k], ref.sums.view(1, 3, C)[0, k]) < 2e-2, k
 
 
+@pytest.mark.parametrize("mode", ["relu_from_y", "mask_a", "none"])
+@pytest.mark.parametrize("C", [64, 32, 256])
+def test_maxpool_bwd_fused_bn_reduce(mode, C):
+    """Max-pool backward with the producer BN's backward reduction fused in (the ResNet stem):
+    dx unchanged, channel sums == the fp32 CPU oracle (BNReduce.reference_accumulate)."""
+    x = bf(2, 17, 19, C, seed=21)
+    y = bf(2, 17, 19, C, seed=22)
+    a = bf(2, 17, 19, C, seed=23)
+    gen = torch.Generator().manual_seed(24)
+    mu, inv = torch.randn(C, generator=gen) * 0.1, torch.rand(C, generator=gen) + 0.5
+    sc, sh = torch.randn(C, generator=gen), torch.randn(C, generator=gen) * 0.1
+    res = {}
+    for dev in ("cpu", DEV):
+        _, idx = PL.maxpool_fwd(x.to(dev))
+        dy = bf(2, 9, 10, C, seed=25).to(dev)
+        st = BN.BNState(C, dev)
+        st.mean.copy_(mu); st.invstd.copy_(inv); st.scale.copy_(sc); st.shift.copy_(sh)
+        spec = BN.BNReduce(y.to(dev), st, a=a.to(dev) if mode == "mask_a" else None, relu=mode != "none")
+        dx = PL.maxpool_bwd(dy, idx, x.shape, bnr=spec)
+        plain = PL.maxpool_bwd(dy, idx, x.shape)
+        res[dev] = (dx.cpu(), plain.cpu(), st.sums.view(st.shards, 3, C).sum(0).cpu())
+    assert torch.equal(res[DEV][0], res[DEV][1])
+    assert rel(res[DEV][0], res["cpu"][0]) < 1e-2
+    for k in range(2):
+        assert rel(res[DEV][2][k], res["cpu"][2][k]) < 2e-2, k
+
+
 def test_pools():
     x = bf(2, 17, 17, 64, seed=11)
     y_ref, idx_ref = PL.maxpool_fwd(x)

@@ -86,7 +86,14 @@ def test_numa_packed_gang_and_cpu_pinning(tmp_path, control_plane_bin):
     with LocalCluster(gpus=4, root_dir=str(tmp_path / "c"),
                       extra_args=["--gpu-numa", "0,0,1,1", "--numa-cpus", numa_cpus]) as cl:
         c = cl.client
-        node = c.list("nodes", ns=None)[0]
+        # the kubelet registers its Node asynchronously after the cluster is up
+        deadline = time.time() + 20
+        nodes = c.list("nodes", ns=None)
+        while not nodes and time.time() < deadline:
+            time.sleep(0.2)
+            nodes = c.list("nodes", ns=None)
+        assert nodes, "kubelet never registered its node"
+        node = nodes[0]
         assert node["metadata"]["annotations"]["tfk.io/gpu-numa"] == "0,0,1,1"
         # occupy GPU 0 so domain 0 has one free GPU: the 2-pod gang must pack onto domain 1
         c.create(_job("hold", {"Chief": _rs(1, ["python3", "-c", "import time; time.sleep(4)"])}))

@@ -205,6 +205,23 @@ __global__ void dropout_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
   }
 }
 
+// Same mask and arithmetic, 8 elements (16 B) per lane: n % 8 == 0, 16-B aligned x / y. The scalar
+// form moved one bf16 per lane per iteration (19 us for a 16 MB Transformer-big residual gradient).
+__global__ void dropout8_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long long n8, float p,
+                                unsigned long long seed) {
+  const float keep = 1.f - p, inv = 1.f / keep;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long long)gridDim.x * NT) {
+    const bf16x8 v = *(const bf16x8*)(x + i * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool k = u01(hash_u32(seed, (unsigned long long)(i * 8 + e))) < keep;
+      o[e] = f2bf(k ? bf2f(v[e]) * inv : 0.f);
+    }
+    *(bf16x8*)(y + i * 8) = o;
+  }
+}
+
 __global__ void add_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b, bf16* __restrict__ y, long long n,
                            float alpha, float beta) {
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
@@ -300,6 +317,10 @@ int tfk_act_bwd(const bf16* dy, const bf16* x, bf16* dx, long long n, int act, h
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_dropout(const bf16* x, bf16* y, long long n, float p, unsigned long long seed, hipStream_t s) {
+  if ((n & 7) == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
+    hipLaunchKernelGGL(dropout8_kernel, dim3(grid_for(n / 8)), dim3(NT), 0, s, x, y, n / 8, p, seed);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n, p, seed);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -134,8 +134,9 @@ class EncoderLayer:
         cfg = self.cfg
         x, b, st, z, f = saved
         dy = E.dropout(dx2, cfg.dropout if training else 0.0, _mix(seed, 6))
-        dfz = self.ff2.backward(dy, f, dact_src=z, dact="relu")
-        dz = E.dropout(dfz, cfg.relu_dropout if training else 0.0, _mix(seed, 5))
+        # relu backward and the relu-dropout backward in the ff2 dgrad epilogue (forward mask regenerated)
+        dz = self.ff2.backward(dy, f, dact_src=z, dact="relu", drop_p=cfg.relu_dropout if training else 0.0,
+                               drop_seed=_mix(seed, 5))
         db = self.ff1.backward(dz, b)
         return self.ffn_ln.backward(db, x, st, dres=dx2)
 

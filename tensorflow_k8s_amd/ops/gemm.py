@@ -238,8 +238,11 @@ def act_grad_ref(z: torch.Tensor, act: str | None) -> torch.Tensor:
 
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None = None,
-                 dact_src: torch.Tensor | None = None, dact: str | None = None) -> torch.Tensor:
-    """dx[M,K] = (dy[M,N] @ w[N,K]) * act'(dact_src) (+ resid)."""
+                 dact_src: torch.Tensor | None = None, dact: str | None = None, drop_p: float = 0.0,
+                 drop_seed: int = 0) -> torch.Tensor:
+    """dx[M,K] = dropout((dy[M,N] @ w[N,K]) * act'(dact_src)) (+ resid). drop_p/drop_seed: the
+    backward of a forward dropout on this layer's INPUT (mask = ops.elementwise.dropout_keep(drop_seed,
+    M*K, drop_p), e.g. the FFN's relu dropout) fused into the epilogue instead of a separate pass."""
     N, K = w.shape
     dy2 = dy.reshape(-1, N)
     M = dy2.shape[0]
@@ -247,6 +250,9 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
         dx = dy2.float() @ w.float()
         if dact_src is not None:
             dx = dx * act_grad_ref(dact_src.reshape(-1, K), dact)
+        if drop_p > 0:
+            from .elementwise import dropout_keep
+            dx = dx * dropout_keep(drop_seed, dx.numel(), drop_p).reshape(dx.shape) / (1 - drop_p)
         dx = dx.to(torch.bfloat16)
         if resid is not None:
             dx = (dx.float() + resid.reshape(-1, K).float()).to(torch.bfloat16)
@@ -255,7 +261,7 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
     _gemm(dy2, w, dx, M, K, N, N, K, K, A_KIN, B_KOUT, EPI_BF16, pick_tile(M, K, big_ok=True, K=N, g4=K % 8 == 0),
           resid=resid.reshape(-1, K) if resid is not None else None,
           dact_src=dact_src.reshape(-1, K) if dact_src is not None else None,
-          dact=ACT[dact] if dact_src is not None else 0)
+          dact=ACT[dact] if dact_src is not None else 0, drop_p=drop_p, drop_seed=drop_seed)
     return dx
 
 

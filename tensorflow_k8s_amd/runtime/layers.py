@@ -44,13 +44,17 @@ def linear_wgrad(dy, x, gw, fp8: bool, accumulate: bool = False, split_target=No
     return G.linear_wgrad(dy, x, gw, accumulate=accumulate, split_target=split_target)
 
 
-def linear_dgrad(dy, w, fp8: bool, **kw):
-    """Input gradient: MX-fp8 when fp8 and the output width tiles (N % 128), else bf16."""
+def linear_dgrad(dy, w, fp8: bool, drop_p: float = 0.0, drop_seed: int = 0, **kw):
+    """Input gradient: MX-fp8 when fp8 and the output width tiles (N % 128), else bf16 (with the
+    input-dropout backward fused into the epilogue; the fp8 path runs it as a separate pass)."""
     if fp8:
         from ..ops.fp8 import linear_dgrad_mx, mx_backward_ok
         if mx_backward_ok(dy.shape[0], dy.shape[1], w.shape[1])[0]:
-            return linear_dgrad_mx(dy, w, **kw)
-    return G.linear_dgrad(dy, w, **kw)
+            if drop_p > 0 and kw.get("resid") is not None:
+                raise ValueError("fp8 dgrad: input dropout with a residual is not supported")
+            from ..ops.elementwise import dropout
+            return dropout(linear_dgrad_mx(dy, w, **kw), drop_p, drop_seed)
+    return G.linear_dgrad(dy, w, drop_p=drop_p, drop_seed=drop_seed, **kw)
 
 
 class Conv2d:
@@ -175,8 +179,9 @@ class Linear:
                               aux=aux, drop_p=drop_p, drop_seed=drop_seed)
 
     def backward(self, dy, x, need_dx: bool = True, resid=None, accumulate: bool = False, dact_src=None,
-                 dact=None):
-        """dy: gradient of this layer's (pre-dropout, post-activation-backward) output."""
+                 dact=None, drop_p: float = 0.0, drop_seed: int = 0):
+        """dy: gradient of this layer's (pre-dropout, post-activation-backward) output. drop_p/drop_seed:
+        a forward dropout on this layer's input, whose backward is fused into the dgrad epilogue."""
         linear_wgrad(dy, x, self.w.grad, self.fp8, accumulate=accumulate, split_target=self.split_target)
         if self.b is not None:
             G.bias_grad(dy, self.b.grad, accumulate=accumulate or self.arena.prezeroed)
@@ -185,7 +190,8 @@ class Linear:
             self.arena.grad_ready(self.w)
         if not need_dx:
             return None
-        return linear_dgrad(dy, self.w.compute, self.fp8, resid=resid, dact_src=dact_src, dact=dact)
+        return linear_dgrad(dy, self.w.compute, self.fp8, resid=resid, dact_src=dact_src, dact=dact, drop_p=drop_p,
+                            drop_seed=drop_seed)
 
 
 class FusedLinear:

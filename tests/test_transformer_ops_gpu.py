@@ -66,6 +66,30 @@ def test_attention_fwd_bwd(case):
     assert torch.allclose(res[DEV]["lse"].cpu()[finite], res["cpu"]["lse"][finite], atol=1e-2)
 
 
+@pytest.mark.parametrize("n", [8192 * 4, 1001])
+def test_dropout_kernel_matches_cpu(n):
+    """Standalone dropout (8-wide vector kernel for n % 8 == 0, scalar otherwise) == the CPU hash
+    mask bit for bit."""
+    from tensorflow_k8s_amd.ops import elementwise as E
+    x = bf(n, seed=31)
+    assert torch.equal(E.dropout(x.to(DEV), 0.3, 1234).cpu(), E.dropout(x, 0.3, 1234))
+
+
+def test_linear_dgrad_fused_input_dropout():
+    """FFN backward: relu' and the relu-dropout backward fused into the ff2 dgrad epilogue == the
+    CPU reference, and == the unfused GEMM + standalone dropout up to one bf16 rounding."""
+    from tensorflow_k8s_amd.ops import elementwise as E
+    from tensorflow_k8s_amd.ops import gemm as G
+    M, N, K = 300, 136, 264
+    dy, w, z = bf(M, N, seed=32), bf(N, K, seed=33, scale=0.1), bf(M, K, seed=34)
+    ref = G.linear_dgrad(dy, w, dact_src=z, dact="relu", drop_p=0.1, drop_seed=77)
+    fused = G.linear_dgrad(dy.to(DEV), w.to(DEV), dact_src=z.to(DEV), dact="relu", drop_p=0.1, drop_seed=77)
+    plain = E.dropout(G.linear_dgrad(dy.to(DEV), w.to(DEV), dact_src=z.to(DEV), dact="relu"), 0.1, 77)
+    assert rel(fused, ref) < 1e-2
+    assert rel(fused, plain) < 1e-2
+    assert torch.equal(fused.cpu() == 0, plain.cpu() == 0)
+
+
 def test_dropout_mask_rate():
     m = T.dropout_keep_mask(7, 2, 3, 64, 64, 0.1)
     assert abs(float(m.float().mean()) - 0.9) < 0.01

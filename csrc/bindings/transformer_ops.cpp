@@ -12,7 +12,7 @@ extern "C" {
 void tfk_attn_set_waves(int w);
 int tfk_layernorm_fwd(const void*, const float*, const float*, void*, float*, float*, int, int, float, hipStream_t);
 int tfk_layernorm_bwd(const void*, const void*, const float*, const float*, const float*, const void*, void*, float*,
-                      float*, int, int, hipStream_t);
+                      float*, int, int, void*, float, unsigned long long, hipStream_t);
 int tfk_embedding_fwd(const int*, const void*, int, const void*, int, const int*, const void*, int, void*, long long, int,
                       float, hipStream_t);
 int tfk_embedding_bwd(const int*, const void*, int, float*, float*, int, const int*, float*, int, long long, int, float,
@@ -39,7 +39,7 @@ void layernorm_fwd(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, tor
 
 void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor gamma, torch::Tensor mean, torch::Tensor rstd,
                    c10::optional<torch::Tensor> dres, torch::Tensor dx, torch::Tensor dgamma, torch::Tensor dbeta,
-                   int64_t M, int W) {
+                   int64_t M, int W, c10::optional<torch::Tensor> dxd, double drop_p, int64_t drop_seed) {
   need_bf16(dy, "dy"); need_bf16(x, "x"); need_bf16(dx, "dx");
   for (auto* t : {&gamma, &mean, &rstd, &dgamma, &dbeta}) need_f32(*t, "ln vector");
   TORCH_CHECK(W % 8 == 0 && W <= 2048, "layernorm needs W%8==0 and W<=2048");
@@ -47,9 +47,14 @@ void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor gamma, torch
   need_numel(gamma, W, "gamma"); need_numel(dgamma, W, "dgamma"); need_numel(dbeta, W, "dbeta");
   need_numel(mean, M, "mean"); need_numel(rstd, M, "rstd");
   if (dres.has_value() && dres->defined()) { need_bf16(*dres, "dres"); need_numel(*dres, M * W, "dres"); }
+  if (dxd.has_value() && dxd->defined()) {
+    need_bf16(*dxd, "dxd"); need_numel(*dxd, M * W, "dxd");
+    TORCH_CHECK(drop_p > 0.0 && drop_p < 1.0, "dxd needs 0 < drop_p < 1");
+  }
   check_rc(tfk_layernorm_bwd(dy.data_ptr(), x.data_ptr(), gamma.data_ptr<float>(), mean.data_ptr<float>(),
                              rstd.data_ptr<float>(), opt_ptr<const void>(dres), dx.data_ptr(), dgamma.data_ptr<float>(),
-                             dbeta.data_ptr<float>(), (int)M, W, cur_stream()),
+                             dbeta.data_ptr<float>(), (int)M, W, opt_ptr<void>(dxd), (float)drop_p,
+                             (unsigned long long)drop_seed, cur_stream()),
            "layernorm_bwd");
 }
 

@@ -71,7 +71,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, const bf16* __restrict__ dres,
                                                     bf16* __restrict__ dx, float* __restrict__ dgamma,
-                                                    float* __restrict__ dbeta, int M, int W) {
+                                                    float* __restrict__ dbeta, int M, int W, bf16* __restrict__ dxd,
+                                                    float drop_p, unsigned long long drop_seed) {
   extern __shared__ float red[];  // [NT/64][2][W]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nch = W >> 3;
@@ -123,6 +124,17 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
           o[e] = f2bf(v);
         }
         *(bf16x8*)(dx + (long long)row * W + c * 8) = o;
+        if (dxd) {
+          // the consumer's dropout backward on the stored dx (misc.hip dropout_kernel's mask and
+          // arithmetic, index row*W + col): saves that pass's read + write of dx
+          const float keep = 1.f - drop_p, inv = 1.f / keep;
+          const unsigned long long base = (unsigned long long)row * W + c * 8;
+          bf16x8 od;
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            od[e] = f2bf(u01(hash_u32(drop_seed, base + e)) < keep ? bf2f(o[e]) * inv : 0.f);
+          *(bf16x8*)(dxd + base) = od;
+        }
       }
     }
   }
@@ -256,17 +268,23 @@ int tfk_layernorm_fwd(const bf16* x, const float* gamma, const float* beta, bf16
   else return -3;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+// dxd (optional): also write dropout(dx; drop_p, drop_seed) -- the gradient the consumer's dropout
+// backward would produce from dx
 int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const float* mean, const float* rstd,
-                      const bf16* dres, bf16* dx, float* dgamma, float* dbeta, int M, int W, hipStream_t s) {
+                      const bf16* dres, bf16* dx, float* dgamma, float* dbeta, int M, int W, bf16* dxd, float drop_p,
+                      unsigned long long drop_seed, hipStream_t s) {
   const int cpl = (W / 8 + 63) / 64;
   dim3 grid(grid_for(M, (NT / 64) * 8, 1024));
   const size_t sh = (size_t)(NT / 64) * 2 * W * sizeof(float);
   if (cpl <= 1)
-    hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W);
+    hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
+                       dxd, drop_p, drop_seed);
   else if (cpl <= 2)
-    hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W);
+    hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
+                       dxd, drop_p, drop_seed);
   else if (cpl <= 4)
-    hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W);
+    hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
+                       dxd, drop_p, drop_seed);
   else return -3;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -111,15 +111,20 @@ class EncoderLayer:
         x1 = self.att.out.forward(o, resid=x, drop_p=cfg.dropout if training else 0.0, drop_seed=_mix(seed, 2))
         return x1, (x, a, st1, qkv, sp, o, lse)
 
-    def _self_attn_bwd(self, dx1, saved, seed, training):
+    # Backward plumbing of the residual dropouts: every sublayer's LayerNorm backward also writes the
+    # gradient its CONSUMER's dropout backward needs (out_drop = (p, seed) of that dropout), so the
+    # consumer takes it as `din` instead of running a separate dropout pass over dx.
+    def _self_attn_bwd(self, dx1, saved, seed, training, din=None, out_drop=None):
         x, a, st1, qkv, sp, o, lse = saved
         n = self.att.names
-        do = self.att.out.backward(E.dropout(dx1, self.cfg.dropout if training else 0.0, _mix(seed, 2)), o)
+        if din is None:
+            din = E.dropout(dx1, self.cfg.dropout if training else 0.0, _mix(seed, 2))
+        do = self.att.out.backward(din, o)
         dqkv = torch.empty_like(qkv)
         TR.attention_bwd(sp, o, do, lse, (dqkv, self.att.qkv.col(n["q"])), (dqkv, self.att.qkv.col(n["k"])),
                          (dqkv, self.att.qkv.col(n["v"])))
         da = self.att.qkv.backward(dqkv, a)
-        return self.ln1.backward(da, x, st1, dres=dx1)
+        return self.ln1.backward(da, x, st1, dres=dx1, drop=out_drop)
 
     def _ffn(self, x, seed, training):
         cfg = self.cfg
@@ -130,15 +135,15 @@ class EncoderLayer:
         x2 = self.ff2.forward(f, resid=x, drop_p=cfg.dropout if training else 0.0, drop_seed=_mix(seed, 6))
         return x2, (x, b, st, z, f)
 
-    def _ffn_bwd(self, dx2, saved, seed, training):
+    def _ffn_bwd(self, dx2, saved, seed, training, din=None, out_drop=None):
         cfg = self.cfg
         x, b, st, z, f = saved
-        dy = E.dropout(dx2, cfg.dropout if training else 0.0, _mix(seed, 6))
+        dy = din if din is not None else E.dropout(dx2, cfg.dropout if training else 0.0, _mix(seed, 6))
         # relu backward and the relu-dropout backward in the ff2 dgrad epilogue (forward mask regenerated)
         dz = self.ff2.backward(dy, f, dact_src=z, dact="relu", drop_p=cfg.relu_dropout if training else 0.0,
                                drop_seed=_mix(seed, 5))
         db = self.ff1.backward(dz, b)
-        return self.ffn_ln.backward(db, x, st, dres=dx2)
+        return self.ffn_ln.backward(db, x, st, dres=dx2, drop=out_drop)
 
     def forward(self, x, B, S, kv_len, seed, training):
         x1, s1 = self._self_attn(x, B, S, kv_len, False, seed, training)
@@ -146,11 +151,19 @@ class EncoderLayer:
         self.saved = (s1, s2, seed, training) if training else None
         return x2
 
-    def backward(self, dx2):
+    def in_drop(self, training: bool, seed: int):
+        """(p, seed) of the dropout whose backward consumes this layer's output gradient first (the
+        FFN output dropout), for the producer's fused LayerNorm-backward output."""
+        return (self.cfg.dropout if training else 0.0, _mix(seed, 6))
+
+    def backward(self, dx2, din=None, out_drop=None):
+        """din: dropout(dx2) already produced by the caller's LayerNorm backward (None: computed
+        here). out_drop: (p, seed) of the consumer of the returned gradient -> returns (dx, dxd)."""
         s1, s2, seed, training = self.saved
         self.saved = None
-        dx1 = self._ffn_bwd(dx2, s2, seed, training)
-        return self._self_attn_bwd(dx1, s1, seed, training)
+        dx1, dx1d = self._ffn_bwd(dx2, s2, seed, training, din=din,
+                                  out_drop=(self.cfg.dropout if training else 0.0, _mix(seed, 2)))
+        return self._self_attn_bwd(dx1, s1, seed, training, din=dx1d, out_drop=out_drop)
 
 
 class DecoderLayer(EncoderLayer):
@@ -185,22 +198,24 @@ class DecoderLayer(EncoderLayer):
         self.saved = (s1, (y1, c, st2, q, kv, sp, o2, lse2), s3, seed, training) if training else None
         return y3
 
-    def backward(self, dy3, mem, dmem):
-        """Returns dy; accumulates this layer's encoder-memory gradient into dmem (in place)."""
+    def backward(self, dy3, mem, dmem, din=None, out_drop=None):
+        """Returns dy (or (dy, dropout(dy)) with out_drop, see EncoderLayer.backward); accumulates this
+        layer's encoder-memory gradient into dmem (in place)."""
         s1, s2, s3, seed, training = self.saved
         self.saved = None
         cfg = self.cfg
-        dy2 = self._ffn_bwd(dy3, s3, seed, training)
+        p = cfg.dropout if training else 0.0
+        dy2, dy2d = self._ffn_bwd(dy3, s3, seed, training, din=din, out_drop=(p, _mix(seed, 4)))
         y1, c, st2, q, kv, sp, o2, lse2 = s2
         n = self.xatt.names
-        do2 = self.xatt.out.backward(E.dropout(dy2, cfg.dropout if training else 0.0, _mix(seed, 4)), o2)
+        do2 = self.xatt.out.backward(dy2d, o2)
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
         TR.attention_bwd(sp, o2, do2, lse2, (dq, 0), (dkv, self.xatt.kv.col(n["k"])), (dkv, self.xatt.kv.col(n["v"])))
         dmem.copy_(self.xatt.kv.backward(dkv, mem, resid=dmem))
         dc = self.xatt.q.backward(dq, c)
-        dy1 = self.ln2.backward(dc, y1, st2, dres=dy2)
-        return self._self_attn_bwd(dy1, s1, seed, training)
+        dy1, dy1d = self.ln2.backward(dc, y1, st2, dres=dy2, drop=(p, _mix(seed, 2)))
+        return self._self_attn_bwd(dy1, s1, seed, training, din=dy1d, out_drop=out_drop)
 
 
 class Transformer:
@@ -279,18 +294,21 @@ class Transformer:
         from ..runtime.layers import linear_dgrad, linear_wgrad
         linear_wgrad(dlogits, yo, self.emb.table.grad, cfg.fp8)  # first writer of the shared table's grad
         dyo = linear_dgrad(dlogits, self.emb.table.compute, cfg.fp8)
-        dy = self.dec_ln.backward(dyo, y, st_y)
+        # each LayerNorm backward also emits dropout(dx) for the dropout its gradient flows into next
+        p = cfg.dropout if tr else 0.0
+        nd, ne = len(self.dec), len(self.enc)
+        dy, dyd = self.dec_ln.backward(dyo, y, st_y, drop=self.dec[-1].in_drop(tr, _mix(seed, 200 + nd - 1)))
         dmem = torch.zeros_like(mem)
-        for layer in reversed(self.dec):
-            dy = layer.backward(dy, mem, dmem)
+        for i in range(nd - 1, -1, -1):
+            nxt = self.dec[i - 1].in_drop(tr, _mix(seed, 200 + i - 1)) if i > 0 else (p, _mix(seed, 0xE1))
+            dy, dyd = self.dec[i].backward(dy, mem, dmem, din=dyd, out_drop=nxt)
         scale = math.sqrt(cfg.hidden)
-        TR.embedding_bwd(tgt_in, E.dropout(dy, cfg.dropout if tr else 0.0, _mix(seed, 0xE1)), self.emb.table.grad,
-                         None, St, scale=scale)
-        dx = self.enc_ln.backward(dmem, x, st_m)
-        for layer in reversed(self.enc):
-            dx = layer.backward(dx)
-        TR.embedding_bwd(src, E.dropout(dx, cfg.dropout if tr else 0.0, _mix(seed, 0xE0)), self.emb.table.grad,
-                         None, Ss, scale=scale)
+        TR.embedding_bwd(tgt_in, dyd, self.emb.table.grad, None, St, scale=scale)
+        dx, dxd = self.enc_ln.backward(dmem, x, st_m, drop=self.enc[-1].in_drop(tr, _mix(seed, 100 + ne - 1)))
+        for i in range(ne - 1, -1, -1):
+            nxt = self.enc[i - 1].in_drop(tr, _mix(seed, 100 + i - 1)) if i > 0 else (p, _mix(seed, 0xE0))
+            dx, dxd = self.enc[i].backward(dx, din=dxd, out_drop=nxt)
+        TR.embedding_bwd(src, dxd, self.emb.table.grad, None, Ss, scale=scale)
         self.arena.grad_ready(self.emb.table)
         return loss.view(B, St).mean(1), corr
 

@@ -53,8 +53,12 @@ def _zero_pair(a: torch.Tensor, b: torch.Tensor) -> None:
     a.zero_(); b.zero_()
 
 
-def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate: bool = False):
-    """dx (+ dres) bf16; dgamma/dbeta (f32, written or accumulated)."""
+def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate: bool = False, drop=None):
+    """dx (+ dres) bf16; dgamma/dbeta (f32, written or accumulated). drop=(p, seed): also return
+    dropout(dx, p, seed) (the consumer's dropout backward, written by the same kernel) -> (dx, dxd)."""
+    if drop is not None and drop[0] <= 0.0:
+        dx = layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres, accumulate)
+        return dx, dx
     W = x.shape[-1]
     M = x.numel() // W
     if not on_gpu(dy):
@@ -69,12 +73,18 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate
             dgamma.add_(dg); dbeta.add_(db)
         else:
             dgamma.copy_(dg); dbeta.copy_(db)
-        return dx.to(torch.bfloat16).reshape(dy.shape)
+        dx = dx.to(torch.bfloat16).reshape(dy.shape)
+        if drop is not None:
+            from .elementwise import dropout
+            return dx, dropout(dx, drop[0], drop[1])
+        return dx
     if not accumulate:
         _zero_pair(dgamma, dbeta)
     dx = torch.empty_like(dy)
-    lib().layernorm_bwd(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W)
-    return dx
+    dxd = torch.empty_like(dy) if drop is not None else None
+    lib().layernorm_bwd(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W, dxd,
+                        float(drop[0]) if drop is not None else 0.0, int(drop[1]) if drop is not None else 0)
+    return (dx, dxd) if drop is not None else dx
 
 
 # ----------------------------------------------------------------------------- embeddings

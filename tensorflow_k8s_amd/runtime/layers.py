@@ -258,11 +258,12 @@ class LayerNorm:
         y, mu, rs = TR.layernorm_fwd(x, self.gamma.master, self.beta.master, self.eps)
         return y, (mu, rs)
 
-    def backward(self, dy, x, stats, dres=None):
-        """dx = LN'(x)^T dy (+ dres: gradient arriving through a residual connection)."""
+    def backward(self, dy, x, stats, dres=None, drop=None):
+        """dx = LN'(x)^T dy (+ dres: gradient arriving through a residual connection). drop=(p, seed):
+        returns (dx, dropout(dx, p, seed)) from one kernel (the consumer's dropout backward)."""
         mu, rs = stats
         dx = TR.layernorm_bwd(dy, x, self.gamma.master, mu, rs, self.gamma.grad, self.beta.grad, dres=dres,
-                              accumulate=self.arena.prezeroed)
+                              accumulate=self.arena.prezeroed, drop=drop)
         self.arena.grad_ready(self.gamma, self.beta)
         return dx
 

@@ -113,6 +113,24 @@ def test_layernorm(W):
         assert rel(out[DEV][k], out["cpu"][k]) < 1e-2, k
 
 
+@pytest.mark.parametrize("W", [1024, 264])
+def test_layernorm_bwd_fused_consumer_dropout(W):
+    """LayerNorm backward also emitting dropout(dx) for its consumer: dx unchanged and the second
+    output == the standalone dropout of dx, bit for bit (same hash mask, same arithmetic)."""
+    from tensorflow_k8s_amd.ops import elementwise as E
+    M = 300
+    x, dy, dres = bf(M, W, seed=41, scale=2.0), bf(M, W, seed=42), bf(M, W, seed=43)
+    g, b = torch.rand(W) + 0.5, torch.randn(W) * 0.1
+    y, mu, rs = T.layernorm_fwd(x.to(DEV), g.to(DEV), b.to(DEV))
+    outs = []
+    for drop in (None, (0.3, 99)):
+        dg, db = torch.zeros(W, device=DEV), torch.zeros(W, device=DEV)
+        outs.append(T.layernorm_bwd(dy.to(DEV), x.to(DEV), g.to(DEV), mu, rs, dg, db, dres=dres.to(DEV), drop=drop))
+    dx, (dx2, dxd) = outs
+    assert torch.equal(dx, dx2)
+    assert torch.equal(dxd, E.dropout(dx, 0.3, 99))
+
+
 def test_embedding():
     V, W, S, B = 1000, 768, 128, 4
     word, pos, typ = bf(V, W, seed=8), bf(S, W, seed=9), bf(2, W, seed=10)

@@ -108,12 +108,11 @@ class BertLayer:
     def backward(self, dh2):
         h, qkv, sp, o, lse, s1, st1, h1, z, f, s2, st2, hd, s_ao, s_ff = self.saved
         self.saved = None
-        ds2 = self.ln2.backward(dh2, s2, st2)
-        dy2 = E.dropout(ds2, hd, s_ff)
+        # LayerNorm backward also emits the hidden-dropout backward of its gradient (one kernel)
+        ds2, dy2 = self.ln2.backward(dh2, s2, st2, drop=(hd, s_ff))
         dz = self.ff2.backward(dy2, f, dact_src=z, dact="gelu")
         dh1 = self.ff1.backward(dz, h1, resid=ds2)
-        ds1 = self.ln1.backward(dh1, s1, st1)
-        dy1 = E.dropout(ds1, hd, s_ao)
+        ds1, dy1 = self.ln1.backward(dh1, s1, st1, drop=(hd, s_ao))
         do = self.ao.backward(dy1, o)
         dqkv = torch.empty_like(qkv)
         TR.attention_bwd(sp, o, do, lse, (dqkv, self.qkv.col(self.qn)), (dqkv, self.qkv.col(self.kn)),

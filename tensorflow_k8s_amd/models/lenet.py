@@ -14,6 +14,7 @@ import torch
 from ..ops import elementwise as E
 from ..ops import pool as PL
 from ..ops.loss import softmax_xent
+from ..runtime import streams
 from ..runtime.arena import ParamArena
 from ..runtime.layers import Conv2d, Linear
 
@@ -74,6 +75,7 @@ class LeNet:
         dp1 = self.conv2.backward(E.act_bwd(da2, a2, "relu"), p1)
         da1 = PL.maxpool_bwd(dp1, i1, a1.shape, 2, 2, 0)
         self.conv1.backward(E.act_bwd(da1, a1, "relu"), x, need_dx=False)
+        streams.join()  # side-stream weight gradients complete before anyone reads arena.grad
         return loss, corr
 
 

@@ -15,6 +15,7 @@ import torch
 from ..ops import norm as BN
 from ..ops import pool as PL
 from ..ops.loss import softmax_xent
+from ..runtime import streams
 from ..runtime.arena import ParamArena
 from ..runtime.layers import BatchNorm, Conv2d, Linear
 
@@ -217,6 +218,7 @@ class ResNet:
                                    self.bn1.beta.grad, y0.numel() // y0.shape[-1], relu_from_y=True, reduced=fuse)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
         self.conv1.backward(dy0, x0, need_dx=False)
+        streams.join()  # side-stream weight gradients complete before anyone reads arena.grad
         return loss, corr
 
 

@@ -170,7 +170,7 @@ def _gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile, *, alpha=1.0
 
 
 def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, accumulate: bool, device,
-                    force_splits: int | None = None, split_target: int | None = None):
+                    force_splits: int | None = None, split_target: int | None = None, slot: str = "splitk"):
     """Run an f32-epilogue GEMM with split-K into a workspace, then reduce into `out` ([M][N] f32)."""
     splits = force_splits if force_splits is not None else pick_splits(tiles, K, target=split_target)
     ns = int(lib().gemm_splits(K, splits))
@@ -184,7 +184,7 @@ def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, 
         run(out, splits, -1, 0.0)
         return
     stride = ((M * N + 3) // 4) * 4
-    ws = workspace(device, ns * stride)
+    ws = workspace(device, ns * stride, slot=slot)
     run(ws, splits, stride, 0.0)
     lib().splitk_reduce(ws, ns, stride, M * N, out, None, accumulate, 1.0)
 
@@ -549,4 +549,6 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
         else:
             _gemm(dy, x, C, g.K, Nn, Kp, g.K, 0, Nn, A_KOUT, B_CONV_WGRAD, EPI_F32, tile, beta=beta, splits=sp,
                   split_stride=stride, conv=g.vec())
-    _f32_out_splitk(run, g.K, Nn, Kp, tiles, gw.view(-1), accumulate, dy.device, force_splits=splits)
+    # own slab workspace: conv weight gradients may run on the side stream (runtime/streams.py)
+    _f32_out_splitk(run, g.K, Nn, Kp, tiles, gw.view(-1), accumulate, dy.device, force_splits=splits,
+                    slot="splitk_wgrad")

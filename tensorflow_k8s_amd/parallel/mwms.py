@@ -121,6 +121,8 @@ class MultiWorkerMirroredStrategy:
 
     def _launch(self, b: Bucket):
         b.launched = True
+        from ..runtime import streams
+        streams.sync()  # the bucket may hold weight gradients produced on the side stream
         view = self.arena.grad[b.start:b.end]
         if self.wire is not None:
             from ..ops.optim import cast_f32_bf16

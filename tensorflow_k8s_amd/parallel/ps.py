@@ -137,11 +137,15 @@ class ParameterServerStrategy:
             return
         pl.pending[b] -= 1
         while self._next < len(pl.buckets) and pl.pending[self._next] <= 0:
+            from ..runtime import streams
+            streams.sync()  # side-stream weight gradients of this bucket first
             self._red.append(pl.reduce(self._next, self.arena.grad))
             self._next += 1
 
     def finish_step(self):
         if self.plan is not None:
+            from ..runtime import streams
+            streams.sync()
             while self._next < len(self.plan.buckets):
                 self._red.append(self.plan.reduce(self._next, self.arena.grad))
                 self._next += 1

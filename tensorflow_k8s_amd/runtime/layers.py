@@ -12,6 +12,7 @@ import torch
 from ..ops import gemm as G
 from ..ops import norm as BN
 from ..ops import transformer as TR
+from . import streams
 from .arena import ParamArena, ParamSpec
 
 
@@ -105,7 +106,7 @@ class Conv2d:
 
     def backward(self, dy, x, need_dx: bool = True, resid=None, bnr=None, resid_stride: int = 1):
         g = self.geom(x.shape)
-        G.conv_wgrad(dy, x, g, self.w.grad)
+        streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad), dy, x)
         if self.b is not None:
             G.bias_grad(dy, self.b.grad)
             self.arena.grad_ready(self.w, self.b)
@@ -122,7 +123,7 @@ class Conv2d:
         g = self.geom(x.shape)
         if self.k != 1 or self.pad != 0 or self.b is not None:
             raise ValueError("backward_lattice is for bias-free 1x1 convs")
-        G.conv_wgrad(dy, x, g, self.w.grad)
+        streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad), dy, x)
         self.arena.grad_ready(self.w)
         w2 = self.w.compute.view(self.cout, self.cin)
         return G.linear_dgrad(dy.reshape(-1, self.cout), w2).view(g.N, g.P, g.Q, g.C)

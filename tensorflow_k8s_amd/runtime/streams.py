@@ -1,0 +1,70 @@
+"""Side HIP stream for weight-gradient GEMMs.
+
+A conv's weight gradient dW = dY^T im2col(X) and its input gradient dX = dY W^T both depend only on
+dY, so the weight gradients run on a second stream, concurrent with the main stream's serial
+input-gradient chain (dgrad GEMMs, BatchNorm backward passes). On MI355X the late ResNet stages
+issue dgrad grids far smaller than 256 CUs x occupancy, so the concurrent wgrad grids fill the idle
+CUs. Under hipGraph capture the fork (side waits on the capture stream) and the join become graph
+edges.
+
+Ordering contract:
+* ``run_wgrad(fn, *tensors)`` forks after everything queued on the current stream and keeps
+  ``tensors`` (what fn reads) alive until the next ``join()``. The caching allocator may otherwise
+  hand their memory to later main-stream kernels while the side stream still reads it.
+* ``sync()``: the current stream waits for all side-stream work. Gradient-reduction hooks call it
+  before launching a bucket (MWMS all-reduce, PS reduce), because a bucket mixes gradients from
+  both streams.
+* ``join()``: sync plus release the kept tensors. Models call it at the end of backward, before the
+  optimizer reads ``arena.grad``.
+
+Mode (TFK_CONCURRENT_WGRAD): "auto" (default) forks only while a hipGraph is being captured, "1"
+always, "0" never. Measured on MI355X (ResNet-50 bs256, same box):
+* hipGraph replay: 25.90 ms/step with the side stream vs 26.48 without.
+* eager steps (the multi-GPU path), forced RCCL: 26.91 vs 26.11. The per-layer fork/join adds host
+  work that makes the eager step launch-bound.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+MODE = os.environ.get("TFK_CONCURRENT_WGRAD", "auto")
+_side: dict[int, torch.cuda.Stream] = {}
+_keep: list[torch.Tensor] = []
+
+
+def _stream(dev: torch.device) -> torch.cuda.Stream:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _side.get(idx)
+    if s is None:
+        s = _side[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+def run_wgrad(fn, *tensors: torch.Tensor) -> None:
+    """Run fn() (weight-gradient GEMMs reading `tensors`) on the side stream."""
+    if not (tensors and tensors[0].is_cuda and MODE != "0"
+            and (MODE == "1" or torch.cuda.is_current_stream_capturing())):
+        fn()
+        return
+    main = torch.cuda.current_stream(tensors[0].device)
+    side = _stream(tensors[0].device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        fn()
+    _keep.extend(tensors)
+
+
+def sync() -> None:
+    """The current stream waits for every weight gradient queued on the side stream."""
+    if _side and torch.cuda.is_available():
+        main = torch.cuda.current_stream()
+        for s in _side.values():
+            main.wait_stream(s)
+
+
+def join() -> None:
+    """sync() + release the tensors the side-stream work read."""
+    sync()
+    _keep.clear()

@@ -41,3 +41,26 @@ def test_hipgraph_replay_matches_eager():
         runs.append((r.last_loss(), m.arena.master.clone()))
     assert abs(runs[0][0] - runs[1][0]) < 1e-2
     assert float((runs[0][1] - runs[1][1]).norm() / runs[0][1].norm()) < 1e-2
+
+
+@pytest.mark.parametrize("mode", ["1", "auto"])
+def test_side_stream_wgrad_matches_single_stream(mode, monkeypatch):
+    """Weight gradients on the side HIP stream (runtime/streams.py), eager (mode "1") and
+    hipGraph-captured ("auto"): the same training trajectory as the single-stream step."""
+    from tensorflow_k8s_amd.runtime import streams
+    torch.manual_seed(0)
+    ms = [ResNet(50, num_classes=10).to("cuda") for _ in range(2)]
+    ms[1].arena.master.copy_(ms[0].arena.master)
+    ms[1].arena.refresh_compute()
+    x, y = synthetic_imagenet(16, "cuda", image_size=96, num_classes=10)
+    runs = []
+    for m, smode in zip(ms, ("0", mode)):
+        monkeypatch.setattr(streams, "MODE", smode)
+        opt = SGD(m.arena, lr=0.01)
+        r = StepRunner(m, opt, None, (x, y), use_graph=mode == "auto")
+        for _ in range(4):
+            r.step()
+        torch.cuda.synchronize()
+        runs.append((r.last_loss(), m.arena.master.clone()))
+    assert abs(runs[0][0] - runs[1][0]) < 1e-2
+    assert float((runs[0][1] - runs[1][1]).norm() / runs[0][1].norm()) < 1e-2

@@ -23,6 +23,8 @@ from ..runtime.layers import BatchNorm, Conv2d, Linear
 # neutral on MI355X (ResNet-50 bs256, same box: fused 26.71/26.76 ms vs standalone reduce 26.67/26.69) --
 # the gather-form pool backward is latency-bound and absorbs the saved pass in its own time
 FUSE_POOL_BNR = os.environ.get("TFK_FUSE_POOL_BNR", "0") == "1"
+# projection shortcut (forward conv, lattice dgrad) on the side stream (runtime/streams.py)
+SIDE_SHORTCUT = os.environ.get("TFK_SIDE_SHORTCUT", "1") == "1"
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
 
@@ -50,6 +52,17 @@ class Bottleneck:
     def forward(self, x, training=True):
         dev = x.device
         s1, s2, s3 = self.bn1.state(dev), self.bn2.state(dev), self.bn3.state(dev)
+        sc = []
+        if self.proj and SIDE_SHORTCUT:
+            # the projection shortcut only needs x: on the side stream, concurrent with conv1..conv3
+            ssc = self.bn_sc.state(dev)
+
+            def shortcut():
+                ysc = self.conv_sc.forward(x, ssc if training else None)
+                if training:
+                    self.bn_sc.finalize(ysc.numel() // ysc.shape[-1])
+                sc.append(ysc)
+            streams.run_wgrad(shortcut, x)
         y1 = self.conv1.forward(x, s1 if training else None)
         if training:
             self.bn1.finalize(y1.numel() // y1.shape[-1])
@@ -63,10 +76,14 @@ class Bottleneck:
             self.bn3.finalize(y3.numel() // y3.shape[-1])
         ysc = None
         if self.proj:
-            ssc = self.bn_sc.state(dev)
-            ysc = self.conv_sc.forward(x, ssc if training else None)
-            if training:
-                self.bn_sc.finalize(ysc.numel() // ysc.shape[-1])
+            if not SIDE_SHORTCUT:
+                ssc = self.bn_sc.state(dev)
+                ysc = self.conv_sc.forward(x, ssc if training else None)
+                if training:
+                    self.bn_sc.finalize(ysc.numel() // ysc.shape[-1])
+                sc.append(ysc)
+            streams.sync()
+            ysc = sc[0]
             out = BN.bn_apply(y3, s3, relu=True, r=ysc, rst=ssc, mask=training)
         else:
             out = BN.bn_apply(y3, s3, relu=True, r=x, mask=training)
@@ -100,6 +117,12 @@ class Bottleneck:
             dy3, _, dres = BN.bn_backward(dout, mk, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
                                           self.bn3.beta.grad, cnt3, want_dres=True, reduced=dout_reduced)
             self.arena.grad_ready(self.bn3.gamma, self.bn3.beta)
+        lattice = self.proj and self.stride > 1 and need_dx and next_bnr is not None
+        tl = []
+        if lattice and SIDE_SHORTCUT:
+            # the strided projection's lattice dgrad only needs dysc: side stream, concurrent with the
+            # conv3 -> conv2 chain, joined before conv1's dgrad epilogue adds it
+            streams.run_wgrad(lambda: tl.append(self.conv_sc.lattice_dgrad(dysc, x)), dysc, x)
         # bn2/bn1 have no residual input: relu mask recomputed from y, sums fused into the dgrad epilogue
         da2 = self.conv3.backward(dy3, a2, bnr=BN.BNReduce(y2, self.bn2.st))
         dy2, _, _ = BN.bn_backward(da2, None, y2, self.bn2.st, self.bn2.gamma.master, self.bn2.gamma.grad,
@@ -109,11 +132,15 @@ class Bottleneck:
         dy1, _, _ = BN.bn_backward(da1, None, y1, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
                                    self.bn1.beta.grad, y1.numel() // y1.shape[-1], relu_from_y=True, reduced=True)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
-        if self.proj and self.stride > 1 and need_dx and next_bnr is not None:
+        if lattice:
             # strided projection: its dgrad only touches the stride lattice -> a dense GEMM over the
             # P x Q rows, added on the lattice inside conv1's dgrad epilogue (which also carries the
             # previous block's fused BN reduction) instead of a 3/4-zero strided gather
-            t = self.conv_sc.backward_lattice(dysc, x)
+            if not SIDE_SHORTCUT:
+                tl.append(self.conv_sc.lattice_dgrad(dysc, x))
+            self.conv_sc.wgrad(dysc, x)
+            streams.sync()
+            t = tl[0]
             dx = self.conv1.backward(dy1, x, need_dx=True, resid=t, resid_stride=self.stride, bnr=next_bnr)
         elif self.proj:
             dx = self.conv1.backward(dy1, x, need_dx=need_dx)

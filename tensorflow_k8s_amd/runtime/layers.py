@@ -123,8 +123,18 @@ class Conv2d:
         g = self.geom(x.shape)
         if self.k != 1 or self.pad != 0 or self.b is not None:
             raise ValueError("backward_lattice is for bias-free 1x1 convs")
+        self.wgrad(dy, x)
+        return self.lattice_dgrad(dy, x)
+
+    def wgrad(self, dy, x):
+        """Weight gradient only (side stream when enabled) + readiness notification."""
+        g = self.geom(x.shape)
         streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad), dy, x)
         self.arena.grad_ready(self.w)
+
+    def lattice_dgrad(self, dy, x):
+        """The input gradient of backward_lattice only (no weight gradient, no hooks)."""
+        g = self.geom(x.shape)
         w2 = self.w.compute.view(self.cout, self.cin)
         return G.linear_dgrad(dy.reshape(-1, self.cout), w2).view(g.N, g.P, g.Q, g.C)
 

@@ -88,6 +88,8 @@ def on_gpu(*ts) -> bool:
 
 # ---------------------------------------------------------------- workspaces
 _ws: dict = {}
+# split-K slab workspace slot of conv weight gradients; runtime/streams.py sets one per side stream
+WGRAD_SLOT = "splitk_wgrad"
 
 
 def workspace(device: torch.device, numel: int, dtype=torch.float32, slot: str = "splitk") -> torch.Tensor:

@@ -13,6 +13,7 @@ import torch
 import torch.nn.functional as F
 
 from . import tuning
+from . import _lib as _lib_mod
 from ._lib import lib, on_gpu, workspace
 
 A_KIN, A_KOUT, A_CONV_FWD, A_CONV_DGRAD = 0, 1, 2, 3
@@ -551,4 +552,4 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
                   split_stride=stride, conv=g.vec())
     # own slab workspace: conv weight gradients may run on the side stream (runtime/streams.py)
     _f32_out_splitk(run, g.K, Nn, Kp, tiles, gw.view(-1), accumulate, dy.device, force_splits=splits,
-                    slot="splitk_wgrad")
+                    slot=_lib_mod.WGRAD_SLOT)

@@ -30,16 +30,24 @@ import os
 import torch
 
 MODE = os.environ.get("TFK_CONCURRENT_WGRAD", "auto")
-_side: dict[int, torch.cuda.Stream] = {}
+# side streams used round-robin (each with its own split-K workspace slot): a weight gradient's slab
+# reduce then overlaps the next weight gradient's GEMM. Measured (ResNet-50 bs256, same box):
+# 1 -> 25.64 ms, 2 -> 25.41 ms, 3 -> 25.76 ms
+NSIDE = int(os.environ.get("TFK_WGRAD_STREAMS", "2"))
+_side: dict[tuple[int, int], torch.cuda.Stream] = {}
 _keep: list[torch.Tensor] = []
+_rr = 0
 
 
-def _stream(dev: torch.device) -> torch.cuda.Stream:
+def _stream(dev: torch.device) -> tuple[int, torch.cuda.Stream]:
+    global _rr
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    s = _side.get(idx)
+    k = _rr % max(1, NSIDE)
+    _rr += 1
+    s = _side.get((idx, k))
     if s is None:
-        s = _side[idx] = torch.cuda.Stream(device=idx)
-    return s
+        s = _side[(idx, k)] = torch.cuda.Stream(device=idx)
+    return k, s
 
 
 def run_wgrad(fn, *tensors: torch.Tensor) -> None:
@@ -48,11 +56,17 @@ def run_wgrad(fn, *tensors: torch.Tensor) -> None:
             and (MODE == "1" or torch.cuda.is_current_stream_capturing())):
         fn()
         return
+    from ..ops import _lib
     main = torch.cuda.current_stream(tensors[0].device)
-    side = _stream(tensors[0].device)
+    k, side = _stream(tensors[0].device)
     side.wait_stream(main)
-    with torch.cuda.stream(side):
-        fn()
+    prev = _lib.WGRAD_SLOT
+    _lib.WGRAD_SLOT = f"splitk_wgrad{k}"
+    try:
+        with torch.cuda.stream(side):
+            fn()
+    finally:
+        _lib.WGRAD_SLOT = prev
     _keep.extend(tensors)
 
 

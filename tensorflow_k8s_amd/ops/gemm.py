@@ -408,6 +408,9 @@ DGRAD_AS_FWD_MIN_C = int(os.environ.get("TFK_DGRAD_AS_FWD_MIN_C", 128))
 # Strided-conv dgrad phases (BN-reduce epilogue with the phase out-map) as forward convs over dY on
 # the LDS-DMA gather (needs the conv's Cout % 64 == 0); TFK_PHASES_AS_FWD=0: register-engine gather.
 PHASES_AS_FWD = os.environ.get("TFK_PHASES_AS_FWD", "1") == "1"
+# scale on the measured (isolated-kernel) split-K counts of conv weight gradients, for A/B under the
+# side-stream overlap (runtime/streams.py), where fewer, larger slabs may pay off
+WGRAD_SPLIT_SCALE = float(os.environ.get("TFK_WGRAD_SPLIT_SCALE", "1.0"))
 # Non-pointwise weight gradients on the LDS-DMA engine's im2col gather (B_CONV_WGRAD, C % 8 == 0).
 G4_WGRAD = os.environ.get("TFK_G4_WGRAD", "1") == "1"
 
@@ -536,6 +539,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
     tuned = tuning.wgrad_config(g.K, Nn, Kp) if (g.pointwise and g.K % 8 == 0 and g.C % 8 == 0) else None
     if splits is None and tuned is not None:
         tile, splits = tuned
+        if WGRAD_SPLIT_SCALE != 1.0:
+            splits = max(1, int(round(splits * WGRAD_SPLIT_SCALE)))
     else:
         tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp,
                          wide_ok=WIDE_WGRAD and not g.pointwise and g.C <= WIDE_WGRAD_MAX_C,

@@ -82,7 +82,10 @@ class StepRunner:
                 return
             self.graph = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
-            with torch.cuda.graph(self.graph):
+            # thread-local capture: RCCL's process-group watchdog thread polls its work events while
+            # this thread captures; under the default global mode that poll fails the capture
+            # ("operation not permitted when stream is capturing")
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self._loss, self._corr = self._step_body()
         self.graph.replay()
 

@@ -366,6 +366,9 @@ TEST(http_server_sheds_connections_over_the_cap) {
   ssize_t n = recv(fd, buf, sizeof buf - 1, 0);
   CHECK(n > 0 && std::string(buf).find("503") != std::string::npos);
   ::close(fd);
+  // the server counts the shed connection after writing the 503 the client already read
+  for (int i = 0; i < 200 && srv.connections_rejected() < 1; ++i)
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
   CHECK(srv.connections_rejected() >= 1);
   for (int h : held) ::close(h);
   srv.stop();

@@ -194,10 +194,17 @@ void Store::syncer_loop() {
     int fd = -1;
     {
       std::lock_guard<std::mutex> g(mu_);
-      if (wal_) fd = fileno(wal_);  // records are already fflush'ed under the lock
+      // records are already fflush'ed under the lock. dup() the descriptor while holding it: a
+      // concurrent compact_wal_locked() may fclose/reopen wal_, and fdatasync on the bare fileno
+      // could then hit a closed fd or a number reused by another file or socket. The dup keeps
+      // the old file description alive (syncing a compacted-away file is harmless).
+      if (wal_) fd = dup(fileno(wal_));
       if (fd >= 0) ops_["wal_fsync"]++;
     }
-    if (fd >= 0) fdatasync(fd);
+    if (fd >= 0) {
+      fdatasync(fd);
+      close(fd);
+    }
   }
 }
 

@@ -327,8 +327,15 @@ void HttpServer::stop() {
     ::close(lfd_);
   }
   if (accept_thr_.joinable()) accept_thr_.join();
-  // connection threads are detached and touch this object until they exit: wait for all of them
-  // (idle keep-alive reads poll the stop flag every 200 ms; handlers poll ResponseWriter::alive())
+  // Connection threads are detached and touch this object until they exit. Shut their sockets down
+  // so a thread blocked in send() to a watch client that stopped reading, or in SSL_read() on a
+  // partial record, returns at once; idle keep-alive reads poll the stop flag every 200 ms and
+  // handlers poll ResponseWriter::alive(). Accepted sockets also carry send/receive timeouts, so
+  // every blocking call is bounded even without the shutdown.
+  {
+    std::lock_guard<std::mutex> g(conns_mu_);
+    for (int fd : conn_fds_) ::shutdown(fd, SHUT_RDWR);
+  }
   while (active_.load() > 0) usleep(5000);
 }
 
@@ -367,7 +374,34 @@ void HttpServer::accept_loop() {
   }
 }
 
+// Per-socket I/O bounds: a peer that stops reading fails send() after kSendTimeoutS instead of
+// blocking its thread forever; SSL_read on a partial TLS record returns WANT_READ after
+// kRecvSliceMs (read_some() treats that as "no data yet" and the caller re-checks its stop flag).
+static constexpr int kSendTimeoutS = 10;
+static constexpr int kRecvSliceMs = 1000;
+
+static void set_io_timeouts(int fd, int send_s, int recv_ms) {
+  timeval sv{send_s, 0};
+  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &sv, sizeof sv);
+  timeval rv{recv_ms / 1000, (recv_ms % 1000) * 1000};
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &rv, sizeof rv);
+}
+
 void HttpServer::handle_conn(int fd, std::string peer) {
+  {
+    std::lock_guard<std::mutex> g(conns_mu_);
+    conn_fds_.insert(fd);
+  }
+  // drop the fd from conn_fds_ BEFORE it is closed, so stop() never shuts down a reused fd number
+  auto untrack = [this, fd] {
+    std::lock_guard<std::mutex> g(conns_mu_);
+    conn_fds_.erase(fd);
+  };
+  if (stopping_) {  // raced with stop(): it may have swept conn_fds_ before the insert
+    untrack();
+    ::close(fd);
+    return;
+  }
   SSL* ssl = nullptr;
   if (tls_) {
     ssl = SSL_new(tls_->ctx());
@@ -377,12 +411,12 @@ void HttpServer::handle_conn(int fd, std::string peer) {
     if (SSL_accept(ssl) != 1) {
       ERR_clear_error();
       SSL_free(ssl);
+      untrack();
       ::close(fd);
       return;
     }
-    timeval none{0, 0};
-    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof none);
   }
+  set_io_timeouts(fd, kSendTimeoutS, kRecvSliceMs);
   Conn conn(fd, ssl);
   std::string buf;
   while (!stopping_) {
@@ -428,6 +462,7 @@ void HttpServer::handle_conn(int fd, std::string peer) {
     if (c != req.headers.end() && to_lower(c->second) == "close") break;
   }
   conn.shutdown();
+  untrack();  // ~Conn closes the fd right after
 }
 
 // ----------------------------------------------------------------------------------- client
@@ -530,8 +565,11 @@ std::unique_ptr<Conn> HttpClient::dial(std::string* err) {
     ::close(fd);
     return nullptr;
   }
-  timeval none{0, 0};
-  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof none);
+  // Keep SSL_read bounded after the handshake: a server that stalls mid-record (or sends only
+  // non-data records such as TLS 1.3 session tickets) yields WANT_READ, which read_some() reports
+  // as "no data yet", so timeouts and RestWatch's stop flag keep working over HTTPS.
+  SSL_clear_mode(ssl, SSL_MODE_AUTO_RETRY);
+  set_io_timeouts(fd, std::max(1, timeout_ms_ / 1000), kRecvSliceMs);
   return std::unique_ptr<Conn>(new Conn(fd, ssl));
 }
 
@@ -630,8 +668,12 @@ HttpResponse HttpClient::request(const std::string& method, const std::string& p
   if (!has_ct && !body.empty()) wire += "Content-Type: application/json\r\n";
   wire += "\r\n" + body;
   // A pooled connection the server already closed fails before any response byte: retry once on
-  // a fresh connection (the request never reached a handler).
-  for (int attempt = 0; attempt < 2; ++attempt) {
+  // a fresh connection. Only idempotent methods are retried -- the server may have processed a
+  // POST/PATCH and dropped the connection before replying, and a blind retry would run it twice
+  // (callers of non-idempotent requests handle the failure, e.g. with an AlreadyExists check).
+  const bool idempotent = method == "GET" || method == "HEAD" || method == "PUT" || method == "DELETE" ||
+                          method == "OPTIONS";
+  for (int attempt = 0; attempt < (idempotent ? 2 : 1); ++attempt) {
     std::unique_ptr<Conn> c = keepalive_ ? take_idle() : nullptr;
     bool reused = c != nullptr;
     HttpResponse r;

@@ -10,6 +10,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -134,6 +135,8 @@ class HttpServer {
   HttpHandler handler_;
   std::thread accept_thr_;
   std::shared_ptr<TlsContext> tls_;
+  std::mutex conns_mu_;
+  std::set<int> conn_fds_;  // live connection sockets: stop() shuts them down so no thread stays blocked
 };
 
 std::string http_status_text(int code);

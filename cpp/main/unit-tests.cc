@@ -374,6 +374,39 @@ TEST(http_server_sheds_connections_over_the_cap) {
   srv.stop();
 }
 
+TEST(http_server_stop_returns_with_a_stalled_stream_client) {
+  // A watch-style handler streams to a client that stops reading: its send() blocks once the
+  // socket buffers fill. stop() must still return promptly (shutdown of live sockets
+  // plus SO_SNDTIMEO on accepted connections).
+  HttpServer srv;
+  std::string err;
+  CHECK(srv.listen("127.0.0.1", 0, &err));
+  srv.serve([](const HttpRequest&, ResponseWriter& w) {
+    w.start_stream(200, "application/json");
+    std::string chunk(64 << 10, 'x');
+    while (w.alive() && w.write_chunk(chunk)) {
+    }
+  });
+  int fd = socket(AF_INET, SOCK_STREAM, 0);
+  int small = 4096;
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &small, sizeof small);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)srv.port());
+  inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+  CHECK(connect(fd, (sockaddr*)&a, sizeof a) == 0);
+  std::string req = "GET /watch HTTP/1.1\r\nHost: x\r\n\r\n";
+  CHECK(send(fd, req.data(), req.size(), 0) == (ssize_t)req.size());
+  std::this_thread::sleep_for(std::chrono::milliseconds(500));  // buffers full, handler blocked in send
+  CHECK_EQ(srv.connections_active(), 1);
+  auto t0 = std::chrono::steady_clock::now();
+  srv.stop();
+  double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  CHECK(s < 5.0);
+  CHECK_EQ(srv.connections_active(), 0);
+  ::close(fd);
+}
+
 TEST(store_watch_replay_and_gone) {
   auto s = std::make_shared<Store>("", 4);  // tiny history window
   Json out;

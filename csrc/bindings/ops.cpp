@@ -459,7 +459,7 @@ void maxpool_bwd(torch::Tensor dy, torch::Tensor idx, torch::Tensor dx, std::vec
     TORCH_CHECK(bnr.size() == 10, "bnr needs 10 entries");
     for (int i : {0, 2, 3, 9}) TORCH_CHECK(bnr[i].has_value() && bnr[i]->defined(), "bnr missing required entry ", i);
     TORCH_CHECK(!(bnr[6].has_value() && bnr[6]->defined()), "maxpool_bwd BN reduce: no second BN");
-    TORCH_CHECK(256 % (g[3] / 8) == 0 && g[3] % 8 == 0, "maxpool_bwd BN reduce needs (C/8) | 256");
+    TORCH_CHECK(g[3] % 8 == 0 && g[3] >= 8 && 256 % (g[3] / 8) == 0, "maxpool_bwd BN reduce needs C % 8 == 0 and (C/8) | 256");
     need_bf16(*bnr[0], "bn_y"); need_numel(*bnr[0], nx, "bn_y");
     const void* bn_a = nullptr;
     amask = relu_bitmask(bnr[1], nx, &bn_a);

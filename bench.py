@@ -32,12 +32,13 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--comm-dtype", default="bf16", choices=["bf16", "f32"],
                     help="gradient all-reduce wire dtype (bf16: half the xGMI bytes; f32 master update either way)")
-    ap.add_argument("--graph", type=int, default=-1, help="capture step in a hipGraph (default: on for 1 GPU)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the step in a hipGraph (default: on, at every world size, unless the model has host-side per-step state)")
     ap.add_argument("--rccl-algo", default="", help="RCCL algorithm (Ring|Tree|...), see parallel/comm.py")
     ap.add_argument("--rccl-proto", default="", help="RCCL protocol (Simple|LL|LL128)")
     ap.add_argument("--rccl-channels", type=int, default=0, help="minimum RCCL channels (concurrent rings)")
     ap.add_argument("--force-comm", action="store_true",
-                    help="1 GPU: still run the RCCL gradient all-reduce (world-size-1 process group)")
+                    help="1 GPU: still run the RCCL gradient all-reduce (world-size-1 tfk_comm communicator)")
     ap.add_argument("--fp8", type=int, default=0, help="transformer models: MX-fp8 linear GEMMs (fwd, dgrad, wgrad)")
     ap.add_argument("--via-operator", action="store_true",
                     help="measure through a TFJob: tfk-cluster gang-schedules one pod per GPU (TF_CONFIG rendezvous)")
@@ -62,20 +63,22 @@ def main():
                  "--master-addr 127.0.0.1 bench.py --gpus N")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    import torch.distributed as dist
 
-    from tensorflow_k8s_amd.parallel import comm
+    from tensorflow_k8s_amd.parallel import comm, tfk_comm
     rccl_cfg = comm.configure_rccl(args.rccl_algo or None, args.rccl_proto or None, args.rccl_channels)
     if world > 1 or args.force_comm:
         comm.enable_transport_log()
-    if args.force_comm and world == 1:
-        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29541", rank=0, world_size=1, device_id=dev)
-    elif world > 1 and info is not None:
+    # the world communicator is the runtime's own RCCL binding (parallel/tfk_comm.py): no
+    # torch.distributed process group, collectives enqueued on a comm stream the step graph captures
+    world_comm = None
+    if world > 1 and info is not None:
         from tensorflow_k8s_amd.parallel import cluster
-        cluster.init_process_group(info, "nccl", timeout_s=300, device_id=dev)
+        world_comm = cluster.init_comm(info, dev, "rccl", timeout_s=300)
     elif world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        world_comm = tfk_comm.init(tfk_comm.env_store(rank, world), rank, world, dev)
+    elif args.force_comm:
+        import torch.distributed as dist
+        world_comm = tfk_comm.init(dist.HashStore(), 0, 1, dev)
 
     from tensorflow_k8s_amd.models import build_model, synthetic_batch
     from tensorflow_k8s_amd.parallel.mwms import MultiWorkerMirroredStrategy
@@ -93,21 +96,26 @@ def main():
     else:
         opt = AdamW(model.arena, lr=1e-4, b2=0.98, eps=1e-9, weight_decay=0.0)
         opt_name = "Adam (fused HIP)"
-    strat = MultiWorkerMirroredStrategy(model.arena, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype,
-                                        force=args.force_comm)
+    strat = MultiWorkerMirroredStrategy(model.arena, comm=world_comm, bucket_mb=args.bucket_mb,
+                                        comm_dtype=args.comm_dtype, force=args.force_comm)
     strat.configure_optimizer(opt)
     strat.broadcast_parameters()
     batch = synthetic_batch(model, args.batch, dev, seed=1000 + rank)
-    # dropout seeds advance per step on the host -> transformer steps stay eager
-    use_graph = (world == 1 and is_cnn) if args.graph < 0 else bool(args.graph)
+    # the whole step (fwd, bwd, RCCL bucket all-reduces, optimizer) replays from one hipGraph at every
+    # world size; only a model with host-side per-step state (graph_hazards) runs eager
+    from tensorflow_k8s_amd.runtime.trainer import graph_hazards
+    use_graph = (not graph_hazards(model)) if args.graph < 0 else bool(args.graph)
     runner = StepRunner(model, opt, strat, batch, use_graph=use_graph)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world_comm is not None:
+            world_comm.barrier()
+        torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         runner.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    barrier()
     # per-step device timestamps (no host sync inside the timed loop) for the median / p90
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
@@ -115,14 +123,12 @@ def main():
     for i in range(args.steps):
         runner.step()
         evs[i + 1].record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    barrier()
     dt = time.perf_counter() - t0
+    mine_ms = dt / args.steps * 1000.0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        world_comm.all_reduce(t, op="max")
     dt = float(t.item())
     ms = dt / args.steps * 1000.0
     step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
@@ -131,14 +137,15 @@ def main():
                "min": round(step_ms[0], 3), "max": round(step_ms[-1], 3)}
     per_rank = [ms]
     if world > 1:
-        g = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
-        dist.all_gather(g, torch.tensor([dt / args.steps * 1000.0], dtype=torch.float64, device=dev))
-        per_rank = [round(float(x.item()), 3) for x in g]
+        g = torch.zeros(world, dtype=torch.float64, device=dev)
+        world_comm.all_gather(g, torch.tensor([mine_ms], dtype=torch.float64, device=dev))
+        per_rank = [round(float(x), 3) for x in g.tolist()]
     gb = args.batch * world
     value = gb / (ms / 1000.0)
     comm_cfg = {"comm_dtype": args.comm_dtype, "bucket_mb": args.bucket_mb, "buckets": len(strat.buckets),
                 "wire_mb_per_step": round(strat.wire_bytes() / 2**20, 1) if strat.enabled else 0.0}
     if strat.enabled:
+        comm_cfg["backend"] = "tfk_comm RCCL (own binding, librccl %s)" % _rccl_version()
         comm_cfg["rccl_transport"] = comm.transport_summary()
         comm_cfg["rccl_config"] = rccl_cfg
     loss = runner.last_loss()
@@ -154,7 +161,7 @@ def main():
             "dtype": "bf16+mxfp8" if args.fp8 else "bf16",
             "data": "synthetic token ids, random-init weights",
             "config": {"model": args.model, "global_batch": gb, "seq_len": seq, "per_gpu_batch": args.batch,
-                       "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (RCCL all-reduce)",
+                       "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (tfk_comm RCCL all-reduce)",
                        "optimizer": opt_name, "hipgraph": use_graph, "comm": comm_cfg},
             "loss": loss}), flush=True)
     elif rank == 0:
@@ -169,12 +176,17 @@ def main():
             "vs_baseline": round(value / base, 4) if base else None, "dtype": "bf16",
             "data": "synthetic (on-device ImageNet-shaped 224x224x3 bf16 batch, random-init weights)",
             "config": {"model": args.model, "global_batch": gb, "seq_len": None, "per_gpu_batch": args.batch,
-                       "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (RCCL all-reduce)",
+                       "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (tfk_comm RCCL all-reduce)",
                        "optimizer": opt_name, "hipgraph": use_graph, "comm": comm_cfg},
             "loss": loss,
         }), flush=True)
-    if dist.is_initialized():
-        dist.destroy_process_group()
+    tfk_comm.shutdown()
+
+
+def _rccl_version() -> str:
+    from tensorflow_k8s_amd import _C
+    v = _C.rccl_version()
+    return f"{v // 10000}.{v // 100 % 100}.{v % 100}"
 
 
 def run_via_operator(args) -> int:

@@ -647,6 +647,7 @@ void add(torch::Tensor a, torch::Tensor b, torch::Tensor y, double alpha, double
 
 void register_transformer_ops(pybind11::module& m);
 void register_ckpt_ops(pybind11::module& m);
+void register_comm_ops(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "tfk gfx950 HIP kernel library";
@@ -697,4 +698,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("add", &add);
   register_transformer_ops(m);
   register_ckpt_ops(m);
+  register_comm_ops(m);
 }

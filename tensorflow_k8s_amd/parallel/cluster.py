@@ -93,26 +93,20 @@ def resolve(env: dict | None = None) -> ClusterInfo:
     return ClusterInfo(worker_ranks=[0], source="local")
 
 
-def init_process_group(info: ClusterInfo, backend: str, timeout_s: float = 600.0, retries: int = 5, device_id=None):
-    """Rendezvous on the chief's TCP store (torch's C++ TCPStore on tfPort) and create the
-    RCCL/gloo world. A port-in-use at the chief (k8s-operator.md:5 failure mode, typically the
-    previous restart generation still shutting down) is retried, then reported as a retryable
-    exit so the operator restarts the gang."""
+def make_store(info: ClusterInfo, timeout_s: float = 600.0, retries: int = 5):
+    """The job's rendezvous store: torch's C++ TCPStore hosted by the chief on its tfPort. A
+    port-in-use at the chief (k8s-operator.md:5 failure mode, typically the previous restart
+    generation still shutting down) is retried, then reported as a retryable exit so the operator
+    restarts the gang."""
     import datetime
     import time
 
     import torch.distributed as dist
-    if info.world_size <= 1 or info.rank < 0:
-        return False
     last = None
     for attempt in range(retries):
         try:
-            store = dist.TCPStore(info.master_addr, info.master_port, info.world_size, info.rank == 0,
-                                  timeout=datetime.timedelta(seconds=timeout_s))
-            kw = {"device_id": device_id} if device_id is not None else {}
-            dist.init_process_group(backend, store=store, rank=info.rank, world_size=info.world_size,
-                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
-            return True
+            return dist.TCPStore(info.master_addr, info.master_port, info.world_size, info.rank == 0,
+                                 timeout=datetime.timedelta(seconds=timeout_s))
         except (RuntimeError, OSError) as e:
             last = e
             msg = str(e).lower()
@@ -121,6 +115,36 @@ def init_process_group(info: ClusterInfo, backend: str, timeout_s: float = 600.0
                 continue
             raise
     raise RendezvousError(f"rendezvous at {info.master_addr}:{info.master_port} failed: port already in use ({last})")
+
+
+def init_comm(info: ClusterInfo, device, backend: str = "auto", timeout_s: float = 600.0, retries: int = 5):
+    """Rendezvous on the chief's store and create the world communicator (parallel/tfk_comm):
+    ``rccl`` = the runtime's own RCCL communicator (GPU ranks), ``gloo`` = torch.distributed gloo
+    (CPU ranks, CPU parameter servers). Returns None for a single process / the evaluator."""
+    import torch
+
+    from . import tfk_comm
+    if info.world_size <= 1 or info.rank < 0:
+        return None
+    if backend == "auto":
+        backend = "rccl" if torch.device(device).type == "cuda" else "gloo"
+    store = make_store(info, timeout_s, retries)
+    dev = torch.device(device) if backend == "rccl" else torch.device("cpu")
+    return tfk_comm.init(store, info.rank, info.world_size, dev, timeout_s)
+
+
+def init_process_group(info: ClusterInfo, backend: str, timeout_s: float = 600.0, retries: int = 5, device_id=None):
+    """torch.distributed world on the chief's store (gloo tier and tools)."""
+    import datetime
+
+    import torch.distributed as dist
+    if info.world_size <= 1 or info.rank < 0:
+        return False
+    store = make_store(info, timeout_s, retries)
+    kw = {"device_id": device_id} if device_id is not None else {}
+    dist.init_process_group(backend, store=store, rank=info.rank, world_size=info.world_size,
+                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return True
 
 
 class RendezvousError(RuntimeError):

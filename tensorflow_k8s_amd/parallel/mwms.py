@@ -1,11 +1,15 @@
-"""MultiWorkerMirroredStrategy: synchronous data parallelism over RCCL (torch.distributed "nccl"
-backend on ROCm) / gloo on CPU.
+"""MultiWorkerMirroredStrategy: synchronous data parallelism over tfk_comm -- the runtime's own
+RCCL communicator on GPUs (parallel/tfk_comm.py, csrc/bindings/comm.cpp), torch.distributed gloo
+on the CPU tier.
 
 MI355X design: gradients live in ONE flat f32 arena buffer laid out in backward-completion order,
 so a bucket is a contiguous slice -> one ``all_reduce`` per bucket with no flatten copies. Buckets
 are launched the moment the backward pass has written their last gradient (executor readiness
-callbacks), so ring all-reduce over xGMI overlaps the remaining backward compute; RCCL runs on its
-own internal stream and the compute stream only waits on it right before the optimizer.
+callbacks), so ring all-reduce over xGMI overlaps the remaining backward compute; RCCL runs on the
+communicator's high-priority comm stream (forked from the compute stream at launch) and the compute
+stream only waits on it right before the optimizer. Under hipGraph capture those forks/joins are
+graph edges: the captured step (forward, backward, bucket all-reduces, optimizer) is the step that
+runs at every world size.
 
 * Launch order is the bucket order on every rank (a bucket that completes early waits for its
   predecessors), so all ranks issue the same collective sequence whatever the readiness callbacks
@@ -23,9 +27,9 @@ own internal stream and the compute stream only waits on it right before the opt
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
 from ..runtime.arena import ParamArena
+from . import tfk_comm
 
 _COMM_DTYPES = {"f32": torch.float32, "fp32": torch.float32, "float32": torch.float32,
                 "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
@@ -55,13 +59,13 @@ class Bucket:
 class MultiWorkerMirroredStrategy:
     name = "mwms"
 
-    def __init__(self, arena: ParamArena, group=None, bucket_mb: float = 32.0, comm_dtype=torch.float32,
+    def __init__(self, arena: ParamArena, comm=None, bucket_mb: float = 32.0, comm_dtype=torch.bfloat16,
                  force: bool = False):
         self.arena = arena
-        self.group = group
-        inited = dist.is_available() and dist.is_initialized()
-        self.world = dist.get_world_size(group) if inited else 1
-        self.rank = dist.get_rank(group) if inited else 0
+        self.comm = comm if comm is not None else tfk_comm.world()
+        inited = self.comm is not None
+        self.world = self.comm.world if inited else 1
+        self.rank = self.comm.rank if inited else 0
         self.comm_dtype = comm_dtype_of(comm_dtype)
         self.buckets: list[Bucket] = []
         self.bucket_of: dict[int, Bucket] = {}
@@ -129,7 +133,7 @@ class MultiWorkerMirroredStrategy:
             w = self.wire[b.start:b.end]
             cast_f32_bf16(view, w)
             view = w
-        b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        b.work = self.comm.all_reduce(view, async_op=True)
 
     def finish_step(self):
         """Launch stragglers (in order), wait for every bucket (compute stream waits on the RCCL
@@ -155,13 +159,13 @@ class MultiWorkerMirroredStrategy:
         the buffers (BN moving statistics, ...) are coalesced into one flat tensor per dtype."""
         if not self.enabled:
             return
-        dist.broadcast(self.arena.master, src, group=self.group)
+        self.comm.broadcast(self.arena.master, src)
         by_dtype: dict = {}
         for b in self.arena.buffers:
             by_dtype.setdefault((b.tensor.dtype, b.tensor.device), []).append(b.tensor)
         for ts in by_dtype.values():
             flat = torch.cat([t.reshape(-1) for t in ts])
-            dist.broadcast(flat, src, group=self.group)
+            self.comm.broadcast(flat, src)
             o = 0
             for t in ts:
                 t.copy_(flat[o:o + t.numel()].view_as(t))
@@ -170,5 +174,5 @@ class MultiWorkerMirroredStrategy:
 
     def all_reduce_metrics(self, t: torch.Tensor) -> torch.Tensor:
         if self.enabled:
-            dist.all_reduce(t, group=self.group)
+            self.comm.all_reduce(t)
         return t

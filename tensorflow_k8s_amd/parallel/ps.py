@@ -22,20 +22,27 @@ Two transports:
   -> reply shard f32; DONE=2; FETCH=3 (reply master + slots, for checkpoints); LOAD=4 (payload
   master + slots, restore); PULL=5 (reply master shard).
 * ``transport="rccl"`` (ps tasks own a GPU, e.g. BASELINE's PS=2/worker=6 on one 8xMI355X node;
-  sync only), bucketed and overlapped (``CollectivePlan``):
-  - each shard is cut into parameter-aligned buckets (<= bucket_mb); every shard s has two RCCL
-    communicators over {its owner} + workers -- one for gradient ``reduce``, one for parameter
-    ``broadcast`` -- so a bucket's broadcast does not queue behind later buckets' reduces, and no
-    other ps task contributes zeros to s's traffic;
+  sync only), bucketed and overlapped (``CollectivePlan``) on tfk_comm (the runtime's own RCCL
+  communicator, parallel/tfk_comm.py; torch.distributed gloo on the CPU tier):
+  - each shard is cut into parameter-aligned buckets (<= bucket_mb); every shard s has two
+    sub-communicators (ncclCommSplit) over {its owner} + workers -- one for gradient ``reduce``, one
+    for parameter ``broadcast`` -- so a bucket's broadcast does not queue behind later buckets'
+    reduces, and no other ps task contributes zeros to s's traffic;
+  - bf16 on the wire in both directions: workers pack each gradient bucket f32->bf16 and ``reduce``
+    it to the owner; the owner ships back the bf16 COMPUTE copy of weight-decayed buckets (what the
+    workers' GEMMs read; the f32 master never leaves the owner) and the small f32 no-decay buckets
+    (biases, BN/LayerNorm gamma+beta, which kernels read in f32). Per BERT-base step that is
+    ~220 MB up + ~220 MB down per worker instead of 440 + 440 MB in f32;
   - workers launch the ``reduce`` of a bucket the moment backward has produced its last gradient
     (arena readiness callbacks, in bucket order -- the same order on every rank), overlapping the
-    rest of backward, exactly like MWMS buckets;
+    rest of backward, exactly like MWMS buckets; the worker step has no host synchronisation and
+    is captured in a hipGraph like the MWMS step;
   - the owner zeroes ONLY its own shard's gradient, posts its buckets' reduces, and per bucket:
-    stream-waits for that reduce, runs the fused HIP optimizer on the bucket, posts its broadcast;
-    so early buckets are updated and shipped back while later ones are still being reduced;
-  - workers stream-wait for the broadcasts and refresh the bf16 compute copy.
+    stream-waits for that reduce, unpacks it, runs the fused HIP optimizer on the bucket (device LR
+    schedule supported: the step advances once per global step), posts its broadcast; so early
+    buckets are updated and shipped back while later ones are still being reduced.
   The schedule is identical on every rank (steps and checkpoint steps are known), so no control
-  messages are needed; for a checkpoint the owners ``send`` master + slots to the chief.
+  messages are needed; for a checkpoint the owners ``send`` f32 master + slots to the chief.
 """
 from __future__ import annotations
 
@@ -43,6 +50,7 @@ import torch
 import torch.distributed as dist
 
 from ..runtime.arena import ALIGN, ParamArena
+from . import tfk_comm
 
 PUSH, DONE, FETCH, LOAD, PULL = 1, 2, 3, 4, 5
 
@@ -97,7 +105,7 @@ class ParameterServerStrategy:
     name = "ps"
 
     def __init__(self, arena: ParamArena, ps_ranks: list[int], worker_ranks: list[int], mode: str = "sync",
-                 group=None, transport: str = "gloo", bucket_mb: float = 32.0):
+                 group=None, transport: str = "gloo", bucket_mb: float = 32.0, comm=None, wire_dtype=torch.bfloat16):
         if mode not in ("sync", "async"):
             raise ValueError(f"ps mode must be sync|async, got {mode}")
         if transport not in ("gloo", "rccl"):
@@ -106,7 +114,8 @@ class ParameterServerStrategy:
             raise ValueError("the rccl (collective) transport is synchronous; use transport=gloo for async")
         self.arena, self.ps_ranks, self.worker_ranks, self.mode, self.group = arena, list(ps_ranks), list(worker_ranks), mode, group
         self.transport = transport
-        self.rank = dist.get_rank()
+        self.comm = comm if comm is not None else tfk_comm.world()
+        self.rank = self.comm.rank if self.comm is not None else dist.get_rank()
         self.shards = shard_bounds(arena.numel, len(self.ps_ranks), _param_spans(arena))
         self.plan = None
         if transport == "gloo":
@@ -114,11 +123,22 @@ class ParameterServerStrategy:
             self._g = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
             self._p = [torch.empty(hi - lo, dtype=torch.float32, pin_memory=pin) for lo, hi in self.shards]
         else:
-            self.plan = CollectivePlan(arena, self.shards, self.ps_ranks, self.worker_ranks, bucket_mb)
+            self.plan = CollectivePlan(arena, self.shards, self.ps_ranks, self.worker_ranks, bucket_mb, self.comm,
+                                       wire_dtype)
             arena.on_grad_ready(self._on_ready)
         self.step_count = 0
         self._next = 0
         self._red = []
+
+    @property
+    def capturable(self) -> bool:
+        """The collective worker step (async reduce launches, stream waits on the broadcasts, bf16
+        unpack) has no host synchronisation -> hipGraph-capturable; the gloo transport is not."""
+        return self.plan is not None and self.comm is not None and self.comm.backend == "rccl"
+
+    def wire_bytes(self) -> int:
+        """Bytes one worker moves per step (up + down)."""
+        return self.plan.wire_bytes() if self.plan is not None else 2 * 4 * self.arena.numel
 
     @property
     def num_workers(self) -> int:
@@ -173,11 +193,11 @@ class ParameterServerStrategy:
         a = self.arena
         if self.transport == "rccl":
             self.finish_step()  # (no-op when the runner already called it)
-            works = [self.plan.broadcast(i, a.master) for i in range(len(self.plan.buckets))]
+            works = [self.plan.broadcast(i) for i in range(len(self.plan.buckets))]
             for w in self._red + works:
                 w.wait()  # stream waits: the next forward is ordered after the pulled parameters
             self._red = []
-            a.refresh_compute()
+            self.plan.finish_pull()
             self.step_count += 1
             if opt is not None:
                 opt.step_count = self.step_count
@@ -197,9 +217,7 @@ class ParameterServerStrategy:
     def pull(self) -> None:
         """Initial (or resync) read of every variable from the ps tasks."""
         if self.transport == "rccl":
-            for (lo, hi), ps in zip(self.shards, self.ps_ranks):
-                dist.broadcast(self.arena.master[lo:hi], ps, group=self.group)
-            self.arena.refresh_compute()
+            self.plan.pull_master()
             return
         self._exchange(PULL, None, self._p)
         for s, (lo, hi) in enumerate(self.shards):
@@ -214,7 +232,9 @@ class ParameterServerStrategy:
             dev = self.arena.master.device
             bufs = [torch.empty((1 + len(names)) * (hi - lo), dtype=torch.float32, device=dev) for lo, hi in self.shards]
             for b, ps in zip(bufs, self.ps_ranks):
-                dist.recv(b, ps, group=self.group)
+                self.comm.recv(b, ps)
+            if dev.type == "cuda":
+                torch.cuda.current_stream().synchronize()
         else:
             bufs = [torch.empty((1 + len(names)) * (hi - lo), dtype=torch.float32) for lo, hi in self.shards]
             self._exchange(FETCH, None, bufs)
@@ -252,8 +272,11 @@ class CollectivePlan:
     decay/no-decay boundary (so an optimizer region per bucket is valid, LAMB's per-tensor trust
     ratio included), listed in arena order = backward-completion order."""
 
-    def __init__(self, arena: ParamArena, shards, ps_ranks, worker_ranks, bucket_mb: float = 32.0):
+    def __init__(self, arena: ParamArena, shards, ps_ranks, worker_ranks, bucket_mb: float = 32.0, comm=None,
+                 wire_dtype=torch.bfloat16):
         self.arena, self.shards, self.ps_ranks = arena, list(shards), list(ps_ranks)
+        self.comm = comm if comm is not None else tfk_comm.world()
+        self.me = self.comm.rank
         cap = max(ALIGN, int(bucket_mb * (1 << 20)) // 4)
         cuts = sorted({lo for lo, _ in shards} | {hi for _, hi in shards} | set(arena.decay_region())
                       | set(arena.nodecay_region()))
@@ -277,12 +300,18 @@ class CollectivePlan:
             if cur:
                 self._add(start, hi_c, shard, cur)
         self.pending = list(self._nparams)
-        # two communicators per shard (reduce / broadcast): every rank creates every group, in order
-        self.red_groups, self.bc_groups = [], []
+        self.n_decay = arena.n_decay
+        # bf16 wire: gradients packed into `wire`, decay-region weights shipped as the bf16 compute copy
+        self.wire_dtype = wire_dtype
+        self.wire = torch.empty(arena.numel, dtype=wire_dtype, device=arena.grad.device) \
+            if wire_dtype != torch.float32 else None
+        # two sub-communicators per shard (reduce / broadcast): every rank splits every one, in order
+        self.red, self.bc, self.root = [], [], []
         for owner in self.ps_ranks:
             ranks = sorted({owner} | set(worker_ranks))
-            self.red_groups.append(dist.new_group(ranks))
-            self.bc_groups.append(dist.new_group(ranks))
+            self.red.append(self.comm.split(ranks, f"ps{owner}/reduce"))
+            self.bc.append(self.comm.split(ranks, f"ps{owner}/bcast"))
+            self.root.append(ranks.index(owner))
 
     def _add(self, lo, hi, shard, params):
         i = len(self.buckets)
@@ -297,14 +326,59 @@ class CollectivePlan:
     def buckets_of(self, shard: int) -> list[int]:
         return [i for i, b in enumerate(self.buckets) if b[2] == shard]
 
-    def reduce(self, i: int, grad: torch.Tensor):
-        lo, hi, s = self.buckets[i]
-        return dist.reduce(grad[lo:hi], self.ps_ranks[s], op=dist.ReduceOp.SUM, group=self.red_groups[s],
-                           async_op=True)
+    def is_decay(self, i: int) -> bool:
+        return self.buckets[i][0] < self.n_decay
 
-    def broadcast(self, i: int, master: torch.Tensor):
+    def wire_bytes(self) -> int:
+        """Bytes one worker pushes + pulls per step."""
+        esz = 4 if self.wire is None else self.wire.element_size()
+        up = sum(hi - lo for lo, hi, _ in self.buckets) * esz
+        down = sum((hi - lo) * (esz if self.is_decay(i) else 4) for i, (lo, hi, _) in enumerate(self.buckets))
+        return up + down
+
+    # ---------------------------------------------------------------- per bucket
+    def reduce(self, i: int, grad: torch.Tensor):
+        """Worker: push bucket i's gradient to its owner (packed to the wire dtype first)."""
         lo, hi, s = self.buckets[i]
-        return dist.broadcast(master[lo:hi], self.ps_ranks[s], group=self.bc_groups[s], async_op=True)
+        t = grad[lo:hi]
+        if self.wire is not None:
+            from ..ops.optim import cast_f32_bf16
+            cast_f32_bf16(t, self.wire[lo:hi])
+            t = self.wire[lo:hi]
+        return self.red[s].reduce(t, self.root[s], async_op=True)
+
+    def unpack(self, i: int) -> None:
+        """Owner: the reduced bf16 bucket -> f32 gradient (after its reduce completed)."""
+        if self.wire is not None:
+            from ..ops.optim import cast_bf16_f32
+            lo, hi, _ = self.buckets[i]
+            cast_bf16_f32(self.wire[lo:hi], self.arena.grad[lo:hi])
+
+    def broadcast(self, i: int):
+        """Owner sends / workers receive bucket i's updated weights: the bf16 compute copy for
+        weight-decayed buckets (bf16 wire), f32 master for the no-decay buckets."""
+        lo, hi, s = self.buckets[i]
+        a = self.arena
+        t = a.compute[lo:hi] if (self.wire is not None and self.is_decay(i)) else a.master[lo:hi]
+        return self.bc[s].broadcast(t, self.root[s], async_op=True)
+
+    def finish_pull(self) -> None:
+        """Worker, after every broadcast: refresh the compute copy of what arrived in f32."""
+        from ..ops.optim import cast_f32_bf16
+        a = self.arena
+        if self.wire is None:
+            a.refresh_compute()
+            return
+        lo, hi = a.nodecay_region()
+        if hi > lo:
+            cast_f32_bf16(a.master[lo:hi], a.compute[lo:hi])
+
+    def pull_master(self) -> None:
+        """Initial / resync read of every f32 master shard from its owner (all ranks call)."""
+        for s, (lo, hi) in enumerate(self.shards):
+            if self.bc[s] is not None:  # another ps task's shard: not a member of its communicator
+                self.bc[s].broadcast(self.arena.master[lo:hi], self.root[s])
+        self.arena.refresh_compute()
 
 
 class ParameterServer:
@@ -387,39 +461,42 @@ class ParameterServer:
 
     # ------------------------------------------------------------------ rccl transport
     def serve_collective(self, start_step: int, total_steps: int, checkpoint_every: int = 0,
-                         chief: int = 0, final_checkpoint: bool = True, bucket_mb: float = 32.0) -> int:
-        """Mirror of the workers' step schedule over RCCL (CollectivePlan): initial broadcast, then
-        per step: zero the own shard's gradient, post the own buckets' reduces, and per bucket
-        stream-wait -> fused optimizer on that bucket -> post its broadcast. Ships master + slots to
-        the chief at its checkpoint steps."""
+                         chief: int = 0, final_checkpoint: bool = True, bucket_mb: float = 32.0, comm=None,
+                         wire_dtype=torch.bfloat16) -> int:
+        """Mirror of the workers' step schedule over tfk_comm (CollectivePlan): initial broadcast,
+        then per step: zero the own shard's gradient, post the own buckets' reduces, and per bucket
+        stream-wait -> unpack -> fused optimizer on that bucket -> post its broadcast. The global step
+        (host counter or device schedule) advances once per step. Ships f32 master + slots to the
+        chief at its checkpoint steps."""
         a = self.arena
-        if self.opt._dev is not None:
-            raise RuntimeError("collective PS updates per bucket with host schedules (no device schedule)")
-        # groups first: the workers create theirs in ParameterServerStrategy.__init__, before pull()
-        plan = CollectivePlan(a, self.shards, self.ps_ranks, self.worker_ranks, bucket_mb)
-        for (lo, hi), ps in zip(self.shards, self.ps_ranks):
-            dist.broadcast(a.master[lo:hi], ps, group=self.group)
-        me = self.ps_ranks.index(dist.get_rank())
+        comm = comm if comm is not None else tfk_comm.world()
+        # sub-communicators first: the workers create theirs in ParameterServerStrategy.__init__
+        plan = CollectivePlan(a, self.shards, self.ps_ranks, self.worker_ranks, bucket_mb, comm, wire_dtype)
+        plan.pull_master()
+        me = self.ps_ranks.index(comm.rank)
         mine = plan.buckets_of(me)
+        opt = self.opt
         for step in range(start_step + 1, total_steps + 1):
             a.grad[self.lo:self.hi].zero_()  # the owner's own (zero) contribution to its reduces
+            if plan.wire is not None:
+                plan.wire[self.lo:self.hi].zero_()
             reds = [plan.reduce(i, a.grad) for i in mine]
             bcs = []
-            n0 = self.opt.step_count
             for k, (i, w) in enumerate(zip(mine, reds)):
                 w.wait()
+                plan.unpack(i)
                 lo, hi, _ = plan.buckets[i]
-                self.opt.region = (lo, hi)
-                self.opt.step()
-                if k + 1 < len(mine):
-                    self.opt.step_count = n0  # one global step: advance once, after the last bucket
-                bcs.append(plan.broadcast(i, a.master))
+                opt.region = (lo, hi)
+                opt.step_region(advance=k == 0)
+                bcs.append(plan.broadcast(i))
             for w in bcs:
                 w.wait()
-            self.opt.region = (self.lo, self.hi)
+            opt.region = (self.lo, self.hi)
             self.updates += 1
             ckpt = (checkpoint_every and step % checkpoint_every == 0 and step < total_steps) or \
                 (final_checkpoint and step == total_steps)
             if ckpt:
-                dist.send(self._state(), chief, group=self.group)
+                comm.send(self._state(), chief)
+                if a.master.is_cuda:
+                    torch.cuda.current_stream().synchronize()
         return self.updates

@@ -69,9 +69,29 @@ class Optimizer:
         """Advance the device schedule (inside the step, hence inside a captured graph)."""
         if self._dev is None:
             return None
+        if self._frozen:
+            return self._dev["hp"]
         b1, b2 = self._betas
         O.opt_hyper(self._dev["step"], self._dev["lr"], 0, b1, b2, self._dev["hp"])
         return self._dev["hp"]
+
+    _frozen = False
+
+    def step_region(self, advance: bool = True) -> None:
+        """Update ``self.region`` as one part of a global step that spans several region calls (the
+        collective parameter server updates its shard bucket by bucket): the first call
+        (advance=True) advances the step counter / device schedule, later calls of the same global
+        step reuse its learning rate and bias corrections."""
+        if advance:
+            self._before = self.step_count
+            self.step()
+            return
+        after = self.step_count
+        self.step_count, self._frozen = self._before, True
+        try:
+            self.step()
+        finally:
+            self.step_count, self._frozen = after, False
 
     def sync_step(self) -> int:
         """Host step counter (reads the device counter when the schedule lives on device)."""

@@ -4,8 +4,9 @@ This is the program a TFJob replica runs (the reference's pods run a TF script t
 ``TFConfigClusterResolver`` + ``MultiWorkerMirroredStrategy`` / ``ParameterServerStrategy`` from
 the operator-injected TF_CONFIG). Per role:
 
-* chief / worker: one process per GPU (HIP_VISIBLE_DEVICES set by the node agent), RCCL world over
-  all workers (MWMS) or gloo point-to-point to the ps tasks (PS strategy); restore-or-init, train
+* chief / worker: one process per GPU (HIP_VISIBLE_DEVICES set by the node agent), a tfk_comm RCCL
+  world over all workers (MWMS; bf16 gradient wire, the whole step captured in a hipGraph) or the
+  ps tasks (PS strategy: collective RCCL transport, or gloo point-to-point to CPU ps tasks); restore-or-init, train
   ``--steps`` global steps on synthetic data of the model's shape, chief writes TF-bundle
   checkpoints every ``--checkpoint-every`` steps and at the end, JSON-lines metrics on stdout;
 * ps: holds one shard of the variables + optimizer slots on the CPU and serves push/pull;
@@ -65,9 +66,12 @@ def parse_args(argv=None):
     ap.add_argument("--ps-transport", default="gloo", choices=["gloo", "rccl"],
                     help="gloo: ps tasks on CPU (sync/async); rccl: ps tasks own a GPU, RCCL reduce/broadcast (sync)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
-    ap.add_argument("--comm-dtype", default="f32", choices=["f32", "bf16"], help="MWMS gradient all-reduce wire dtype")
+    ap.add_argument("--comm-dtype", default="bf16", choices=["f32", "bf16"],
+                    help="gradient wire dtype (MWMS all-reduce, collective PS push/pull)")
     ap.add_argument("--device", default="auto", choices=["auto", "cpu", "cuda"])
-    ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph (1 GPU, MWMS)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the step in a hipGraph (default: on for GPU workers at any world size, unless the "
+                         "model has host-side per-step state)")
     ap.add_argument("--checkpoint-dir", default="")
     ap.add_argument("--checkpoint-every", type=int, default=0)
     ap.add_argument("--keep", type=int, default=5)
@@ -147,10 +151,9 @@ def maybe_fault(step: int, rank: int):
     os._exit(code)
 
 
-def run_ps(args, info, dev) -> int:
-    import torch.distributed as dist
-
+def run_ps(args, info, dev, world_comm) -> int:
     from ..models import build_model
+    from ..parallel import tfk_comm
     from ..parallel.ps import ParameterServer
     from .checkpoint import CheckpointManager
     model = build_model(args.model, **model_kwargs(args)).to(dev, seed=args.seed)
@@ -167,18 +170,22 @@ def run_ps(args, info, dev) -> int:
           "transport": args.ps_transport, "device": str(dev)})
     if args.ps_transport == "rccl":
         n = server.serve_collective(start, args.steps, args.checkpoint_every if args.checkpoint_dir else 0,
-                                    chief=0, final_checkpoint=bool(args.checkpoint_dir), bucket_mb=args.bucket_mb)
+                                    chief=0, final_checkpoint=bool(args.checkpoint_dir), bucket_mb=args.bucket_mb,
+                                    comm=world_comm, wire_dtype=_wire(args))
     else:
         n = server.serve()
     _log({"event": "done", "role": "ps", "index": info.task_index, "updates": n})
-    dist.destroy_process_group()
+    tfk_comm.shutdown()
     return EXIT_OK
 
 
-def run_worker(args, info, dev) -> int:
-    import torch.distributed as dist
+def _wire(args):
+    return torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32
 
+
+def run_worker(args, info, dev, world_comm) -> int:
     from ..models import build_model, synthetic_batch
+    from ..parallel import tfk_comm
     from .checkpoint import CheckpointManager
     from .trainer import StepRunner
 
@@ -190,11 +197,13 @@ def run_worker(args, info, dev) -> int:
         if not info.ps_ranks:
             raise SystemExit("--strategy ps needs ps tasks in TF_CONFIG")
         strat = ParameterServerStrategy(model.arena, info.ps_ranks, info.worker_ranks, args.ps_mode,
-                                        transport=args.ps_transport, bucket_mb=args.bucket_mb)
+                                        transport=args.ps_transport, bucket_mb=args.bucket_mb, comm=world_comm,
+                                        wire_dtype=_wire(args))
         strat.configure_optimizer(opt)
     else:
         from ..parallel.mwms import MultiWorkerMirroredStrategy
-        strat = MultiWorkerMirroredStrategy(model.arena, bucket_mb=args.bucket_mb, comm_dtype=args.comm_dtype)
+        strat = MultiWorkerMirroredStrategy(model.arena, comm=world_comm, bucket_mb=args.bucket_mb,
+                                            comm_dtype=args.comm_dtype)
         strat.configure_optimizer(opt)
     nworkers = max(1, len(info.worker_ranks))
     wrank = info.worker_ranks.index(info.rank) if info.rank in info.worker_ranks else 0
@@ -213,11 +222,15 @@ def run_worker(args, info, dev) -> int:
     batches = [synthetic_batch(model, args.batch, dev, seed=args.seed * 7919 + wrank * 1009 + i, **data_kwargs(args))
                for i in range(max(1, args.data_batches))]
     static = tuple(t.clone() for t in batches[0])
-    runner = StepRunner(model, opt, strat, static, use_graph=bool(args.graph) and nworkers == 1)
+    from .trainer import graph_hazards
+    use_graph = dev.type == "cuda" and (not graph_hazards(model) if args.graph < 0 else bool(args.graph))
+    runner = StepRunner(model, opt, strat, static, use_graph=use_graph)
     metrics_fh = open(args.metrics_file, "a") if (args.metrics_file and info.is_chief) else None
     gb = args.batch * nworkers
     _log({"event": "start", "rank": info.rank, "world": info.world_size, "workers": nworkers, "model": model.name,
           "params": model.arena.num_parameters(), "device": str(dev), "strategy": strat.name, "start_step": start,
+          "wire_mb_per_step": round(strat.wire_bytes() / 2**20, 3) if hasattr(strat, "wire_bytes") else 0.0,
+          "hipgraph": runner.use_graph,
           "global_batch": gb, "restart_generation": int(os.environ.get("TFK_RESTART_GENERATION", "0"))})
     from ..utils.tracing import NULL_TRACER, Tracer
     tracer = Tracer(rank=info.rank, device_events=dev.type == "cuda") if args.trace_file else NULL_TRACER
@@ -254,6 +267,7 @@ def run_worker(args, info, dev) -> int:
             with tracer.span("checkpoint", cat="io", step=step):
                 if use_ps:
                     strat.fetch_state(opt)
+                    opt.step_count = step  # the ps tasks ran the updates (a captured step keeps no host count)
                 path = ckpt.save(model.arena, opt, step)
             _log({"event": "checkpoint", "step": step, "path": path}, metrics_fh)
         maybe_fault(step, info.rank)
@@ -266,16 +280,16 @@ def run_worker(args, info, dev) -> int:
     if ckpt is not None and info.is_chief:
         if use_ps:
             strat.fetch_state(opt)
+            opt.step_count = step
         path = ckpt.save(model.arena, opt, step, blocking=True)
         _log({"event": "checkpoint", "step": step, "path": path, "final": True}, metrics_fh)
         with open(os.path.join(args.checkpoint_dir, "DONE"), "w") as f:
             f.write(str(step))
     if use_ps:
         strat.shutdown()
-    if dist.is_initialized():
-        if not use_ps:
-            dist.barrier()
-        dist.destroy_process_group()
+    if world_comm is not None and not use_ps:
+        world_comm.barrier()
+    tfk_comm.shutdown()
     if info.is_chief:
         _log({"event": "done", "step": step, "loss": runner.last_loss()}, metrics_fh)
     return EXIT_OK
@@ -294,15 +308,15 @@ def main(argv=None) -> int:
         if dev.type == "cpu" and info.world_size > 1 and "OMP_NUM_THREADS" not in os.environ:
             # co-located CPU replicas: split the cores instead of oversubscribing them
             torch.set_num_threads(max(1, (os.cpu_count() or 1) // info.world_size))
+        world_comm = None
         if info.world_size > 1:
             use_ps = args.strategy == "ps" or (args.strategy == "auto" and info.ps_ranks)
-            backend = "nccl" if (dev.type == "cuda" and (not use_ps or args.ps_transport == "rccl")) else "gloo"
-            cluster.init_process_group(info, backend, timeout_s=args.rendezvous_timeout,
-                                       retries=int(os.environ.get("TFK_RENDEZVOUS_RETRIES", "5")),
-                                       device_id=dev if backend == "nccl" else None)
+            backend = "rccl" if (dev.type == "cuda" and (not use_ps or args.ps_transport == "rccl")) else "gloo"
+            world_comm = cluster.init_comm(info, dev, backend, timeout_s=args.rendezvous_timeout,
+                                           retries=int(os.environ.get("TFK_RENDEZVOUS_RETRIES", "5")))
         if info.is_ps:
-            return run_ps(args, info, dev)
-        return run_worker(args, info, dev)
+            return run_ps(args, info, dev, world_comm)
+        return run_worker(args, info, dev, world_comm)
     except torch.cuda.OutOfMemoryError as e:
         _termination_message("OOMKilled")
         _log({"event": "error", "kind": "oom", "message": str(e)[:500]})

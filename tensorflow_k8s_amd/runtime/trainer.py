@@ -3,8 +3,9 @@ all-reduce + fused optimizer).
 
 hipGraph (``torch.cuda.CUDAGraph`` on ROCm) removes the ~600 host launches of a ResNet-50 step:
 after two eager warm-up steps (which also size every workspace) the whole step is captured once
-and replayed. Capture is used for single-GPU runs; multi-GPU runs stay eager so RCCL buckets can
-be issued as soon as backward produces them.
+and replayed -- at every world size: the data-parallel strategies enqueue their RCCL collectives
+(parallel/tfk_comm.py) on a comm stream forked from the capturing stream at the moment backward
+produces each bucket, so the replayed graph keeps the bucket/backward overlap.
 
 Everything a replay must see change per step lives on the device: the optimizer's learning-rate
 schedule, step counter and Adam bias corrections (Optimizer.enable_device_schedule). Host-side
@@ -34,8 +35,9 @@ class StepRunner:
     def __init__(self, model, opt, strategy, batch, use_graph: bool = False, warmup_eager: int = 2):
         self.model, self.opt, self.strategy = model, opt, strategy
         self.batch = batch
+        # a parameter-server strategy is capturable only on its collective (RCCL) transport
         self.use_graph = (use_graph and torch.cuda.is_available() and batch[0].is_cuda
-                          and not hasattr(strategy, "apply_gradients"))
+                          and (not hasattr(strategy, "apply_gradients") or getattr(strategy, "capturable", False)))
         if self.use_graph:
             bad = graph_hazards(model)
             if bad:

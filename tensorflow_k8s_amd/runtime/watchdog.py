@@ -4,8 +4,8 @@ A collective whose peer died never returns: RCCL (and gloo) block inside the all
 own timeout, which is minutes by default, and a wedged rank keeps its GPU busy. The watchdog is a
 daemon thread that expects a heartbeat (``beat(step)``) at least every ``timeout_s`` seconds once
 training has started. When the heartbeat stops it writes the termination message, logs one JSON
-event, aborts the process group (best effort, so RCCL tears its communicators down instead of
-spinning) and exits with 143, the retryable code of the operator's ExitCode restart policy: the
+event, aborts every live tfk_comm RCCL communicator (``ncclCommAbort``: the rank's outstanding RCCL
+kernels exit instead of spinning on a dead peer) and exits with 143, the retryable code of the operator's ExitCode restart policy: the
 operator bumps the restart generation, every rank re-rendezvouses and training resumes from the
 latest checkpoint (runtime/train.py, runtime/checkpoint.py).
 """
@@ -86,20 +86,18 @@ class StepWatchdog:
                 pass
         print(json.dumps({"event": "error", "kind": "watchdog", "step": step, "idle_s": round(idle, 2),
                           "message": msg}, sort_keys=True), flush=True)
-        abort_process_group()
+        n = abort_communicators()
+        print(json.dumps({"event": "comm_aborted", "communicators": n}, sort_keys=True), flush=True)
         sys.stdout.flush()
         sys.stderr.flush()
         os._exit(EXIT_RETRY)
 
 
-def abort_process_group() -> None:
-    """Best-effort abort of the default process group so RCCL communicators are torn down."""
+def abort_communicators() -> int:
+    """ncclCommAbort every live RCCL communicator of this process (parallel/tfk_comm). gloo groups
+    of the CPU tier need no abort: os._exit closes their sockets and the peers' pending ops fail."""
     try:
-        import torch.distributed as dist
-        if not dist.is_available() or not dist.is_initialized():
-            return
-        abort = getattr(dist.distributed_c10d, "_abort_process_group", None)
-        if abort is not None:
-            abort()
+        from ..parallel import tfk_comm
+        return tfk_comm.abort_all()
     except Exception:  # pragma: no cover - the process is exiting anyway
-        pass
+        return 0

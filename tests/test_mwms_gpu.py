@@ -1,7 +1,9 @@
-"""MWMS over RCCL on one MI355X: a world-size-1 "nccl" process group with forced collectives runs
-the real RCCL all-reduce path (bf16 wire buckets, in-order launch, unpack) eagerly and captured in
-a hipGraph, and both agree with the no-comm step (an all-reduce over one rank is the identity up to
-the bf16 wire rounding). Multi-GPU rings are the driver's 8-GPU run; this pins the code path.
+"""MWMS over tfk_comm (the runtime's own RCCL communicator) on one MI355X: a world-size-1
+communicator with forced collectives runs the real RCCL all-reduce path (bf16 wire buckets,
+in-order launch on the comm stream, unpack) eagerly and captured in a hipGraph -- with the
+weight-gradient side streams active in BOTH modes -- and both agree with the no-comm step (an
+all-reduce over one rank is the identity up to the bf16 wire rounding). Multi-GPU rings are the
+driver's 8-GPU run; this pins the code path the N-GPU bench replays.
 Reference behaviour: SURVEY §2 D4 (MWMS), D6 (graph executor)."""
 import os
 import subprocess
@@ -9,25 +11,29 @@ import sys
 
 import pytest
 
-from conftest import ROOT, free_port
+from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
 SCRIPT = r"""
 import os, sys, json, torch, torch.distributed as dist
+os.environ["TFK_CONCURRENT_WGRAD"] = "1"   # side-stream weight gradients in eager steps too
 sys.path.insert(0, os.environ["TFK_ROOT"])
 from tensorflow_k8s_amd.models.resnet import ResNet, synthetic_imagenet
+from tensorflow_k8s_amd.parallel import tfk_comm
 from tensorflow_k8s_amd.parallel.mwms import MultiWorkerMirroredStrategy
+from tensorflow_k8s_amd.runtime import streams
 from tensorflow_k8s_amd.runtime.optimizer import SGD
 from tensorflow_k8s_amd.runtime.trainer import StepRunner
+assert streams.MODE == "1"
 dev = torch.device("cuda", 0); torch.cuda.set_device(dev)
-dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + os.environ["TFK_PORT"], rank=0, world_size=1,
-                        device_id=dev)
+comm = tfk_comm.init(dist.HashStore(), 0, 1, dev)
 out = {}
 for mode in ("nocomm", "eager", "graph"):
     m = ResNet(50, stages=[1, 1, 1, 1], num_classes=100).to(dev, seed=7)
     opt = SGD(m.arena, lr=0.05, momentum=0.9)
-    s = MultiWorkerMirroredStrategy(m.arena, bucket_mb=2.0, comm_dtype="bf16", force=mode != "nocomm")
+    s = MultiWorkerMirroredStrategy(m.arena, comm=comm if mode != "nocomm" else None, bucket_mb=2.0,
+                                    comm_dtype="bf16", force=mode != "nocomm")
     s.configure_optimizer(opt)
     s.broadcast_parameters()
     x, y = synthetic_imagenet(16, dev, num_classes=100, seed=3)
@@ -35,16 +41,16 @@ for mode in ("nocomm", "eager", "graph"):
     for _ in range(6):
         r.step()
     torch.cuda.synchronize()
-    out[mode] = {"loss": r.last_loss(), "buckets": len(s.buckets), "enabled": s.enabled,
+    out[mode] = {"loss": r.last_loss(), "buckets": len(s.buckets), "enabled": s.enabled, "side": len(streams._side),
                  "w": m.arena.master.double().sum().item(), "wabs": m.arena.master.abs().double().sum().item()}
     torch.save(m.arena.master.cpu(), os.environ["TFK_OUT"] + "." + mode)
-dist.destroy_process_group()
+tfk_comm.shutdown()
 print(json.dumps(out))
 """
 
 
 def test_rccl_mwms_eager_and_graph_match_nocomm(tmp_path):
-    env = dict(os.environ, TFK_ROOT=ROOT, TFK_PORT=str(free_port()), TFK_OUT=str(tmp_path / "w"))
+    env = dict(os.environ, TFK_ROOT=ROOT, TFK_OUT=str(tmp_path / "w"))
     r = subprocess.run([sys.executable, "-c", SCRIPT], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     import json
@@ -53,6 +59,7 @@ def test_rccl_mwms_eager_and_graph_match_nocomm(tmp_path):
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["eager"]["enabled"] and out["graph"]["enabled"] and not out["nocomm"]["enabled"]
     assert out["eager"]["buckets"] > 3
+    assert out["eager"]["side"] >= 1  # the eager run really forked weight gradients onto side streams
     ref = torch.load(str(tmp_path / "w.nocomm"), weights_only=True)
     for mode in ("eager", "graph"):
         w = torch.load(str(tmp_path / f"w.{mode}"), weights_only=True)

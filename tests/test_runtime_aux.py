@@ -47,8 +47,41 @@ def test_watchdog_default_exits_retryable(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
     assert r.returncode == EXIT_RETRY, r.stderr
     assert "watchdog" in term.read_text()
-    ev = json.loads(r.stdout.strip().splitlines()[-1])
-    assert ev["kind"] == "watchdog"
+    evs = [json.loads(l) for l in r.stdout.strip().splitlines() if l.startswith("{")]
+    assert evs[0]["kind"] == "watchdog"
+    assert evs[-1] == {"event": "comm_aborted", "communicators": 0}
+
+
+def test_watchdog_aborts_live_communicators_then_exits_143(tmp_path):
+    """The watchdog path tears the rank's communicators down before exiting: every communicator
+    registered with tfk_comm (RcclComm registers itself at construction) gets abort() -- the
+    ncclCommAbort of the native binding -- and the process exits with the retryable 143. Here the
+    registered communicators are stand-ins that record the call (no GPU in the CPU tier); the
+    native abort itself is exercised on the MI355X by tests/test_tfk_comm_gpu.py."""
+    mark = tmp_path / "aborted"
+    code = f"""
+import time
+from tensorflow_k8s_amd.parallel import tfk_comm
+from tensorflow_k8s_amd.runtime.watchdog import StepWatchdog
+class Stub:
+    def __init__(self, name): self.name = name
+    def abort(self):
+        with open({str(mark)!r}, "a") as f: f.write(self.name + "\\n")
+        return True
+keep = [Stub("world"), Stub("ps0/reduce")]
+for c in keep: tfk_comm._LIVE.add(c)
+w = StepWatchdog(0.3, poll_s=0.02).start()
+for step in range(3):      # progress, then a 'hung collective'
+    w.beat(step); time.sleep(0.05)
+time.sleep(10)
+"""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == EXIT_RETRY, r.stderr
+    assert sorted(mark.read_text().split()) == ["ps0/reduce", "world"]
+    evs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert evs[0]["kind"] == "watchdog" and evs[0]["step"] == 2
+    assert evs[-1] == {"event": "comm_aborted", "communicators": 2}
 
 
 def test_tracer_chrome_trace(tmp_path):

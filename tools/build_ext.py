@@ -109,6 +109,9 @@ def build_kernels(jobs: int | None = None, verbose: bool = False) -> str:
         tlib = [p for p in libs if "torch" in p][0]
         cmd = ["g++", "-shared", "-o", so] + objs + [f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
                                                      "-ltorch_hip", "-ltorch_python", "-lamdhip64",
+                                                     # torch's own librccl.so (SONAME librccl.so.1): one RCCL
+                                                     # instance in the process, shared with torch.distributed
+                                                     "-lrccl",
                                                      f"-Wl,-rpath,{tlib}"]
         _run(cmd)
     if verbose:

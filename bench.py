@@ -57,7 +57,9 @@ def main():
         # one pod per GPU (HIP_VISIBLE_DEVICES pinned by the kubelet): the world comes from TF_CONFIG
         from tensorflow_k8s_amd.parallel import cluster
         info = cluster.resolve()
-        world, rank, local = info.world_size, info.rank, 0
+        # TFK_LOCAL_DEVICE: this pod's GPU within the visible list (gang-visible pods see all the
+        # gang's GPUs, so RCCL can reach its peers over xGMI P2P/IPC)
+        world, rank, local = info.world_size, info.rank, int(os.environ.get("TFK_LOCAL_DEVICE", "0"))
     if args.gpus > 1 and world == 1:
         sys.exit("for --gpus > 1 launch with: python -m torch.distributed.run --nproc-per-node N "
                  "--master-addr 127.0.0.1 bench.py --gpus N")
@@ -211,7 +213,9 @@ def run_via_operator(args) -> int:
     specs = {"Chief": rs(1)}
     if n > 1:
         specs["Worker"] = rs(n - 1)
-    job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": f"bench-{args.model}", "namespace": "default"},
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob",
+           "metadata": {"name": f"bench-{args.model}", "namespace": "default",
+                        "annotations": {"scheduling.tfk.io/gang-visible-gpus": "true"}},
            "spec": {"tfReplicaSpecs": specs, "runPolicy": {"backoffLimit": 0, "cleanPodPolicy": "None"}}}
     with LocalCluster(gpus=n, root_dir=tempfile.mkdtemp(prefix="tfk-bench-")) as c:
         c.client.create(job)

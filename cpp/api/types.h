@@ -22,6 +22,11 @@ constexpr const char* kSingular = "tfjob";
 constexpr const char* kShortName = "tfj";
 constexpr const char* kContainerName = "tensorflow";
 constexpr const char* kPortName = "tfjob-port";
+// TFJob/pod annotation (any non-empty value): the gang scheduler records the union of the gang's
+// GPU ids on a node (tfk.io/gang-gpu-ids) and the kubelet exposes all of them to every member pod
+// with TFK_LOCAL_DEVICE = the pod's own index in that list (RCCL then finds its peers for P2P/IPC).
+constexpr const char* kGangVisibleGpus = "scheduling.tfk.io/gang-visible-gpus";
+constexpr const char* kGangGpuIds = "tfk.io/gang-gpu-ids";
 constexpr int kDefaultPort = 2222;
 constexpr const char* kFinalizer = "tfjob.kubeflow.org/cleanup";
 constexpr const char* kGPUResource = "amd.com/gpu";

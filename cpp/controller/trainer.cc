@@ -137,6 +137,10 @@ Json Trainer::make_pod(const api::TFJob& job, RType t, int index, int generation
   md["annotations"]["scheduling.tfk.io/min-available"] = std::to_string(min_avail);
   md["annotations"]["tfk.io/restart-generation"] = std::to_string(generation);
   md["annotations"]["tfk.io/world"] = world_signature(job);
+  // opt-in (TFJob annotation): every gang member sees all of the gang's GPUs, so RCCL between the
+  // pods of one node rides xGMI peer-to-peer (IPC) instead of falling back to host shared memory
+  const Json& gv = job.metadata.path("annotations").at(api::kGangVisibleGpus);
+  if (gv.is_string() && !gv.str().empty()) md["annotations"][api::kGangVisibleGpus] = gv.str();
   md["ownerReferences"] = Json(Json::array_t{api::as_owner(job)});
   pod["metadata"] = md;
   Json spec = tmpl.at("spec").is_object() ? tmpl.at("spec").clone() : Json::object();

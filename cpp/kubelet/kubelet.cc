@@ -1,5 +1,7 @@
 #include "kubelet.h"
 
+#include "../api/types.h"
+
 #include <dirent.h>
 #include <sched.h>
 #include <fcntl.h>
@@ -200,7 +202,21 @@ void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
     env[e.at("name").str()] = v;
   }
   std::string gpu_ids = pr.pod.path("metadata.annotations").at("tfk.io/gpu-ids").str();
-  if (!gpu_ids.empty()) env["HIP_VISIBLE_DEVICES"] = gpu_ids;
+  std::string gang_ids = pr.pod.path("metadata.annotations").at(api::kGangGpuIds).str();
+  if (!gang_ids.empty() && !gpu_ids.empty()) {
+    // gang-visible: the pod sees every GPU of its gang on this node; its own device is
+    // TFK_LOCAL_DEVICE (index of its first assigned GPU in the visible list)
+    auto vis = split(gang_ids, ',');
+    std::string own = split(gpu_ids, ',')[0];
+    int local = 0;
+    for (size_t i = 0; i < vis.size(); ++i)
+      if (vis[i] == own) local = (int)i;
+    env["HIP_VISIBLE_DEVICES"] = gang_ids;
+    env["TFK_LOCAL_DEVICE"] = std::to_string(local);
+  } else if (!gpu_ids.empty()) {
+    env["HIP_VISIBLE_DEVICES"] = gpu_ids;
+    env["TFK_LOCAL_DEVICE"] = "0";
+  }
   // NUMA-local CPUs of the pod's GPUs (built here: the child only calls sched_setaffinity)
   std::vector<int> gids;
   for (auto& x : split(gpu_ids, ','))

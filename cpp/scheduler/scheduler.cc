@@ -1,5 +1,7 @@
 #include "scheduler.h"
 
+#include "../api/types.h"
+
 #include <algorithm>
 #include <climits>
 
@@ -209,6 +211,12 @@ int GangScheduler::schedule_once() {
       }
       continue;
     }
+    // gang-visible opt-in: the union of this gang's GPUs per node (sorted), recorded on each member
+    std::map<std::string, std::set<int>> gang_gpus;
+    for (auto& p : kv.second) {
+      auto& pl = plan[p.path("metadata.namespace").str() + "/" + p.path("metadata.name").str()];
+      gang_gpus[pl.first].insert(pl.second.begin(), pl.second.end());
+    }
     for (auto& p : kv.second) {
       std::string k = p.path("metadata.namespace").str() + "/" + p.path("metadata.name").str();
       auto& pl = plan[k];
@@ -217,6 +225,12 @@ int GangScheduler::schedule_once() {
       std::string ids;
       for (size_t i = 0; i < pl.second.size(); ++i) ids += (i ? "," : "") + std::to_string(pl.second[i]);
       next["metadata"]["annotations"]["tfk.io/gpu-ids"] = ids;
+      const Json& gv = p.path("metadata.annotations").at(api::kGangVisibleGpus);
+      if (gv.is_string() && !gv.str().empty() && gv.str() != "false") {
+        std::string all;
+        for (int g : gang_gpus[pl.first]) all += (all.empty() ? "" : ",") + std::to_string(g);
+        next["metadata"]["annotations"][api::kGangGpuIds] = all;
+      }
       Json out;
       ApiStatus st = client_->update("pods", p.path("metadata.namespace").str(), next, &out);
       if (st.ok()) {

@@ -44,6 +44,17 @@ def abort_all() -> int:
     return n
 
 
+def exchange_unique_id(store, rank: int, tag: str, make_uid, timeout_s: float = 300.0) -> bytes:
+    """Rank 0 draws the communicator's unique id and publishes it under ``tfk_comm/<tag>/uid`` in the
+    job store; every other rank waits for the key and reads it."""
+    key = f"tfk_comm/{tag}/uid"
+    if rank == 0:
+        store.set(key, make_uid())
+    else:
+        store.wait([key], datetime.timedelta(seconds=timeout_s))
+    return bytes(store.get(key))
+
+
 class _StreamHandle:
     """Completion of an RCCL call on the comm stream; wait() = the caller's stream waits on it."""
     __slots__ = ("event",)
@@ -99,12 +110,7 @@ class RcclComm:
                    timeout_s: float = 300.0) -> "RcclComm":
         """Chief publishes the unique id under ``tfk_comm/<tag>/uid``; all ranks init."""
         from .. import _C
-        key = f"tfk_comm/{tag}/uid"
-        if rank == 0:
-            store.set(key, _C.rccl_unique_id())
-        else:
-            store.wait([key], datetime.timedelta(seconds=timeout_s))
-        uid = bytes(store.get(key))
+        uid = exchange_unique_id(store, rank, tag, _C.rccl_unique_id, timeout_s)
         native = _C.RcclComm(uid, world, rank, device.index if device.index is not None else torch.cuda.current_device())
         return cls(native, device, tag)
 

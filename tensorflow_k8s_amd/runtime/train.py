@@ -129,7 +129,10 @@ def pick_device(args, info) -> torch.device:
         return torch.device("cpu")
     if not torch.cuda.is_available():
         raise SystemExit("--device cuda but no GPU is visible")
-    local = int(os.environ.get("LOCAL_RANK", "0")) if info.source == "torchrun" else 0
+    # torchrun: LOCAL_RANK; a TFJob pod: TFK_LOCAL_DEVICE (its GPU in the visible list -- all of the
+    # gang's GPUs under the gang-visible-gpus opt-in, else just its own)
+    local = int(os.environ.get("LOCAL_RANK", "0")) if info.source == "torchrun" else \
+        int(os.environ.get("TFK_LOCAL_DEVICE", "0"))
     torch.cuda.set_device(local)
     return torch.device("cuda", local)
 

@@ -171,3 +171,43 @@ def test_configure_rccl_env(monkeypatch):
     assert comm.configure_rccl("Ring")["NCCL_ALGO"] == "Tree"
     with pytest.raises(ValueError):
         comm.configure_rccl("Butterfly")
+
+
+TORCHRUN_SCRIPT = r"""
+import hashlib, json, os, sys, torch
+from tensorflow_k8s_amd.parallel import tfk_comm
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+store = tfk_comm.env_store(rank, world, timeout_s=60)
+uid = tfk_comm.exchange_unique_id(store, rank, "world", lambda: os.urandom(128), 60)
+c = tfk_comm.init(store, rank, world, torch.device("cpu"), 60)
+x = torch.full((8,), float(rank + 1)); c.all_reduce(x)
+mx = torch.tensor([float(rank)]); c.all_reduce(mx, op="max")
+g = torch.zeros(world); c.all_gather(g, torch.tensor([float(rank * 10)]))
+sub = c.split([0, 1], "pair"); y = torch.ones(3)
+assert (sub is None) == (rank == 2)  # non-members get no sub-communicator
+if sub is not None:
+    sub.all_reduce(y)
+c.barrier()
+print(json.dumps({"rank": rank, "uid": hashlib.sha1(uid).hexdigest(), "sum": x[0].item(), "max": mx.item(),
+                  "gather": g.tolist(), "sub": y[0].item(), "backend": c.backend}), flush=True)
+tfk_comm.shutdown()
+"""
+
+
+def test_tfk_comm_bootstrap_under_torchrun(tmp_path):
+    """bench.py's N-GPU bootstrap path on the CPU tier: under torchrun (the driver's launcher, whose
+    agent hosts the store) every rank reaches the launcher's TCP store through env://, rank 0's
+    unique id reaches all ranks unchanged, and the world communicator's collectives and a split
+    sub-communicator work at world size 3."""
+    script = tmp_path / "boot.py"
+    script.write_text(TORCHRUN_SCRIPT)
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    r = subprocess.run([PY, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
+                        "127.0.0.1", "--master-port", str(free_port()), str(script)], env=env, capture_output=True,
+                       text=True, timeout=240, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rows = sorted((json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"rank"')), key=lambda d: d["rank"])
+    assert len(rows) == 3 and len({d["uid"] for d in rows}) == 1
+    for d in rows:
+        assert d["sum"] == 6.0 and d["max"] == 2.0 and d["gather"] == [0.0, 10.0, 20.0] and d["backend"] == "gloo"
+    assert [d["sub"] for d in rows] == [2.0, 2.0, 1.0]

@@ -107,3 +107,34 @@ def test_numa_packed_gang_and_cpu_pinning(tmp_path, control_plane_bin):
             out = [json.loads(l) for l in c.logs(pod).splitlines() if l.startswith("{")][-1]
             assert set(out["aff"]) == dom1, out
             assert out["env"] == ",".join(str(x) for x in sorted(dom1))
+
+
+PRINT_VIS = ["python3", "-c", "import os, json; print(json.dumps({'gpus': os.environ.get('HIP_VISIBLE_DEVICES'), "
+             "'local': os.environ.get('TFK_LOCAL_DEVICE')}))"]
+
+
+def test_gang_visible_gpus_opt_in(tmp_path, control_plane_bin):
+    """With the TFJob annotation scheduling.tfk.io/gang-visible-gpus, every gang member sees ALL of
+    the gang's GPUs on the node (so RCCL between the pods can use xGMI P2P/IPC) and TFK_LOCAL_DEVICE
+    names its own one; without it a pod sees only its own GPU (local device 0)."""
+    with LocalCluster(gpus=4, root_dir=str(tmp_path / "c")) as cl:
+        c = cl.client
+        job = _job("vis", {"Chief": _rs(1, PRINT_VIS), "Worker": _rs(2, PRINT_VIS)})
+        job["metadata"]["annotations"] = {"scheduling.tfk.io/gang-visible-gpus": "true"}
+        c.create(job)
+        c.create(_job("iso", {"Chief": _rs(1, PRINT_VIS)}))
+        for n in ("vis", "iso"):
+            assert tfjob_condition(c.wait_tfjob(n, timeout=90)) == "Succeeded", n
+        own, seen = [], set()
+        for pod in ("vis-chief-0", "vis-worker-0", "vis-worker-1"):
+            an = c.get("pods", pod)["metadata"]["annotations"]
+            out = [json.loads(l) for l in c.logs(pod).splitlines() if l.startswith("{")][-1]
+            vis = out["gpus"].split(",")
+            assert out["gpus"] == an["tfk.io/gang-gpu-ids"] and len(vis) == 3, (pod, out, an)
+            assert vis[int(out["local"])] == an["tfk.io/gpu-ids"], (pod, out, an)
+            own.append(an["tfk.io/gpu-ids"])
+            seen.add(out["gpus"])
+        assert len(set(own)) == 3 and len(seen) == 1  # disjoint own GPUs, one shared visible list
+        an = c.get("pods", "iso-chief-0")["metadata"]["annotations"]
+        out = [json.loads(l) for l in c.logs("iso-chief-0").splitlines() if l.startswith("{")][-1]
+        assert "tfk.io/gang-gpu-ids" not in an and out == {"gpus": an["tfk.io/gpu-ids"], "local": "0"}

@@ -89,6 +89,8 @@ def main():
 
     is_cnn = args.model.startswith("resnet")
     model = build_model(args.model, **({"fp8": True} if args.fp8 else {})).to(dev)
+    if hasattr(model, "rng_stream"):
+        model.rng_stream = rank  # each replica draws its own dropout masks
     if is_cnn:
         opt = SGD(model.arena, lr=0.1 * args.batch * world / 256, momentum=0.9, weight_decay=5e-5)
         opt_name = "SGD momentum 0.9 (fused HIP)"

@@ -22,6 +22,9 @@ int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_quant_t(const void*, void*, void*, int, int, hipStream_t);
 int tfk_mx_probe(const int*, const int*, const int*, const int*, float*, hipStream_t);
 int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, hipStream_t s);
+const unsigned long long* tfk_seed_key();
+void tfk_set_seed_key(const unsigned long long* k);
+int tfk_rng_advance(unsigned long long* st, unsigned long long stream, hipStream_t s);
 int tfk_bn_finalize(float*, int, int, float, const float*, const float*, float, float, float*, float*, float*, float*,
                     float*, float*, hipStream_t);
 int tfk_bn_stats(const void*, long long, int, float*, int, hipStream_t);
@@ -207,6 +210,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   p.drop_p = (float)drop_p;
   p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
   p.drop_seed = (unsigned long long)drop_seed;
+  p.drop_seed_key = tfk_seed_key();
   const bool dense_a = amode == A_KIN || amode == A_KOUT;
   // the conv-fwd-gather / wgrad-gather 256x256 tiles and the 64x128 tile exist on the LDS-DMA engine
   // (gemm_g4.hip) only; the launcher falls back to 128x128 where that engine declines the shape
@@ -317,6 +321,7 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
   p.drop_p = (float)drop_p;
   p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
   p.drop_seed = (unsigned long long)drop_seed;
+  p.drop_seed_key = tfk_seed_key();
   if (dact_src.has_value() && dact_src->defined()) {
     need_bf16(*dact_src, "dact_src"); need_numel(*dact_src, (long long)M * N, "dact_src");
     TORCH_CHECK(dact >= 1 && dact <= 3, "dact");
@@ -634,6 +639,25 @@ void act_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor dx, int act) {
   need_numel(x, dy.numel(), "x"); need_numel(dx, dy.numel(), "dx");
   check_rc(tfk_act_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), dy.numel(), act, cur_stream()), "act_bwd");
 }
+// rng state of a model: int64 [counter, key]. set_rng_key registers &state[1] as the per-step key
+// every dropout-capable launch adds to its salt (None: unregister); rng_advance steps it on device.
+void set_rng_key(c10::optional<torch::Tensor> st) {
+  if (!st.has_value() || !st->defined()) {
+    tfk_set_seed_key(nullptr);
+    return;
+  }
+  need(*st, at::kLong, "rng state");
+  need_numel(*st, 2, "rng state");
+  tfk_set_seed_key(reinterpret_cast<const unsigned long long*>(st->data_ptr<int64_t>()) + 1);
+}
+void rng_advance(torch::Tensor st, int64_t stream) {
+  need(st, at::kLong, "rng state");
+  need_numel(st, 2, "rng state");
+  check_rc(tfk_rng_advance(reinterpret_cast<unsigned long long*>(st.data_ptr<int64_t>()), (unsigned long long)stream,
+                           cur_stream()),
+           "rng_advance");
+}
+
 void dropout(torch::Tensor x, torch::Tensor y, double p, int64_t seed) {
   need_bf16(x, "x"); need_bf16(y, "y"); need_numel(y, x.numel(), "y");
   check_rc(tfk_dropout(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (unsigned long long)seed, cur_stream()), "dropout");
@@ -695,6 +719,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("dropout", &dropout);
+  m.def("set_rng_key", &set_rng_key);
+  m.def("rng_advance", &rng_advance);
   m.def("add", &add);
   register_transformer_ops(m);
   register_ckpt_ops(m);

@@ -38,7 +38,8 @@ struct AttnParams {
   float scale;
   int causal;
   float p_drop;
-  unsigned long long seed;
+  unsigned long long seed;         // per-site salt
+  const unsigned long long* seed_key;  // per-step device key (common.h eff_seed) or null
 };
 
 __device__ __forceinline__ f32x4 mfma(bf16x8 x, bf16x8 y, f32x4 c) {
@@ -110,7 +111,8 @@ __device__ __forceinline__ bf16x8 pack2(const f32x4& a, const f32x4& b) {
 // keep iff the element's 24-bit uniform >= p_drop; element index q*Sk + key of head (b, h), the
 // seed folded with the head index (ops/transformer.py dropout_keep_mask is the bit-exact reference)
 __device__ __forceinline__ uint32_t head_seed(const AttnParams& p, int bh) {
-  return hash32((uint32_t)p.seed ^ (uint32_t)(p.seed >> 32) ^ ((uint32_t)bh * 0x9E3779B9u));
+  const unsigned long long s = eff_seed(p.seed, p.seed_key);
+  return hash32((uint32_t)s ^ (uint32_t)(s >> 32) ^ ((uint32_t)bh * 0x9E3779B9u));
 }
 __device__ __forceinline__ bool keep_elem(const AttnParams& p, uint32_t hs, int q, int key) {
   return u01(hash32(hs ^ (uint32_t)(q * p.Sk + key))) >= p.p_drop;
@@ -421,7 +423,7 @@ int tfk_attn_fwd(const void* q, const void* k, const void* v, void* out, float* 
   p.B = (int)shape[0]; p.H = (int)shape[1]; p.Sq = (int)shape[2]; p.Sk = (int)shape[3];
   p.q_bs = strides[0]; p.q_rs = (int)strides[1]; p.k_bs = strides[2]; p.k_rs = (int)strides[3];
   p.v_bs = strides[4]; p.v_rs = (int)strides[5]; p.o_bs = strides[6]; p.o_rs = (int)strides[7];
-  p.kv_len = kv_len; p.scale = scale; p.causal = causal; p.p_drop = p_drop; p.seed = seed;
+  p.kv_len = kv_len; p.scale = scale; p.causal = causal; p.p_drop = p_drop; p.seed = seed; p.seed_key = tfk_seed_key();
   if (attn_waves() == 8) {
     hipLaunchKernelGGL(attn_fwd_kernel<8>, dim3((p.Sq + 127) / 128, p.H, p.B), dim3(512), 0, s, p);
   } else {
@@ -442,7 +444,7 @@ int tfk_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
   p.v_bs = strides[4]; p.v_rs = (int)strides[5]; p.o_bs = strides[6]; p.o_rs = (int)strides[7];
   p.dq_bs = gstrides[0]; p.dq_rs = (int)gstrides[1]; p.dk_bs = gstrides[2]; p.dk_rs = (int)gstrides[3];
   p.dv_bs = gstrides[4]; p.dv_rs = (int)gstrides[5];
-  p.kv_len = kv_len; p.scale = scale; p.causal = causal; p.p_drop = p_drop; p.seed = seed;
+  p.kv_len = kv_len; p.scale = scale; p.causal = causal; p.p_drop = p_drop; p.seed = seed; p.seed_key = tfk_seed_key();
   const long long n = (long long)p.B * p.H * p.Sq;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, s, p);
   if (attn_waves() == 8) {

@@ -101,6 +101,15 @@ __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
   return (uint32_t)x;
 }
 __device__ __forceinline__ float u01(uint32_t h) { return (h >> 8) * (1.0f / 16777216.0f); }
+
+// Dropout seeds = host per-site salt + a per-step device key. The key (a model's rng state
+// [counter, key], advanced on the device at the start of every training step by rng_advance) makes
+// masks change per step INSIDE a replayed hipGraph; the salt separates the sites of one step. The
+// launchers pick up the key pointer registered by tfk_set_seed_key (null: salt only).
+__device__ __forceinline__ unsigned long long eff_seed(unsigned long long salt, const unsigned long long* key) {
+  return key ? salt + *key : salt;
+}
+extern "C" const unsigned long long* tfk_seed_key();
 // 32-bit integer hash ("lowbias32": 2 multiplies, 3 xor-shifts, all 32-bit) for the per-element
 // attention-dropout masks, which are regenerated in every attention pass: the 64-bit hash_u32
 // above costs ~35 VALU ops per element there and was the largest cost of the dropout passes.

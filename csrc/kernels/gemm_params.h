@@ -45,7 +45,8 @@ struct GemmParams {
   // inverted dropout after the activation, before the residual add; mask = hash(seed, m*N + n),
   // identical to misc.hip's dropout kernel on the contiguous [M][N] output (backward regenerates it)
   float drop_p, drop_scale;
-  unsigned long long drop_seed;
+  unsigned long long drop_seed;            // per-site salt
+  const unsigned long long* drop_seed_key; // per-step device key (common.h eff_seed) or null
   // MX-fp8 engine (fp8.hip): e8m0 block scales, [rows][K/32] bytes, one per 32 K-elements
   const void* a_scale;
   const void* b_scale;

@@ -197,8 +197,9 @@ __global__ void act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restri
 
 // Inverted dropout; mask regenerated from (seed, index) in backward -> no mask tensor stored.
 __global__ void dropout_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long long n, float p,
-                               unsigned long long seed) {
+                               unsigned long long salt, const unsigned long long* __restrict__ key) {
   const float keep = 1.f - p, inv = 1.f / keep;
+  const unsigned long long seed = eff_seed(salt, key);
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
     bool k = u01(hash_u32(seed, i)) < keep;
     y[i] = f2bf(k ? bf2f(x[i]) * inv : 0.f);
@@ -208,8 +209,9 @@ __global__ void dropout_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
 // Same mask and arithmetic, 8 elements (16 B) per lane: n % 8 == 0, 16-B aligned x / y. The scalar
 // form moved one bf16 per lane per iteration (19 us for a 16 MB Transformer-big residual gradient).
 __global__ void dropout8_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long long n8, float p,
-                                unsigned long long seed) {
+                                unsigned long long salt, const unsigned long long* __restrict__ key) {
   const float keep = 1.f - p, inv = 1.f / keep;
+  const unsigned long long seed = eff_seed(salt, key);
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long long)gridDim.x * NT) {
     const bf16x8 v = *(const bf16x8*)(x + i * 8);
     bf16x8 o;
@@ -316,12 +318,31 @@ int tfk_act_bwd(const bf16* dy, const bf16* x, bf16* dx, long long n, int act, h
   hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(NT), 0, s, dy, x, dx, n, act);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+// rng state [counter, key] (int64): counter += 1; key = splitmix64(counter ^ stream). One lane.
+__global__ void rng_advance_kernel(unsigned long long* st, unsigned long long stream) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const unsigned long long c = st[0] + 1;
+    unsigned long long z = (c ^ stream) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    st[0] = c;
+    st[1] = z ^ (z >> 31);
+  }
+}
+
+static const unsigned long long* g_seed_key = nullptr;
+const unsigned long long* tfk_seed_key() { return g_seed_key; }
+void tfk_set_seed_key(const unsigned long long* k) { g_seed_key = k; }
+int tfk_rng_advance(unsigned long long* st, unsigned long long stream, hipStream_t s) {
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(64), 0, s, st, stream);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 int tfk_dropout(const bf16* x, bf16* y, long long n, float p, unsigned long long seed, hipStream_t s) {
   if ((n & 7) == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
-    hipLaunchKernelGGL(dropout8_kernel, dim3(grid_for(n / 8)), dim3(NT), 0, s, x, y, n / 8, p, seed);
+    hipLaunchKernelGGL(dropout8_kernel, dim3(grid_for(n / 8)), dim3(NT), 0, s, x, y, n / 8, p, seed, tfk_seed_key());
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
-  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n, p, seed);
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n, p, seed, tfk_seed_key());
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_add(const bf16* a, const bf16* b, bf16* y, long long n, float alpha, float beta, hipStream_t s) {

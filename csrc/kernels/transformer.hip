@@ -72,8 +72,10 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
                                                     const float* __restrict__ rstd, const bf16* __restrict__ dres,
                                                     bf16* __restrict__ dx, float* __restrict__ dgamma,
                                                     float* __restrict__ dbeta, int M, int W, bf16* __restrict__ dxd,
-                                                    float drop_p, unsigned long long drop_seed) {
+                                                    float drop_p, unsigned long long drop_salt,
+                                                    const unsigned long long* __restrict__ drop_key) {
   extern __shared__ float red[];  // [NT/64][2][W]
+  const unsigned long long drop_seed = eff_seed(drop_salt, drop_key);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nch = W >> 3;
   float dg[CPL][8], db[CPL][8], gm[CPL][8];
@@ -278,13 +280,13 @@ int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const f
   const size_t sh = (size_t)(NT / 64) * 2 * W * sizeof(float);
   if (cpl <= 1)
     hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
-                       dxd, drop_p, drop_seed);
+                       dxd, drop_p, drop_seed, tfk_seed_key());
   else if (cpl <= 2)
     hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
-                       dxd, drop_p, drop_seed);
+                       dxd, drop_p, drop_seed, tfk_seed_key());
   else if (cpl <= 4)
     hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
-                       dxd, drop_p, drop_seed);
+                       dxd, drop_p, drop_seed, tfk_seed_key());
   else return -3;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -11,7 +11,8 @@ tanh pooler. MI355X mapping:
   the FFN1 epilogue (aux) and its derivative is applied in the FFN2 dgrad epilogue (dact);
 * flash attention (MFMA, online softmax, dropout regenerated from a hash in backward);
 * vocab padded to a multiple of 64 rows (padding rows stay zero, loss masks them).
-Dropout seeds are derived per (step, layer, site) on the host, so every mask is reproducible.
+Dropout seeds = per-(layer, site) host salt + a per-step key kept and advanced on the device, so
+every mask is reproducible and a hipGraph-captured step draws fresh masks on every replay.
 """
 from __future__ import annotations
 
@@ -132,6 +133,12 @@ class BertForPreTraining:
         self.step = 0
         W, std = cfg.hidden, cfg.init_std
         a = self.arena = ParamArena()
+        # dropout RNG: int64 [counter, key] on the device, advanced INSIDE every training step
+        # (hipGraph-replayable); kernels use seed = per-site host salt + key (ops.elementwise.rng_key).
+        # A checkpointed buffer, so a resumed job continues the mask sequence; rng_stream (e.g. the
+        # data-parallel rank) gives each replica its own masks.
+        self.rng_state = a.add_buffer("tfk/dropout_rng_state", torch.zeros(2, dtype=torch.int64))
+        self.rng_stream = 0
         # registration order = forward order (the arena reverses it so backward fills grads front-to-back)
         self.word = Embedding(a, "bert/embeddings/word_embeddings", cfg.vocab_size, W, std)
         self.pos = Embedding(a, "bert/embeddings/position_embeddings", cfg.max_position, W, std)
@@ -195,8 +202,10 @@ class BertForPreTraining:
         """One training step's forward + backward (see _forward_backward). The no-decay gradients
         (biases, LayerNorm gamma/beta) are zeroed in one fill up front and accumulated by their kernels."""
         self.arena.zero_nodecay_grads()
+        E.rng_advance(self.rng_state, self.rng_stream)
         try:
-            return self._forward_backward(ids, tt, mlm_pos, mlm_ids, nsp_labels, loss_scale)
+            with E.rng_key(self.rng_state):
+                return self._forward_backward(ids, tt, mlm_pos, mlm_ids, nsp_labels, loss_scale)
         finally:
             self.arena.prezeroed = False
 
@@ -207,7 +216,7 @@ class BertForPreTraining:
         S = ids.numel() // B
         P = mlm_pos.shape[1]
         self.step += 1
-        seed = _mix(0xBE27, self.step)
+        seed = 0xBE27  # salt base; the per-step part is the device key (rng_state)
         h, emb_saved = self._encode(ids, tt, B, S, None, seed)
         logits, nsp_logits, hs = self._heads(h, B, S, mlm_pos)
         rows, hm, zt, t, tl, stt, cls_rows, hc, zp, pooled = hs

@@ -230,6 +230,12 @@ class Transformer:
         self.step = 0
         W = cfg.hidden
         a = self.arena = ParamArena()
+        # dropout RNG: int64 [counter, key] on the device, advanced INSIDE every training step
+        # (hipGraph-replayable); kernels use seed = per-site host salt + key (ops.elementwise.rng_key).
+        # A checkpointed buffer, so a resumed job continues the mask sequence; rng_stream (e.g. the
+        # data-parallel rank) gives each replica its own masks.
+        self.rng_state = a.add_buffer("tfk/dropout_rng_state", torch.zeros(2, dtype=torch.int64))
+        self.rng_stream = 0
         self.emb = Embedding(a, f"transformer/symbol_modality_{cfg.vocab_size}_{W}/shared/weights", cfg.vocab_size, W,
                              std=W ** -0.5)
         self.enc = [EncoderLayer(a, cfg, f"transformer/body/encoder/layer_{i}") for i in range(cfg.enc_layers)]
@@ -276,8 +282,10 @@ class Transformer:
         """One training step's forward + backward (see _forward_backward). The no-decay gradients
         (biases, LayerNorm gamma/beta) are zeroed in one fill up front and accumulated by their kernels."""
         self.arena.zero_nodecay_grads()
+        E.rng_advance(self.rng_state, self.rng_stream)
         try:
-            return self._forward_backward(src, tgt_in, tgt_out, src_len, loss_scale)
+            with E.rng_key(self.rng_state):
+                return self._forward_backward(src, tgt_in, tgt_out, src_len, loss_scale)
         finally:
             self.arena.prezeroed = False
 
@@ -286,7 +294,7 @@ class Transformer:
         B = src_len.shape[0]
         Ss, St = src.numel() // B, tgt_in.numel() // B
         self.step += 1
-        seed = _mix(0x7EA, self.step)
+        seed = 0x7EA  # salt base; the per-step part is the device key (rng_state)
         tr = self.training
         logits, (x, mem, st_m, y, yo, st_y) = self._forward(src, tgt_in, src_len, B, Ss, St, seed, tr)
         loss, dlogits, corr = softmax_xent(logits, tgt_out, smoothing=cfg.label_smoothing,

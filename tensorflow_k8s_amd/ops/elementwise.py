@@ -5,6 +5,8 @@ the remaining producers. act: None | "relu" | "gelu" (tanh form, as TF's gelu(ap
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 
 from ._lib import lib, on_gpu
@@ -38,6 +40,50 @@ def u01(h: torch.Tensor) -> torch.Tensor:
     return (h >> 8).float() * (1.0 / 16777216.0)
 
 
+# ------------------------------------------------------------------ per-step device RNG key
+# Dropout seed = host per-site salt + a per-step key that lives ON THE DEVICE in the model's rng state
+# (int64 [counter, key]). rng_advance() steps it inside the training step, so a replayed hipGraph
+# draws fresh masks every step; rng_key() registers the state for every dropout-capable launch
+# (GEMM epilogues, dropout, LayerNorm-backward dropout, attention) while a step runs.
+_KEY: torch.Tensor | None = None
+
+
+@contextlib.contextmanager
+def rng_key(state: torch.Tensor | None):
+    global _KEY
+    prev, _KEY = _KEY, state
+    gpu = state is not None and state.is_cuda
+    if gpu:
+        lib().set_rng_key(state)
+    try:
+        yield
+    finally:
+        _KEY = prev
+        if gpu:
+            lib().set_rng_key(prev if prev is not None and prev.is_cuda else None)
+
+
+def rng_advance(state: torch.Tensor, stream: int = 0) -> None:
+    """counter += 1; key = splitmix64(counter ^ stream) (misc.hip rng_advance_kernel)."""
+    if state.is_cuda:
+        lib().rng_advance(state, int(stream))
+        return
+    m = _M64
+    c = (int(state[0]) + 1) & m
+    z = ((c ^ (int(stream) & m)) + 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    state[0] = _s64(c)
+    state[1] = _s64(z ^ (z >> 31))
+
+
+def eff_seed(salt: int) -> int:
+    """The seed a kernel launched now uses for this salt (host reference of common.h eff_seed)."""
+    if _KEY is None:
+        return int(salt)
+    return _s64(int(salt) + int(_KEY[1]))
+
+
 def dropout_keep(seed: int, n: int, p: float) -> torch.Tensor:
     """Keep-mask of the dropout kernel / fused GEMM dropout over a contiguous tensor of n elements."""
     return u01(hash_u32(seed, torch.arange(n, dtype=torch.int64))) < (1.0 - p)
@@ -66,7 +112,7 @@ def dropout(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
     if p <= 0.0:
         return x
     if not on_gpu(x):
-        keep = dropout_keep(seed, x.numel(), p).reshape(x.shape)
+        keep = dropout_keep(eff_seed(seed), x.numel(), p).reshape(x.shape)
         return (x.float() * keep / (1 - p)).to(torch.bfloat16)
     y = torch.empty_like(x)
     lib().dropout(x, y, p, int(seed))

@@ -75,8 +75,8 @@ def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = 
             aux.view(-1, N).copy_(y)
         y = act_ref(y, act)
         if drop_p > 0:
-            from .elementwise import dropout_keep
-            y = y * dropout_keep(drop_seed, y.numel(), drop_p).reshape(y.shape) / (1 - drop_p)
+            from .elementwise import dropout_keep, eff_seed
+            y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) / (1 - drop_p)
         y = y.to(torch.bfloat16)
         if resid is not None:
             y = (y.float() + resid.reshape(-1, N).float()).to(torch.bfloat16)

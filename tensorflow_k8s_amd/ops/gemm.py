@@ -196,7 +196,8 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
                aux: torch.Tensor | None = None, drop_p: float = 0.0, drop_seed: int = 0) -> torch.Tensor:
     """y[M,N] = dropout(act(x[M,K] @ w[N,K]^T + bias)) (+ resid). bf16 in/out, f32 accumulate.
     aux: also store the pre-activation (bf16) there, for the activation backward. Dropout mask =
-    ops.elementwise.dropout_keep(drop_seed, M*N, drop_p) (backward: elementwise.dropout(dy))."""
+    ops.elementwise.dropout_keep(eff_seed(drop_seed), M*N, drop_p) (backward: elementwise.dropout(dy));
+    eff_seed adds the per-step device key of the running step (elementwise.rng_key)."""
     M, K = x.shape[0], x.shape[-1]
     N = w.shape[0]
     if not on_gpu(x):
@@ -207,8 +208,8 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
             aux.view(-1, N).copy_(y)
         y = act_ref(y, act)
         if drop_p > 0:
-            from .elementwise import dropout_keep
-            y = y * dropout_keep(drop_seed, y.numel(), drop_p).reshape(y.shape) / (1 - drop_p)
+            from .elementwise import dropout_keep, eff_seed
+            y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) / (1 - drop_p)
         y = y.to(torch.bfloat16)
         if resid is not None:
             y = (y.float() + resid.float()).to(torch.bfloat16)
@@ -242,7 +243,7 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
                  dact_src: torch.Tensor | None = None, dact: str | None = None, drop_p: float = 0.0,
                  drop_seed: int = 0) -> torch.Tensor:
     """dx[M,K] = dropout((dy[M,N] @ w[N,K]) * act'(dact_src)) (+ resid). drop_p/drop_seed: the
-    backward of a forward dropout on this layer's INPUT (mask = ops.elementwise.dropout_keep(drop_seed,
+    backward of a forward dropout on this layer's INPUT (mask = ops.elementwise.dropout_keep(eff_seed(drop_seed),
     M*K, drop_p), e.g. the FFN's relu dropout) fused into the epilogue instead of a separate pass."""
     N, K = w.shape
     dy2 = dy.reshape(-1, N)
@@ -252,8 +253,8 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
         if dact_src is not None:
             dx = dx * act_grad_ref(dact_src.reshape(-1, K), dact)
         if drop_p > 0:
-            from .elementwise import dropout_keep
-            dx = dx * dropout_keep(drop_seed, dx.numel(), drop_p).reshape(dx.shape) / (1 - drop_p)
+            from .elementwise import dropout_keep, eff_seed
+            dx = dx * dropout_keep(eff_seed(drop_seed), dx.numel(), drop_p).reshape(dx.shape) / (1 - drop_p)
         dx = dx.to(torch.bfloat16)
         if resid is not None:
             dx = (dx.float() + resid.reshape(-1, K).float()).to(torch.bfloat16)

@@ -13,6 +13,7 @@ import math
 import torch
 
 from ._lib import lib, on_gpu
+from .elementwise import eff_seed
 
 HEAD_DIM = 64
 
@@ -190,7 +191,7 @@ def attention_fwd(sp: AttnSpec):
         s = torch.einsum("bqhd,bkhd->bhqk", q, k) * sp.scale
         lse = torch.logsumexp(s.masked_fill(pr == 0, float("-inf")), -1)
         if sp.p_drop > 0:
-            pr = pr * dropout_keep_mask(sp.seed, B, H, Sq, Sk, sp.p_drop) / (1 - sp.p_drop)
+            pr = pr * dropout_keep_mask(eff_seed(sp.seed), B, H, Sq, Sk, sp.p_drop) / (1 - sp.p_drop)
         o = torch.einsum("bhqk,bkhd->bqhd", pr, v).reshape(B * Sq, H * HEAD_DIM)
         return o.to(torch.bfloat16), lse
     out = torch.empty(B * Sq, H * HEAD_DIM, dtype=torch.bfloat16, device=dev)
@@ -210,7 +211,7 @@ def attention_bwd(sp: AttnSpec, out, dout, lse, dq, dk, dv):
         with torch.enable_grad():
             pr = _ref_probs(q, k, sp.kv_len, sp.causal, sp.scale)
             if sp.p_drop > 0:
-                pr = pr * dropout_keep_mask(sp.seed, B, H, Sq, Sk, sp.p_drop) / (1 - sp.p_drop)
+                pr = pr * dropout_keep_mask(eff_seed(sp.seed), B, H, Sq, Sk, sp.p_drop) / (1 - sp.p_drop)
             o = torch.einsum("bhqk,bkhd->bqhd", pr, v)
             gq, gk, gv = torch.autograd.grad(o, (q, k, v), dout.float().reshape(B, Sq, H, HEAD_DIM))
         for (buf, col), g, S in ((dq, gq, Sq), (dk, gk, Sk), (dv, gv, Sk)):

@@ -194,6 +194,8 @@ def run_worker(args, info, dev, world_comm) -> int:
 
     use_ps = args.strategy == "ps" or (args.strategy == "auto" and info.ps_ranks)
     model = build_model(args.model, **model_kwargs(args)).to(dev, seed=args.seed)
+    if hasattr(model, "rng_stream"):
+        model.rng_stream = info.rank  # each replica draws its own dropout masks
     opt = make_optimizer(args, model.arena)
     if use_ps:
         from ..parallel.ps import ParameterServerStrategy

@@ -8,9 +8,9 @@ and replayed -- at every world size: the data-parallel strategies enqueue their 
 produces each bucket, so the replayed graph keeps the bucket/backward overlap.
 
 Everything a replay must see change per step lives on the device: the optimizer's learning-rate
-schedule, step counter and Adam bias corrections (Optimizer.enable_device_schedule). Host-side
-per-step values that would freeze inside a graph -- dropout seeds drawn on the host -- make
-capture refuse (GraphUnsafe) instead of silently training wrong.
+schedule, step counter and Adam bias corrections (Optimizer.enable_device_schedule) and the models'
+dropout RNG state (ops.elementwise.rng_advance/rng_key). Host-side per-step values that would
+freeze inside a graph make capture refuse (GraphUnsafe) instead of silently training wrong.
 """
 from __future__ import annotations
 
@@ -22,9 +22,12 @@ class GraphUnsafe(RuntimeError):
 
 
 def graph_hazards(model) -> list[str]:
-    """Reasons a model's step cannot be replayed from a hipGraph (empty = safe)."""
+    """Reasons a model's step cannot be replayed from a hipGraph (empty = safe). Dropout is safe when
+    the model keeps its RNG state on the device (``rng_state``, advanced inside the step)."""
     out = []
     cfg = getattr(model, "cfg", None)
+    if getattr(model, "rng_state", None) is not None:
+        return out
     for k in ("dropout", "hidden_dropout", "attn_dropout", "relu_dropout"):
         if cfg is not None and float(getattr(cfg, k, 0.0) or 0.0) > 0.0 and getattr(model, "training", True):
             out.append(f"{type(model).__name__}.cfg.{k}={getattr(cfg, k)} (dropout seeds are drawn on the host per step)")

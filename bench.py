@@ -29,9 +29,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: 256 ResNet, 64 BERT, 32 Transformer)")
     ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--strategy", default="mwms", choices=["mwms", "ps"],
+                    help="mwms: all-reduce data parallelism; ps: ParameterServerStrategy (the last --ps ranks serve)")
+    ap.add_argument("--ps", type=int, default=2, help="--strategy ps: number of parameter-server ranks")
+    ap.add_argument("--ps-transport", default="rccl", choices=["rccl", "gloo"],
+                    help="rccl: ps ranks own a GPU (bucketed bf16 reduce/broadcast); gloo: ps ranks on the CPU")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--comm-dtype", default="bf16", choices=["bf16", "f32"],
-                    help="gradient all-reduce wire dtype (bf16: half the xGMI bytes; f32 master update either way)")
+                    help="gradient wire dtype (bf16: half the xGMI bytes; f32 master update either way)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a hipGraph (default: on, at every world size, unless the model has host-side per-step state)")
     ap.add_argument("--rccl-algo", default="", help="RCCL algorithm (Ring|Tree|...), see parallel/comm.py")
@@ -43,6 +48,8 @@ def main():
     ap.add_argument("--via-operator", action="store_true",
                     help="measure through a TFJob: tfk-cluster gang-schedules one pod per GPU (TF_CONFIG rendezvous)")
     ap.add_argument("--tfjob-worker", action="store_true", help=argparse.SUPPRESS)  # a pod of --via-operator
+    # CPU rehearsal of the multi-rank code path (gloo, fp32 CPU executor; tests only -- not a measurement)
+    ap.add_argument("--cpu-rehearsal", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.via_operator:
         return run_via_operator(args)
@@ -63,36 +70,55 @@ def main():
     if args.gpus > 1 and world == 1:
         sys.exit("for --gpus > 1 launch with: python -m torch.distributed.run --nproc-per-node N "
                  "--master-addr 127.0.0.1 bench.py --gpus N")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # roles: parameter servers are the last ranks (TF_CONFIG order: chief, workers, ps)
+    if info is not None:
+        ps_ranks, worker_ranks = list(info.ps_ranks), list(info.worker_ranks)
+    else:
+        nps = args.ps if args.strategy == "ps" else 0
+        ps_ranks, worker_ranks = list(range(world - nps, world)), list(range(world - nps))
+    use_ps = args.strategy == "ps" or bool(ps_ranks)
+    if use_ps and (not ps_ranks or not worker_ranks):
+        sys.exit(f"--strategy ps needs at least one worker and one ps rank (world {world}, --ps {args.ps})")
+    is_ps = rank in ps_ranks
+    ps_on_cpu = (use_ps and args.ps_transport == "gloo") or args.cpu_rehearsal
+    if (is_ps and ps_on_cpu) or args.cpu_rehearsal:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
 
     from tensorflow_k8s_amd.parallel import comm, tfk_comm
     rccl_cfg = comm.configure_rccl(args.rccl_algo or None, args.rccl_proto or None, args.rccl_channels)
-    if world > 1 or args.force_comm:
+    if (world > 1 or args.force_comm) and not ps_on_cpu:
         comm.enable_transport_log()
     # the world communicator is the runtime's own RCCL binding (parallel/tfk_comm.py): no
     # torch.distributed process group, collectives enqueued on a comm stream the step graph captures
+    # (gloo only when the parameter servers live on the CPU)
     world_comm = None
-    if world > 1 and info is not None:
-        from tensorflow_k8s_amd.parallel import cluster
-        world_comm = cluster.init_comm(info, dev, "rccl", timeout_s=300)
-    elif world > 1:
-        world_comm = tfk_comm.init(tfk_comm.env_store(rank, world), rank, world, dev)
+    cdev = torch.device("cpu") if ps_on_cpu else dev
+    if world > 1:
+        if info is not None:
+            from tensorflow_k8s_amd.parallel import cluster
+            world_comm = cluster.init_comm(info, cdev, "gloo" if ps_on_cpu else "rccl", timeout_s=300)
+        else:
+            world_comm = tfk_comm.init(tfk_comm.env_store(rank, world), rank, world, cdev)
     elif args.force_comm:
         import torch.distributed as dist
         world_comm = tfk_comm.init(dist.HashStore(), 0, 1, dev)
+    # barrier / timing group: the workers (parameter servers serve on their own schedule)
+    wcomm = world_comm.split(worker_ranks, "workers") if (use_ps and world_comm is not None) else world_comm
 
     from tensorflow_k8s_amd.models import build_model, synthetic_batch
-    from tensorflow_k8s_amd.parallel.mwms import MultiWorkerMirroredStrategy
     from tensorflow_k8s_amd.runtime.optimizer import LAMB, SGD, AdamW
     from tensorflow_k8s_amd.runtime.trainer import StepRunner
 
     is_cnn = args.model.startswith("resnet")
+    nworkers = len(worker_ranks)
     model = build_model(args.model, **({"fp8": True} if args.fp8 else {})).to(dev)
     if hasattr(model, "rng_stream"):
         model.rng_stream = rank  # each replica draws its own dropout masks
     if is_cnn:
-        opt = SGD(model.arena, lr=0.1 * args.batch * world / 256, momentum=0.9, weight_decay=5e-5)
+        opt = SGD(model.arena, lr=0.1 * args.batch * nworkers / 256, momentum=0.9, weight_decay=5e-5)
         opt_name = "SGD momentum 0.9 (fused HIP)"
     elif args.model.startswith("bert"):
         opt = LAMB(model.arena, lr=1e-4, weight_decay=0.01)
@@ -100,60 +126,94 @@ def main():
     else:
         opt = AdamW(model.arena, lr=1e-4, b2=0.98, eps=1e-9, weight_decay=0.0)
         opt_name = "Adam (fused HIP)"
-    strat = MultiWorkerMirroredStrategy(model.arena, comm=world_comm, bucket_mb=args.bucket_mb,
-                                        comm_dtype=args.comm_dtype, force=args.force_comm)
+    wire = torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    if is_ps:
+        # parameter-server rank: holds one shard (f32 master + slots), serves every worker step
+        from tensorflow_k8s_amd.parallel.ps import ParameterServer
+        server = ParameterServer(model.arena, opt, ps_ranks.index(rank), ps_ranks, worker_ranks, "sync")
+        if args.ps_transport == "gloo":
+            server.serve()
+        else:
+            server.setup_collective(args.bucket_mb, world_comm, wire)
+            server.serve_steps(0, args.warmup + args.steps)
+            sync()
+        _gather_times(world_comm, cdev, world, 0.0)  # (the workers' clock defines the result)
+        tfk_comm.shutdown()
+        return 0
+
+    if use_ps:
+        from tensorflow_k8s_amd.parallel.ps import ParameterServerStrategy
+        strat = ParameterServerStrategy(model.arena, ps_ranks, worker_ranks, "sync", transport=args.ps_transport,
+                                        bucket_mb=args.bucket_mb, comm=world_comm, wire_dtype=wire)
+        strat_name = f"ParameterServerStrategy ps={len(ps_ranks)} worker={nworkers} ({args.ps_transport} transport)"
+    else:
+        from tensorflow_k8s_amd.parallel.mwms import MultiWorkerMirroredStrategy
+        strat = MultiWorkerMirroredStrategy(model.arena, comm=world_comm, bucket_mb=args.bucket_mb,
+                                            comm_dtype=args.comm_dtype, force=args.force_comm)
+        strat_name = "MultiWorkerMirroredStrategy (tfk_comm RCCL all-reduce)"
     strat.configure_optimizer(opt)
     strat.broadcast_parameters()
     batch = synthetic_batch(model, args.batch, dev, seed=1000 + rank)
-    # the whole step (fwd, bwd, RCCL bucket all-reduces, optimizer) replays from one hipGraph at every
+    # the whole step (fwd, bwd, RCCL bucket collectives, optimizer) replays from one hipGraph at every
     # world size; only a model with host-side per-step state (graph_hazards) runs eager
     from tensorflow_k8s_amd.runtime.trainer import graph_hazards
     use_graph = (not graph_hazards(model)) if args.graph < 0 else bool(args.graph)
     runner = StepRunner(model, opt, strat, batch, use_graph=use_graph)
 
     def barrier():
-        torch.cuda.synchronize()
-        if world_comm is not None:
-            world_comm.barrier()
-        torch.cuda.synchronize()
+        sync()
+        if wcomm is not None:
+            wcomm.barrier()
+        sync()
 
     for _ in range(args.warmup):
         runner.step()
     barrier()
     # per-step device timestamps (no host sync inside the timed loop) for the median / p90
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    gpu = dev.type == "cuda"
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if gpu else []
     t0 = time.perf_counter()
-    evs[0].record()
+    if gpu:
+        evs[0].record()
     for i in range(args.steps):
         runner.step()
-        evs[i + 1].record()
+        if gpu:
+            evs[i + 1].record()
     barrier()
     dt = time.perf_counter() - t0
     mine_ms = dt / args.steps * 1000.0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        world_comm.all_reduce(t, op="max")
-    dt = float(t.item())
-    ms = dt / args.steps * 1000.0
-    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    if use_ps and args.ps_transport == "gloo":
+        strat.shutdown()  # DONE to the CPU parameter servers (their serve() loop ends)
+    dt, per_rank = _gather_times(world_comm, cdev, world, mine_ms, worker_ranks)
+    ms = dt
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)) if gpu else [ms] * args.steps
     dist_ms = {"median": round(step_ms[len(step_ms) // 2], 3),
                "p90": round(step_ms[min(len(step_ms) - 1, int(0.9 * len(step_ms)))], 3),
                "min": round(step_ms[0], 3), "max": round(step_ms[-1], 3)}
-    per_rank = [ms]
-    if world > 1:
-        g = torch.zeros(world, dtype=torch.float64, device=dev)
-        world_comm.all_gather(g, torch.tensor([mine_ms], dtype=torch.float64, device=dev))
-        per_rank = [round(float(x), 3) for x in g.tolist()]
-    gb = args.batch * world
+    gb = args.batch * nworkers
     value = gb / (ms / 1000.0)
-    comm_cfg = {"comm_dtype": args.comm_dtype, "bucket_mb": args.bucket_mb, "buckets": len(strat.buckets),
-                "wire_mb_per_step": round(strat.wire_bytes() / 2**20, 1) if strat.enabled else 0.0}
-    if strat.enabled:
+    comm_cfg = {"comm_dtype": args.comm_dtype, "bucket_mb": args.bucket_mb}
+    if use_ps:
+        comm_cfg.update({"ps_ranks": ps_ranks, "worker_ranks": worker_ranks, "transport": args.ps_transport,
+                         "buckets": len(strat.plan.buckets) if strat.plan is not None else 0,
+                         "wire_mb_per_step": round(strat.wire_bytes() / 2**20, 1)})
+        enabled = True
+    else:
+        comm_cfg.update({"buckets": len(strat.buckets),
+                         "wire_mb_per_step": round(strat.wire_bytes() / 2**20, 1) if strat.enabled else 0.0})
+        enabled = strat.enabled
+    if enabled and dev.type == "cuda" and not ps_on_cpu:
         comm_cfg["backend"] = "tfk_comm RCCL (own binding, librccl %s)" % _rccl_version()
         comm_cfg["rccl_transport"] = comm.transport_summary()
         comm_cfg["rccl_config"] = rccl_cfg
     loss = runner.last_loss()
-    if rank == 0 and not is_cnn:
+    par = f"ps{len(ps_ranks)}+worker{nworkers}" if use_ps else f"dp{world}"
+    if rank == worker_ranks[0] and not is_cnn:
         seq = model.cfg.seq_len if args.model.startswith("bert") else model.cfg.tgt_len
         toks = gb * (seq if args.model.startswith("bert") else model.cfg.src_len + model.cfg.tgt_len)
         print(json.dumps({
@@ -161,16 +221,16 @@ def main():
             "unit": "tokens/sec", "sequences_per_sec": round(value, 2), "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "step_ms": dist_ms, "per_rank_ms": per_rank,
             "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": _token_baseline(args.model, toks / (ms / 1000.0), world),
+            "vs_baseline": _token_baseline(args.model, toks / (ms / 1000.0), nworkers),
             "dtype": "bf16+mxfp8" if args.fp8 else "bf16",
             "data": "synthetic token ids, random-init weights",
             "config": {"model": args.model, "global_batch": gb, "seq_len": seq, "per_gpu_batch": args.batch,
-                       "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (tfk_comm RCCL all-reduce)",
-                       "optimizer": opt_name, "hipgraph": use_graph, "comm": comm_cfg},
+                       "parallelism": par, "strategy": strat_name,
+                       "optimizer": opt_name, "hipgraph": runner.use_graph, "comm": comm_cfg},
             "loss": loss}), flush=True)
-    elif rank == 0:
+    elif rank == worker_ranks[0]:
         is_r50 = args.model == "resnet50"
-        base = _baseline(world) if is_r50 else None
+        base = _baseline(nworkers) if is_r50 else None
         print(json.dumps({
             "metric": ("images/sec (whole node) ResNet-50 TFJob at 1/2/4/8 MI355X workers" if is_r50
                        else f"{args.model} images/sec (whole node)"),
@@ -180,8 +240,8 @@ def main():
             "vs_baseline": round(value / base, 4) if base else None, "dtype": "bf16",
             "data": "synthetic (on-device ImageNet-shaped 224x224x3 bf16 batch, random-init weights)",
             "config": {"model": args.model, "global_batch": gb, "seq_len": None, "per_gpu_batch": args.batch,
-                       "parallelism": f"dp{world}", "strategy": "MultiWorkerMirroredStrategy (tfk_comm RCCL all-reduce)",
-                       "optimizer": opt_name, "hipgraph": use_graph, "comm": comm_cfg},
+                       "parallelism": par, "strategy": strat_name,
+                       "optimizer": opt_name, "hipgraph": runner.use_graph, "comm": comm_cfg},
             "loss": loss,
         }), flush=True)
     tfk_comm.shutdown()
@@ -191,6 +251,19 @@ def _rccl_version() -> str:
     from tensorflow_k8s_amd import _C
     v = _C.rccl_version()
     return f"{v // 10000}.{v // 100 % 100}.{v % 100}"
+
+
+def _gather_times(world_comm, cdev, world: int, mine_ms: float, worker_ranks=None):
+    """MAX over ranks of the timed ms/step, and every worker's own value (all ranks must call)."""
+    if world <= 1 or world_comm is None:
+        return mine_ms, [round(mine_ms, 3)]
+    t = torch.tensor([mine_ms], dtype=torch.float64, device=cdev)
+    world_comm.all_reduce(t, op="max")
+    g = torch.zeros(world, dtype=torch.float64, device=cdev)
+    world_comm.all_gather(g, torch.tensor([mine_ms], dtype=torch.float64, device=cdev))
+    vals = g.tolist()
+    per = [round(vals[r], 3) for r in (worker_ranks if worker_ranks is not None else range(world))]
+    return float(t.item()), per
 
 
 def run_via_operator(args) -> int:
@@ -205,21 +278,30 @@ def run_via_operator(args) -> int:
     root = os.path.dirname(os.path.abspath(__file__))
     cmd = ["python3", os.path.join(root, "bench.py"), "--tfjob-worker", "--gpus", str(n), "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--model", args.model, "--bucket-mb", str(args.bucket_mb), "--comm-dtype", args.comm_dtype, "--graph",
-           str(args.graph), "--fp8", str(args.fp8)] + (["--batch", str(args.batch)] if args.batch else [])
+           str(args.graph), "--fp8", str(args.fp8), "--strategy", args.strategy, "--ps-transport",
+           args.ps_transport] + (["--batch", str(args.batch)] if args.batch else [])
+    nps = args.ps if args.strategy == "ps" else 0
+    if nps and n - nps < 1:
+        raise SystemExit(f"--strategy ps needs --gpus > --ps ({n} <= {nps})")
 
-    def rs(k):
+    def rs(k, gpus=1):
         return {"replicas": k, "restartPolicy": "Never", "template": {"spec": {"containers": [{
             "name": "tensorflow", "image": "tfk/runtime", "command": cmd,
             "env": [{"name": "PYTHONPATH", "value": root}],
-            "resources": {"limits": {"amd.com/gpu": 1}}}]}}}
+            "resources": {"limits": {"amd.com/gpu": gpus}}}]}}}
+    # TF replica map: Chief + Workers compute; PS replicas (BASELINE config 3: PS=2/worker=6) own a
+    # GPU on the rccl transport, none on the gloo (CPU parameter server) transport
     specs = {"Chief": rs(1)}
-    if n > 1:
-        specs["Worker"] = rs(n - 1)
+    if n - nps > 1:
+        specs["Worker"] = rs(n - nps - 1)
+    if nps:
+        specs["PS"] = rs(nps, 0 if args.ps_transport == "gloo" else 1)
     job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob",
            "metadata": {"name": f"bench-{args.model}", "namespace": "default",
                         "annotations": {"scheduling.tfk.io/gang-visible-gpus": "true"}},
            "spec": {"tfReplicaSpecs": specs, "runPolicy": {"backoffLimit": 0, "cleanPodPolicy": "None"}}}
-    with LocalCluster(gpus=n, root_dir=tempfile.mkdtemp(prefix="tfk-bench-")) as c:
+    with LocalCluster(gpus=n - (nps if args.ps_transport == "gloo" else 0),
+                      root_dir=tempfile.mkdtemp(prefix="tfk-bench-")) as c:
         c.client.create(job)
         j = c.client.wait_tfjob(job["metadata"]["name"], timeout=1800)
         log = c.client.logs(f"bench-{args.model}-chief-0")

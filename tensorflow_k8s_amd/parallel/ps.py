@@ -468,15 +468,25 @@ class ParameterServer:
         stream-wait -> unpack -> fused optimizer on that bucket -> post its broadcast. The global step
         (host counter or device schedule) advances once per step. Ships f32 master + slots to the
         chief at its checkpoint steps."""
+        self.setup_collective(bucket_mb, comm, wire_dtype)
+        return self.serve_steps(start_step, total_steps, checkpoint_every, chief, final_checkpoint)
+
+    def setup_collective(self, bucket_mb: float = 32.0, comm=None, wire_dtype=torch.bfloat16) -> None:
+        """Create the per-shard sub-communicators (in the same order as the workers'
+        ParameterServerStrategy) and serve the initial parameter pull."""
         a = self.arena
-        comm = comm if comm is not None else tfk_comm.world()
-        # sub-communicators first: the workers create theirs in ParameterServerStrategy.__init__
-        plan = CollectivePlan(a, self.shards, self.ps_ranks, self.worker_ranks, bucket_mb, comm, wire_dtype)
-        plan.pull_master()
+        self._comm = comm if comm is not None else tfk_comm.world()
+        self._plan = CollectivePlan(a, self.shards, self.ps_ranks, self.worker_ranks, bucket_mb, self._comm, wire_dtype)
+        self._plan.pull_master()
+
+    def serve_steps(self, start_step: int, end_step: int, checkpoint_every: int = 0, chief: int = 0,
+                    final_checkpoint: bool = False, total_steps: int | None = None) -> int:
+        """Serve global steps start_step+1 .. end_step (after setup_collective)."""
+        a, plan, comm, opt = self.arena, self._plan, self._comm, self.opt
+        total = end_step if total_steps is None else total_steps
         me = self.ps_ranks.index(comm.rank)
         mine = plan.buckets_of(me)
-        opt = self.opt
-        for step in range(start_step + 1, total_steps + 1):
+        for step in range(start_step + 1, end_step + 1):
             a.grad[self.lo:self.hi].zero_()  # the owner's own (zero) contribution to its reduces
             if plan.wire is not None:
                 plan.wire[self.lo:self.hi].zero_()
@@ -493,8 +503,8 @@ class ParameterServer:
                 w.wait()
             opt.region = (self.lo, self.hi)
             self.updates += 1
-            ckpt = (checkpoint_every and step % checkpoint_every == 0 and step < total_steps) or \
-                (final_checkpoint and step == total_steps)
+            ckpt = (checkpoint_every and step % checkpoint_every == 0 and step < total) or \
+                (final_checkpoint and step == total)
             if ckpt:
                 comm.send(self._state(), chief)
                 if a.master.is_cuda:

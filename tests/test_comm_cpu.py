@@ -211,3 +211,24 @@ def test_tfk_comm_bootstrap_under_torchrun(tmp_path):
     for d in rows:
         assert d["sum"] == 6.0 and d["max"] == 2.0 and d["gather"] == [0.0, 10.0, 20.0] and d["backend"] == "gloo"
     assert [d["sub"] for d in rows] == [2.0, 2.0, 1.0]
+
+
+@pytest.mark.parametrize("extra,par", [([], "dp2"), (["--strategy", "ps", "--ps", "1", "--ps-transport", "rccl"], "ps1+worker1"),
+                                       (["--strategy", "ps", "--ps", "1", "--ps-transport", "gloo"], "ps1+worker1")])
+def test_bench_multi_rank_path_cpu_rehearsal(tmp_path, native_ext, extra, par):
+    """bench.py's N-rank code path (torchrun bootstrap, world communicator, MWMS / both PS
+    transports, barriers, MAX-over-ranks timing, per-rank gather, the one JSON line) rehearsed on
+    the CPU tier with gloo and the fp32 executor -- the path the driver's multi-GPU run takes,
+    minus the GPU. Not a measurement."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    r = subprocess.run([PY, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+                        "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--cpu-rehearsal", "--model", "resnet50", "--batch", "2", "--steps", "1", "--warmup", "1"] + extra,
+                       env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{") and '"metric"' in l]
+    assert len(lines) == 1, r.stdout[-2000:]  # exactly one rank prints
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == par and d["value"] > 0
+    assert d["config"]["global_batch"] == (4 if par == "dp2" else 2)
+    assert len(d["per_rank_ms"]) == (2 if par == "dp2" else 1)

@@ -123,3 +123,45 @@ def test_20_step_loss_trajectory_matches_cpu(which):
     assert lc[-1] < lc[0], lc  # it trains
     rel = [abs(a - b) / abs(a) for a, b in zip(lc, lg)]
     assert max(rel) <= 0.02, [(i, round(a, 4), round(b, 4)) for i, (a, b) in enumerate(zip(lc, lg))]
+
+
+def _fullwidth(which, seq):
+    """Full-width BERT-base / Transformer-big layers (hidden 768 x 12 heads / 1024 x 16 heads, FFN
+    3072 / 4096, the real vocabularies), 2 layers deep, dropout ON at the models' defaults."""
+    if which == "bert-base":
+        from tensorflow_k8s_amd.models.bert import BertConfig, BertForPreTraining
+        return lambda: BertForPreTraining(BertConfig(layers=2, seq_len=seq, max_position=max(512, seq)))
+    from tensorflow_k8s_amd.models.transformer import Transformer, TransformerConfig
+    return lambda: Transformer(TransformerConfig(enc_layers=1, dec_layers=1, src_len=seq, tgt_len=seq))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("which,seq", [("bert-base", 128), ("bert-base", 512), ("transformer-big", 256)])
+def test_fullwidth_dropout_on_gradient_cosine(which, seq):
+    """GPU kernels vs the fp32 CPU executor at full layer width with dropout ON: both sides draw the
+    same masks (the hash RNG of salt + device key has a bit-exact CPU reference), batch 2, one step;
+    every non-negligible parameter gradient has cosine >= 0.99 and the losses agree within 2 %."""
+    mk = _fullwidth(which, seq)
+    out = {}
+    for dev in ("cpu", "cuda"):
+        m = mk().to(dev, seed=3)
+        assert m.training and m.rng_state is not None
+        batch = tuple(t.to(dev) for t in m.synthetic_batch(2, "cpu", seed=5))
+        loss, _ = m.forward_backward(*batch)
+        out[dev] = (float(loss.float().mean()), {p.name: p.grad.detach().float().cpu().clone() for p in m.arena.params},
+                    m.rng_state.cpu().clone())
+    (lc, gc, sc), (lg, gg, sg) = out["cpu"], out["cuda"]
+    assert torch.equal(sc, sg) and int(sc[0]) == 1  # same per-step key on both sides
+    assert abs(lc - lg) <= 0.02 * abs(lc), (lc, lg)
+    norms = sorted(float(v.norm()) for v in gc.values())
+    floor = 1e-3 * norms[len(norms) // 2]
+    worst, checked = [], 0
+    for n in gc:
+        if float(gc[n].norm()) <= floor:
+            continue
+        checked += 1
+        c = _cos(gg[n], gc[n])
+        if c < 0.99:
+            worst.append((n, round(c, 4)))
+    assert checked >= 0.9 * len(gc), (checked, len(gc))
+    assert not worst, worst

@@ -12,6 +12,7 @@ restart semantics :44-52, operator-managed TFJob CRUD :228).
 """
 import json
 import os
+import time
 
 import pytest
 
@@ -78,3 +79,53 @@ def test_resnet50_tfjob_trains_on_gpu_and_restarts(gpu_cluster, tmp_path):
     restored = [e for e in ev if e["event"] == "restored"]
     assert restored and restored[-1]["step"] in (4, 8), [e for e in ev if e["event"] != "train"]
     assert [e for e in ev if e["event"] == "done"][-1]["step"] == 12
+
+
+@pytest.mark.timeout(420)
+def test_config4_resnet152_chief_evaluator_fault_restart(gpu_cluster, tmp_path):
+    """BASELINE config 4 on the MI355X: ResNet-152 Chief (GPU) + Evaluator (same GPU, outside the
+    training world). The chief SIGKILLs itself at step 9 (exit 137, retryable) -> gang restart ->
+    resume from the newest complete checkpoint -> Succeeded; the evaluator follows the checkpoint
+    directory and reports an eval for the final checkpoint, which was written after the restart."""
+    c = gpu_cluster.client
+    ck = str(tmp_path / "ck152")
+    common = ["--model", "resnet152", "--image-size", "64", "--num-classes", "100", "--device", "cuda",
+              "--checkpoint-dir", ck]
+    chief = {"name": "tensorflow", "image": "tfk/runtime", "command": TRAIN,
+             "args": common + ["--batch", "16", "--steps", "12", "--checkpoint-every", "4", "--log-every", "2"],
+             "env": [{"name": "TFK_FAULT_AT_STEP", "value": "9"}, {"name": "TFK_FAULT_EXIT", "value": "137"}],
+             "resources": {"limits": {"amd.com/gpu": 1}}}
+    evaluator = {"name": "tensorflow", "image": "tfk/runtime", "command": TRAIN,
+                 "args": common + ["--batch", "8", "--eval-batches", "2", "--eval-timeout", "300"]}
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": "r152", "namespace": "default"},
+           "spec": {"runPolicy": {"backoffLimit": 2, "cleanPodPolicy": "None"},
+                    "tfReplicaSpecs": {
+                        "Chief": {"replicas": 1, "restartPolicy": "ExitCode", "template": {"spec": {"containers": [chief]}}},
+                        "Evaluator": {"replicas": 1, "restartPolicy": "OnFailure",
+                                      "template": {"spec": {"containers": [evaluator]}}}}}}
+    c.create(job)
+    j = c.wait_tfjob("r152", timeout=360)
+    st = j["status"]
+    assert tfjob_condition(j) == "Succeeded", (st, c.logs("r152-chief-0")[-3000:])
+    assert st.get("restartCount") == 1, st
+    ev = _events(c.logs("r152-chief-0"))
+    restored = [e for e in ev if e["event"] == "restored"]
+    assert restored and restored[-1]["step"] in (4, 8), [e for e in ev if e["event"] != "train"]
+    assert [e for e in ev if e["event"] == "done"][-1]["step"] == 12
+    start = [e for e in ev if e["event"] == "start"][-1]
+    assert start["model"] == "resnet152" and start["restart_generation"] == 1, start
+    # the evaluator is not in the training world: TF_CONFIG task only, no cluster slot
+    pod = c.get("pods", "r152-evaluator-0")
+    env = {e["name"]: e.get("value") for e in pod["spec"]["containers"][0]["env"]}
+    tf = json.loads(env["TF_CONFIG"])
+    assert tf["task"] == {"type": "evaluator", "index": 0} and "evaluator" not in tf["cluster"], tf
+    deadline = time.time() + 120
+    evals = []
+    while time.time() < deadline:
+        evals = [e for e in _events(c.logs("r152-evaluator-0")) if e.get("event") == "eval"]
+        if any(e["step"] == 12 for e in evals):
+            break
+        time.sleep(1)
+    assert any(e["step"] == 12 for e in evals), (evals, c.logs("r152-evaluator-0")[-2000:])
+    last = [e for e in evals if e["step"] == 12][-1]
+    assert last["loss"] == last["loss"] and 0.0 <= last["accuracy"] <= 1.0 and last["examples"] == 16

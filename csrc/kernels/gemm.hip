@@ -464,9 +464,13 @@ static int launch_reg(GemmParams p, int bm, int bn, int amode, int bmode, int ep
   // Cout=64 conv weight gradients (stem 7x7, stage-1 3x3): a 64x256 tile gives each wave a 32x128
   // sub-tile (2x8 MFMA fragments per LDS fragment load instead of 64x64's 2x2)
   TFK_GEMM_CASE(64, 256, A_KOUT, B_CONV_WGRAD, EPI_F32)
-  // transformer epilogue extras: fwd (aux/dropout) and dgrad (activation backward)
-  TFK_GEMM_TILES_BIG(A_KIN, B_KIN, EPI_BF16_EXT)
-  TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_BF16_EXT)
+  // transformer epilogue extras: fwd (aux/dropout) and dgrad (activation backward). Register-engine
+  // fallback only (g4 serves every aligned shape); the 256x64 tiles and the 128x128 K-outer-B tile
+  // spill with this epilogue (8-32 B/lane of scratch under hipcc 7.2), so they are not built -- the
+  // launcher falls back to 128x64 / 64x64 for them.
+  TFK_GEMM_TILES3(A_KIN, B_KIN, EPI_BF16_EXT) TFK_GEMM_CASE(256, 256, A_KIN, B_KIN, EPI_BF16_EXT)
+  TFK_GEMM_CASE(128, 64, A_KIN, B_KOUT, EPI_BF16_EXT) TFK_GEMM_CASE(64, 64, A_KIN, B_KOUT, EPI_BF16_EXT)
+  TFK_GEMM_CASE(256, 256, A_KIN, B_KOUT, EPI_BF16_EXT)
   // fused BN-backward reduction: only the dgrad producers of a BN input
   TFK_GEMM_TILES_BIG(A_KIN, B_KOUT, EPI_BF16_BNR)
   TFK_GEMM_TILES3(A_CONV_DGRAD, B_KIN, EPI_BF16_BNR)
@@ -496,9 +500,13 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
       if (r != -1) return r;
     }
   }
-  const int r = launch_reg(p, bm, bn, amode, bmode, epi, batch, splits, stream);
-  if (r != -1 || (bm == 128 && bn == 128)) return r;
-  return launch_reg(p, 128, 128, amode, bmode, epi, batch, splits, stream);
+  // requested tile, else the 128x128 / 128x64 / 64x64 tiles every combination instantiates at
+  // least one of
+  int r = launch_reg(p, bm, bn, amode, bmode, epi, batch, splits, stream);
+  const int fb[3][2] = {{128, 128}, {128, 64}, {64, 64}};
+  for (int i = 0; i < 3 && r == -1; ++i)
+    if (!(bm == fb[i][0] && bn == fb[i][1])) r = launch_reg(p, fb[i][0], fb[i][1], amode, bmode, epi, batch, splits, stream);
+  return r;
 }
 
 // Number of split-K slabs the launcher will actually use (for workspace sizing).

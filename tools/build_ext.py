@@ -36,16 +36,20 @@ def _stale(out: str, deps: list[str]) -> bool:
 
 
 def _check_scratch(stderr: str, src: str) -> None:
-    """Kernels must not spill: a scratch-using GEMM/attention kernel runs several times slower."""
+    """Kernels must not spill: a scratch-using GEMM/attention kernel runs several times slower, so a
+    kernel with scratch is a build ERROR (drop or retile the variant)."""
     import re
     fn = None
+    bad = []
     for line in stderr.splitlines():
         m = re.search(r"Function Name: (\S+)", line)
         if m:
             fn = m.group(1)
         m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
         if m and int(m.group(1)) > 0:
-            sys.stderr.write(f"[tfk build] WARNING: {os.path.basename(src)}: {fn} uses {m.group(1)} B/lane of scratch\n")
+            bad.append(f"{os.path.basename(src)}: {fn} uses {m.group(1)} B/lane of scratch")
+    if bad:
+        raise RuntimeError("kernels spill to scratch:\n  " + "\n  ".join(bad))
 
 
 def _run(cmd: list[str]) -> None:
@@ -54,7 +58,11 @@ def _run(cmd: list[str]) -> None:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("build failed: " + " ".join(cmd[:3]) + " ... " + cmd[-1])
     if "-Rpass-analysis=kernel-resource-usage" in cmd:
-        _check_scratch(r.stderr, cmd[-3])
+        try:
+            _check_scratch(r.stderr, cmd[-3])
+        except RuntimeError:
+            os.remove(cmd[-1])  # keep the spilling object from looking up to date
+            raise
 
 
 def ext_path() -> str:

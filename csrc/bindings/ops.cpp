@@ -186,7 +186,8 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
     p.bn_mean2 = opt_ptr<const float>(bnr[7]);
     p.bn_invstd2 = opt_ptr<const float>(bnr[8]);
     p.bn_sums = bnr[9]->data_ptr<float>();
-    p.bn_relu = bn_relu;
+    p.bn_relu = bn_relu & 1;            // bit 0: relu mask from y*scale+shift
+    p.bn_store_dz = (bn_relu >> 1) & 1;  // bit 1: store dz (masked dA) instead of dA
     p.bn_shards = bn_shards;
     TORCH_CHECK(!(p.bn_relu && !p.bn_amask && !(p.bn_scale && p.bn_shift)), "relu mask needs a or scale/shift");
   }

@@ -156,14 +156,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     // the centring (y - mean) * invstd is applied once after the loop (r1 <- (r1 - mean*r0) *
     // invstd), so mean/invstd need no registers inside the store pass -- those 32 VGPRs pay for a
     // second chunk in flight on the 128-VGPR (4 waves/SIMD) instantiations.
-    float r0[8], r1[8], r2[8], sc[8], sh[8];
+    // (the relu-from-y mask's scale/shift are re-read per chunk from L1/L2 instead of pinning 16
+    // VGPRs for the whole store pass)
+    float r0[8], r1[8], r2[8];
     if constexpr (bnr) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int n = min(n0 + ccol * 8 + e, p.N - 1);
-        r0[e] = r1[e] = r2[e] = 0.f;
-        sc[e] = p.bn_scale ? p.bn_scale[n] : 1.f; sh[e] = p.bn_shift ? p.bn_shift[n] : 0.f;
-      }
+      for (int e = 0; e < 8; ++e) r0[e] = r1[e] = r2[e] = 0.f;
     }
     // Interior tile (block-uniform): the store pass runs in groups of G chunks whose global loads
     // (residual, BN inputs, activation-backward source) are ALL issued before the group's first
@@ -245,13 +243,34 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[g][e]));
           }
+          // relu keep-bits of the chunk (one VGPR); store_dz masks v with them before the store
+          unsigned keepm = 0xffu;
+          if constexpr (bnr) {
+            if (p.bn_amask) {
+              keepm = mk[g];
+            } else if (p.bn_relu) {
+              keepm = 0;
+              const f32x4* scp = (const f32x4*)(p.bn_scale + nlog[g]);
+              const f32x4* shp = (const f32x4*)(p.bn_shift + nlog[g]);
+              const f32x4 s0 = scp[0], s1 = scp[1], h0 = shp[0], h1 = shp[1];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const float scl = e < 4 ? s0[e & 3] : s1[e & 3], shf = e < 4 ? h0[e & 3] : h1[e & 3];
+                keepm |= (bf2f(yv[g][e]) * scl + shf > 0.f) ? (1u << e) : 0u;
+              }
+            }
+            if (p.bn_store_dz) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                if (!((keepm >> e) & 1u)) v[e] = f2bf(0.f);
+            }
+          }
           *(bf16x8*)((bf16*)p.C + off[g]) = v;
           if constexpr (bnr) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float y = bf2f(yv[g][e]);
-              const bool keep = p.bn_amask ? ((mk[g] >> e) & 1u) != 0 : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
-              const float dz = keep ? bf2f(v[e]) : 0.f;
+              const float dz = ((keepm >> e) & 1u) ? bf2f(v[e]) : 0.f;
               r0[e] += dz;
               r1[e] += dz * y;
               if (p.bn_y2) r2[e] += dz * bf2f(y2v[g][e]);
@@ -302,22 +321,30 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[e]));
         }
-        *(bf16x8*)dst = v;
         if constexpr (bnr) {
           bf16x8 yv = *(const bf16x8*)((const bf16*)p.bn_y + off);
           bf16x8 y2v;
           if (p.bn_y2) y2v = *(const bf16x8*)((const bf16*)p.bn_y2 + off);
           const unsigned mk = p.bn_amask ? p.bn_amask[off >> 3] : 0xffu;
+          unsigned keepm = 0;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float y = bf2f(yv[e]);
-            bool keep = p.bn_amask ? ((mk >> e) & 1u) != 0 : (p.bn_relu ? (y * sc[e] + sh[e] > 0.f) : true);
+            bool keep = p.bn_amask ? ((mk >> e) & 1u) != 0
+                                   : (p.bn_relu ? (y * p.bn_scale[n + e] + p.bn_shift[n + e] > 0.f) : true);
+            keepm |= keep ? (1u << e) : 0u;
             const float dz = keep ? bf2f(v[e]) : 0.f;
             r0[e] += dz;
             r1[e] += dz * y;
             if (p.bn_y2) r2[e] += dz * bf2f(y2v[e]);
           }
+          if (p.bn_store_dz) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (!((keepm >> e) & 1u)) v[e] = f2bf(0.f);
+          }
         }
+        *(bf16x8*)dst = v;
       } else {
         for (int e = 0; e < 8 && n + e < p.N; ++e) {
           const long long off = bz * p.sC + mo * p.ldc + n + e;

@@ -32,6 +32,10 @@ struct GemmParams {
   const float* bn_scale;
   const float* bn_shift;
   int bn_relu;
+  // store dz (= dA * mask, the value the sums see) instead of dA: the consumer of dA is the BN
+  // backward, which then needs neither the mask nor a separate residual-gradient output (for an
+  // identity shortcut d(residual) = dz)
+  int bn_store_dz;
   const void* bn_y2;
   const float* bn_mean2;
   const float* bn_invstd2;

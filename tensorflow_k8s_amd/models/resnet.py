@@ -25,6 +25,10 @@ from ..runtime.layers import BatchNorm, Conv2d, Linear
 FUSE_POOL_BNR = os.environ.get("TFK_FUSE_POOL_BNR", "0") == "1"
 # projection shortcut (forward conv, lattice dgrad) on the side stream (runtime/streams.py)
 SIDE_SHORTCUT = os.environ.get("TFK_SIDE_SHORTCUT", "1") == "1"
+# the dgrad epilogues that feed a BN backward store dz = dA * relu-mask (BNReduce premask): the
+# BN-backward apply then reads no mask and an identity block's residual gradient is dz itself (no
+# second output pass). TFK_BN_PREMASK=0 restores the unmasked dA + separate dres for A/B.
+PREMASK = os.environ.get("TFK_BN_PREMASK", "1") == "1"
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
 
@@ -98,7 +102,7 @@ class Bottleneck:
         """BN-backward reduction spec of this block's tail (relu(bn3(y3) + shortcut)); fused into
         the epilogue of the NEXT block's final dgrad, which produces this block's dout."""
         x, y1, a1, y2, a2, y3, ysc, mk = self.saved
-        return BN.BNReduce(y3, self.bn3.st, a=mk, y2=ysc, st2=self.bn_sc.st if self.proj else None)
+        return BN.BNReduce(y3, self.bn3.st, a=mk, y2=ysc, st2=self.bn_sc.st if self.proj else None, premask=PREMASK)
 
     def backward(self, dout, need_dx=True, dout_reduced=False, next_bnr: BN.BNReduce | None = None):
         """dout_reduced: the producer of dout already accumulated this block's tail BN sums.
@@ -110,12 +114,14 @@ class Bottleneck:
             dy3, dysc, _ = BN.bn_backward(dout, mk, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
                                           self.bn3.beta.grad, cnt3, y2=ysc, st2=self.bn_sc.st,
                                           gamma2=self.bn_sc.gamma.master, dgamma2=self.bn_sc.gamma.grad,
-                                          dbeta2=self.bn_sc.beta.grad, reduced=dout_reduced)
+                                          dbeta2=self.bn_sc.beta.grad, reduced=dout_reduced,
+                                          premasked=dout_reduced and PREMASK)
             dres = None
             self.arena.grad_ready(self.bn3.gamma, self.bn3.beta, self.bn_sc.gamma, self.bn_sc.beta)
         else:
             dy3, _, dres = BN.bn_backward(dout, mk, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
-                                          self.bn3.beta.grad, cnt3, want_dres=True, reduced=dout_reduced)
+                                          self.bn3.beta.grad, cnt3, want_dres=True, reduced=dout_reduced,
+                                          premasked=dout_reduced and PREMASK)
             self.arena.grad_ready(self.bn3.gamma, self.bn3.beta)
         lattice = self.proj and self.stride > 1 and need_dx and next_bnr is not None
         tl = []
@@ -124,13 +130,15 @@ class Bottleneck:
             # conv3 -> conv2 chain, joined before conv1's dgrad epilogue adds it
             streams.run_wgrad(lambda: tl.append(self.conv_sc.lattice_dgrad(dysc, x)), dysc, x)
         # bn2/bn1 have no residual input: relu mask recomputed from y, sums fused into the dgrad epilogue
-        da2 = self.conv3.backward(dy3, a2, bnr=BN.BNReduce(y2, self.bn2.st))
+        da2 = self.conv3.backward(dy3, a2, bnr=BN.BNReduce(y2, self.bn2.st, premask=PREMASK))
         dy2, _, _ = BN.bn_backward(da2, None, y2, self.bn2.st, self.bn2.gamma.master, self.bn2.gamma.grad,
-                                   self.bn2.beta.grad, y2.numel() // y2.shape[-1], relu_from_y=True, reduced=True)
+                                   self.bn2.beta.grad, y2.numel() // y2.shape[-1], relu_from_y=True, reduced=True,
+                                   premasked=PREMASK)
         self.arena.grad_ready(self.bn2.gamma, self.bn2.beta)
-        da1 = self.conv2.backward(dy2, a1, bnr=BN.BNReduce(y1, self.bn1.st))
+        da1 = self.conv2.backward(dy2, a1, bnr=BN.BNReduce(y1, self.bn1.st, premask=PREMASK))
         dy1, _, _ = BN.bn_backward(da1, None, y1, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
-                                   self.bn1.beta.grad, y1.numel() // y1.shape[-1], relu_from_y=True, reduced=True)
+                                   self.bn1.beta.grad, y1.numel() // y1.shape[-1], relu_from_y=True, reduced=True,
+                                   premasked=PREMASK)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
         if lattice:
             # strided projection: its dgrad only touches the stride lattice -> a dense GEMM over the

@@ -166,7 +166,8 @@ def _gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile, *, alpha=1.0
           aux=None, dact_src=None, dact=0, drop_p=0.0, drop_seed=0, rowmap=()):
     lib().gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile[0], tile[1], alpha, beta, bias, resid, act,
                stats, shards, splits, batch, sA, sB, sC, split_stride, conv,
-               bnr.gemm_args() if bnr is not None else [], int(bnr.relu) if bnr is not None else 0,
+               bnr.gemm_args() if bnr is not None else [],
+               (int(bnr.relu) | (2 if bnr.premask else 0)) if bnr is not None else 0,
                bnr.st.shards if bnr is not None else 1, aux, dact_src, dact, drop_p, drop_seed, list(rowmap))
 
 
@@ -461,7 +462,9 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
             dx = dx.to(torch.bfloat16).float() + resid.float()
         dx = dx.to(torch.bfloat16).contiguous()
         if bnr is not None:
-            bnr.reference_accumulate(dx)
+            dz = bnr.reference_accumulate(dx)
+            if bnr.premask:
+                dx = dz.to(torch.bfloat16).reshape(dx.shape).contiguous()
         return dx
     M = g.N * g.H * g.W
     dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)

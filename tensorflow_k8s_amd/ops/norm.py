@@ -115,10 +115,13 @@ class BNReduce:
     """Spec for fusing a BN-backward reduction into the epilogue of the GEMM that produces dA
     (dz = dA * mask; sums into st.sums). mask: `a > 0` if a is given (a: the bf16 activation or its
     packed relu bitmask), else `y*scale+shift > 0` when relu, else 1. y2/st2: projection-shortcut
-    BN sharing the same dz."""
+    BN sharing the same dz. premask: the GEMM stores dz instead of dA (the BN backward is dA's only
+    consumer: it then reads no mask, and an identity shortcut's gradient IS dz -- no second output)."""
 
-    def __init__(self, y, st: BNState, a=None, relu: bool = True, y2=None, st2: BNState | None = None):
+    def __init__(self, y, st: BNState, a=None, relu: bool = True, y2=None, st2: BNState | None = None,
+                 premask: bool = False):
         self.y, self.st, self.a, self.relu, self.y2, self.st2 = y, st, a, relu, y2, st2
+        self.premask = premask
 
     def gemm_args(self):
         st, st2 = self.st, self.st2
@@ -128,8 +131,8 @@ class BNReduce:
                 st.shift if (self.relu and self.a is None) else None, self.y2, st2.mean if st2 else None,
                 st2.invstd if st2 else None, st.sums]
 
-    def reference_accumulate(self, dA: torch.Tensor) -> None:
-        """CPU oracle of the fused reduction (shard 0 of st.sums)."""
+    def reference_accumulate(self, dA: torch.Tensor) -> torch.Tensor:
+        """CPU oracle of the fused reduction (shard 0 of st.sums). Returns dz (f32 [rows, C])."""
         C = self.st.C
         dz = dA.float().reshape(-1, C)
         y = self.y.float().reshape(-1, C)
@@ -143,19 +146,25 @@ class BNReduce:
         if self.y2 is not None:
             y2 = self.y2.float().reshape(-1, C)
             v[0, 2] += (dz * (y2 - self.st2.mean) * self.st2.invstd).sum(0)
+        return dz
 
 
 def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=None, st2: BNState | None = None,
                 gamma2=None, dgamma2=None, dbeta2=None, want_dres: bool = False, relu_from_y: bool = False,
-                reduced: bool = False):
+                reduced: bool = False, premasked: bool = False):
     """Backward of a = relu?(bn(y) [+ bn2(y2) | + r]).
 
     a: post-activation output (bf16, or its packed relu bitmask) used for the relu mask (None -> no
     relu, unless relu_from_y: the mask
     is recomputed as y*scale+shift > 0, valid when there is no residual input). reduced: the
     per-channel sums were already accumulated into st.sums by the producer's GEMM epilogue
-    (BNReduce). Returns (dy, dy2, dres). Writes dgamma/dbeta (and the second BN's)."""
+    (BNReduce). premasked: da already is dz (BNReduce(premask=True) producer): no mask is read
+    and dres is da itself. Returns (dy, dy2, dres). Writes dgamma/dbeta (and the second BN's)."""
     C = st.C
+    if premasked:
+        if not reduced:
+            raise ValueError("bn_backward: premasked da comes from a fused-reduce producer (reduced=True)")
+        a, relu_from_y = None, False
     if not on_gpu(da):
         dz = da.float()
         if a is not None:
@@ -174,7 +183,7 @@ def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=No
             s2 = (dz2 * xh2).sum(0)
             dgamma2.copy_(s2); dbeta2.copy_(s0)
             dy2 = ((gamma2 * st2.invstd) * (dz2 - s0 / count - xh2 * (s2 / count))).reshape(da.shape).to(torch.bfloat16)
-        dres = dz.to(torch.bfloat16) if want_dres else None
+        dres = (da if premasked else dz.to(torch.bfloat16)) if want_dres else None
         return dy, dy2, dres
     M = da.numel() // C
     L = lib()
@@ -188,6 +197,8 @@ def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=No
                       st2.coef if st2 else None)
     dy = torch.empty_like(da)
     dy2 = torch.empty_like(da) if y2 is not None else None
-    dres = torch.empty_like(da) if want_dres else None
+    dres = torch.empty_like(da) if (want_dres and not premasked) else None
     L.bn_bwd_apply(da, a, y, st.coef, dy, y2, st2.coef if st2 else None, dy2, dres, M, C, msc, msh)
+    if want_dres and premasked:
+        dres = da  # d(identity residual) = dz = da
     return dy, dy2, dres

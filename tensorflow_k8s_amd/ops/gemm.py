@@ -407,6 +407,20 @@ def dgrad_as_fwd_geom(g: ConvGeom) -> ConvGeom | None:
 DGRAD_AS_FWD = os.environ.get("TFK_DGRAD_AS_FWD", "1") == "1"
 # 64-channel dx: the 2-wave 128x64 BN epilogue measured slower (0.28 vs 0.22 ms); TFK_DGRAD_AS_FWD_MIN_C
 DGRAD_AS_FWD_MIN_C = int(os.environ.get("TFK_DGRAD_AS_FWD_MIN_C", 128))
+# 3x3 / stride-1 / pad-1 convs of ResNet stages 1-2 (56x56x64, 28x28x128) run on the halo-tile
+# direct conv (csrc/kernels/conv_halo.hip; the C++ g4 launcher picks it for these shapes), forward
+# and -- as a forward conv over dY -- dgrad. TFK_HALO=0 restores the implicit-GEMM gather.
+HALO = os.environ.get("TFK_HALO", "1") != "0"
+
+
+def halo_ok(f: ConvGeom) -> bool:
+    """The forward conv f is one the halo kernel serves (mirrors tfk_halo_launch's eligibility)."""
+    if not (HALO and G4_ENABLED and f.R == 3 and f.S == 3 and f.sh == 1 and f.sw == 1 and f.ph == 1
+            and f.pw == 1 and f.dh == 1 and f.dw == 1 and f.P == f.H and f.Q == f.W and f.H % 4 == 0):
+        return False
+    return (f.W == 56 and f.C == 64 and f.K == 64) or (f.W == 28 and f.C == 128 and f.K == 128)
+
+
 # Strided-conv dgrad phases (BN-reduce epilogue with the phase out-map) as forward convs over dY on
 # the LDS-DMA gather (needs the conv's Cout % 64 == 0); TFK_PHASES_AS_FWD=0: register-engine gather.
 PHASES_AS_FWD = os.environ.get("TFK_PHASES_AS_FWD", "1") == "1"
@@ -484,8 +498,9 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
     if g.pointwise:
         _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid, bnr=bnr)
         return dx
-    f = dgrad_as_fwd_geom(g) if (DGRAD_AS_FWD and G4_ENABLED and g.K % 64 == 0 and g.C >= DGRAD_AS_FWD_MIN_C
-                                 and g.C % 8 == 0) else None
+    f = dgrad_as_fwd_geom(g) if (DGRAD_AS_FWD and G4_ENABLED and g.K % 64 == 0 and g.C % 8 == 0) else None
+    if f is not None and g.C < DGRAD_AS_FWD_MIN_C and not halo_ok(f):
+        f = None
     if f is not None:
         wf = conv_weight_t(w, g, flip=True)  # [C][R][S][K]: the forward conv's OHWI weight
         Kd = g.R * g.S * g.K

@@ -239,3 +239,57 @@ def test_collective_ps_bf16_wire_tracks_f32(tmp_path, native_ext):
     assert max(abs(x - y) / abs(x) for x, y in zip(a, b)) <= 1e-2, traj
     assert a != b, traj
     assert 0.45 < wire["bf16"] / wire["f32"] < 0.6, wire
+
+
+def test_collective_ps_lr_schedule_matches_mwms(tmp_path, native_ext):
+    """LR warmup + cosine decay with the collective PS's bucket-by-bucket owner updates: the global
+    step (and so the learning rate / bias corrections) advances once per step however many buckets
+    a shard has (Optimizer.step_region), so the trajectory equals MWMS under the same schedule."""
+    sched = ["--warmup-steps", "3", "--lr-schedule", "cosine", "--comm-dtype", "f32", "--optimizer", "adamw",
+             "--lr", "0.01"]
+    p = free_port()
+    mw = _launch([("chief", 0), ("worker", 0)], {"chief": [f"c.svc:{p}"], "worker": ["w.svc:1"]}, BASE + sched,
+                 str(tmp_path))
+    assert all(v[0] == 0 for v in mw.values()), {k: v[2][-1500:] for k, v in mw.items()}
+    p = free_port()
+    out = _launch([("chief", 0), ("worker", 0), ("ps", 0), ("ps", 1)],
+                  {"chief": [f"c.svc:{p}"], "worker": ["w.svc:1"], "ps": ["p0.svc:1", "p1.svc:1"]},
+                  BASE + sched + ["--ps-transport", "rccl", "--bucket-mb", "0.01"], str(tmp_path))
+    assert all(v[0] == 0 for v in out.values()), {k: v[2][-1500:] for k, v in out.items()}
+    # the chief's own final loss (the logged train losses are a worker mean under MWMS only). Not
+    # bit-exact: the CPU AdamW update of a shard/bucket slice vs the whole arena rounds a few tail
+    # elements 1 ulp differently (vectorized vs scalar remainder loops) and Adam's 1/sqrt(v)
+    # amplifies that over 12 steps (~0.15 %); a step-count or schedule error would show as a
+    # whole-lr-factor difference (warmup lr(0) is 1/3 of lr(2)).
+    a, b = _final_loss(mw[("chief", 0)][1]), _final_loss(out[("chief", 0)][1])
+    assert abs(a - b) <= 5e-3 * max(1.0, abs(a)), (a, b)
+
+
+@pytest.mark.parametrize("device_schedule", [False, True])
+def test_step_region_advances_once_per_global_step(device_schedule):
+    """Three region updates per global step (PS buckets) == one whole-arena update, host or device
+    LR schedule (warmup), AdamW bias corrections included."""
+    from tensorflow_k8s_amd.models import build_model
+    from tensorflow_k8s_amd.runtime.optimizer import AdamW, LRSchedule
+    sched = LRSchedule(0.01, warmup=3, total=8, kind="cosine")
+    res = []
+    for split in (False, True):
+        m = build_model("lenet").to("cpu", seed=1)
+        opt = AdamW(m.arena, sched)
+        if device_schedule:
+            opt.enable_device_schedule()
+        n = m.arena.numel
+        cuts = [0, n // 3 // 64 * 64, 2 * n // 3 // 64 * 64, n]
+        for s in range(6):
+            g = torch.Generator().manual_seed(s)
+            m.arena.grad.copy_(torch.randn(n, generator=g))
+            if not split:
+                opt.step()
+                continue
+            for k in range(3):
+                opt.region = (cuts[k], cuts[k + 1])
+                opt.step_region(advance=k == 0)
+            opt.region = None
+        res.append((m.arena.master.clone(), opt.sync_step()))
+    assert res[0][1] == res[1][1] == 6
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-6, atol=1e-7)

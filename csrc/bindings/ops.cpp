@@ -25,6 +25,7 @@ int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, hipStream_t s);
 const unsigned long long* tfk_seed_key();
 void tfk_set_seed_key(const unsigned long long* k);
 int tfk_rng_advance(unsigned long long* st, unsigned long long stream, hipStream_t s);
+void tfk_halo_set(int on);
 int tfk_bn_finalize(float*, int, int, float, const float*, const float*, float, float, float*, float*, float*, float*,
                     float*, float*, hipStream_t);
 int tfk_bn_stats(const void*, long long, int, float*, int, hipStream_t);
@@ -721,6 +722,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("act_bwd", &act_bwd);
   m.def("dropout", &dropout);
   m.def("set_rng_key", &set_rng_key);
+  m.def("halo_set", &tfk_halo_set);  // 1/0: halo-tile 3x3 conv on/off, -1: back to TFK_HALO
   m.def("rng_advance", &rng_advance);
   m.def("add", &add);
   register_transformer_ops(m);

@@ -5,6 +5,8 @@
 #include "common.h"
 #include "gemm_params.h"
 
+#include <type_traits>
+
 namespace tfk {
 
 // BNR: + fused BN-backward reduction; EXT: + aux (pre-activation) store, activation-backward
@@ -178,22 +180,24 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     // load below is from an in-bounds address: absent tensors are not loaded at all (block-uniform
     // branches), and off the residual lattice the (unused) residual load reads C.
     constexpr int GB = BNRG > 0 ? BNRG : 1;
-    constexpr int G = bnr ? (NIT < GB ? NIT : GB) : (EPI == EPI_BF16_EXT ? (NIT < 2 ? NIT : 2) : (NIT < 4 ? NIT : 4));
+    constexpr int GCAP = bnr ? GB : (EPI == EPI_BF16_EXT ? 2 : 4);
+    constexpr int G = NIT < GCAP ? NIT : GCAP;
     if (tile_fast) {
       const bf16* resid_b = p.resid ? (const bf16*)p.resid : (const bf16*)p.C;
       const bf16* dsrc_b = (EPI == EPI_BF16_EXT && p.dact_src) ? (const bf16*)p.dact_src : (const bf16*)p.C;
       const bf16* y_b = bnr ? (const bf16*)p.bn_y : nullptr;
       const bf16* y2_b = bnr ? (p.bn_y2 ? (const bf16*)p.bn_y2 : y_b) : nullptr;
       const unsigned char* mk_b = bnr ? (p.bn_amask ? p.bn_amask : (const unsigned char*)y_b) : nullptr;
-#pragma unroll (bnr ? 1 : NIT)
-      for (int g0 = 0; g0 < NIT; g0 += G) {
-        bf16x8 cv[G], rr[G], zv[G], yv[G], y2v[G];
-        unsigned mk[G];
-        long long off[G];
-        bool rok[G];
-        int mlog[G], nlog[G];
+      // one group of GS chunks whose loads are all issued before its first store
+      auto group = [&](auto gsz, int g0) {
+        constexpr int GS = decltype(gsz)::value;
+        bf16x8 cv[GS], rr[GS], zv[GS], yv[GS], y2v[GS];
+        unsigned mk[GS];
+        long long off[GS];
+        bool rok[GS];
+        int mlog[GS], nlog[GS];
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
+        for (int g = 0; g < GS; ++g) {
           const int idx = tid + (g0 + g) * NT;
           const int row = idx / CPR, cc = idx - row * CPR;
           const int m = m0 + row, n = n0 + cc * 8;
@@ -216,7 +220,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           }
         }
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
+        for (int g = 0; g < GS; ++g) {
           bf16x8 v = cv[g];
           if constexpr (EPI == EPI_BF16_EXT) {
             // pre-activation chunk: [* act'(z)] -> [aux copy] -> act -> [dropout]
@@ -277,7 +281,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             }
           }
         }
-      }
+            };
+      // full groups of G chunks (rolled for BNR: VGPR budget), then a compile-time remainder group
+      // when G does not divide NIT (the halo conv's tiles: NIT = 7)
+      constexpr int NF = NIT / G, REM = NIT - NF * G;
+#pragma unroll (bnr ? 1 : NF)
+      for (int k = 0; k < NF; ++k) group(std::integral_constant<int, G>{}, k * G);
+      if constexpr (REM > 0) group(std::integral_constant<int, REM>{}, NF * G);
     } else {
 #pragma unroll 1
     for (int it = 0; it < NIT; ++it) {

@@ -407,10 +407,11 @@ def dgrad_as_fwd_geom(g: ConvGeom) -> ConvGeom | None:
 DGRAD_AS_FWD = os.environ.get("TFK_DGRAD_AS_FWD", "1") == "1"
 # 64-channel dx: the 2-wave 128x64 BN epilogue measured slower (0.28 vs 0.22 ms); TFK_DGRAD_AS_FWD_MIN_C
 DGRAD_AS_FWD_MIN_C = int(os.environ.get("TFK_DGRAD_AS_FWD_MIN_C", 128))
-# 3x3 / stride-1 / pad-1 convs of ResNet stages 1-2 (56x56x64, 28x28x128) run on the halo-tile
-# direct conv (csrc/kernels/conv_halo.hip; the C++ g4 launcher picks it for these shapes), forward
-# and -- as a forward conv over dY -- dgrad. TFK_HALO=0 restores the implicit-GEMM gather.
-HALO = os.environ.get("TFK_HALO", "1") != "0"
+# 3x3 / stride-1 / pad-1 convs of ResNet stage 1 (56x56x64) run on the halo-tile direct conv
+# (csrc/kernels/conv_halo.hip; the C++ g4 launcher picks it for these shapes), forward and -- as a
+# forward conv over dY -- dgrad. TFK_HALO=0 restores the implicit-GEMM gather; TFK_HALO=2 also
+# routes stage 2 (28x28x128, measured level with the gather).
+HALO = int(os.environ.get("TFK_HALO", "1"))
 
 
 def halo_ok(f: ConvGeom) -> bool:
@@ -418,7 +419,7 @@ def halo_ok(f: ConvGeom) -> bool:
     if not (HALO and G4_ENABLED and f.R == 3 and f.S == 3 and f.sh == 1 and f.sw == 1 and f.ph == 1
             and f.pw == 1 and f.dh == 1 and f.dw == 1 and f.P == f.H and f.Q == f.W and f.H % 4 == 0):
         return False
-    return (f.W == 56 and f.C == 64 and f.K == 64) or (f.W == 28 and f.C == 128 and f.K == 128)
+    return (f.W == 56 and f.C == 64 and f.K == 64) or (HALO >= 2 and f.W == 28 and f.C == 128 and f.K == 128)
 
 
 # Strided-conv dgrad phases (BN-reduce epilogue with the phase out-map) as forward convs over dY on

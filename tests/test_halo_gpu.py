@@ -11,7 +11,7 @@ from tensorflow_k8s_amd.ops._lib import lib
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(2, 56, 64), (2, 28, 128), (3, 28, 128)]
+SHAPES = [(2, 56, 64), (3, 56, 64), (2, 28, 128)]
 
 
 def _rel(a, b):
@@ -22,7 +22,7 @@ def _rel(a, b):
 @pytest.mark.parametrize("N,HW,C", SHAPES)
 def test_halo_forward_with_stats(N, HW, C):
     g = G.ConvGeom(N, HW, HW, C, C, 3, 3, 1, 1, 1, 1)
-    assert G.halo_ok(g)
+    level = 2 if C == 128 else 1  # stage-2 shapes are opt-in (TFK_HALO=2)
     torch.manual_seed(0)
     x = torch.randn(N, HW, HW, C).to(torch.bfloat16)
     w = (torch.randn(C, 3, 3, C) * 0.05).to(torch.bfloat16)
@@ -30,7 +30,7 @@ def test_halo_forward_with_stats(N, HW, C):
     y_ref = G.conv_fwd(x, w, g, stats=st_ref, shards=1)
     out = {}
     for halo in (1, 0):
-        lib().halo_set(halo)
+        lib().halo_set(level if halo else 0)
         try:
             st = torch.zeros(16 * 2 * C, device="cuda")
             y = G.conv_fwd(x.cuda(), w.cuda(), g, stats=st, shards=16)
@@ -49,7 +49,8 @@ def test_halo_forward_with_stats(N, HW, C):
 @pytest.mark.parametrize("premask", [False, True])
 def test_halo_dgrad_with_bn_reduce(N, HW, C, premask):
     g = G.ConvGeom(N, HW, HW, C, C, 3, 3, 1, 1, 1, 1)
-    assert G.halo_ok(G.dgrad_as_fwd_geom(g))
+    level = 2 if C == 128 else 1
+    assert G.dgrad_as_fwd_geom(g) is not None
     torch.manual_seed(1)
     dy = torch.randn(N, HW, HW, C).to(torch.bfloat16)
     w = (torch.randn(C, 3, 3, C) * 0.05).to(torch.bfloat16)
@@ -65,7 +66,7 @@ def test_halo_dgrad_with_bn_reduce(N, HW, C, premask):
     dx_ref = G.conv_dgrad(dy, w, g, bnr=ref)
     res = {}
     for halo in (1, 0):
-        lib().halo_set(halo)
+        lib().halo_set(level if halo else 0)
         try:
             b = spec("cuda")
             dx = G.conv_dgrad(dy.cuda(), w.cuda(), g, bnr=b)

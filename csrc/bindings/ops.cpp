@@ -26,6 +26,8 @@ const unsigned long long* tfk_seed_key();
 void tfk_set_seed_key(const unsigned long long* k);
 int tfk_rng_advance(unsigned long long* st, unsigned long long stream, hipStream_t s);
 void tfk_halo_set(int on);
+void tfk_w128_set(int v);
+void tfk_fp8_set_tile(int t);
 int tfk_bn_finalize(float*, int, int, float, const float*, const float*, float, float, float*, float*, float*, float*,
                     float*, float*, hipStream_t);
 int tfk_bn_stats(const void*, long long, int, float*, int, hipStream_t);
@@ -722,7 +724,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("act_bwd", &act_bwd);
   m.def("dropout", &dropout);
   m.def("set_rng_key", &set_rng_key);
-  m.def("halo_set", &tfk_halo_set);  // 1/0: halo-tile 3x3 conv on/off, -1: back to TFK_HALO
+  m.def("halo_set", &tfk_halo_set);
+  m.def("w128_set", &tfk_w128_set);
+  m.def("fp8_set_tile", &tfk_fp8_set_tile);  // fp8 g4 tile: 0 by shape, 128 / 256 forced, -1 -> TFK_FP8_TILE  // 0: g4 256x256, 1..4: w128 variant, -1: back to TFK_W128  // 1/0: halo-tile 3x3 conv on/off, -1: back to TFK_HALO
   m.def("rng_advance", &rng_advance);
   m.def("add", &add);
   register_transformer_ops(m);

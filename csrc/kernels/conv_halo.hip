@@ -145,14 +145,21 @@ __global__ __launch_bounds__(256, 2) void hconv_kernel(GemmParams p) {
     if (HB == 2 && tap == 0 && ch + 1 < CH) halo_issue<W, TR>(p, himg(ch + 1), n, h0, ch + 1, w, lane);
     const char* hs = himg(ch);
     const int toff = (tap / 3) * G::HW2 + (tap % 3);
+    // all of the tap's A fragments are read before its MFMAs: issued back to back, the ds_reads
+    // overlap each other and the first MFMAs wait for one fragment only (read-then-use per
+    // fragment exposed the LDS latency on every pair of MFMAs)
+    bf16x8 a[2][FM];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < FM; ++f) a[kk][f] = hfrag(hs, pix0[f], toff, kk);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
-        const bf16x8 a = hfrag(hs, pix0[f], toff, kk);
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(breg[s % D][kk][j], a, acc[f][j], 0, 0, 0);
+          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(breg[s % D][kk][j], a[kk][f], acc[f][j], 0, 0, 0);
       }
     }
     if (s + D < NSTEP) bload(s + D, breg[s % D]);

@@ -309,7 +309,9 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), (occ_default<BM, BN>())) v
                                                                                                int sld) {
   constexpr int NW = nwaves<BM, BN>(), NTH = NW * 64, WGM = BM / 64, WGN = BN / 64;
   constexpr int FM = 4, FN = 4;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  // + the K-tile's scale words of every A and B row ([BM] + [BN] u32), DMA'd with the operands
+  constexpr int SA_OFF = A_BYTES + B_BYTES, SB_OFF = SA_OFF + BM * 4, STAGE = SB_OFF + BN * 4;
   constexpr int MAIN = 2 * STAGE, EPIB = epi_lds_bytes<BM, BN, WGM>();
   __shared__ __attribute__((aligned(16))) char smem[MAIN > EPIB ? MAIN : EPIB];
 
@@ -334,16 +336,30 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), (occ_default<BM, BN>())) v
   la.init(p, lane, w, p.lda, m0, p.M);
   lb.init(p, lane, w, p.ldb, n0, p.N);
 
-  // scale rows of this lane's fragments (clamped: rows past M/N multiply zero-filled operands)
+  // Scales: the K-tile's 4 scale bytes of each row (one u32) go to LDS by LDS-DMA next to the
+  // operands (buffer_load_dword ... lds: 64 rows per instruction, lane-linear; rows past M/N are
+  // past num_records -> 0 and multiply zero-filled operands); waves 0 .. BM/64 + BN/64 - 1 issue
+  // one instruction each. Lane group g of a fragment then reads byte g of its row's word.
   const int g = lane >> 4, li = lane & 15;
-  const unsigned* sa_row[FM];
-  const unsigned* sb_row[FN];
+  constexpr int SCA_I = BM / 64, SC_I = BM / 64 + BN / 64;
+  static_assert(SC_I <= NW, "one scale DMA per wave");
+  const bool sc_issuer = w < SC_I;  // wave-uniform
+  const bool sc_is_a = w < SCA_I;
+  const int sc_row = (sc_is_a ? m0 + w * 64 : n0 + (w - SCA_I) * 64) + lane;
+  const int sc_img = sc_is_a ? SA_OFF + w * 256 : SB_OFF + (w - SCA_I) * 256;
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(sc_is_a ? p.a_scale : p.b_scale), (short)0,
+      (int)min((long long)(sc_is_a ? p.M : p.N) * sld, (long long)NREC), 0x00020000);
+  auto issue_scales = [&](int kt, char* stg) {
+    if (sc_issuer)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsc, (LDS_AS void*)(stg + sc_img), 4, sc_row * sld + kt * 4, 0, 0, 0);
+  };
+  auto read_scales = [&](const char* stg, int (&sa)[FM], int (&sb)[FN]) {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
-    sa_row[i] = (const unsigned*)((const unsigned char*)p.a_scale + (long long)min(m0 + wm * 64 + i * 16 + li, p.M - 1) * sld);
+    for (int i = 0; i < FM; ++i) sa[i] = *(const unsigned char*)(stg + SA_OFF + (wm * 64 + i * 16 + li) * 4 + g);
 #pragma unroll
-  for (int j = 0; j < FN; ++j)
-    sb_row[j] = (const unsigned*)((const unsigned char*)p.b_scale + (long long)min(n0 + wn * 64 + j * 16 + li, p.N - 1) * sld);
+    for (int j = 0; j < FN; ++j) sb[j] = *(const unsigned char*)(stg + SB_OFF + (wn * 64 + j * 16 + li) * 4 + g);
+  };
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -352,14 +368,10 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), (occ_default<BM, BN>())) v
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto stage_ptr = [&](int st) { return smem + st * STAGE; };
-  unsigned sa[FM], sb[FN];
   if (kt0 < kt1) {
     la.issue(p, Ab, BK * 2, kt0, lim_a, stage_ptr(0), w, lane);
     lb.issue(p, Bb, BK * 2, kt0, lim_b, stage_ptr(0) + A_BYTES, w, lane);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) sa[i] = sa_row[i][kt0];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) sb[j] = sb_row[j][kt0];
+    issue_scales(kt0, stage_ptr(0));
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -372,38 +384,29 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), (occ_default<BM, BN>())) v
     const char* As = stage_ptr(st);
     const char* Bs = As + A_BYTES;
     const bool more = kt + 1 < kt1;
-    unsigned sa_n[FM], sb_n[FN];
     if (more) {
       char* nx = stage_ptr(st ^ 1);
       la.issue(p, Ab, BK * 2, kt + 1, lim_a, nx, w, lane);
       lb.issue(p, Bb, BK * 2, kt + 1, lim_b, nx + A_BYTES, w, lane);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) sa_n[i] = sa_row[i][kt + 1];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) sb_n[j] = sb_row[j][kt + 1];
+      issue_scales(kt + 1, nx);
     }
+    int sa[FM], sb[FN];
+    read_scales(As, sa, sb);
     i32x8 bfr[FN];
-    int scb[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const bf16x8 lo = frag<false>(Bs, bc + j * 16, 0), hi = frag<false>(Bs, bc + j * 16, 1);
       bfr[j] = pack8(lo, hi);
-      scb[j] = (sb[j] >> (8 * g)) & 0xff;
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const bf16x8 lo = frag<false>(As, ar + i * 16, 0), hi = frag<false>(As, ar + i * 16, 1);
       const i32x8 a = pack8(lo, hi);
-      const int sca = (sa[i] >> (8 * g)) & 0xff;
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], a, acc[i][j], 0, 0, 0, scb[j], 0, sca);
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], a, acc[i][j], 0, 0, 0, sb[j], 0, sa[i]);
     }
     if (more) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) sa[i] = sa_n[i];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) sb[j] = sb_n[j];
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -518,6 +521,8 @@ static void fast_div(unsigned d, unsigned* mul, int* shift) {
 
 // p.tiles_n / p.kt_per_split set by the caller (tfk_gemm_launch). Returns -1 if not instantiated.
 extern "C" int tfk_halo_launch(const GemmParams& p, int epi, int batch, int splits, hipStream_t stream);
+extern "C" int tfk_w128_launch(const GemmParams& p, int amode, int bmode, int epi, int tiles, int batch, int splits,
+                               hipStream_t stream);
 
 extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, int bmode, int epi, int batch,
                              int splits, hipStream_t stream) {
@@ -536,6 +541,11 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
   if (amode == 2 && p.Cin < 64) {
     fast_div((unsigned)p.S, &p.fd_q_mul, &p.fd_q_shift);
     fast_div((unsigned)p.Cin, &p.fd_pq_mul, &p.fd_pq_shift);
+  }
+  // dense 256x256: the 1-wave-per-SIMD 128x128-wave-tile engine when selected (gemm_w128.h)
+  if (bm == 256 && bn == 256) {
+    const int r = tfk_w128_launch(p, amode, bmode, epi, tiles, batch, splits, stream);
+    if (r != -1) return r;
   }
   // many tiles: the persistent kernel on a resident grid (opt-in TFK_G4_PERSIST=1; measured slower
   // than the one-shot grid: sq4096 fwd 814 vs 854 TF, tfm_ffn1 772 vs 840, ResNet-50 29.01 vs
@@ -594,11 +604,19 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
 
 // MX-fp8 GEMM on the g4 engine. p in BYTES (K, lda, ldb = bytes per row); needs K % 128 == 0,
 // lda/ldb % 16 == 0 and 16-B aligned operands. Returns -1 when not eligible (caller falls back).
+// Tile of the fp8 engine: 0 = by shape (256x256 16-wave blocks when they fill the chip, else
+// 128x128), 128 / 256 = forced (TFK_FP8_TILE or tfk_fp8_set_tile).
+static int g_fp8_tile = -1;
+extern "C" void tfk_fp8_set_tile(int t) { g_fp8_tile = t; }
 extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hipStream_t stream) {
   GemmParams p = p_in;
   if ((p.K & 127) || (p.lda & 15) || (p.ldb & 15) || (((uintptr_t)p.A | (uintptr_t)p.B) & 15) ||
       (((uintptr_t)p.a_scale | (uintptr_t)p.b_scale) & 3))
     return -1;
+  if (g_fp8_tile < 0) {
+    const char* e = getenv("TFK_FP8_TILE");
+    g_fp8_tile = e ? atoi(e) : 0;
+  }
   const int sld = p.K / 32;
   p.K /= 2;
   p.lda /= 2;
@@ -608,15 +626,27 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
   if (splits > nkt) splits = nkt;
   p.kt_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
-  p.tiles_n = (p.N + 127) / 128;
-  const int tiles = ((p.M + 127) / 128) * p.tiles_n;
+  const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256);
+  const bool big = g_fp8_tile == 256 || (g_fp8_tile == 0 && p.M >= 256 && p.N >= 256 && t256 * splits >= 240);
+  const int T = big ? 256 : 128;
+  p.tiles_n = (p.N + T - 1) / T;
+  const int tiles = ((p.M + T - 1) / T) * p.tiles_n;
   if (p.stats_shards < 1) p.stats_shards = 1;
-  const dim3 grid(tiles, 1, splits), block(g4::nwaves<128, 128>() * 64);
-  if (epi == EPI_F32)
-    hipLaunchKernelGGL((g4::g4_fp8_kernel<128, 128, EPI_F32>), grid, block, 0, stream, p, sld);
-  else if (epi == EPI_BF16_EXT)
-    hipLaunchKernelGGL((g4::g4_fp8_kernel<128, 128, EPI_BF16_EXT>), grid, block, 0, stream, p, sld);
+  const dim3 grid(tiles, 1, splits);
+#define TFK_FP8_G4(BT)                                                                                          \
+  {                                                                                                             \
+    const dim3 block(g4::nwaves<BT, BT>() * 64);                                                                \
+    if (epi == EPI_F32)                                                                                         \
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_F32>), grid, block, 0, stream, p, sld);                 \
+    else if (epi == EPI_BF16_EXT)                                                                               \
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_BF16_EXT>), grid, block, 0, stream, p, sld);            \
+    else                                                                                                        \
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_BF16>), grid, block, 0, stream, p, sld);                \
+  }
+  if (big)
+    TFK_FP8_G4(256)
   else
-    hipLaunchKernelGGL((g4::g4_fp8_kernel<128, 128, EPI_BF16>), grid, block, 0, stream, p, sld);
+    TFK_FP8_G4(128)
+#undef TFK_FP8_G4
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

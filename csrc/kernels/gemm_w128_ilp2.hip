@@ -1,0 +1,27 @@
+// hipcc-flags: -mllvm -amdgpu-sched-strategy=iterative-ilp
+// w128 GEMM variant 3 (iterative-ILP scheduler, single-basic-block loop body); kernel body: gemm_w128.h
+#define W128_NS w128c
+#define W128_V2 1
+#define W128_SGB 0
+#include "gemm_w128.h"
+
+using namespace tfk;
+
+
+#define W128_CASE(AM_, BM2_, EPI_)                                                                 \
+  if (amode == AM_ && bmode == BM2_ && epi == EPI_) {                                              \
+    hipLaunchKernelGGL((w128c::w128_kernel<AM_, BM2_, EPI_>), dim3(tiles, batch, splits),            \
+                       dim3(w128c::NTH), 0, stream, p);                                             \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                               \
+  }
+// p.tiles_n / p.kt_per_split already set for 256x256 tiles by the caller (tfk_g4_launch)
+extern "C" int tfk_w128c_launch(const GemmParams& p, int amode, int bmode, int epi, int tiles, int batch, int splits,
+                              hipStream_t stream) {
+  W128_CASE(0, 0, EPI_BF16)
+  W128_CASE(0, 0, EPI_F32)
+  W128_CASE(0, 1, EPI_BF16)
+  W128_CASE(0, 1, EPI_F32)
+  W128_CASE(1, 1, EPI_F32)
+  W128_CASE(1, 1, EPI_BF16)
+  return -1;
+}

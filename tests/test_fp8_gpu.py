@@ -127,11 +127,13 @@ def test_fp8_training_tracks_bf16_200_steps():
     assert abs(mf - mb) <= 0.05 * mb + 0.02, (b[::20], f[::20])
 
 
+@pytest.mark.parametrize("tile", [128, 256])
 @pytest.mark.parametrize("M,N,K", [(512, 1024, 1024), (300, 200, 256), (1000, 520, 384)])
-def test_g4_fp8_engine_matches_register_engine(M, N, K):
+def test_g4_fp8_engine_matches_register_engine(M, N, K, tile):
     """The LDS-DMA (g4) MX-fp8 kernel and the register-staged one run the same quantized operands
     through the same scaled MFMAs in the same K order: results agree to f32 rounding, for the bf16
-    (bias/relu/residual), EXT (GELU-backward) and f32 (accumulate) epilogues, incl. ragged M/N."""
+    (bias/relu/residual), EXT (GELU-backward) and f32 (accumulate) epilogues, incl. ragged M/N, on
+    both g4 tiles (128x128 4-wave and 256x256 16-wave blocks; scales staged by LDS-DMA)."""
     from tensorflow_k8s_amd.ops._lib import lib
     g = torch.Generator().manual_seed(7)
     x = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
@@ -142,6 +144,7 @@ def test_g4_fp8_engine_matches_register_engine(M, N, K):
     dy = torch.randn(M, N, generator=g).to(torch.bfloat16).cuda()
     out = {}
     try:
+        lib().fp8_set_tile(tile)
         for eng in (1, 0):
             lib().fp8_set_engine(eng)
             y = F8.linear_fwd_mx(x, w, b, act="relu", resid=r)
@@ -153,6 +156,7 @@ def test_g4_fp8_engine_matches_register_engine(M, N, K):
             out[eng] = (y, dx, gw)
     finally:
         lib().fp8_set_engine(0)
+        lib().fp8_set_tile(-1)
     for a, c in zip(out[1], out[0]):
         if a is not None:
             assert rel(a, c) < 1e-5, rel(a, c)

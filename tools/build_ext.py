@@ -65,6 +65,17 @@ def _run(cmd: list[str]) -> None:
             raise
 
 
+def _extra_flags(src: str) -> list[str]:
+    """Per-file hipcc flags from a `// hipcc-flags: ...` line in the first lines of a .hip source
+    (e.g. a scheduler strategy for one GEMM variant)."""
+    with open(src) as f:
+        for _ in range(5):
+            line = f.readline()
+            if line.startswith("// hipcc-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
 def ext_path() -> str:
     return os.path.join(PKG, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
 
@@ -90,7 +101,7 @@ def build_kernels(jobs: int | None = None, verbose: bool = False) -> str:
         objs.append(out)
         if _stale(out, [src] + headers):
             tasks.append([HIPCC, "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}",
-                          "-munsafe-fp-atomics", "-Rpass-analysis=kernel-resource-usage", src, "-o", out])
+                          "-munsafe-fp-atomics"] + _extra_flags(src) + ["-Rpass-analysis=kernel-resource-usage", src, "-o", out])
     py_inc = sysconfig.get_paths()["include"]
     cpp_hdrs = glob.glob(os.path.join(ROOT, "cpp", "*", "*.h"))
     for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "bindings", "*.cpp"))):

@@ -21,7 +21,7 @@ extern "C" void tfk_fp8_set_engine(int e);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_quant_t(const void*, void*, void*, int, int, hipStream_t);
 int tfk_mx_probe(const int*, const int*, const int*, const int*, float*, hipStream_t);
-int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, hipStream_t s);
+int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, int splits, hipStream_t s);
 const unsigned long long* tfk_seed_key();
 void tfk_set_seed_key(const unsigned long long* k);
 int tfk_rng_advance(unsigned long long* st, unsigned long long stream, hipStream_t s);
@@ -334,7 +334,17 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
   p.dact = dact;
   p.beta = (float)beta;
   const int ext = f32 ? 2 : ((p.aux || drop_p > 0.0 || p.dact_src) ? 1 : 0);
-  check_rc(tfk_gemm_mxfp8(p, ext, cur_stream()), "gemm_mxfp8");
+  int splits = 1;
+  if (f32) {
+    // weight gradients: split-K chosen by the launcher (0 = auto), every split adding its partial
+    // into C with f32 atomics -- C is zeroed first unless accumulating (beta 1)
+    TORCH_CHECK(beta == 0.0 || beta == 1.0, "gemm_mxfp8: f32 output needs beta 0 or 1");
+    if (beta == 0.0) C.zero_();
+    p.beta = 1.f;
+    p.split_stride = -1;
+    splits = 0;
+  }
+  check_rc(tfk_gemm_mxfp8(p, ext, splits, cur_stream()), "gemm_mxfp8");
 }
 
 void bn_finalize(torch::Tensor stats, int shards, int C, double count, torch::Tensor gamma, torch::Tensor beta, double eps,

@@ -268,15 +268,19 @@ int tfk_mx_quant(const void* x, void* q, void* s, long long nblocks, hipStream_t
 // ext: 0 bf16 (bias/act/resid), 1 bf16 EXT (aux, dropout, activation backward), 2 f32 (alpha/beta:
 // weight gradients accumulate into the f32 arena).
 extern "C" int tfk_g4_fp8_launch(const GemmParams& p, int epi, int splits, hipStream_t stream);
-static int g_fp8_engine = -1;  // 1 = g4 LDS-DMA engine (TFK_FP8_ENGINE=g4), 0 = register-staged kernel below
+// 1 = g4 LDS-DMA engine (default; 256x256 16-wave tiles measured 1.4-1.7x the bf16 g4 GEMM,
+// profiles/fp8_engine_r3a.jsonl), 0 = the register-staged kernel below (TFK_FP8_ENGINE=reg).
+static int g_fp8_engine = -1;
 extern "C" void tfk_fp8_set_engine(int e) { g_fp8_engine = e; }
-int tfk_gemm_mxfp8(GemmParams p, int ext, hipStream_t st) {
+// splits: split-K count for the f32 (weight-gradient) output, 0 = chosen by the g4 launcher; the
+// caller set p.split_stride = -1 (atomic accumulation into a zeroed / accumulating C) for f32.
+int tfk_gemm_mxfp8(GemmParams p, int ext, int splits, hipStream_t st) {
   if (g_fp8_engine < 0) {
     const char* e = getenv("TFK_FP8_ENGINE");
-    g_fp8_engine = (e && e[0] == 'g') ? 1 : 0;
+    g_fp8_engine = (e && e[0] == 'r') ? 0 : 1;
   }
   if (g_fp8_engine == 1) {
-    const int r = tfk_g4_fp8_launch(p, ext == 2 ? EPI_F32 : (ext ? EPI_BF16_EXT : EPI_BF16), 1, st);
+    const int r = tfk_g4_fp8_launch(p, ext == 2 ? EPI_F32 : (ext ? EPI_BF16_EXT : EPI_BF16), splits, st);
     if (r != -1) return r;
   }
   const int BM = 128, BN = 128;

@@ -27,6 +27,7 @@
 // channels of one tap, so C % 8 == 0; the pixel of a K-tile row is found with magic-number
 // division). Epilogues: gemm_epilogue.h (LDS-staged).
 #include "common.h"
+#include <algorithm>
 #include "gemm_params.h"
 #include "gemm_epilogue.h"
 #include "g4_loader.h"
@@ -622,11 +623,21 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
   p.lda /= 2;
   p.ldb /= 2;
   const int nkt = (p.K + g4::BK - 1) / g4::BK;
+  const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256);
+  const long long t128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
+  if (splits == 0) {
+    // auto split-K (f32 atomic output only): fill ~one round of 256x256 blocks (or two of 128x128)
+    // with >= 8 K-tiles per split
+    const bool b = p.M >= 256 && p.N >= 256;
+    const long long t = b ? t256 : t128, target = b ? 256 : 512;
+    const long long want = (target + t - 1) / t;
+    splits = (int)std::max(1LL, std::min(want, (long long)std::max(1, nkt / 8)));
+    if (p.split_stride >= 0) splits = 1;
+  }
   if (splits < 1) splits = 1;
   if (splits > nkt) splits = nkt;
   p.kt_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
-  const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256);
   const bool big = g_fp8_tile == 256 || (g_fp8_tile == 0 && p.M >= 256 && p.N >= 256 && t256 * splits >= 240);
   const int T = big ? 256 : 128;
   p.tiles_n = (p.N + T - 1) / T;

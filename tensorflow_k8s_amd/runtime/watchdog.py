@@ -96,8 +96,11 @@ class StepWatchdog:
 def abort_communicators() -> int:
     """ncclCommAbort every live RCCL communicator of this process (parallel/tfk_comm). gloo groups
     of the CPU tier need no abort: os._exit closes their sockets and the peers' pending ops fail."""
+    import sys
+    mod = sys.modules.get(__name__.rsplit(".", 2)[0] + ".parallel.tfk_comm")
+    if mod is None:  # never imported -> no communicator exists; do not pay a torch import here
+        return 0
     try:
-        from ..parallel import tfk_comm
-        return tfk_comm.abort_all()
+        return mod.abort_all()
     except Exception:  # pragma: no cover - the process is exiting anyway
         return 0

@@ -155,7 +155,7 @@ def test_g4_fp8_engine_matches_register_engine(M, N, K, tile):
             torch.cuda.synchronize()
             out[eng] = (y, dx, gw)
     finally:
-        lib().fp8_set_engine(0)
+        lib().fp8_set_engine(-1)
         lib().fp8_set_tile(-1)
     for a, c in zip(out[1], out[0]):
         if a is not None:

@@ -42,7 +42,7 @@ def test_watchdog_default_exits_retryable(tmp_path):
     termination message."""
     term = tmp_path / "term"
     code = ("from tensorflow_k8s_amd.runtime.watchdog import StepWatchdog\n"
-            "import time\nStepWatchdog(0.2, poll_s=0.02).start()\ntime.sleep(5)\n")
+            "import time\nStepWatchdog(0.2, poll_s=0.02).start()\ntime.sleep(60)\n")
     env = dict(os.environ, TFK_TERMINATION_LOG=str(term), PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
     assert r.returncode == EXIT_RETRY, r.stderr

@@ -66,6 +66,16 @@ def main():
         lib().fp8_set_tile(-1)
         row["bf16_g4"] = tflops(lambda: G.linear_fwd(x, w, out=y), fl, args.iters)
         row["bf16_blas"] = tflops(lambda: x @ w.t(), fl, args.iters)
+        # backward GEMMs through the production entry points (fp8: incl. their quantize passes)
+        dy = (torch.rand(M, N, device="cuda") * 2 - 1).to(torch.bfloat16)
+        gw = torch.zeros(N, K, device="cuda")
+        if N % 128 == 0:
+            row["fp8_dgrad_incl_quant"] = tflops(lambda: F8.linear_dgrad_mx(dy, w), fl, args.iters)
+        row["bf16_dgrad"] = tflops(lambda: G.linear_dgrad(dy, w), fl, args.iters)
+        if M % 128 == 0:
+            row["fp8_wgrad_incl_quant"] = tflops(lambda: F8.linear_wgrad_mx(dy, x, gw), fl, args.iters)
+        row["bf16_wgrad"] = tflops(lambda: G.linear_wgrad(dy, x, gw), fl, args.iters)
+        del dy, gw
         print(json.dumps(row), flush=True)
         del x, w, xq, wq, y
         torch.cuda.empty_cache()

@@ -20,6 +20,7 @@ void tfk_g4_set_persist(int on);
 extern "C" void tfk_fp8_set_engine(int e);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_quant_t(const void*, void*, void*, int, int, hipStream_t);
+int tfk_mx_quant_dual(const void*, void*, void*, void*, void*, int, int, hipStream_t);
 int tfk_mx_probe(const int*, const int*, const int*, const int*, float*, hipStream_t);
 int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, int splits, hipStream_t s);
 const unsigned long long* tfk_seed_key();
@@ -291,13 +292,27 @@ void mx_quant_t(torch::Tensor x, torch::Tensor q, torch::Tensor s, int64_t R, in
   check_rc(tfk_mx_quant_t(x.data_ptr(), q.data_ptr(), s.data_ptr(), (int)R, (int)C, cur_stream()), "mx_quant_t");
 }
 
+// Both MX quantizations in one read: x bf16 [R][C] -> row blocks (qr [R][C], sr [R][C/32]) and
+// column blocks (qc [C][R], sc [C][R/32]); R % 32 == 0, C % 32 == 0
+void mx_quant_dual(torch::Tensor x, torch::Tensor qr, torch::Tensor sr, torch::Tensor qc, torch::Tensor sc, int64_t R,
+                   int64_t C) {
+  need_bf16(x, "x");
+  for (auto* t : {&qr, &sr, &qc, &sc}) need(*t, at::kByte, "mx dual out");
+  TORCH_CHECK(R % 32 == 0 && C % 32 == 0 && R > 0 && C > 0, "mx_quant_dual needs R % 32 == 0 and C % 32 == 0");
+  need_numel(x, R * C, "x"); need_numel(qr, R * C, "qr"); need_numel(qc, R * C, "qc");
+  need_numel(sr, R * C / 32, "sr"); need_numel(sc, R * C / 32, "sc");
+  for (auto* t : {&x, &qr, &qc}) need_aligned(*t, 16, "mx dual tensor");
+  check_rc(tfk_mx_quant_dual(x.data_ptr(), qr.data_ptr(), sr.data_ptr(), qc.data_ptr(), sc.data_ptr(), (int)R, (int)C,
+                             cur_stream()), "mx_quant_dual");
+}
+
 // C[M][N] = epilogue(Aq[M][K] . Bq[N][K]^T) with e8m0 block scales (one per 32 K-elements).
 // C bf16: bias / act / resid / aux / dropout / activation backward (dact_src, dact);
 // C f32: C = alpha * AB + beta * C (weight gradients).
 void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tensor Bs, torch::Tensor C, int M, int N, int K,
                 c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, int act,
                 c10::optional<torch::Tensor> aux, double drop_p, int64_t drop_seed,
-                c10::optional<torch::Tensor> dact_src, int dact, double beta) {
+                c10::optional<torch::Tensor> dact_src, int dact, double beta, int splits, int64_t split_stride) {
   for (auto* t : {&A, &As, &B, &Bs}) need(*t, at::kByte, "mx operand");
   const bool f32 = C.scalar_type() == at::kFloat;
   if (!f32) need_bf16(C, "C");
@@ -306,7 +321,8 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
   TORCH_CHECK(M > 0 && N > 0 && K > 0 && K % 128 == 0, "gemm_mxfp8 needs K % 128 == 0, got ", K);
   need_numel(A, (long long)M * K, "A"); need_numel(B, (long long)N * K, "B");
   need_numel(As, (long long)M * K / 32, "As"); need_numel(Bs, (long long)N * K / 32, "Bs");
-  need_numel(C, (long long)M * N, "C");
+  TORCH_CHECK(splits >= 1 && (splits == 1 || (f32 && split_stride >= (long long)M * N)), "gemm_mxfp8: split-K needs f32 slabs");
+  need_numel(C, splits > 1 ? (long long)(splits - 1) * split_stride + (long long)M * N : (long long)M * N, "C");
   for (auto* t : {&A, &B, &C}) need_aligned(*t, 16, "gemm_mxfp8 operand");
   for (auto* t : {&As, &Bs}) need_aligned(*t, 4, "gemm_mxfp8 scales");
   TORCH_CHECK(act >= 0 && act <= 3, "act");
@@ -334,16 +350,8 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
   p.dact = dact;
   p.beta = (float)beta;
   const int ext = f32 ? 2 : ((p.aux || drop_p > 0.0 || p.dact_src) ? 1 : 0);
-  int splits = 1;
-  if (f32) {
-    // weight gradients: split-K chosen by the launcher (0 = auto), every split adding its partial
-    // into C with f32 atomics -- C is zeroed first unless accumulating (beta 1)
-    TORCH_CHECK(beta == 0.0 || beta == 1.0, "gemm_mxfp8: f32 output needs beta 0 or 1");
-    if (beta == 0.0) C.zero_();
-    p.beta = 1.f;
-    p.split_stride = -1;
-    splits = 0;
-  }
+  // f32 split-K: split z writes its partial to the slab C + z * split_stride (ops.fp8 reduces them)
+  p.split_stride = splits > 1 ? split_stride : 0;
   check_rc(tfk_gemm_mxfp8(p, ext, splits, cur_stream()), "gemm_mxfp8");
 }
 
@@ -698,10 +706,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("fp8_set_engine", &fp8_set_engine);
   m.def("mx_quant", &mx_quant);
   m.def("mx_quant_t", &mx_quant_t);
+  m.def("mx_quant_dual", &mx_quant_dual);
   m.def("mx_probe", &mx_probe);
   m.def("gemm_mxfp8", &gemm_mxfp8, py::arg("A"), py::arg("As"), py::arg("B"), py::arg("Bs"), py::arg("C"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("bias"), py::arg("resid"), py::arg("act"), py::arg("aux"), py::arg("drop_p"),
-        py::arg("drop_seed"), py::arg("dact_src") = py::none(), py::arg("dact") = 0, py::arg("beta") = 0.0);
+        py::arg("drop_seed"), py::arg("dact_src") = py::none(), py::arg("dact") = 0, py::arg("beta") = 0.0,
+        py::arg("splits") = 1, py::arg("split_stride") = 0);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);

@@ -117,3 +117,13 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
 }
+// Elementwise dropout masks (GEMM epilogues, dropout kernels, LayerNorm-backward dropout): the
+// 64-bit seed (salt + per-step key) folds once into a 32-bit stream seed, then ONE hash32 per
+// element index (indices < 2^32): ~7 VALU ops per element instead of hash_u32's ~35, which made the
+// dropout-carrying GEMM epilogues VALU-bound (ops/elementwise.py dropout_keep is the CPU copy).
+__device__ __forceinline__ uint32_t drop_seed32(unsigned long long s) {
+  return hash32((uint32_t)s ^ hash32((uint32_t)(s >> 32) ^ 0x9E3779B9u));
+}
+__device__ __forceinline__ bool drop_keep(uint32_t s32, unsigned long long idx, float keep) {
+  return u01(hash32(s32 ^ (uint32_t)idx)) < keep;
+}

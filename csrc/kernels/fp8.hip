@@ -149,8 +149,84 @@ __global__ __launch_bounds__(NTF, 2) void mxfp8_gemm_kernel(GemmParams p) {
   gemm_epilogue<BM, BN, NTF, WM, EPI>(p, acc, smem, m0, n0, 0);
 }
 
-// x bf16 [rows][K] -> q e4m3 [rows][K] + s e8m0 [rows][K/32]; one thread per 32-element block.
+// One MX block: 32 values -> 32 e4m3 bytes (w[0..7], little-endian in K order) + the e8m0 exponent.
 // scale exponent e = ceil(log2(amax / 448)) so every |x| * 2^-e <= 448 (no saturation).
+__device__ __forceinline__ int mx_block(const float (&v)[32], unsigned (&w)[8]) {
+  float amax = 0.f;
+#pragma unroll
+  for (int e = 0; e < 32; ++e) amax = fmaxf(amax, fabsf(v[e]));
+  int ex = amax > 0.f ? (int)ceilf(log2f(amax * (1.f / 448.f))) : -127;
+  ex = ex < -127 ? -127 : (ex > 127 ? 127 : ex);
+  const float inv = ldexpf(1.f, -ex);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float a0 = fminf(fmaxf(v[4 * k] * inv, -448.f), 448.f), a1 = fminf(fmaxf(v[4 * k + 1] * inv, -448.f), 448.f);
+    float a2 = fminf(fmaxf(v[4 * k + 2] * inv, -448.f), 448.f), a3 = fminf(fmaxf(v[4 * k + 3] * inv, -448.f), 448.f);
+    int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+    pk = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, pk, true);
+    w[k] = (unsigned int)pk;
+  }
+  return ex;
+}
+
+// Both MX quantizations of x bf16 [R][C] in ONE read: row blocks (q_r [R][C], s_r [R][C/32], the
+// forward / dgrad operand) and column blocks (q_c [C][R], s_c [C][R/32] = MX of x^T, the weight-
+// gradient operand). Block = a 128 x 128 tile staged in LDS (16-B lane-linear loads); 256 threads
+// each quantize 2 row blocks and 2 column blocks. 128 x 128 makes every e4m3 store pattern full
+// 128-B lines per block: a row of q_r gets 4 consecutive 32-B blocks, a row of q_c (a column of x)
+// gets its 4 row groups -- with 32-row tiles each q_c line was written in 4 quarters by 4
+// different blocks (measured 45% of the HBM floor in Transformer-big). R % 32 == 0, C % 32 == 0.
+constexpr int QT = 128, QLD = QT + 8;
+__global__ __launch_bounds__(256) void mx_quant_dual_kernel(const bf16* __restrict__ x, unsigned char* __restrict__ qr,
+                                                            unsigned char* __restrict__ sr, unsigned char* __restrict__ qc,
+                                                            unsigned char* __restrict__ sc, int R, int C) {
+  __shared__ __attribute__((aligned(16))) bf16 tile[QT][QLD];
+  const int r0 = blockIdx.y * QT, c0 = blockIdx.x * QT, t = threadIdx.x;
+  const int rows = min(QT, R - r0), cols = min(QT, C - c0);
+#pragma unroll
+  for (int i = 0; i < QT * QT / 8 / 256; ++i) {
+    const int idx = t + i * 256, row = idx >> 4, ch = (idx & 15) * 8;
+    if (row < rows && ch < cols) *(bf16x8*)&tile[row][ch] = *(const bf16x8*)(x + (long long)(r0 + row) * C + c0 + ch);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int pr = t + k * 256, row = pr >> 2, blk = pr & 3;
+    if (row < rows && blk * 32 < cols) {
+      float v[32];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bf16x8 h = *(const bf16x8*)&tile[row][blk * 32 + q * 8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[q * 8 + e] = bf2f(h[e]);
+      }
+      unsigned w[8];
+      const int ex = mx_block(v, w);
+      const int c = c0 + blk * 32;
+      unsigned char* dst = qr + (long long)(r0 + row) * C + c;
+      *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+      *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+      sr[(long long)(r0 + row) * (C / 32) + c / 32] = (unsigned char)(ex + 127);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int pc = t + k * 256, col = pc & (QT - 1), rg = pc >> 7;
+    if (col < cols && rg * 32 < rows) {
+      float v[32];
+#pragma unroll
+      for (int r = 0; r < 32; ++r) v[r] = bf2f(tile[rg * 32 + r][col]);
+      unsigned w[8];
+      const int ex = mx_block(v, w);
+      unsigned char* dst = qc + (long long)(c0 + col) * R + r0 + rg * 32;
+      *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+      *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+      sc[(long long)(c0 + col) * (R / 32) + r0 / 32 + rg] = (unsigned char)(ex + 127);
+    }
+  }
+}
+
+// x bf16 [rows][K] -> q e4m3 [rows][K] + s e8m0 [rows][K/32]; one thread per 32-element block.
 __global__ void mx_quant_kernel(const bf16* __restrict__ x, unsigned char* __restrict__ q,
                                 unsigned char* __restrict__ s, long long nblocks) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nblocks; i += (long long)gridDim.x * 256) {
@@ -256,6 +332,13 @@ int tfk_mx_quant_t(const void* x, void* q, void* s, int R, int C, hipStream_t st
   hipLaunchKernelGGL(mx_quant_t_kernel, grid, dim3(256), 0, st, (const bf16*)x, (unsigned char*)q, (unsigned char*)s, R, C);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+int tfk_mx_quant_dual(const void* x, void* qr, void* sr, void* qc, void* sc, int R, int C, hipStream_t st) {
+  if (R % 32 || C % 32 || R <= 0 || C <= 0) return -1;
+  dim3 grid((unsigned)((C + QT - 1) / QT), (unsigned)((R + QT - 1) / QT));
+  hipLaunchKernelGGL(mx_quant_dual_kernel, grid, dim3(256), 0, st, (const bf16*)x, (unsigned char*)qr,
+                     (unsigned char*)sr, (unsigned char*)qc, (unsigned char*)sc, R, C);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 int tfk_mx_quant(const void* x, void* q, void* s, long long nblocks, hipStream_t st) {
   long long g = (nblocks + 255) / 256;
   if (g > 8192) g = 8192;
@@ -272,8 +355,8 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p, int epi, int splits, hipSt
 // profiles/fp8_engine_r3a.jsonl), 0 = the register-staged kernel below (TFK_FP8_ENGINE=reg).
 static int g_fp8_engine = -1;
 extern "C" void tfk_fp8_set_engine(int e) { g_fp8_engine = e; }
-// splits: split-K count for the f32 (weight-gradient) output, 0 = chosen by the g4 launcher; the
-// caller set p.split_stride = -1 (atomic accumulation into a zeroed / accumulating C) for f32.
+// splits: split-K count of the f32 (weight-gradient) output, slab z at C + z * p.split_stride (the
+// register engine below runs unsplit: only the g4 engine takes splits > 1).
 int tfk_gemm_mxfp8(GemmParams p, int ext, int splits, hipStream_t st) {
   if (g_fp8_engine < 0) {
     const char* e = getenv("TFK_FP8_ENGINE");
@@ -283,6 +366,7 @@ int tfk_gemm_mxfp8(GemmParams p, int ext, int splits, hipStream_t st) {
     const int r = tfk_g4_fp8_launch(p, ext == 2 ? EPI_F32 : (ext ? EPI_BF16_EXT : EPI_BF16), splits, st);
     if (r != -1) return r;
   }
+  if (splits > 1) return -1;
   const int BM = 128, BN = 128;
   p.tiles_n = (p.N + BN - 1) / BN;
   if (p.stats_shards < 1) p.stats_shards = 1;

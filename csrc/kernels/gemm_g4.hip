@@ -624,16 +624,6 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
   p.ldb /= 2;
   const int nkt = (p.K + g4::BK - 1) / g4::BK;
   const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256);
-  const long long t128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
-  if (splits == 0) {
-    // auto split-K (f32 atomic output only): fill ~one round of 256x256 blocks (or two of 128x128)
-    // with >= 8 K-tiles per split
-    const bool b = p.M >= 256 && p.N >= 256;
-    const long long t = b ? t256 : t128, target = b ? 256 : 512;
-    const long long want = (target + t - 1) / t;
-    splits = (int)std::max(1LL, std::min(want, (long long)std::max(1, nkt / 8)));
-    if (p.split_stride >= 0) splits = 1;
-  }
   if (splits < 1) splits = 1;
   if (splits > nkt) splits = nkt;
   p.kt_per_split = (nkt + splits - 1) / splits;

@@ -199,9 +199,9 @@ __global__ void act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restri
 __global__ void dropout_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long long n, float p,
                                unsigned long long salt, const unsigned long long* __restrict__ key) {
   const float keep = 1.f - p, inv = 1.f / keep;
-  const unsigned long long seed = eff_seed(salt, key);
+  const uint32_t s32 = drop_seed32(eff_seed(salt, key));
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
-    bool k = u01(hash_u32(seed, i)) < keep;
+    bool k = drop_keep(s32, (unsigned long long)i, keep);
     y[i] = f2bf(k ? bf2f(x[i]) * inv : 0.f);
   }
 }
@@ -211,13 +211,13 @@ __global__ void dropout_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
 __global__ void dropout8_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long long n8, float p,
                                 unsigned long long salt, const unsigned long long* __restrict__ key) {
   const float keep = 1.f - p, inv = 1.f / keep;
-  const unsigned long long seed = eff_seed(salt, key);
+  const uint32_t s32 = drop_seed32(eff_seed(salt, key));
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long long)gridDim.x * NT) {
     const bf16x8 v = *(const bf16x8*)(x + i * 8);
     bf16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const bool k = u01(hash_u32(seed, (unsigned long long)(i * 8 + e))) < keep;
+      const bool k = drop_keep(s32, (unsigned long long)(i * 8 + e), keep);
       o[e] = f2bf(k ? bf2f(v[e]) * inv : 0.f);
     }
     *(bf16x8*)(y + i * 8) = o;

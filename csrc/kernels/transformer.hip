@@ -134,7 +134,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
           bf16x8 od;
 #pragma unroll
           for (int e = 0; e < 8; ++e)
-            od[e] = f2bf(u01(hash_u32(drop_seed, base + e)) < keep ? bf2f(o[e]) * inv : 0.f);
+            od[e] = f2bf(drop_keep(drop_seed32(drop_seed), base + e, keep) ? bf2f(o[e]) * inv : 0.f);
           *(bf16x8*)(dxd + base) = od;
         }
       }

@@ -283,6 +283,9 @@ class Transformer:
         (biases, LayerNorm gamma/beta) are zeroed in one fill up front and accumulated by their kernels."""
         self.arena.zero_nodecay_grads()
         E.rng_advance(self.rng_state, self.rng_stream)
+        if self.cfg.fp8:
+            from ..ops.fp8 import clear_saved
+            clear_saved()  # transposed MX operands live from this step's forward to its backward
         try:
             with E.rng_key(self.rng_state):
                 return self._forward_backward(src, tgt_in, tgt_out, src_len, loss_scale)

@@ -40,6 +40,23 @@ def u01(h: torch.Tensor) -> torch.Tensor:
     return (h >> 8).float() * (1.0 / 16777216.0)
 
 
+def hash32(x):
+    """Bit-exact copy of common.h hash32 (lowbias32) on int64 tensors holding uint32 (or ints)."""
+    m = 0xFFFFFFFF
+    x = x & m
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & m
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & m
+    return x ^ (x >> 16)
+
+
+def drop_seed32(seed: int) -> int:
+    """common.h drop_seed32: the 64-bit dropout seed folded to the 32-bit stream seed."""
+    s = int(seed) & 0xFFFFFFFFFFFFFFFF
+    return int(hash32((s & 0xFFFFFFFF) ^ int(hash32(((s >> 32) ^ 0x9E3779B9) & 0xFFFFFFFF))))
+
+
 # ------------------------------------------------------------------ per-step device RNG key
 # Dropout seed = host per-site salt + a per-step key that lives ON THE DEVICE in the model's rng state
 # (int64 [counter, key]). rng_advance() steps it inside the training step, so a replayed hipGraph
@@ -86,7 +103,8 @@ def eff_seed(salt: int) -> int:
 
 def dropout_keep(seed: int, n: int, p: float) -> torch.Tensor:
     """Keep-mask of the dropout kernel / fused GEMM dropout over a contiguous tensor of n elements."""
-    return u01(hash_u32(seed, torch.arange(n, dtype=torch.int64))) < (1.0 - p)
+    idx = torch.arange(n, dtype=torch.int64) & 0xFFFFFFFF
+    return u01(hash32(drop_seed32(seed) ^ idx)) < (1.0 - p)
 
 
 def act_fwd(x: torch.Tensor, act: str | None, bias: torch.Tensor | None = None) -> torch.Tensor:

@@ -56,17 +56,68 @@ def mx_dequantize(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
     return (v * torch.exp2(s.cpu().float() - 127)[..., None]).reshape(rows, K)
 
 
+def mx_quantize_dual(x: torch.Tensor):
+    """bf16 [R, C] (R, C % 32 == 0) -> (MX of x along C, MX of x^T along R) from ONE read of x:
+    ((q [R, C], s [R, C/32]), (qt [C, R], st [C, R/32]))."""
+    R, C = x.shape
+    if R % MX_BLOCK or C % MX_BLOCK:
+        raise ValueError(f"dual MX quantization needs R, C % 32 == 0, got {R}x{C}")
+    if not on_gpu(x):
+        return mx_quantize(x), mx_quantize(x.t().contiguous())
+    q = torch.empty(R, C, dtype=torch.uint8, device=x.device)
+    s = torch.empty(R, C // MX_BLOCK, dtype=torch.uint8, device=x.device)
+    qt = torch.empty(C, R, dtype=torch.uint8, device=x.device)
+    st = torch.empty(C, R // MX_BLOCK, dtype=torch.uint8, device=x.device)
+    lib().mx_quant_dual(x.contiguous(), q, s, qt, st, R, C)
+    return (q, s), (qt, st)
+
+
+# Transposed MX operands produced in the forward for the backward of the same step: the forward
+# quantizes its input x and weight w in both directions with one read each (mx_quantize_dual) and
+# parks MX(x^T) (weight-gradient operand) and MX(w^T) (dgrad operand) here, keyed by the data
+# pointer of the tensor the backward will pass. An entry holds a reference to its source tensor,
+# so that memory cannot be reused by another tensor while the entry exists; the backward pops it.
+_SAVED: dict[int, tuple] = {}
+
+
+def save_t(x: torch.Tensor, qt) -> None:
+    if len(_SAVED) > 4096:  # forwards without backwards (evaluation): do not grow without bound
+        _SAVED.clear()
+    _SAVED[x.data_ptr()] = (x, tuple(x.shape), qt)
+
+
+def take_t(x: torch.Tensor):
+    e = _SAVED.pop(x.data_ptr(), None)
+    return e[2] if e is not None and e[1] == tuple(x.shape) else None
+
+
+def clear_saved() -> None:
+    _SAVED.clear()
+
+
 def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
                   resid: torch.Tensor | None = None, aux: torch.Tensor | None = None, drop_p: float = 0.0,
-                  drop_seed: int = 0, wq=None) -> torch.Tensor:
-    """y[M,N] = dropout(act(MX(x) @ MX(w)^T + bias)) (+ resid), bf16 out. wq: pre-quantized weight."""
+                  drop_seed: int = 0, wq=None, save: bool = False) -> torch.Tensor:
+    """y[M,N] = dropout(act(MX(x) @ MX(w)^T + bias)) (+ resid), bf16 out. wq: pre-quantized weight.
+    save: also produce MX(x^T) / MX(w^T) for this step's backward (save_t) where it will use fp8."""
     K = x.shape[-1]
     x2 = x.reshape(-1, K)
     M, N = x2.shape[0], w.shape[0]
     if K % 128:
         raise ValueError(f"MX-fp8 GEMM needs K % 128 == 0, got {K}")
-    xq, xs = mx_quantize(x2)
-    wq_, ws_ = wq if wq is not None else mx_quantize(w)
+    dg_ok, wg_ok = mx_backward_ok(M, N, K)
+    if save and wg_ok:
+        (xq, xs), xt = mx_quantize_dual(x2)
+        save_t(x2, xt)
+    else:
+        xq, xs = mx_quantize(x2)
+    if wq is not None:
+        wq_, ws_ = wq
+    elif save and dg_ok and w.is_contiguous():
+        (wq_, ws_), wt = mx_quantize_dual(w)
+        save_t(w, wt)
+    else:
+        wq_, ws_ = mx_quantize(w)
     if not on_gpu(x):
         y = mx_dequantize(xq, xs) @ mx_dequantize(wq_, ws_).t()
         if bias is not None:
@@ -107,37 +158,70 @@ def mx_backward_ok(M: int, N: int, K: int) -> tuple[bool, bool]:
 
 
 def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None = None,
-                    dact_src: torch.Tensor | None = None, dact: str | None = None, wt=None) -> torch.Tensor:
-    """dx[M,K] = (MX(dy) @ MX(w^T)^T) [* act'(dact_src)] (+ resid), bf16. wt: pre-quantized w^T."""
+                    dact_src: torch.Tensor | None = None, dact: str | None = None, wt=None, dyq=None,
+                    drop_p: float = 0.0, drop_seed: int = 0) -> torch.Tensor:
+    """dx[M,K] = dropout((MX(dy) @ MX(w^T)^T) [* act'(dact_src)]) (+ resid), bf16 -- the bf16
+    linear_dgrad's epilogue order. wt: pre-quantized w^T (else the one the forward saved, else
+    quantized here); dyq: pre-quantized dy."""
     M, N = dy.shape
     K = w.shape[1]
-    dq, ds = mx_quantize(dy)
+    dq, ds = dyq if dyq is not None else mx_quantize(dy)
+    if wt is None:
+        wt = take_t(w)
     wq_, ws_ = wt if wt is not None else mx_quantize_t(w)
     if not on_gpu(dy):
         from .gemm import act_grad_ref
         y = mx_dequantize(dq, ds) @ mx_dequantize(wq_, ws_).t()
         if dact_src is not None:
             y = y * act_grad_ref(dact_src.float(), dact)
+        if drop_p > 0:
+            from .elementwise import dropout_keep, eff_seed
+            y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) / (1 - drop_p)
         y = y.to(torch.bfloat16)
         if resid is not None:
             y = (y.float() + resid.float()).to(torch.bfloat16)
         return y
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
-    lib().gemm_mxfp8(dq, ds, wq_, ws_, dx, M, K, N, None, resid, 0, None, 0.0, 0,
+    lib().gemm_mxfp8(dq, ds, wq_, ws_, dx, M, K, N, None, resid, 0, None, drop_p, drop_seed,
                      dact_src=dact_src, dact=ACT[dact] if dact_src is not None else 0)
     return dx
 
 
-def linear_wgrad_mx(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate: bool = False) -> None:
-    """gw[N,K] (f32) (+)= MX(dy^T) @ MX(x^T)^T (reduction over the M tokens)."""
+def linear_wgrad_mx(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate: bool = False,
+                    dyt=None) -> None:
+    """gw[N,K] (f32) (+)= MX(dy^T) @ MX(x^T)^T (reduction over the M tokens). dyt: pre-quantized
+    dy^T; x^T: the forward's saved one when present."""
     M, N = dy.shape
     K = x.shape[1]
-    aq, as_ = mx_quantize_t(dy)
-    bq, bs = mx_quantize_t(x)
+    aq, as_ = dyt if dyt is not None else mx_quantize_t(dy)
+    xt = take_t(x)
+    bq, bs = xt if xt is not None else mx_quantize_t(x)
     if not on_gpu(dy):
         g = mx_dequantize(aq, as_) @ mx_dequantize(bq, bs).t()
         v = gw.view(N, K)
         v.add_(g) if accumulate else v.copy_(g)
         return
-    lib().gemm_mxfp8(aq, as_, bq, bs, gw.view(N, K), N, K, M, None, None, 0, None, 0.0, 0,
-                     beta=1.0 if accumulate else 0.0)
+    splits = wgrad_splits(N, K, M)
+    if splits == 1:
+        lib().gemm_mxfp8(aq, as_, bq, bs, gw.view(N, K), N, K, M, None, None, 0, None, 0.0, 0,
+                         beta=1.0 if accumulate else 0.0)
+        return
+    # split-K into f32 slabs, then one reduce pass (f32 atomics from the epilogue measured 2.5x
+    # slower end to end: Transformer-big fp8 33.3 ms/step, 11 ms of it in atomic weight gradients)
+    from . import _lib as _lib_mod
+    stride = ((N * K + 3) // 4) * 4
+    ws = _lib_mod.workspace(dy.device, splits * stride, slot=_lib_mod.WGRAD_SLOT)
+    lib().gemm_mxfp8(aq, as_, bq, bs, ws, N, K, M, None, None, 0, None, 0.0, 0, splits=splits, split_stride=stride)
+    lib().splitk_reduce(ws, splits, stride, N * K, gw.view(-1), None, accumulate, 1.0)
+
+
+def wgrad_splits(N: int, K: int, M: int) -> int:
+    """Split-K slabs of an fp8 weight gradient [N, K] reduced over M tokens: fill ~one round of
+    256x256 blocks (two of 128x128 when a side is < 256) with >= 8 K-tiles of 128 per split; the
+    count the g4 launcher will actually run (ceil(K-tiles / per-split))."""
+    nkt = M // 128
+    big = N >= 256 and K >= 256
+    t = (-(-N // 256)) * (-(-K // 256)) if big else (-(-N // 128)) * (-(-K // 128))
+    s = max(1, min(-(-(256 if big else 512) // t), max(1, nkt // 8)))
+    per = -(-nkt // s)
+    return -(-nkt // per)

@@ -29,32 +29,44 @@ def _hwio_to_ohwi(a: np.ndarray, cin_pad: int | None = None) -> np.ndarray:
 
 
 def linear_forward(x, w, b, fp8: bool, **kw):
-    """bf16 GEMM, or the MX-fp8 block-scaled MFMA GEMM when fp8 and K % 128 == 0."""
+    """bf16 GEMM, or the MX-fp8 block-scaled MFMA GEMM when fp8 and K % 128 == 0 (which also
+    leaves MX(x^T) / MX(w^T) for this step's backward: ops.fp8.save_t)."""
     if fp8 and x.shape[-1] % 128 == 0:
         from ..ops.fp8 import linear_fwd_mx
-        return linear_fwd_mx(x, w, b, **kw)
+        return linear_fwd_mx(x, w, b, save=True, **kw)
     return G.linear_fwd(x, w, b, **kw)
 
 
-def linear_wgrad(dy, x, gw, fp8: bool, accumulate: bool = False, split_target=None):
+def fp8_dy(dy, K: int, fp8: bool):
+    """The backward's MX operands of dy [M, N] for a layer with K inputs: (MX(dy) for dgrad,
+    MX(dy^T) for wgrad), both from one read when both GEMMs run in fp8; None where a GEMM stays
+    bf16 (or fp8 is off)."""
+    if not fp8:
+        return None, None
+    from ..ops.fp8 import mx_backward_ok, mx_quantize_dual
+    M, N = dy.shape
+    dg, wg = mx_backward_ok(M, N, K)
+    if dg and wg:
+        return mx_quantize_dual(dy)
+    return None, None
+
+
+def linear_wgrad(dy, x, gw, fp8: bool, accumulate: bool = False, split_target=None, dyt=None):
     """Weight gradient: MX-fp8 when fp8 and the token count tiles (M % 128), else bf16 split-K."""
     if fp8:
         from ..ops.fp8 import linear_wgrad_mx, mx_backward_ok
         if mx_backward_ok(dy.shape[0], dy.shape[1], x.shape[1])[1]:
-            return linear_wgrad_mx(dy, x, gw, accumulate=accumulate)
+            return linear_wgrad_mx(dy, x, gw, accumulate=accumulate, dyt=dyt)
     return G.linear_wgrad(dy, x, gw, accumulate=accumulate, split_target=split_target)
 
 
-def linear_dgrad(dy, w, fp8: bool, drop_p: float = 0.0, drop_seed: int = 0, **kw):
-    """Input gradient: MX-fp8 when fp8 and the output width tiles (N % 128), else bf16 (with the
-    input-dropout backward fused into the epilogue; the fp8 path runs it as a separate pass)."""
+def linear_dgrad(dy, w, fp8: bool, drop_p: float = 0.0, drop_seed: int = 0, dyq=None, **kw):
+    """Input gradient: MX-fp8 when fp8 and the output width tiles (N % 128), else bf16; either way
+    the input-dropout backward runs in the GEMM epilogue."""
     if fp8:
         from ..ops.fp8 import linear_dgrad_mx, mx_backward_ok
         if mx_backward_ok(dy.shape[0], dy.shape[1], w.shape[1])[0]:
-            if drop_p > 0 and kw.get("resid") is not None:
-                raise ValueError("fp8 dgrad: input dropout with a residual is not supported")
-            from ..ops.elementwise import dropout
-            return dropout(linear_dgrad_mx(dy, w, **kw), drop_p, drop_seed)
+            return linear_dgrad_mx(dy, w, dyq=dyq, drop_p=drop_p, drop_seed=drop_seed, **kw)
     return G.linear_dgrad(dy, w, drop_p=drop_p, drop_seed=drop_seed, **kw)
 
 
@@ -193,7 +205,8 @@ class Linear:
                  dact=None, drop_p: float = 0.0, drop_seed: int = 0):
         """dy: gradient of this layer's (pre-dropout, post-activation-backward) output. drop_p/drop_seed:
         a forward dropout on this layer's input, whose backward is fused into the dgrad epilogue."""
-        linear_wgrad(dy, x, self.w.grad, self.fp8, accumulate=accumulate, split_target=self.split_target)
+        dyq, dyt = fp8_dy(dy.reshape(-1, dy.shape[-1]), self.fin, self.fp8 and need_dx)
+        linear_wgrad(dy, x, self.w.grad, self.fp8, accumulate=accumulate, split_target=self.split_target, dyt=dyt)
         if self.b is not None:
             G.bias_grad(dy, self.b.grad, accumulate=accumulate or self.arena.prezeroed)
             self.arena.grad_ready(self.w, self.b)
@@ -202,7 +215,7 @@ class Linear:
         if not need_dx:
             return None
         return linear_dgrad(dy, self.w.compute, self.fp8, resid=resid, dact_src=dact_src, dact=dact, drop_p=drop_p,
-                            drop_seed=drop_seed)
+                            drop_seed=drop_seed, dyq=dyq)
 
 
 class FusedLinear:
@@ -248,13 +261,14 @@ class FusedLinear:
 
     def backward(self, dy, x, need_dx: bool = True, resid=None):
         w, gw, _, gb = self.views()
-        linear_wgrad(dy, x, gw, self.fp8, split_target=getattr(self, "split_target", None))
+        dyq, dyt = fp8_dy(dy.reshape(-1, dy.shape[-1]), self.fin, self.fp8 and need_dx)
+        linear_wgrad(dy, x, gw, self.fp8, split_target=getattr(self, "split_target", None), dyt=dyt)
         if gb is not None:
             G.bias_grad(dy, gb, accumulate=self.arena.prezeroed)
         self.arena.grad_ready(*[p.w for p in self.parts], *[p.b for p in self.parts if p.b is not None])
         if not need_dx:
             return None
-        return linear_dgrad(dy, w, self.fp8, resid=resid)
+        return linear_dgrad(dy, w, self.fp8, resid=resid, dyq=dyq)
 
 
 class LayerNorm:

@@ -160,3 +160,17 @@ def test_g4_fp8_engine_matches_register_engine(M, N, K, tile):
     for a, c in zip(out[1], out[0]):
         if a is not None:
             assert rel(a, c) < 1e-5, rel(a, c)
+
+
+@pytest.mark.parametrize("R,C", [(256, 1024), (4096, 96), (96, 4128)])
+def test_dual_quantizer_matches_row_and_transposing_quantizers(R, C):
+    """mx_quantize_dual (one read of x) produces bit-identical bytes and scales to mx_quantize(x)
+    and mx_quantize_t(x) (ragged column tiles included)."""
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(R, C, generator=g) * torch.logspace(-3, 3, C)).to(torch.bfloat16).cuda()
+    (q, s), (qt, st) = F8.mx_quantize_dual(x)
+    q1, s1 = F8.mx_quantize(x)
+    qt1, st1 = F8.mx_quantize_t(x)
+    torch.cuda.synchronize()
+    assert torch.equal(q, q1) and torch.equal(s, s1)
+    assert torch.equal(qt, qt1) and torch.equal(st, st1)

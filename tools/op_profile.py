@@ -60,6 +60,12 @@ def describe(rec):
         label = f"{tag} M{M} N{N} K{K}{geo}"
         # A operand of a conv gather is the whole activation; tensors passed cover everything touched
         return label, 2.0 * M * N * K * batch, _bytes(a), tag
+    if op == "gemm_mxfp8":
+        M, N, K = a[5], a[6], a[7]
+        f32 = a[4].get("esize") == 4 if isinstance(a[4], dict) else False
+        tag = f"mxfp8 {'wgrad.f32' if f32 else 'bf16'}"
+        # the fp8 MFMA peak is twice bf16's: count half the FLOPs against PEAK
+        return f"{tag} M{M} N{N} K{K}", 2.0 * M * N * K / 2, _bytes(a[:5]), tag
     return op, 0.0, _bytes(a), op
 
 
@@ -98,6 +104,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--top", type=int, default=60)
     ap.add_argument("--ab-persist", type=int, default=0, help="also profile with the persistent GEMM grid off")
+    ap.add_argument("--fp8", type=int, default=0, help="transformer models: MX-fp8 linear GEMMs")
     args = ap.parse_args()
 
     from tensorflow_k8s_amd.models import build_model, synthetic_batch
@@ -107,7 +114,7 @@ def main():
     from tensorflow_k8s_amd.runtime.trainer import StepRunner
 
     dev = torch.device("cuda", 0)
-    model = build_model(args.model).to(dev)
+    model = build_model(args.model, **({"fp8": True} if args.fp8 else {})).to(dev)
     opt = SGD(model.arena, lr=0.1, momentum=0.9) if args.model.startswith(("resnet", "lenet")) else \
         AdamW(model.arena, lr=1e-4)
     strat = MultiWorkerMirroredStrategy(model.arena)

@@ -58,6 +58,8 @@ int tfk_opt_hyper(int*, const float*, int, int, float, float, float*, hipStream_
 int tfk_sumsq(const float*, long long, float*, hipStream_t);
 int tfk_clip_coef(const float*, float, float*, float*, hipStream_t);
 int tfk_splitk_reduce(const float*, int, long long, long long, float*, void*, int, float, hipStream_t);
+int tfk_hwgrad_slabs(int, int, int, int, int, int, int, int);
+int tfk_hwgrad_launch(const void*, const void*, float*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int tfk_transpose_arb(const void*, void*, int, int, int, int, hipStream_t);
 int tfk_transpose_f32(const float*, float*, int, int, hipStream_t);
 int tfk_cast_f32_bf16(const float*, void*, long long, hipStream_t);
@@ -613,6 +615,21 @@ void splitk_reduce(torch::Tensor slabs, int S, int64_t stride, int64_t n, c10::o
                              accumulate ? 1 : 0, (float)alpha, cur_stream()),
            "splitk_reduce");
 }
+// Halo-tile 3x3 weight gradient (conv_hwgrad.hip): per-block f32 slabs of dW [K][3][3][C] into ws
+int64_t hwgrad_slabs(int N, int H, int W, int P, int Q, int C, int K, int st) {
+  return tfk_hwgrad_slabs(H, W, P, Q, C, K, st, N);
+}
+void hwgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor ws, int N, int H, int W, int P, int Q, int C, int K, int st,
+            int slabs) {
+  need_bf16(x, "x"); need_bf16(dy, "dy"); need_f32(ws, "ws");
+  TORCH_CHECK(x.dim() == 4 && x.size(0) == N && x.size(1) == H && x.size(2) == W && x.size(3) == C, "hwgrad: x shape");
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == N && dy.size(1) == P && dy.size(2) == Q && dy.size(3) == K, "hwgrad: dy shape");
+  need_aligned(x, 16, "x"); need_aligned(dy, 16, "dy"); need_aligned(ws, 16, "ws");
+  TORCH_CHECK(slabs > 0 && slabs == tfk_hwgrad_slabs(H, W, P, Q, C, K, st, N), "hwgrad: shape not served / slab count");
+  need_numel(ws, (long long)slabs * K * 9 * C, "ws");
+  check_rc(tfk_hwgrad_launch(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), N, H, W, P, Q, C, K, st, slabs,
+                             cur_stream()), "hwgrad");
+}
 void transpose_arb(torch::Tensor in, torch::Tensor out, int A, int R, int B, int flip) {
   need_bf16(in, "in"); need_bf16(out, "out");
   need_numel(in, (long long)A * R * B, "in"); need_numel(out, (long long)A * R * B, "out");
@@ -731,6 +748,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sumsq", &sumsq);
   m.def("clip_coef", &clip_coef);
   m.def("splitk_reduce", &splitk_reduce);
+  m.def("hwgrad_slabs", &hwgrad_slabs);
+  m.def("hwgrad", &hwgrad);
   m.def("transpose_arb", &transpose_arb, py::arg("in"), py::arg("out"), py::arg("A"), py::arg("R"), py::arg("B"),
         py::arg("flip") = 0);
   m.def("transpose_f32", &transpose_f32);

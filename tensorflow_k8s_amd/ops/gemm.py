@@ -430,6 +430,18 @@ PHASES_AS_FWD = os.environ.get("TFK_PHASES_AS_FWD", "1") == "1"
 WGRAD_SPLIT_SCALE = float(os.environ.get("TFK_WGRAD_SPLIT_SCALE", "1.0"))
 # Non-pointwise weight gradients on the LDS-DMA engine's im2col gather (B_CONV_WGRAD, C % 8 == 0).
 G4_WGRAD = os.environ.get("TFK_G4_WGRAD", "1") == "1"
+# 3x3 / pad-1 / stride-1|2 weight gradients on the halo-tile direct kernel (csrc/kernels/conv_hwgrad.hip:
+# one L2->LDS load of each band's input halo + dY for all nine taps, per-block f32 slabs + one
+# splitk_reduce). TFK_HWGRAD=0 restores the im2col gather on the g4 engine.
+HWGRAD = os.environ.get("TFK_HWGRAD", "1") == "1"
+
+
+def hwgrad_slabs(g: ConvGeom) -> int:
+    """Slabs the halo weight-gradient kernel uses for conv g (0: shape not served)."""
+    if not (HWGRAD and g.R == 3 and g.S == 3 and g.ph == 1 and g.pw == 1 and g.sh == g.sw and g.dh == 1
+            and g.dw == 1 and g.C % 64 == 0 and g.K % 64 == 0):
+        return 0
+    return int(lib().hwgrad_slabs(g.N, g.H, g.W, g.P, g.Q, g.C, g.K, g.sh))
 
 
 def _phases(g: ConvGeom):
@@ -552,6 +564,13 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
                                           dilation=(g.dh, g.dw)).permute(0, 2, 3, 1).reshape(g.K, Nn)
         v = gw.view(g.K, Nn)
         v.add_(gwt) if accumulate else v.copy_(gwt)
+        return
+    ns = hwgrad_slabs(g) if splits is None else 0
+    if ns > 0:
+        n = g.K * Nn
+        ws = workspace(dy.device, ns * n, slot=_lib_mod.WGRAD_SLOT)
+        lib().hwgrad(x, dy, ws, g.N, g.H, g.W, g.P, g.Q, g.C, g.K, g.sh, ns)
+        lib().splitk_reduce(ws, ns, n, n, gw.view(-1), None, accumulate, 1.0)
         return
     # measured table first (pointwise = dense GEMM shapes, tools/wgrad_sweep.py), else the model
     if RECORD is not None and g.pointwise:

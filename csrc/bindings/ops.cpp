@@ -59,6 +59,10 @@ int tfk_sumsq(const float*, long long, float*, hipStream_t);
 int tfk_clip_coef(const float*, float, float*, float*, hipStream_t);
 int tfk_splitk_reduce(const float*, int, long long, long long, float*, void*, int, float, hipStream_t);
 int tfk_hwgrad_slabs(int, int, int, int, int, int, int, int);
+int tfk_stem_wgrad_slabs(int, int, int);
+int tfk_stem_fwd_ok(int, int, int);
+int tfk_stem_fwd_launch(const void*, const void*, void*, float*, int, int, int, int, hipStream_t);
+int tfk_stem_wgrad_launch(const void*, const void*, float*, int, int, int, int, hipStream_t);
 int tfk_hwgrad_launch(const void*, const void*, float*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int tfk_transpose_arb(const void*, void*, int, int, int, int, hipStream_t);
 int tfk_transpose_f32(const float*, float*, int, int, hipStream_t);
@@ -630,6 +634,39 @@ void hwgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor ws, int N, int H, i
   check_rc(tfk_hwgrad_launch(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), N, H, W, P, Q, C, K, st, slabs,
                              cur_stream()), "hwgrad");
 }
+// Stem 7x7/s2/p3 weight gradient (conv_hwgrad.hip): x [N][H][W][8] (channels >= 4 zero), dy [N][H/2][W/2][64]
+int64_t stem_wgrad_slabs(int N, int H, int W) { return tfk_stem_wgrad_slabs(N, H, W); }
+void stem_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor ws, int N, int H, int W, int slabs) {
+  need_bf16(x, "x"); need_bf16(dy, "dy"); need_f32(ws, "ws");
+  TORCH_CHECK(x.dim() == 4 && x.size(0) == N && x.size(1) == H && x.size(2) == W && x.size(3) == 8, "stem_wgrad: x shape");
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == N && dy.size(1) == H / 2 && dy.size(2) == W / 2 && dy.size(3) == 64,
+              "stem_wgrad: dy shape");
+  need_aligned(x, 16, "x"); need_aligned(dy, 16, "dy"); need_aligned(ws, 16, "ws");
+  TORCH_CHECK(slabs > 0 && slabs == tfk_stem_wgrad_slabs(N, H, W), "stem_wgrad: shape not served / slab count");
+  need_numel(ws, (long long)slabs * 64 * 49 * 8, "ws");
+  check_rc(tfk_stem_wgrad_launch(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), N, H, W, slabs, cur_stream()),
+           "stem_wgrad");
+}
+// Stem 7x7/s2/p3 forward + BN statistics (conv_stem.hip): x [N][H][W][8] (channels >= 4 zero),
+// w [64][7][7][8], y [N][H/2][W/2][64], stats [shards][2][64] (accumulated)
+bool stem_fwd_ok(int N, int H, int W) { return tfk_stem_fwd_ok(N, H, W) != 0; }
+void stem_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::optional<torch::Tensor> stats, int shards) {
+  need_bf16(x, "x"); need_bf16(w, "w"); need_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 8, "stem_fwd: x must be [N][H][W][8]");
+  const int N = x.size(0), H = x.size(1), W = x.size(2);
+  TORCH_CHECK(tfk_stem_fwd_ok(N, H, W), "stem_fwd: shape not served");
+  TORCH_CHECK(w.numel() == 64 * 49 * 8, "stem_fwd: w must be [64][7][7][8]");
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(1) == H / 2 && y.size(2) == W / 2 && y.size(3) == 64,
+              "stem_fwd: y shape");
+  need_aligned(x, 16, "x"); need_aligned(w, 16, "w"); need_aligned(y, 16, "y");
+  float* st = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    need_f32(*stats, "stats");
+    need_numel(*stats, (long long)(shards < 1 ? 1 : shards) * 2 * 64, "stats");
+    st = stats->data_ptr<float>();
+  }
+  check_rc(tfk_stem_fwd_launch(x.data_ptr(), w.data_ptr(), y.data_ptr(), st, shards, N, H, W, cur_stream()), "stem_fwd");
+}
 void transpose_arb(torch::Tensor in, torch::Tensor out, int A, int R, int B, int flip) {
   need_bf16(in, "in"); need_bf16(out, "out");
   need_numel(in, (long long)A * R * B, "in"); need_numel(out, (long long)A * R * B, "out");
@@ -750,6 +787,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("splitk_reduce", &splitk_reduce);
   m.def("hwgrad_slabs", &hwgrad_slabs);
   m.def("hwgrad", &hwgrad);
+  m.def("stem_wgrad_slabs", &stem_wgrad_slabs);
+  m.def("stem_wgrad", &stem_wgrad);
+  m.def("stem_fwd_ok", &stem_fwd_ok);
+  m.def("stem_fwd", &stem_fwd);
   m.def("transpose_arb", &transpose_arb, py::arg("in"), py::arg("out"), py::arg("A"), py::arg("R"), py::arg("B"),
         py::arg("flip") = 0);
   m.def("transpose_f32", &transpose_f32);

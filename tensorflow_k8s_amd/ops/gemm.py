@@ -348,10 +348,23 @@ def _conv_tile(kind: str, g: ConvGeom, default, flags=()):
     return t if t is not None else default()
 
 
+# ResNet stem (7x7/s2/p3, RGB padded to 8 channels -> 64) forward on the direct halo kernel
+# (csrc/kernels/conv_stem.hip); TFK_STEM=0 restores the implicit-GEMM gather.
+STEM = os.environ.get("TFK_STEM", "1") == "1"
+
+
+def stem_fwd_ok(g: ConvGeom, cin_used: int | None) -> bool:
+    return bool(STEM and cin_used is not None and cin_used <= 4 and g.R == 7 and g.S == 7 and g.sh == 2
+                and g.sw == 2 and g.ph == 3 and g.pw == 3 and g.dh == 1 and g.dw == 1 and g.C == 8 and g.K == 64
+                and lib().stem_fwd_ok(g.N, g.H, g.W))
+
+
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor | None = None,
-             shards: int = 1, bias: torch.Tensor | None = None, act: str | None = None) -> torch.Tensor:
+             shards: int = 1, bias: torch.Tensor | None = None, act: str | None = None,
+             cin_used: int | None = None) -> torch.Tensor:
     """y[N,P,Q,K] = act(conv(x[N,H,W,C], w[K,R,S,C]) + bias); optionally accumulates BN batch
-    statistics (sum, sumsq per output channel) of the f32 result into stats[shards][2][K]."""
+    statistics (sum, sumsq per output channel) of the f32 result into stats[shards][2][K].
+    cin_used: input channels that may be nonzero (the rest are zero padding)."""
     if not on_gpu(x):
         y = _ref_conv(x, w, g)
         if bias is not None:
@@ -364,6 +377,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
         return y.to(torch.bfloat16).contiguous()
     M = g.N * g.P * g.Q
     y = torch.empty(g.N, g.P, g.Q, g.K, dtype=torch.bfloat16, device=x.device)
+    if bias is None and act is None and stem_fwd_ok(g, cin_used):
+        lib().stem_fwd(x, w, y, stats, shards)
+        return y
     tile = _conv_tile("fwd", g, lambda: pick_tile(M, g.K, big_ok=g.pointwise, K=g.R * g.S * g.C, mid_ok=g.pointwise,
                                                   g4=g.pointwise or g.C % 64 == 0 or (g.C % 8 == 0 and g.C < 64)),
                       (stats is not None, bias is not None, act is not None))
@@ -552,9 +568,19 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
     return dx
 
 
+def stem_wgrad_slabs(g: ConvGeom, cin_used: int | None) -> int:
+    """Slabs of the direct stem weight-gradient kernel (ResNet conv1: 7x7/s2/p3, 8-channel padded
+    input of which at most 4 are nonzero, 64 outputs); 0 when the conv is not of that kind."""
+    if not (HWGRAD and cin_used is not None and cin_used <= 4 and g.R == 7 and g.S == 7 and g.sh == 2
+            and g.sw == 2 and g.ph == 3 and g.pw == 3 and g.dh == 1 and g.dw == 1 and g.C == 8 and g.K == 64):
+        return 0
+    return int(lib().stem_wgrad_slabs(g.N, g.H, g.W))
+
+
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor, accumulate: bool = False,
-               splits: int | None = None) -> None:
-    """gw[K][R][S][C] (f32) (+)= sum over (n,p,q) dy[n,p,q,k] * x[n, p*sh-ph+r, q*sw-pw+s, c]."""
+               splits: int | None = None, cin_used: int | None = None) -> None:
+    """gw[K][R][S][C] (f32) (+)= sum over (n,p,q) dy[n,p,q,k] * x[n, p*sh-ph+r, q*sw-pw+s, c].
+    cin_used: input channels that may be nonzero (the rest are zero padding, whose gradient is 0)."""
     Nn = g.R * g.S * g.C
     Kp = g.N * g.P * g.Q
     if not on_gpu(dy):
@@ -564,6 +590,13 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
                                           dilation=(g.dh, g.dw)).permute(0, 2, 3, 1).reshape(g.K, Nn)
         v = gw.view(g.K, Nn)
         v.add_(gwt) if accumulate else v.copy_(gwt)
+        return
+    ns = stem_wgrad_slabs(g, cin_used) if splits is None else 0
+    if ns > 0:
+        n = g.K * Nn
+        ws = workspace(dy.device, ns * n, slot=_lib_mod.WGRAD_SLOT)
+        lib().stem_wgrad(x, dy, ws, g.N, g.H, g.W, ns)
+        lib().splitk_reduce(ws, ns, n, n, gw.view(-1), None, accumulate, 1.0)
         return
     ns = hwgrad_slabs(g) if splits is None else 0
     if ns > 0:

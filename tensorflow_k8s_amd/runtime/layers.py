@@ -79,6 +79,7 @@ class Conv2d:
         (e.g. RGB stem, LeNet's 1->6 conv); padded weights start and stay exactly zero, and the
         checkpoint holds only the real [k, k, cin_real, cout_real] kernel."""
         self.cin, self.cout, self.k, self.stride = cin, cout, k, stride
+        self.cin_real = cin_real if cin_real is not None else cin
         self.pad = (k - 1) // 2 if pad is None else pad
         real = cin_real if cin_real is not None else cin
         oreal = cout_real if cout_real is not None else cout
@@ -114,11 +115,11 @@ class Conv2d:
     def forward(self, x, stats: BN.BNState | None = None, act: str | None = None):
         g = self.geom(x.shape)
         return G.conv_fwd(x, self.w.compute, g, stats.stats if stats else None, stats.shards if stats else 1,
-                          bias=self.b.master if self.b is not None else None, act=act)
+                          bias=self.b.master if self.b is not None else None, act=act, cin_used=self.cin_real)
 
     def backward(self, dy, x, need_dx: bool = True, resid=None, bnr=None, resid_stride: int = 1):
         g = self.geom(x.shape)
-        streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad), dy, x)
+        streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad, cin_used=self.cin_real), dy, x)
         if self.b is not None:
             G.bias_grad(dy, self.b.grad)
             self.arena.grad_ready(self.w, self.b)
@@ -141,7 +142,7 @@ class Conv2d:
     def wgrad(self, dy, x):
         """Weight gradient only (side stream when enabled) + readiness notification."""
         g = self.geom(x.shape)
-        streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad), dy, x)
+        streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad, cin_used=self.cin_real), dy, x)
         self.arena.grad_ready(self.w)
 
     def lattice_dgrad(self, dy, x):

@@ -44,6 +44,25 @@ def main():
                               "slabs": G.hwgrad_slabs(g) if hw else None, "ms": round(t, 4),
                               "TF/s": round(fl / t / 1e9, 1)}), flush=True)
         G.HWGRAD = True
+    # ResNet conv1 (7x7/s2, 3 real of 8 channels): direct stem kernel vs the gather
+    g = G.ConvGeom(N, 224, 224, 8, 64, 7, 7, 2, 2, 3, 3)
+    x = torch.zeros(N, 224, 224, 8, device=dev, dtype=torch.bfloat16)
+    x[..., :3] = torch.randn(N, 224, 224, 3, device=dev).to(torch.bfloat16)
+    dy = torch.randn(N, 112, 112, 64, device=dev).to(torch.bfloat16)
+    gw = torch.zeros(64, 7, 7, 8, device=dev)
+    fl = 2.0 * N * 112 * 112 * 64 * 49 * 3
+    for cu in (3, None):
+        t = timeit(lambda: G.conv_wgrad(dy, x, g, gw, cin_used=cu))
+        print(json.dumps({"shape": "stem 224x224x3->64 7x7/s2", "path": "stem" if cu else "gather", "ms": round(t, 4),
+                          "TF/s(real ch)": round(fl / t / 1e9, 1)}), flush=True)
+
+    w = (torch.randn(64, 7, 7, 8, device=dev) * 0.1).to(torch.bfloat16)
+    st = torch.zeros(16 * 2 * 64, device=dev)
+    fl = 2.0 * N * 112 * 112 * 64 * 49 * 3
+    for cu in (3, None):
+        t = timeit(lambda: G.conv_fwd(x, w, g, stats=st, shards=16, cin_used=cu))
+        print(json.dumps({"shape": "stem fwd 224x224x3->64 7x7/s2", "path": "stem" if cu else "gather",
+                          "ms": round(t, 4), "TF/s(real ch)": round(fl / t / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":

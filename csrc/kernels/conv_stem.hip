@@ -46,7 +46,8 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(GemmParams p, int band
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
   const int g = lane >> 4;
-  const int bd = blockIdx.x;
+  // neighbouring bands (7 of their 9 halo rows shared) on one XCD: the shared rows hit its L2
+  const int bd = xcd_remap(blockIdx.x, gridDim.x);
   const int n = bd / bands_per_img, h0 = (bd - n * bands_per_img) * TR;
 
   // halo DMA: 64 pixels (1 KiB) per wave instruction, zero outside the image (= the conv padding)

@@ -14,26 +14,19 @@ int grid_for(long long work, int cap = 8192) {
 }
 
 // out[i] = (acc ? out[i] : 0) + alpha * sum_s slabs[s*stride + i]; optional bf16 output instead.
-// 2-D grid: x over 1024-element chunks (4 per lane, 16-B loads), y over groups of SG slabs, so a
-// small weight with hundreds of split-K slabs still spreads over the whole chip (the 1-D form was
-// latency-bound: 17 blocks each walking 256 slabs serially). Groups > 1 combine with f32 atomics
-// into `out` (pre-initialised by the first group's pass of the launcher below).
-constexpr int SG = 8;
-__global__ void splitk_reduce_kernel(const float* __restrict__ slabs, int S, long long stride, long long n,
-                                     float* __restrict__ out, bf16* __restrict__ outb, int accumulate, float alpha,
-                                     int atomic) {
-  const long long i = ((long long)blockIdx.x * NT + threadIdx.x) * 4;
-  if (i >= n) return;
-  const int s0 = blockIdx.y * SG, s1 = gridDim.y == 1 ? S : min(S, s0 + SG);
+// Two deterministic passes, no atomics. Pass 1: grid (n/256 chunks, G slab groups); a block's 4
+// waves take the group's slabs round-robin (16-B loads, 4 elements per lane) and meet in LDS in a
+// fixed order; with G == 1 it writes `out` directly, else the group partial goes IN PLACE into the
+// group's first slab (only this block reads that chunk of it). Pass 2 (G > 1): partials summed in
+// group order. G is chosen so pass 1 has ~1024 blocks: a small weight with hundreds of split-K slabs
+// (64x64 1x1 wgrad: 256 slabs x 16K) spreads over the chip instead of 16 blocks walking 256 slabs
+// (the previous form: 8-slab groups combined with f32 atomics, 18 us for 16 MB, non-deterministic).
+template <bool FINAL>
+__device__ __forceinline__ void splitk_store(long long i, long long n, f32x4 a, float* out, bf16* outb,
+                                             int accumulate, float alpha) {
+  a *= alpha;
   if (i + 3 < n) {
-    f32x4 a = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int s = s0; s < s1; ++s) a += __builtin_nontemporal_load((const f32x4*)(slabs + s * stride + i));
-    a *= alpha;
-    if (atomic) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(out + i + e, a[e]);
-    } else if (out) {
+    if (out) {
       if (accumulate) a += *(f32x4*)(out + i);
       *(f32x4*)(out + i) = a;
     } else {
@@ -43,15 +36,56 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slabs, int S, lon
       *(bf16x4*)(outb + i) = o;
     }
   } else {
-    for (long long j = i; j < n; ++j) {
-      float a = 0.f;
-      for (int s = s0; s < s1; ++s) a += slabs[s * stride + j];
-      a *= alpha;
-      if (atomic) atomicAdd(out + j, a);
-      else if (out) out[j] = a + (accumulate ? out[j] : 0.f);
-      else outb[j] = f2bf(a + (accumulate ? bf2f(outb[j]) : 0.f));
+    for (int e = 0; e < 4 && i + e < n; ++e) {
+      if (out) out[i + e] = a[e] + (accumulate ? out[i + e] : 0.f);
+      else outb[i + e] = f2bf(a[e] + (accumulate ? bf2f(outb[i + e]) : 0.f));
     }
   }
+}
+
+__global__ __launch_bounds__(256) void splitk_partial_kernel(float* __restrict__ slabs, int S, int SG, long long stride,
+                                                             long long n, float* __restrict__ out, bf16* __restrict__ outb,
+                                                             int accumulate, float alpha) {
+  __shared__ f32x4 red[3][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long i = ((long long)blockIdx.x * 64 + lane) * 4;
+  const int s0 = blockIdx.y * SG, s1 = min(S, s0 + SG);
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (i + 3 < n) {
+#pragma unroll 4
+    for (int s = s0 + w; s < s1; s += 4) a += __builtin_nontemporal_load((const f32x4*)(slabs + s * stride + i));
+  } else if (i < n) {
+    for (int s = s0 + w; s < s1; s += 4)
+      for (int e = 0; e < 4 && i + e < n; ++e) a[e] += slabs[s * stride + i + e];
+  }
+  if (w > 0) red[w - 1][lane] = a;
+  __syncthreads();
+  if (w != 0 || i >= n) return;
+  a += red[0][lane];
+  a += red[1][lane];
+  a += red[2][lane];
+  if (gridDim.y == 1) {
+    splitk_store<true>(i, n, a, out, outb, accumulate, alpha);
+  } else if (i + 3 < n) {
+    *(f32x4*)(slabs + s0 * stride + i) = a;
+  } else {
+    for (int e = 0; e < 4 && i + e < n; ++e) slabs[s0 * stride + i + e] = a[e];
+  }
+}
+
+__global__ void splitk_final_kernel(const float* __restrict__ slabs, int G, int SG, long long stride, long long n,
+                                    float* __restrict__ out, bf16* __restrict__ outb, int accumulate, float alpha) {
+  const long long i = ((long long)blockIdx.x * NT + threadIdx.x) * 4;
+  if (i >= n) return;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (i + 3 < n) {
+#pragma unroll 4
+    for (int g = 0; g < G; ++g) a += *(const f32x4*)(slabs + (long long)g * SG * stride + i);
+  } else {
+    for (int g = 0; g < G; ++g)
+      for (int e = 0; e < 4 && i + e < n; ++e) a[e] += slabs[(long long)g * SG * stride + i + e];
+  }
+  splitk_store<true>(i, n, a, out, outb, accumulate, alpha);
 }
 
 // in [A][R][B] -> out [B][R][A] (bf16), 32x32 LDS tiles; grid (ceil(B/32), ceil(A/32), R).
@@ -234,19 +268,21 @@ __global__ void add_kernel(const bf16* __restrict__ a, const bf16* __restrict__ 
 extern "C" {
 int tfk_splitk_reduce(const float* slabs, int S, long long stride, long long n, float* out, bf16* outb, int accumulate,
                       float alpha, hipStream_t s) {
-  const unsigned gx = (unsigned)((n + NT * 4 - 1) / (NT * 4));
-  const int groups = (S + SG - 1) / SG;
-  if (groups == 1 || !out) {
-    // bf16 output (rare) or few slabs: single pass over all slabs per element
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, 1), dim3(NT), 0, s, slabs, S, stride, n, out, outb, accumulate,
-                       alpha, 0);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-  }
-  // first slab group initialises (or accumulates into) out; the remaining groups add atomically
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, 1), dim3(NT), 0, s, slabs, SG, stride, n, out, outb, accumulate,
-                     alpha, 0);
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, (unsigned)(groups - 1)), dim3(NT), 0, s, slabs + SG * stride,
-                     S - SG, stride, n, out, outb, 1, alpha, 1);
+  if (S < 1 || n < 1) return 0;
+  const long long chunks = (n + 255) / 256;
+  long long G = (1024 + chunks - 1) / chunks;
+  const long long gmax = (S + 3) / 4;  // >= 4 slabs per group (one per wave)
+  if (G > gmax) G = gmax;
+  if (G > 64) G = 64;
+  if (G < 1) G = 1;
+  const int SG = (int)((S + G - 1) / G);
+  G = (S + SG - 1) / SG;
+  float* sl = const_cast<float*>(slabs);  // scratch: pass 1 parks group partials in place
+  hipLaunchKernelGGL(splitk_partial_kernel, dim3((unsigned)chunks, (unsigned)G), dim3(256), 0, s, sl, S, SG, stride, n,
+                     out, outb, accumulate, alpha);
+  if (G > 1)
+    hipLaunchKernelGGL(splitk_final_kernel, dim3((unsigned)((n + NT * 4 - 1) / (NT * 4))), dim3(NT), 0, s, slabs, (int)G,
+                       SG, stride, n, out, outb, accumulate, alpha);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_transpose_arb(const bf16* in, bf16* out, int A, int R, int B, int flip, hipStream_t s) {

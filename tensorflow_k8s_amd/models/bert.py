@@ -10,7 +10,7 @@ tanh pooler. MI355X mapping:
 * bias, GELU, dropout and the residual add run in the GEMM epilogues; the GELU input is saved by
   the FFN1 epilogue (aux) and its derivative is applied in the FFN2 dgrad epilogue (dact);
 * flash attention (MFMA, online softmax, dropout regenerated from a hash in backward);
-* vocab padded to a multiple of 64 rows (padding rows stay zero, loss masks them).
+* vocab padded to a multiple of 128 rows (padding rows stay zero, loss masks them).
 Dropout seeds = per-(layer, site) host salt + a per-step key kept and advanced on the device, so
 every mask is reproducible and a hipGraph-captured step draws fresh masks on every replay.
 """

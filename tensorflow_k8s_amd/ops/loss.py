@@ -9,7 +9,7 @@ from ._lib import lib, on_gpu
 def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.0, ignore_index: int = -100,
                  scale: float = 1.0, want_grad: bool = True, want_correct: bool = False, V: int | None = None):
     """Returns (per-row loss f32 [B], dlogits bf16 [B,ld] = scale*(softmax - target) or None, correct f32 [B] or None).
-    V < logits.shape[1]: only the first V columns are classes (vocab padded to a multiple of 64);
+    V < logits.shape[1]: only the first V columns are classes (vocab padded to a multiple of 128);
     the padding columns of dlogits are zero."""
     B, ld = logits.shape
     V = ld if V is None else V

@@ -294,14 +294,16 @@ class LayerNorm:
         return dx
 
 
-def _pad_rows(rows: int, to: int = 64) -> int:
+def _pad_rows(rows: int, to: int = 128) -> int:
     return (rows + to - 1) // to * to
 
 
 class Embedding:
-    """Token embedding table [V, W] stored with V padded to a multiple of 64 rows (padding rows
+    """Token embedding table [V, W] stored with V padded to a multiple of 128 rows (padding rows
     stay zero; the TF variable is the real [V, W] table). Also used as the tied output
-    projection (logits = h @ table^T over the padded vocab, masked to V by the loss)."""
+    projection (logits = h @ table^T over the padded vocab, masked to V by the loss); 128 = one
+    MX-fp8 K-tile, so that projection's input gradient -- a reduction over the padded vocab --
+    runs on the fp8 GEMM as well."""
 
     def __init__(self, arena: ParamArena, name: str, V: int, W: int, std: float = 0.02, decay: bool = True):
         self.V, self.Vp, self.W = V, _pad_rows(V), W

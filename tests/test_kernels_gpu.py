@@ -666,3 +666,29 @@ def test_g4_persistent_matches_one_shot(case):
             assert torch.equal(u, v), case
         else:
             assert rel(u, v) < 1e-5, case
+
+
+@pytest.mark.parametrize("S,n", [(1, 1000), (3, 4096), (8, 1048576), (256, 16384), (126, 65536), (502, 4100), (5, 1001),
+                                 (7, 2359296)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_splitk_reduce_two_pass(S, n, acc):
+    """Split-K slab reduce (misc.hip): deterministic two-pass tree vs an fp64 sum; f32 and bf16
+    outputs, accumulate on/off, ragged n (not a multiple of 4), hundreds of slabs."""
+    from tensorflow_k8s_amd.ops._lib import lib
+    torch.manual_seed(S + n)
+    stride = (n + 3) // 4 * 4
+    slabs = torch.randn(S * stride, device="cuda")
+    ref = slabs.view(S, stride)[:, :n].double().sum(0) * 0.5
+    base = torch.randn(n, device="cuda")
+    out = base.clone() if acc else torch.full((n,), float("nan"), device="cuda")
+    lib().splitk_reduce(slabs.clone(), S, stride, n, out, None, acc, 0.5)
+    exp = ref + (base.double() if acc else 0)
+    assert float((out.double() - exp).abs().max()) < 1e-3 * (S ** 0.5)
+    # bitwise deterministic across calls
+    out2 = base.clone() if acc else torch.zeros(n, device="cuda")
+    lib().splitk_reduce(slabs.clone(), S, stride, n, out2, None, acc, 0.5)
+    assert torch.equal(out, out2)
+    if n % 4 == 0:
+        ob = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
+        lib().splitk_reduce(slabs.clone(), S, stride, n, None, ob, False, 0.5)
+        assert float((ob.double() - ref).abs().max()) < 0.02 * float(ref.abs().max()) + 1e-2

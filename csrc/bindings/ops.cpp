@@ -21,6 +21,7 @@ extern "C" void tfk_fp8_set_engine(int e);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_quant_t(const void*, void*, void*, int, int, hipStream_t);
 int tfk_mx_quant_dual(const void*, void*, void*, void*, void*, int, int, hipStream_t);
+int tfk_mx_quant_dual_group(const void*, int, int, hipStream_t);
 int tfk_mx_probe(const int*, const int*, const int*, const int*, float*, hipStream_t);
 int tfk_gemm_mxfp8(tfk::GemmParams p, int ext, int splits, hipStream_t s);
 const unsigned long long* tfk_seed_key();
@@ -310,6 +311,15 @@ void mx_quant_dual(torch::Tensor x, torch::Tensor qr, torch::Tensor sr, torch::T
   for (auto* t : {&x, &qr, &qc}) need_aligned(*t, 16, "mx dual tensor");
   check_rc(tfk_mx_quant_dual(x.data_ptr(), qr.data_ptr(), sr.data_ptr(), qc.data_ptr(), sc.data_ptr(), (int)R, (int)C,
                              cur_stream()), "mx_quant_dual");
+}
+
+// Grouped dual quantization: table int64 [n][7] on the device, one QDesc per tensor (x, qr, sr, qc,
+// sc, R | C << 32, t0 | tcols << 32), built and validated by ops/fp8.py GroupQuantizer.
+void mx_quant_dual_group(torch::Tensor table, int64_t n, int64_t total) {
+  need(table, at::kLong, "mx group table");
+  TORCH_CHECK(table.is_cuda() && table.is_contiguous() && table.numel() == n * 7 && n > 0 && total > 0,
+              "mx_quant_dual_group: table must be a contiguous device int64 [n][7]");
+  check_rc(tfk_mx_quant_dual_group(table.data_ptr(), (int)n, (int)total, cur_stream()), "mx_quant_dual_group");
 }
 
 // C[M][N] = epilogue(Aq[M][K] . Bq[N][K]^T) with e8m0 block scales (one per 32 K-elements).
@@ -761,6 +771,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("mx_quant", &mx_quant);
   m.def("mx_quant_t", &mx_quant_t);
   m.def("mx_quant_dual", &mx_quant_dual);
+  m.def("mx_quant_dual_group", &mx_quant_dual_group);
   m.def("mx_probe", &mx_probe);
   m.def("gemm_mxfp8", &gemm_mxfp8, py::arg("A"), py::arg("As"), py::arg("B"), py::arg("Bs"), py::arg("C"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("bias"), py::arg("resid"), py::arg("act"), py::arg("aux"), py::arg("drop_p"),

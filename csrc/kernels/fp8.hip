@@ -171,58 +171,153 @@ __device__ __forceinline__ int mx_block(const float (&v)[32], unsigned (&w)[8]) 
 
 // Both MX quantizations of x bf16 [R][C] in ONE read: row blocks (q_r [R][C], s_r [R][C/32], the
 // forward / dgrad operand) and column blocks (q_c [C][R], s_c [C][R/32] = MX of x^T, the weight-
-// gradient operand). Block = a 128 x 128 tile staged in LDS (16-B lane-linear loads); 256 threads
-// each quantize 2 row blocks and 2 column blocks. 128 x 128 makes every e4m3 store pattern full
-// 128-B lines per block: a row of q_r gets 4 consecutive 32-B blocks, a row of q_c (a column of x)
-// gets its 4 row groups -- with 32-row tiles each q_c line was written in 4 quarters by 4
-// different blocks (measured 45% of the HBM floor in Transformer-big). R % 32 == 0, C % 32 == 0.
+// gradient operand). Unit = a 128 x 128 tile staged in LDS (16-B lane-linear loads); 256 threads
+// each quantize 2 row blocks and one column PAIR (2 column blocks, read as 32-bit LDS words).
+// 128 x 128 makes every e4m3 store pattern full 128-B lines per tile: a row of q_r gets 4
+// consecutive 32-B blocks, a row of q_c (a column of x) its 4 row groups (32-row tiles wrote each
+// q_c line in 4 quarters from 4 blocks: 45% of the HBM floor in Transformer-big).
+//
+// v2: the block scale comes from the integer bf16 magnitudes (packed u16 max), the bytes from
+// v_cvt_scalef32_pk_fp8_bf16 (two bf16 -> two e4m3, x / 2^e, RNE: exact against the reference, as
+// 2^-e scaling of a bf16 is exact) -- no unpack / multiply / clamp per element. Resident blocks walk
+// tiles (t += gridDim.x) with the next tile's 8 16-B loads in flight under this tile's quantize and
+// stores. One launch can cover MANY tensors (a descriptor table: all weights of a model per step).
 constexpr int QT = 128, QLD = QT + 8;
-__global__ __launch_bounds__(256) void mx_quant_dual_kernel(const bf16* __restrict__ x, unsigned char* __restrict__ qr,
-                                                            unsigned char* __restrict__ sr, unsigned char* __restrict__ qc,
-                                                            unsigned char* __restrict__ sc, int R, int C) {
-  __shared__ __attribute__((aligned(16))) bf16 tile[QT][QLD];
-  const int r0 = blockIdx.y * QT, c0 = blockIdx.x * QT, t = threadIdx.x;
-  const int rows = min(QT, R - r0), cols = min(QT, C - c0);
+struct QDesc {
+  const bf16* x;
+  unsigned char *qr, *sr, *qc, *sc;
+  int R, C;
+  int t0, tcols;  // first tile of this tensor in the launch; column tiles
+};
+static_assert(sizeof(QDesc) == 56, "QDesc is packed as 7 int64 by ops/fp8.py");
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int mx_exp_from_bits(unsigned amax_bits) {
+  const float amax = __uint_as_float(amax_bits << 16);
+  int ex = amax > 0.f ? (int)ceilf(log2f(amax * (1.f / 448.f))) : -127;
+  return ex < -127 ? -127 : (ex > 127 ? 127 : ex);
+}
+
+// 16 packed bf16 pairs (K order) -> 8 words of e4m3 bytes; returns the exponent
+__device__ __forceinline__ int mx_block_pk(const unsigned (&p)[16], unsigned (&w)[8]) {
+  u16x2 m = {0, 0};
 #pragma unroll
-  for (int i = 0; i < QT * QT / 8 / 256; ++i) {
+  for (int i = 0; i < 16; ++i) {
+    const unsigned a = p[i] & 0x7fff7fffu;
+    m = __builtin_elementwise_max(m, *(const u16x2*)&a);
+  }
+  const int ex = mx_exp_from_bits(m[0] > m[1] ? m[0] : m[1]);
+  const float s = ldexpf(1.f, ex < -126 ? -126 : ex);  // all-zero block: any normal scale gives 0
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s16x2 r = {0, 0};
+    r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, *(const bf16x2*)&p[2 * k], s, false);
+    r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, *(const bf16x2*)&p[2 * k + 1], s, true);
+    w[k] = *(const unsigned*)&r;
+  }
+  return ex;
+}
+
+__device__ __forceinline__ void qd_load(const QDesc& d, int lt, int t, u32x4 (&r)[8]) {
+  const int r0 = (lt / d.tcols) * QT, c0 = (lt % d.tcols) * QT;
+  const int rows = min(QT, d.R - r0), cols = min(QT, d.C - c0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
     const int idx = t + i * 256, row = idx >> 4, ch = (idx & 15) * 8;
-    if (row < rows && ch < cols) *(bf16x8*)&tile[row][ch] = *(const bf16x8*)(x + (long long)(r0 + row) * C + c0 + ch);
+    r[i] = (row < rows && ch < cols) ? *(const u32x4*)(d.x + (long long)(r0 + row) * d.C + c0 + ch)
+                                     : u32x4{0u, 0u, 0u, 0u};
   }
-  __syncthreads();
+}
+
+template <bool TABLE>
+__device__ __forceinline__ void qd_find(const QDesc* tab, int n, const QDesc& one, int t, QDesc& d) {
+  if constexpr (!TABLE) {
+    d = one;
+  } else {
+    int lo = 0, hi = n - 1;  // last entry with t0 <= t (block-uniform: scalar loads)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tab[mid].t0 <= t) lo = mid; else hi = mid - 1;
+    }
+    d = tab[lo];
+  }
+}
+
+template <bool TABLE>
+__global__ __launch_bounds__(256) void mx_quant_dual_kernel(QDesc one, const QDesc* __restrict__ tab, int n, int total) {
+  __shared__ __attribute__((aligned(16))) bf16 tile[QT][QLD];
+  const int t = threadIdx.x;
+  int ti = blockIdx.x;
+  if (ti >= total) return;
+  QDesc d;
+  qd_find<TABLE>(tab, n, one, ti, d);
+  u32x4 rg[8];
+  qd_load(d, ti - d.t0, t, rg);
+  while (true) {
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int pr = t + k * 256, row = pr >> 2, blk = pr & 3;
-    if (row < rows && blk * 32 < cols) {
-      float v[32];
+    for (int i = 0; i < 8; ++i) {
+      const int idx = t + i * 256;
+      *(u32x4*)&tile[idx >> 4][(idx & 15) * 8] = rg[i];
+    }
+    __syncthreads();
+    const int tn = ti + gridDim.x;  // block-uniform
+    QDesc dn;
+    if (tn < total) {
+      qd_find<TABLE>(tab, n, one, tn, dn);
+      qd_load(dn, tn - dn.t0, t, rg);  // in flight under this tile's quantize + stores
+    }
+    const int lt = ti - d.t0, r0 = (lt / d.tcols) * QT, c0 = (lt % d.tcols) * QT;
+    const int rows = min(QT, d.R - r0), cols = min(QT, d.C - c0);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bf16x8 h = *(const bf16x8*)&tile[row][blk * 32 + q * 8];
+    for (int k = 0; k < 2; ++k) {
+      const int pr = t + k * 256, row = pr >> 2, blk = pr & 3;
+      if (row < rows && blk * 32 < cols) {
+        unsigned p[16];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[q * 8 + e] = bf2f(h[e]);
+        for (int q = 0; q < 4; ++q) {
+          const u32x4 h = *(const u32x4*)&tile[row][blk * 32 + q * 8];
+          p[4 * q] = h[0]; p[4 * q + 1] = h[1]; p[4 * q + 2] = h[2]; p[4 * q + 3] = h[3];
+        }
+        unsigned w[8];
+        const int ex = mx_block_pk(p, w);
+        const int c = c0 + blk * 32;
+        unsigned char* dst = d.qr + (long long)(r0 + row) * d.C + c;
+        *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+        *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+        d.sr[(long long)(r0 + row) * (d.C / 32) + c / 32] = (unsigned char)(ex + 127);
       }
-      unsigned w[8];
-      const int ex = mx_block(v, w);
-      const int c = c0 + blk * 32;
-      unsigned char* dst = qr + (long long)(r0 + row) * C + c;
-      *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
-      *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
-      sr[(long long)(r0 + row) * (C / 32) + c / 32] = (unsigned char)(ex + 127);
     }
-  }
+    {
+      // column pair (2cp, 2cp+1), rows rgp*32 .. +32: one 32-bit LDS word per row holds both
+      const int cp = t & 63, rgp = t >> 6, col = 2 * cp;
+      if (col < cols && rgp * 32 < rows) {
+        unsigned lo[16], hi[16];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int pc = t + k * 256, col = pc & (QT - 1), rg = pc >> 7;
-    if (col < cols && rg * 32 < rows) {
-      float v[32];
-#pragma unroll
-      for (int r = 0; r < 32; ++r) v[r] = bf2f(tile[rg * 32 + r][col]);
-      unsigned w[8];
-      const int ex = mx_block(v, w);
-      unsigned char* dst = qc + (long long)(c0 + col) * R + r0 + rg * 32;
-      *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
-      *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
-      sc[(long long)(c0 + col) * (R / 32) + r0 / 32 + rg] = (unsigned char)(ex + 127);
+        for (int r = 0; r < 16; ++r) {
+          const unsigned a = *(const unsigned*)&tile[rgp * 32 + 2 * r][col];
+          const unsigned b = *(const unsigned*)&tile[rgp * 32 + 2 * r + 1][col];
+          lo[r] = __builtin_amdgcn_perm(b, a, 0x05040100u);  // (a.lo, b.lo): column col, rows 2r, 2r+1
+          hi[r] = __builtin_amdgcn_perm(b, a, 0x07060302u);  // (a.hi, b.hi): column col + 1
+        }
+        unsigned w[8];
+        const long long R = d.R;
+        int ex = mx_block_pk(lo, w);
+        unsigned char* dst = d.qc + (long long)(c0 + col) * R + r0 + rgp * 32;
+        *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+        *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+        d.sc[(long long)(c0 + col) * (R / 32) + r0 / 32 + rgp] = (unsigned char)(ex + 127);
+        ex = mx_block_pk(hi, w);
+        dst += R;
+        *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+        *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+        d.sc[(long long)(c0 + col + 1) * (R / 32) + r0 / 32 + rgp] = (unsigned char)(ex + 127);
+      }
     }
+    if (tn >= total) break;
+    __syncthreads();  // every read of the tile retired before the next one is written
+    ti = tn;
+    d = dn;
   }
 }
 
@@ -332,11 +427,31 @@ int tfk_mx_quant_t(const void* x, void* q, void* s, int R, int C, hipStream_t st
   hipLaunchKernelGGL(mx_quant_t_kernel, grid, dim3(256), 0, st, (const bf16*)x, (unsigned char*)q, (unsigned char*)s, R, C);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+// resident dual-quantizer blocks: 4 per CU fit the 34 KiB tile (TFK_MXQ_GRID overrides, for A/B)
+static int mxq_grid(int total) {
+  static int g = -1;
+  if (g < 0) {
+    const char* e = getenv("TFK_MXQ_GRID");
+    g = e ? atoi(e) : 1024;
+    if (g < 1) g = 1024;
+  }
+  return total < g ? total : g;
+}
 int tfk_mx_quant_dual(const void* x, void* qr, void* sr, void* qc, void* sc, int R, int C, hipStream_t st) {
   if (R % 32 || C % 32 || R <= 0 || C <= 0) return -1;
-  dim3 grid((unsigned)((C + QT - 1) / QT), (unsigned)((R + QT - 1) / QT));
-  hipLaunchKernelGGL(mx_quant_dual_kernel, grid, dim3(256), 0, st, (const bf16*)x, (unsigned char*)qr,
-                     (unsigned char*)sr, (unsigned char*)qc, (unsigned char*)sc, R, C);
+  QDesc d{(const bf16*)x, (unsigned char*)qr, (unsigned char*)sr, (unsigned char*)qc, (unsigned char*)sc, R, C, 0,
+          (C + QT - 1) / QT};
+  const int total = d.tcols * ((R + QT - 1) / QT);
+  hipLaunchKernelGGL(mx_quant_dual_kernel<false>, dim3((unsigned)mxq_grid(total)), dim3(256), 0, st, d,
+                     (const QDesc*)nullptr, 1, total);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// Many tensors in one launch: tab = n device-resident QDesc (t0 ascending, each R, C % 32 == 0).
+int tfk_mx_quant_dual_group(const void* tab, int n, int total, hipStream_t st) {
+  if (n <= 0 || total <= 0) return -1;
+  QDesc none{};
+  hipLaunchKernelGGL(mx_quant_dual_kernel<true>, dim3((unsigned)mxq_grid(total)), dim3(256), 0, st, none,
+                     (const QDesc*)tab, n, total);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_mx_quant(const void* x, void* q, void* s, long long nblocks, hipStream_t st) {

@@ -158,13 +158,17 @@ class BertForPreTraining:
         self.nsp.w.spec.from_tf = None
         self.nsp.w.spec.tf_shape = (2, W)
         self.nsp.b.spec.name = "cls/seq_relationship/output_bias"
+        self._wq = None
+        self._fp8_lins = []
         if cfg.fp8:
             for layer in self.layers:
                 for lin in (layer.qkv, layer.ao, layer.ff1, layer.ff2):
                     lin.fp8 = True
+                    self._fp8_lins.append(lin)
 
     def to(self, device, seed: int = 1234):
         self.arena.finalize(device, seed)
+        self._wq = None
         return self
 
     def train(self, mode: bool = True):
@@ -205,7 +209,9 @@ class BertForPreTraining:
         E.rng_advance(self.rng_state, self.rng_stream)
         if self.cfg.fp8:
             from ..ops.fp8 import clear_saved
+            from ..runtime.layers import weight_quantizer
             clear_saved()  # transposed MX operands live from this step's forward to its backward
+            weight_quantizer(self, self._fp8_lins).run()  # all fp8 weights, both ways, one launch
         try:
             with E.rng_key(self.rng_state):
                 return self._forward_backward(ids, tt, mlm_pos, mlm_ids, nsp_labels, loss_scale)

@@ -245,14 +245,18 @@ class Transformer:
         self.dec_ln = LayerNorm(a, "transformer/body/decoder/layer_prepostprocess/layer_norm", W, cfg.ln_eps,
                                 ("layer_norm_scale", "layer_norm_bias"))
         self._pos = None
+        self._wq = None
+        self._fp8_lins = []
         if cfg.fp8:
             for layer in self.enc + self.dec:
                 for lin in [layer.att.qkv, layer.att.out, layer.ff1, layer.ff2] + (
                         [layer.xatt.q, layer.xatt.kv, layer.xatt.out] if isinstance(layer, DecoderLayer) else []):
                     lin.fp8 = True
+                    self._fp8_lins.append(lin)
 
     def to(self, device, seed: int = 1234):
         self.arena.finalize(device, seed)
+        self._wq = None
         self._pos = timing_signal(self.cfg.max_len, self.cfg.hidden).to(torch.bfloat16).to(device)
         return self
 
@@ -285,7 +289,10 @@ class Transformer:
         E.rng_advance(self.rng_state, self.rng_stream)
         if self.cfg.fp8:
             from ..ops.fp8 import clear_saved
+            from ..runtime.layers import weight_quantizer
             clear_saved()  # transposed MX operands live from this step's forward to its backward
+            # every fp8 weight (and the tied softmax table) quantized both ways in ONE launch
+            weight_quantizer(self, self._fp8_lins, [self.emb.table.compute]).run()
         try:
             with E.rng_key(self.rng_state):
                 return self._forward_backward(src, tgt_in, tgt_out, src_len, loss_scale)

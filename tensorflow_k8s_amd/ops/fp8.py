@@ -72,6 +72,56 @@ def mx_quantize_dual(x: torch.Tensor):
     return (q, s), (qt, st)
 
 
+class GroupQuantizer:
+    """Both MX quantizations of MANY bf16 tensors (a model's fp8 weights) in ONE launch per step
+    (csrc/kernels/fp8.hip mx_quant_dual_kernel<true>: a device table of per-tensor descriptors,
+    resident blocks walk all tensors' 128x128 tiles). Per-weight launches cost ~8 us each on the
+    1024x1024..4096x1024 Transformer-big weights (67 of them per step) at a fraction of the HBM
+    rate. Output buffers and the table are allocated once (fixed addresses: hipGraph-capturable).
+    ``run()`` registers each weight's (MX(w), MX(w^T)) for this step's linear_fwd_mx (lookup by
+    data pointer) and its backward (save_t)."""
+
+    def __init__(self, weights: list[torch.Tensor]):
+        self.ws = [w for w in weights]
+        for w in self.ws:
+            R, C = w.shape
+            if R % MX_BLOCK or C % MX_BLOCK or not w.is_contiguous():
+                raise ValueError(f"group MX quantization needs contiguous [R, C] with R, C % 32 == 0, got {tuple(w.shape)}")
+        dev = self.ws[0].device
+        self.out = []
+        for w in self.ws:
+            R, C = w.shape
+            self.out.append(((torch.empty(R, C, dtype=torch.uint8, device=dev),
+                              torch.empty(R, C // MX_BLOCK, dtype=torch.uint8, device=dev)),
+                             (torch.empty(C, R, dtype=torch.uint8, device=dev),
+                              torch.empty(C, R // MX_BLOCK, dtype=torch.uint8, device=dev))))
+        self.table, self.total = None, 0
+        if on_gpu(self.ws[0]):
+            rows, t0 = [], 0
+            for w, ((q, s), (qt, st)) in zip(self.ws, self.out):
+                R, C = w.shape
+                tc, tr = -(-C // 128), -(-R // 128)
+                rows.append([w.data_ptr(), q.data_ptr(), s.data_ptr(), qt.data_ptr(), st.data_ptr(),
+                             R | (C << 32), t0 | (tc << 32)])
+                t0 += tc * tr
+            self.total = t0
+            self.table = torch.tensor(rows, dtype=torch.int64).to(dev)
+
+    def run(self) -> None:
+        if self.table is not None:
+            lib().mx_quant_dual_group(self.table, len(self.ws), self.total)
+        else:
+            for w, ((q, s), (qt, st)) in zip(self.ws, self.out):
+                (q_, s_), (qt_, st_) = mx_quantize_dual(w)
+                q.copy_(q_); s.copy_(s_); qt.copy_(qt_); st.copy_(st_)
+        for w, o in zip(self.ws, self.out):
+            _WQ[w.data_ptr()] = (w, tuple(w.shape), o)
+
+
+# this step's pre-quantized weights (GroupQuantizer.run): data pointer -> (w, shape, (MX(w), MX(w^T)))
+_WQ: dict[int, tuple] = {}
+
+
 # Transposed MX operands produced in the forward for the backward of the same step: the forward
 # quantizes its input x and weight w in both directions with one read each (mx_quantize_dual) and
 # parks MX(x^T) (weight-gradient operand) and MX(w^T) (dgrad operand) here, keyed by the data
@@ -81,18 +131,38 @@ _SAVED: dict[int, tuple] = {}
 
 
 def save_t(x: torch.Tensor, qt) -> None:
+    """Park MX(x^T) for this step's backward. The same tensor may feed several fp8 GEMMs (the
+    encoder memory feeds every decoder layer's cross-attention K/V): the entry is counted and
+    outlives the backward's take_t of every use."""
     if len(_SAVED) > 4096:  # forwards without backwards (evaluation): do not grow without bound
         _SAVED.clear()
-    _SAVED[x.data_ptr()] = (x, tuple(x.shape), qt)
+    k = x.data_ptr()
+    e = _SAVED.get(k)
+    if e is not None and e[1] == tuple(x.shape) and e[2] is qt:
+        e[3] += 1
+    else:
+        _SAVED[k] = [x, tuple(x.shape), qt, 1]
 
 
 def take_t(x: torch.Tensor):
-    e = _SAVED.pop(x.data_ptr(), None)
-    return e[2] if e is not None and e[1] == tuple(x.shape) else None
+    e = _SAVED.get(x.data_ptr())
+    if e is None or e[1] != tuple(x.shape):
+        return None
+    e[3] -= 1
+    if e[3] <= 0:
+        del _SAVED[x.data_ptr()]
+    return e[2]
+
+
+# this step's MX quantizations of fp8 GEMM inputs, keyed by (data pointer, shape); an entry holds
+# its source tensor, so the memory cannot be reused by another tensor while it exists
+_XQ: dict[tuple, tuple] = {}
 
 
 def clear_saved() -> None:
     _SAVED.clear()
+    _WQ.clear()
+    _XQ.clear()
 
 
 def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
@@ -106,9 +176,23 @@ def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = 
     if K % 128:
         raise ValueError(f"MX-fp8 GEMM needs K % 128 == 0, got {K}")
     dg_ok, wg_ok = mx_backward_ok(M, N, K)
-    if save and wg_ok:
+    if wq is None:
+        e = _WQ.get(w.data_ptr())
+        if e is not None and e[1] == tuple(w.shape):
+            wq = e[2][0]
+            if save and dg_ok:
+                save_t(w, e[2][1])
+    # training forwards only: an input saved for this step's backward is immutable until then, so a
+    # second GEMM on the same tensor (the decoders' encoder memory) reuses its quantization
+    key = (x2.data_ptr(), tuple(x2.shape))
+    xe = _XQ.get(key) if save and wg_ok else None
+    if xe is not None:
+        (xq, xs), xt = xe[1], xe[2]
+        save_t(x2, xt)
+    elif save and wg_ok:
         (xq, xs), xt = mx_quantize_dual(x2)
         save_t(x2, xt)
+        _XQ[key] = (x2, (xq, xs), xt)
     else:
         xq, xs = mx_quantize(x2)
     if wq is not None:

@@ -272,6 +272,20 @@ class FusedLinear:
         return linear_dgrad(dy, w, self.fp8, resid=resid, dyq=dyq)
 
 
+def fp8_weight(lin) -> torch.Tensor:
+    """The bf16 [out, in] weight a Linear / FusedLinear feeds its (MX-fp8) GEMMs."""
+    return lin.views()[0] if isinstance(lin, FusedLinear) else lin.w.compute
+
+
+def weight_quantizer(model, lins: list, extra: list | None = None):
+    """The model's per-step grouped MX quantizer of its fp8 linear weights (built once; reset by
+    ``model._wq = None`` when the arena moves)."""
+    if getattr(model, "_wq", None) is None:
+        from ..ops.fp8 import GroupQuantizer
+        model._wq = GroupQuantizer([fp8_weight(l) for l in lins] + list(extra or []))
+    return model._wq
+
+
 class LayerNorm:
     """TF variables <name>/gamma, <name>/beta (f32, no weight decay)."""
 

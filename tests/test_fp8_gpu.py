@@ -174,3 +174,48 @@ def test_dual_quantizer_matches_row_and_transposing_quantizers(R, C):
     torch.cuda.synchronize()
     assert torch.equal(q, q1) and torch.equal(s, s1)
     assert torch.equal(qt, qt1) and torch.equal(st, st1)
+
+
+def test_dual_quantizer_zero_and_tiny_blocks():
+    """All-zero blocks (scale byte 0, bytes 0) and blocks of tiny values (e4m3 subnormal outputs) come
+    out of the scaled-convert quantizer exactly as from the multiply-then-convert row quantizer."""
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(256, 256, generator=g)
+    x[:32, :] = 0
+    x[:, 64:96] = 0
+    x[100:132, 128:160] *= 1e-30
+    x[200:, 200:] *= torch.logspace(-6, 0, 56)
+    x = x.to(torch.bfloat16).cuda()
+    (q, s), (qt, st) = F8.mx_quantize_dual(x)
+    q1, s1 = F8.mx_quantize(x)
+    qt1, st1 = F8.mx_quantize_t(x)
+    torch.cuda.synchronize()
+    assert torch.equal(q, q1) and torch.equal(s, s1)
+    assert torch.equal(qt, qt1) and torch.equal(st, st1)
+    assert int(s[0, 0]) == 0 and int(q[:32].abs().sum()) == 0
+
+
+def test_group_quantizer_matches_per_tensor_dual():
+    """GroupQuantizer (one launch over a descriptor table, resident blocks walking every tensor's
+    tiles) == mx_quantize_dual of each tensor, bit for bit, for mixed / ragged shapes; the results are
+    registered for linear_fwd_mx (pre-quantized weight + the saved MX(w^T) for the dgrad)."""
+    g = torch.Generator().manual_seed(11)
+    shapes = [(256, 1024), (96, 4128), (4096, 96), (128, 128), (1024, 1024), (32, 32), (33792 // 8, 1024)]
+    ws = [(torch.randn(*sh, generator=g) * 0.05).to(torch.bfloat16).cuda() for sh in shapes]
+    gq = F8.GroupQuantizer(ws)
+    F8.clear_saved()
+    gq.run()
+    torch.cuda.synchronize()
+    for w, ((q, s), (qt, st)) in zip(ws, gq.out):
+        (q1, s1), (qt1, st1) = F8.mx_quantize_dual(w)
+        assert torch.equal(q, q1) and torch.equal(s, s1), w.shape
+        assert torch.equal(qt, qt1) and torch.equal(st, st1), w.shape
+    # the pre-quantized weight is used by the forward: same output as quantizing on the fly
+    x = torch.randn(256, 1024, generator=g).to(torch.bfloat16).cuda()
+    y_pre = F8.linear_fwd_mx(x, ws[4], save=True)
+    assert F8.take_t(ws[4]) is gq.out[4][1]
+    F8.clear_saved()
+    y_fly = F8.linear_fwd_mx(x, ws[4])
+    torch.cuda.synchronize()
+    assert torch.equal(y_pre, y_fly)
+    F8.clear_saved()

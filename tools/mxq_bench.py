@@ -36,6 +36,18 @@ def main():
             t = timeit(fn)
             print(json.dumps({"op": op, "shape": [R, C], "us": round(t * 1e3, 2), "GB/s": round(by / t / 1e6, 1)}),
                   flush=True)
+    # every fp8 weight of Transformer-big (+ the tied 33792x1024 table): per-tensor launches vs ONE
+    # grouped launch (GroupQuantizer)
+    W, F = 1024, 4096
+    shapes = ([(3 * W, W), (W, W), (F, W), (W, F)] * 6 + [(3 * W, W), (W, W), (W, W), (2 * W, W), (W, W), (F, W), (W, F)] * 6
+              + [(33792, W)])
+    ws = [torch.randn(*sh, device="cuda").to(torch.bfloat16) for sh in shapes]
+    by = sum(w.numel() * 4 + 2 * w.numel() // 32 for w in ws)
+    gq = F8.GroupQuantizer(ws)
+    for op, fn in (("weights_per_tensor", lambda: [F8.mx_quantize_dual(w) for w in ws]), ("weights_group", gq.run)):
+        t = timeit(fn, iters=20)
+        print(json.dumps({"op": op, "tensors": len(ws), "us": round(t * 1e3, 2), "GB/s": round(by / t / 1e6, 1)}),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -114,8 +114,34 @@ __device__ __forceinline__ uint32_t head_seed(const AttnParams& p, int bh) {
   const unsigned long long s = eff_seed(p.seed, p.seed_key);
   return hash32((uint32_t)s ^ (uint32_t)(s >> 32) ^ ((uint32_t)bh * 0x9E3779B9u));
 }
-__device__ __forceinline__ bool keep_elem(const AttnParams& p, uint32_t hs, int q, int key) {
-  return u01(hash32(hs ^ (uint32_t)(q * p.Sk + key))) >= p.p_drop;
+// Attention-probability dropout: ONE hash32 per (group of 4 queries, key) gives 4 mask bytes, byte
+// j for query 4*qg + j; keep iff byte >= thr = round(p * 256) (keep scale 256 / (256 - thr)). In
+// the forward / dQ kernels a lane owns one query and 4 consecutive keys, so a lane quad (the 4
+// queries of a group) hashes its 4 keys once each and trades bytes over DPP quad broadcasts; in the
+// dK/dV kernel a lane owns one key and 4 consecutive queries: one hash, 4 bytes. The per-element
+// hash (plus its two quarter-rate multiplies) was the largest VALU cost of all three kernels.
+// ops/transformer.py dropout_keep_mask is the bit-exact CPU copy.
+__device__ __forceinline__ int drop_thr(float p) {
+  const int t = (int)(p * 256.f + 0.5f);
+  return t > 255 ? 255 : t;
+}
+template <int R>
+__device__ __forceinline__ uint32_t qb(uint32_t h) {  // quad-broadcast lane R's h (DPP quad_perm [R,R,R,R])
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)h, R * 0x55, 0xf, 0xf, false);
+}
+// keep bits (bit r) of this lane's query (j = qrow & 3) with keys kb + r, r = 0..3 (kb % 4 == 0)
+__device__ __forceinline__ unsigned keep4_rows(uint32_t hs, int qgbase, int kb, int j, int thr) {
+  const uint32_t h = hash32(hs ^ (uint32_t)(qgbase + kb + j));
+  const uint32_t h0 = qb<0>(h), h1 = qb<1>(h), h2 = qb<2>(h), h3 = qb<3>(h);
+  const int sh = 8 * j;
+  return (((h0 >> sh) & 0xffu) >= (uint32_t)thr ? 1u : 0u) | (((h1 >> sh) & 0xffu) >= (uint32_t)thr ? 2u : 0u) |
+         (((h2 >> sh) & 0xffu) >= (uint32_t)thr ? 4u : 0u) | (((h3 >> sh) & 0xffu) >= (uint32_t)thr ? 8u : 0u);
+}
+// keep bits (bit r) of this lane's key with queries 4*qg + r
+__device__ __forceinline__ unsigned keep4_cols(uint32_t hs, int qg, int Sk, int key, int thr) {
+  const uint32_t h = hash32(hs ^ (uint32_t)(qg * Sk + key));
+  return ((h & 0xffu) >= (uint32_t)thr ? 1u : 0u) | (((h >> 8) & 0xffu) >= (uint32_t)thr ? 2u : 0u) |
+         (((h >> 16) & 0xffu) >= (uint32_t)thr ? 4u : 0u) | ((h >> 24) >= (uint32_t)thr ? 8u : 0u);
 }
 __device__ __forceinline__ void store_rowvec4(bf16* dst, const f32x4& v, float s) {
   bf16x4 o;
@@ -141,7 +167,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   const int qrow = q0 + 16 * w + li;  // this lane's query
   const bf16x8 qf0 = frag_global(Qb, p.q_rs, qrow, p.Sq, 0), qf1 = frag_global(Qb, p.q_rs, qrow, p.Sq, 1);
   const float sl2 = p.scale * LOG2E;
-  const float keep_scale = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+  const int thr = drop_thr(p.p_drop);
+  const float keep_scale = p.p_drop > 0.f ? 256.f / (float)(256 - thr) : 1.f;
+  const int qgbase = (qrow >> 2) * p.Sk;
   float m = -INFINITY, lsum = 0.f;
   f32x4 oacc[4];
 #pragma unroll
@@ -170,16 +198,28 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
       s[bb] = a;
     }
     float mx = -INFINITY;
+    // wave-uniform: every (query, key) of this wave's tile valid -> no per-element mask
+    const bool full = k0 + TILE <= kvl && (!p.causal || k0 + TILE - 1 <= q0 + 16 * w);
+    if (full) {
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb)
+      for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + arow(bb, g, r);
-        float v = s[bb][r] * sl2;
-        if (key >= kvl || (p.causal && key > qrow)) v = -INFINITY;
-        s[bb][r] = v;
-        mx = fmaxf(mx, v);
-      }
+        for (int r = 0; r < 4; ++r) {
+          s[bb][r] *= sl2;
+          mx = fmaxf(mx, s[bb][r]);
+        }
+    } else {
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + arow(bb, g, r);
+          float v = s[bb][r] * sl2;
+          if (key >= kvl || (p.causal && key > qrow)) v = -INFINITY;
+          s[bb][r] = v;
+          mx = fmaxf(mx, v);
+        }
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mnew = fmaxf(m, mx);
@@ -202,10 +242,11 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
     for (int db = 0; db < 4; ++db) oacc[db] *= alpha;
     if (p.p_drop > 0.f) {
 #pragma unroll
-      for (int bb = 0; bb < 4; ++bb)
+      for (int bb = 0; bb < 4; ++bb) {
+        const unsigned kp = keep4_rows(hs, qgbase, k0 + arow(bb, g, 0), li & 3, thr);
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          s[bb][r] = keep_elem(p, hs, qrow, k0 + arow(bb, g, r)) ? s[bb][r] * keep_scale : 0.f;
+        for (int r = 0; r < 4; ++r) s[bb][r] = (kp >> r) & 1u ? s[bb][r] * keep_scale : 0.f;
+      }
     }
     const bf16x8 pf0 = pack2(s[0], s[1]), pf1 = pack2(s[2], s[3]);
 #pragma unroll
@@ -261,7 +302,9 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   const bf16x8 qf0 = frag_global(Qb, p.q_rs, qrow, p.Sq, 0), qf1 = frag_global(Qb, p.q_rs, qrow, p.Sq, 1);
   const bf16x8 df0 = frag_global(dOb, p.o_rs, qrow, p.Sq, 0), df1 = frag_global(dOb, p.o_rs, qrow, p.Sq, 1);
   const float sl2 = p.scale * LOG2E;
-  const float keep_scale = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+  const int thr = drop_thr(p.p_drop);
+  const float keep_scale = p.p_drop > 0.f ? 256.f / (float)(256 - thr) : 1.f;
+  const int qgbase = (qrow >> 2) * p.Sk;
   const float lse2 = qrow < p.Sq ? p.lse[(long long)bh * p.Sq + qrow] * LOG2E : INFINITY;
   const float dlt = qrow < p.Sq ? p.delta[(long long)bh * p.Sq + qrow] : 0.f;
   f32x4 acc[4];
@@ -279,6 +322,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
     tile_store<NTH>(vr, Vs);
     __syncthreads();
     if (t + 1 < ntiles) { tile_load<NTH>(kr, Kb, p.k_rs, k0 + TILE, kvl); tile_load<NTH>(vr, Vb, p.v_rs, k0 + TILE, kvl); }
+    const bool full = k0 + TILE <= kvl && (!p.causal || k0 + TILE - 1 <= q0 + 16 * w);
     f32x4 ds[4];
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
@@ -288,13 +332,14 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
       s = mfma(frag_row(Ks, kr_, 1), qf1, s);
       dp = mfma(frag_row(Vs, kr_, 0), df0, dp);
       dp = mfma(frag_row(Vs, kr_, 1), df1, dp);
+      const unsigned kp = p.p_drop > 0.f ? keep4_rows(hs, qgbase, k0 + arow(bb, g, 0), li & 3, thr) : 0xfu;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + arow(bb, g, r);
-        const bool valid = key < kvl && !(p.causal && key > qrow);
+        const bool valid = full || (key < kvl && !(p.causal && key > qrow));
         const float pr = valid ? exp2f(s[r] * sl2 - lse2) : 0.f;
         float dpv = dp[r];
-        if (p.p_drop > 0.f) dpv = keep_elem(p, hs, qrow, key) ? dpv * keep_scale : 0.f;
+        if (p.p_drop > 0.f) dpv = (kp >> r) & 1u ? dpv * keep_scale : 0.f;
         ds[bb][r] = pr * (dpv - dlt);
       }
     }
@@ -332,7 +377,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(AttnParams p) {
   const bf16x8 kf0 = frag_global(Kb, p.k_rs, krow, kvl, 0), kf1 = frag_global(Kb, p.k_rs, krow, kvl, 1);
   const bf16x8 vf0 = frag_global(Vb, p.v_rs, krow, kvl, 0), vf1 = frag_global(Vb, p.v_rs, krow, kvl, 1);
   const float sl2 = p.scale * LOG2E;
-  const float keep_scale = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+  const int thr = drop_thr(p.p_drop);
+  const float keep_scale = p.p_drop > 0.f ? 256.f / (float)(256 - thr) : 1.f;
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int db = 0; db < 4; ++db) { dk[db] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[db] = f32x4{0.f, 0.f, 0.f, 0.f}; }
@@ -353,6 +399,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(AttnParams p) {
     __syncthreads();
     if (t + 1 < ntiles) { tile_load<NTH>(qr, Qb, p.q_rs, q0 + TILE, p.Sq); tile_load<NTH>(dr, dOb, p.o_rs, q0 + TILE, p.Sq); }
     f32x4 pp[4], ds[4];
+    // wave-uniform: this wave's 16 keys valid against every query of the tile
+    const bool full = k0 + 16 * w + 15 < kvl && q0 + TILE <= p.Sq && (!p.causal || k0 + 16 * w + 15 <= q0);
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
       const int qr_ = prow(bb, li);
@@ -361,16 +409,17 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(AttnParams p) {
       s = mfma(frag_row(Qs, qr_, 1), kf1, s);
       dp = mfma(frag_row(dOs, qr_, 0), vf0, dp);
       dp = mfma(frag_row(dOs, qr_, 1), vf1, dp);
+      const unsigned kp = p.p_drop > 0.f ? keep4_cols(hs, (q0 + arow(bb, g, 0)) >> 2, p.Sk, krow, thr) : 0xfu;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qt = arow(bb, g, r), qq = q0 + qt;
-        const bool valid = krow < kvl && qq < p.Sq && !(p.causal && krow > qq);
+        const bool valid = full || (krow < kvl && qq < p.Sq && !(p.causal && krow > qq));
         const float pr = valid ? exp2f(s[r] * sl2 - lse_s[qt]) : 0.f;
         float pd = pr, dpv = dp[r];
         if (p.p_drop > 0.f) {
-          const bool kp = keep_elem(p, hs, qq, krow);
-          pd = kp ? pr * keep_scale : 0.f;
-          dpv = kp ? dpv * keep_scale : 0.f;
+          const bool keep = (kp >> r) & 1u;
+          pd = keep ? pr * keep_scale : 0.f;
+          dpv = keep ? dpv * keep_scale : 0.f;
         }
         pp[bb][r] = pd;
         ds[bb][r] = pr * (dpv - dlt_s[qt]);

@@ -244,9 +244,16 @@ __device__ __forceinline__ void qd_find(const QDesc* tab, int n, const QDesc& on
   }
 }
 
+// The column blocks' e4m3 bytes and scales are staged in LDS ([128 columns][128 rows] bytes) and
+// written as whole 128-B q_c lines (8 lanes per line, 8 lines per wave store): per-thread 32-B
+// stores scattered over 128 rows ran the dual quantizer at ~4 TB/s against the row quantizer's
+// 6.4 (profiles/mxq_bench_r3b.jsonl).
+constexpr int QCL = QT + 16;
 template <bool TABLE>
 __global__ __launch_bounds__(256) void mx_quant_dual_kernel(QDesc one, const QDesc* __restrict__ tab, int n, int total) {
   __shared__ __attribute__((aligned(16))) bf16 tile[QT][QLD];
+  __shared__ __attribute__((aligned(16))) unsigned char qcl[QT][QCL];
+  __shared__ __attribute__((aligned(16))) unsigned char scl[QT][4];
   const int t = threadIdx.x;
   int ti = blockIdx.x;
   if (ti >= total) return;
@@ -301,21 +308,34 @@ __global__ __launch_bounds__(256) void mx_quant_dual_kernel(QDesc one, const QDe
           hi[r] = __builtin_amdgcn_perm(b, a, 0x07060302u);  // (a.hi, b.hi): column col + 1
         }
         unsigned w[8];
-        const long long R = d.R;
         int ex = mx_block_pk(lo, w);
-        unsigned char* dst = d.qc + (long long)(c0 + col) * R + r0 + rgp * 32;
-        *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
-        *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
-        d.sc[(long long)(c0 + col) * (R / 32) + r0 / 32 + rgp] = (unsigned char)(ex + 127);
+        *(u32x4*)&qcl[col][rgp * 32] = u32x4{w[0], w[1], w[2], w[3]};
+        *(u32x4*)&qcl[col][rgp * 32 + 16] = u32x4{w[4], w[5], w[6], w[7]};
+        scl[col][rgp] = (unsigned char)(ex + 127);
         ex = mx_block_pk(hi, w);
-        dst += R;
-        *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
-        *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
-        d.sc[(long long)(c0 + col + 1) * (R / 32) + r0 / 32 + rgp] = (unsigned char)(ex + 127);
+        *(u32x4*)&qcl[col + 1][rgp * 32] = u32x4{w[0], w[1], w[2], w[3]};
+        *(u32x4*)&qcl[col + 1][rgp * 32 + 16] = u32x4{w[4], w[5], w[6], w[7]};
+        scl[col + 1][rgp] = (unsigned char)(ex + 127);
+      }
+    }
+    __syncthreads();  // column bytes staged; every read of the bf16 tile retired
+    {
+      const long long R = d.R;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int idx = t + i * 256, c = idx >> 3, ch = (idx & 7) * 16;
+        if (c < cols && ch < rows) *(u32x4*)(d.qc + (long long)(c0 + c) * R + r0 + ch) = *(const u32x4*)&qcl[c][ch];
+      }
+      if (t < cols) {
+        unsigned char* sdst = d.sc + (long long)(c0 + t) * (R / 32) + r0 / 32;
+        if (rows == QT && ((R / 32) & 3) == 0) {
+          *(unsigned*)sdst = *(const unsigned*)&scl[t][0];
+        } else {
+          for (int g = 0; g * 32 < rows; ++g) sdst[g] = scl[t][g];
+        }
       }
     }
     if (tn >= total) break;
-    __syncthreads();  // every read of the tile retired before the next one is written
     ti = tn;
     d = dn;
   }

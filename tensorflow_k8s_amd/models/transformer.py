@@ -309,9 +309,12 @@ class Transformer:
         logits, (x, mem, st_m, y, yo, st_y) = self._forward(src, tgt_in, src_len, B, Ss, St, seed, tr)
         loss, dlogits, corr = softmax_xent(logits, tgt_out, smoothing=cfg.label_smoothing,
                                            scale=loss_scale / tgt_out.numel(), want_correct=True, V=cfg.vocab_size)
-        from ..runtime.layers import linear_dgrad, linear_wgrad
-        linear_wgrad(dlogits, yo, self.emb.table.grad, cfg.fp8)  # first writer of the shared table's grad
-        dyo = linear_dgrad(dlogits, self.emb.table.compute, cfg.fp8)
+        from ..runtime.layers import fp8_dy, linear_dgrad, linear_wgrad
+        # fp8: MX(dlogits) and MX(dlogits^T) from ONE read of the [tokens, vocab] gradient (separate
+        # row + transposing passes were 0.53 ms/step; profiles/transformer_big_fp8_bs32_1gpu_kernels_r3b.txt)
+        dyq, dyt = fp8_dy(dlogits, cfg.hidden, cfg.fp8)
+        linear_wgrad(dlogits, yo, self.emb.table.grad, cfg.fp8, dyt=dyt)  # first writer of the shared table's grad
+        dyo = linear_dgrad(dlogits, self.emb.table.compute, cfg.fp8, dyq=dyq)
         # each LayerNorm backward also emits dropout(dx) for the dropout its gradient flows into next
         p = cfg.dropout if tr else 0.0
         nd, ne = len(self.dec), len(self.enc)

@@ -135,16 +135,29 @@ def _hash32(x: torch.Tensor) -> torch.Tensor:
     return x ^ (x >> 16)
 
 
+def attn_drop_thr(p: float) -> int:
+    """8-bit drop threshold of the attention-dropout mask (attention.hip drop_thr)."""
+    return min(255, int(p * 256.0 + 0.5))
+
+
+def attn_keep_scale(p: float) -> float:
+    """Inverse keep probability of the quantized mask: 256 / (256 - thr) (exactly unbiased)."""
+    return 256.0 / (256 - attn_drop_thr(p))
+
+
 def dropout_keep_mask(seed: int, B: int, H: int, Sq: int, Sk: int, p: float) -> torch.Tensor:
-    """The kernels' attention-dropout mask (bool [B,H,Sq,Sk]), bit-exact (attention.hip keep_elem:
-    hash32 of the element index folded with a per-head seed hash)."""
+    """The kernels' attention-dropout mask (bool [B,H,Sq,Sk]), bit-exact (attention.hip keep4_*):
+    one hash32 per (group of 4 queries, key), folded with a per-head seed hash; byte q % 4 of it
+    decides query q (kept iff byte >= round(256 p))."""
     s = int(seed) & 0xFFFFFFFFFFFFFFFF
     base = (s & 0xFFFFFFFF) ^ (s >> 32)
     bh = torch.arange(B * H, dtype=torch.int64)
     hs = _hash32(base ^ ((bh * 0x9E3779B9) & 0xFFFFFFFF))
-    idx = torch.arange(Sq * Sk, dtype=torch.int64)
-    h = _hash32(hs[:, None] ^ idx[None, :])
-    return ((h >> 8).float() * (1.0 / 16777216.0) >= p).reshape(B, H, Sq, Sk)
+    q = torch.arange(Sq, dtype=torch.int64)
+    idx = ((q >> 2)[:, None] * Sk + torch.arange(Sk, dtype=torch.int64)[None, :]).reshape(-1)
+    h = _hash32(hs[:, None] ^ idx[None, :]).reshape(B * H, Sq, Sk)
+    byte = (h >> (8 * (q & 3))[None, :, None]) & 0xFF
+    return (byte >= attn_drop_thr(p)).reshape(B, H, Sq, Sk)
 
 
 def _view(buf, col, B, S, H):
@@ -191,7 +204,7 @@ def attention_fwd(sp: AttnSpec):
         s = torch.einsum("bqhd,bkhd->bhqk", q, k) * sp.scale
         lse = torch.logsumexp(s.masked_fill(pr == 0, float("-inf")), -1)
         if sp.p_drop > 0:
-            pr = pr * dropout_keep_mask(eff_seed(sp.seed), B, H, Sq, Sk, sp.p_drop) / (1 - sp.p_drop)
+            pr = pr * dropout_keep_mask(eff_seed(sp.seed), B, H, Sq, Sk, sp.p_drop) * attn_keep_scale(sp.p_drop)
         o = torch.einsum("bhqk,bkhd->bqhd", pr, v).reshape(B * Sq, H * HEAD_DIM)
         return o.to(torch.bfloat16), lse
     out = torch.empty(B * Sq, H * HEAD_DIM, dtype=torch.bfloat16, device=dev)
@@ -211,7 +224,7 @@ def attention_bwd(sp: AttnSpec, out, dout, lse, dq, dk, dv):
         with torch.enable_grad():
             pr = _ref_probs(q, k, sp.kv_len, sp.causal, sp.scale)
             if sp.p_drop > 0:
-                pr = pr * dropout_keep_mask(eff_seed(sp.seed), B, H, Sq, Sk, sp.p_drop) / (1 - sp.p_drop)
+                pr = pr * dropout_keep_mask(eff_seed(sp.seed), B, H, Sq, Sk, sp.p_drop) * attn_keep_scale(sp.p_drop)
             o = torch.einsum("bhqk,bkhd->bqhd", pr, v)
             gq, gk, gv = torch.autograd.grad(o, (q, k, v), dout.float().reshape(B, Sq, H, HEAD_DIM))
         for (buf, col), g, S in ((dq, gq, Sq), (dk, gk, Sk), (dv, gv, Sk)):

@@ -328,7 +328,8 @@ void mx_quant_dual_group(torch::Tensor table, int64_t n, int64_t total) {
 void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tensor Bs, torch::Tensor C, int M, int N, int K,
                 c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, int act,
                 c10::optional<torch::Tensor> aux, double drop_p, int64_t drop_seed,
-                c10::optional<torch::Tensor> dact_src, int dact, double beta, int splits, int64_t split_stride) {
+                c10::optional<torch::Tensor> dact_src, int dact, double beta, int splits, int64_t split_stride,
+                c10::optional<std::vector<torch::Tensor>> mx_out, bool mx_skip_c) {
   for (auto* t : {&A, &As, &B, &Bs}) need(*t, at::kByte, "mx operand");
   const bool f32 = C.scalar_type() == at::kFloat;
   if (!f32) need_bf16(C, "C");
@@ -365,7 +366,22 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
   p.dact_src = opt_ptr<const void>(dact_src);
   p.dact = dact;
   p.beta = (float)beta;
-  const int ext = f32 ? 2 : ((p.aux || drop_p > 0.0 || p.dact_src) ? 1 : 0);
+  int ext = f32 ? 2 : ((p.aux || drop_p > 0.0 || p.dact_src) ? 1 : 0);
+  if (mx_out.has_value()) {
+    // MX-fp8 copies of C from the epilogue: [qr [M][N], sr [M][N/32], qc [N][M], sc [N][M/32]]
+    const auto& o = *mx_out;
+    TORCH_CHECK(!f32 && splits == 1 && o.size() == 4 && M % 32 == 0 && N % 32 == 0,
+                "gemm_mxfp8 mx_out: bf16 output, no split, M, N % 32 == 0, 4 tensors");
+    for (const auto& t : o) need(t, at::kByte, "mx_out");
+    need_numel(o[0], (long long)M * N, "mx qr"); need_numel(o[1], (long long)M * N / 32, "mx sr");
+    need_numel(o[2], (long long)M * N, "mx qc"); need_numel(o[3], (long long)M * N / 32, "mx sc");
+    need_aligned(o[0], 16, "mx qr"); need_aligned(o[2], 16, "mx qc");
+    p.mx_qr = o[0].data_ptr(); p.mx_sr = o[1].data_ptr(); p.mx_qc = o[2].data_ptr(); p.mx_sc = o[3].data_ptr();
+    p.mx_skip_c = mx_skip_c ? 1 : 0;
+    ext = 3;
+  } else {
+    TORCH_CHECK(!mx_skip_c, "gemm_mxfp8: mx_skip_c without mx_out");
+  }
   // f32 split-K: split z writes its partial to the slab C + z * split_stride (ops.fp8 reduces them)
   p.split_stride = splits > 1 ? split_stride : 0;
   check_rc(tfk_gemm_mxfp8(p, ext, splits, cur_stream()), "gemm_mxfp8");
@@ -776,7 +792,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_mxfp8", &gemm_mxfp8, py::arg("A"), py::arg("As"), py::arg("B"), py::arg("Bs"), py::arg("C"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("bias"), py::arg("resid"), py::arg("act"), py::arg("aux"), py::arg("drop_p"),
         py::arg("drop_seed"), py::arg("dact_src") = py::none(), py::arg("dact") = 0, py::arg("beta") = 0.0,
-        py::arg("splits") = 1, py::arg("split_stride") = 0);
+        py::arg("splits") = 1, py::arg("split_stride") = 0, py::arg("mx_out") = py::none(), py::arg("mx_skip_c") = false);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);

@@ -11,6 +11,8 @@
 extern "C" {
 void tfk_attn_set_waves(int w);
 int tfk_layernorm_fwd(const void*, const float*, const float*, void*, float*, float*, int, int, float, hipStream_t);
+int tfk_layernorm_fwd_mx(const void*, const float*, const float*, void*, float*, float*, int, int, float, void*, void*, void*,
+                         void*, hipStream_t);
 int tfk_layernorm_bwd(const void*, const void*, const float*, const float*, const float*, const void*, void*, float*,
                       float*, int, int, void*, float, unsigned long long, hipStream_t);
 int tfk_embedding_fwd(const int*, const void*, int, const void*, int, const int*, const void*, int, void*, long long, int,
@@ -35,6 +37,26 @@ void layernorm_fwd(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, tor
   check_rc(tfk_layernorm_fwd(x.data_ptr(), gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
                              mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)M, W, (float)eps, cur_stream()),
            "layernorm_fwd");
+}
+
+// LayerNorm forward + both MX-fp8 quantizations of y (qr [M][W], sr [M][W/32], qc [W][M], sc [W][M/32]);
+// y optional (no bf16 store). M % 32 == 0, W % 32 == 0, W <= 1024.
+void layernorm_fwd_mx(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, c10::optional<torch::Tensor> y,
+                      torch::Tensor mean, torch::Tensor rstd, int64_t M, int W, double eps, torch::Tensor qr,
+                      torch::Tensor sr, torch::Tensor qc, torch::Tensor sc) {
+  need_bf16(x, "x"); need_f32(gamma, "gamma"); need_f32(beta, "beta"); need_f32(mean, "mean"); need_f32(rstd, "rstd");
+  TORCH_CHECK(M % 32 == 0 && W % 32 == 0 && W <= 1024, "layernorm_fwd_mx needs M, W % 32 == 0 and W <= 1024");
+  need_numel(x, M * W, "x"); need_numel(gamma, W, "gamma"); need_numel(beta, W, "beta");
+  need_numel(mean, M, "mean"); need_numel(rstd, M, "rstd");
+  if (y.has_value() && y->defined()) { need_bf16(*y, "y"); need_numel(*y, M * W, "y"); }
+  for (auto* t : {&qr, &sr, &qc, &sc}) need(*t, at::kByte, "mx out");
+  need_numel(qr, M * W, "qr"); need_numel(qc, M * W, "qc"); need_numel(sr, M * W / 32, "sr"); need_numel(sc, M * W / 32, "sc");
+  need_aligned(qr, 16, "qr"); need_aligned(qc, 16, "qc");
+  check_rc(tfk_layernorm_fwd_mx(x.data_ptr(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                                (y.has_value() && y->defined()) ? y->data_ptr() : nullptr, mean.data_ptr<float>(),
+                                rstd.data_ptr<float>(), (int)M, W, (float)eps, qr.data_ptr(), sr.data_ptr(), qc.data_ptr(),
+                                sc.data_ptr(), cur_stream()),
+           "layernorm_fwd_mx");
 }
 
 void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor gamma, torch::Tensor mean, torch::Tensor rstd,
@@ -174,6 +196,7 @@ void attn_bwd(torch::Tensor q, int64_t qo, torch::Tensor k, int64_t ko, torch::T
 
 void register_transformer_ops(pybind11::module& m) {
   m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_fwd_mx", &layernorm_fwd_mx);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);

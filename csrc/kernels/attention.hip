@@ -265,24 +265,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   }
 }
 
-// delta[b,h,q] = sum_d dO * O
-__global__ void attn_delta_kernel(AttnParams p) {
-  const long long i = (long long)blockIdx.x * NT + threadIdx.x;
-  const long long n = (long long)p.B * p.H * p.Sq;
-  if (i >= n) return;
-  const int q = (int)(i % p.Sq), bh = (int)(i / p.Sq), b = bh / p.H, h = bh % p.H;
-  const bf16* o = p.o + b * p.o_bs + (long long)q * p.o_rs + h * D;
-  const bf16* d = p.dout + b * p.o_bs + (long long)q * p.o_rs + h * D;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < D / 8; ++c) {
-    bf16x8 a = *(const bf16x8*)(o + c * 8), bb = *(const bf16x8*)(d + c * 8);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += bf2f(a[e]) * bf2f(bb[e]);
-  }
-  p.delta[i] = s;
-}
-
 // =============================================================================== dQ pass
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
@@ -306,7 +288,21 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   const float keep_scale = p.p_drop > 0.f ? 256.f / (float)(256 - thr) : 1.f;
   const int qgbase = (qrow >> 2) * p.Sk;
   const float lse2 = qrow < p.Sq ? p.lse[(long long)bh * p.Sq + qrow] * LOG2E : INFINITY;
-  const float dlt = qrow < p.Sq ? p.delta[(long long)bh * p.Sq + qrow] : 0.f;
+  // delta = rowsum(dO * O) of this lane's query, from the dO fragments already in registers + the
+  // same fragments of O (4 lane groups x 16 of the 64 dims); written for the dK/dV pass, which
+  // runs after this kernel -- no separate delta kernel (a strided 128-B-per-lane pass)
+  float dlt;
+  {
+    const bf16* Ob = p.o + b * p.o_bs + h * D;
+    const bf16x8 of0 = frag_global(Ob, p.o_rs, qrow, p.Sq, 0), of1 = frag_global(Ob, p.o_rs, qrow, p.Sq, 1);
+    float d = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d += bf2f(df0[e]) * bf2f(of0[e]) + bf2f(df1[e]) * bf2f(of1[e]);
+    d += __shfl_xor(d, 16, 64);
+    d += __shfl_xor(d, 32, 64);
+    dlt = d;
+    if (g == 0 && qrow < p.Sq) p.delta[(long long)bh * p.Sq + qrow] = d;
+  }
   f32x4 acc[4];
 #pragma unroll
   for (int db = 0; db < 4; ++db) acc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -494,8 +490,7 @@ int tfk_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
   p.dq_bs = gstrides[0]; p.dq_rs = (int)gstrides[1]; p.dk_bs = gstrides[2]; p.dk_rs = (int)gstrides[3];
   p.dv_bs = gstrides[4]; p.dv_rs = (int)gstrides[5];
   p.kv_len = kv_len; p.scale = scale; p.causal = causal; p.p_drop = p_drop; p.seed = seed; p.seed_key = tfk_seed_key();
-  const long long n = (long long)p.B * p.H * p.Sq;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, s, p);
+  // delta = rowsum(dO * O) is computed and stored by the dQ kernel's prologue
   if (attn_waves() == 8) {
     hipLaunchKernelGGL(attn_bwd_dq_kernel<8>, dim3((p.Sq + 127) / 128, p.H, p.B), dim3(512), 0, s, p);
     hipLaunchKernelGGL(attn_bwd_dkv_kernel<8>, dim3((p.Sk + 127) / 128, p.H, p.B), dim3(512), 0, s, p);

@@ -19,6 +19,7 @@
 #include "common.h"
 #include "gemm_params.h"
 #include "gemm_epilogue.h"
+#include "mx_common.h"
 
 namespace tfk {
 namespace {
@@ -190,35 +191,6 @@ struct QDesc {
   int t0, tcols;  // first tile of this tensor in the launch; column tiles
 };
 static_assert(sizeof(QDesc) == 56, "QDesc is packed as 7 int64 by ops/fp8.py");
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ int mx_exp_from_bits(unsigned amax_bits) {
-  const float amax = __uint_as_float(amax_bits << 16);
-  int ex = amax > 0.f ? (int)ceilf(log2f(amax * (1.f / 448.f))) : -127;
-  return ex < -127 ? -127 : (ex > 127 ? 127 : ex);
-}
-
-// 16 packed bf16 pairs (K order) -> 8 words of e4m3 bytes; returns the exponent
-__device__ __forceinline__ int mx_block_pk(const unsigned (&p)[16], unsigned (&w)[8]) {
-  u16x2 m = {0, 0};
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const unsigned a = p[i] & 0x7fff7fffu;
-    m = __builtin_elementwise_max(m, *(const u16x2*)&a);
-  }
-  const int ex = mx_exp_from_bits(m[0] > m[1] ? m[0] : m[1]);
-  const float s = ldexpf(1.f, ex < -126 ? -126 : ex);  // all-zero block: any normal scale gives 0
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    s16x2 r = {0, 0};
-    r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, *(const bf16x2*)&p[2 * k], s, false);
-    r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, *(const bf16x2*)&p[2 * k + 1], s, true);
-    w[k] = *(const unsigned*)&r;
-  }
-  return ex;
-}
-
 __device__ __forceinline__ void qd_load(const QDesc& d, int lt, int t, u32x4 (&r)[8]) {
   const int r0 = (lt / d.tcols) * QT, c0 = (lt % d.tcols) * QT;
   const int rows = min(QT, d.R - r0), cols = min(QT, d.C - c0);
@@ -484,7 +456,7 @@ int tfk_mx_quant(const void* x, void* q, void* s, long long nblocks, hipStream_t
 }
 // C[M][N] = epilogue(A q[M][K] x B q[N][K]^T), scales in p.a_scale / p.b_scale.
 // ext: 0 bf16 (bias/act/resid), 1 bf16 EXT (aux, dropout, activation backward), 2 f32 (alpha/beta:
-// weight gradients accumulate into the f32 arena).
+// weight gradients accumulate into the f32 arena), 3 EXT + MX-fp8 copies of the output (p.mx_*).
 extern "C" int tfk_g4_fp8_launch(const GemmParams& p, int epi, int splits, hipStream_t stream);
 // 1 = g4 LDS-DMA engine (default; 256x256 16-wave tiles measured 1.4-1.7x the bf16 g4 GEMM,
 // profiles/fp8_engine_r3a.jsonl), 0 = the register-staged kernel below (TFK_FP8_ENGINE=reg).
@@ -498,10 +470,11 @@ int tfk_gemm_mxfp8(GemmParams p, int ext, int splits, hipStream_t st) {
     g_fp8_engine = (e && e[0] == 'r') ? 0 : 1;
   }
   if (g_fp8_engine == 1) {
-    const int r = tfk_g4_fp8_launch(p, ext == 2 ? EPI_F32 : (ext ? EPI_BF16_EXT : EPI_BF16), splits, st);
-    if (r != -1) return r;
+    const int r = tfk_g4_fp8_launch(p, ext == 3 ? EPI_BF16_EXT_MX : ext == 2 ? EPI_F32 : (ext ? EPI_BF16_EXT : EPI_BF16),
+                                    splits, st);
+    if (r != -1 || ext == 3) return r;
   }
-  if (splits > 1) return -1;
+  if (splits > 1 || ext == 3) return -1;  // MX-output epilogue: g4 engine only
   const int BM = 128, BN = 128;
   p.tiles_n = (p.N + BN - 1) / BN;
   if (p.stats_shards < 1) p.stats_shards = 1;

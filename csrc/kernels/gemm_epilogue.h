@@ -4,6 +4,7 @@
 #pragma once
 #include "common.h"
 #include "gemm_params.h"
+#include "mx_common.h"
 
 #include <type_traits>
 
@@ -12,7 +13,68 @@ namespace tfk {
 // BNR: + fused BN-backward reduction; EXT: + aux (pre-activation) store, activation-backward
 // multiplier and dropout. Separate instantiations keep the common epilogue small enough to unroll
 // fully (a rolled epilogue indexes the accumulators dynamically -> they go to scratch).
-enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1, EPI_BF16_BNR = 2, EPI_BF16_EXT = 3 };
+// EXT_MX: EXT + MX-fp8 row and column block copies of the output (GemmParams mx_*), quantized from
+// the LDS C tile after the store pass (the MX-fp8 engine's producer GEMMs: no separate quantize pass).
+enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1, EPI_BF16_BNR = 2, EPI_BF16_EXT = 3, EPI_BF16_EXT_MX = 4 };
+
+// Both MX quantizations of the final [rows < BM][cols < BN] bf16 tile in LDS (row stride LDS_S):
+// row blocks of 32 columns -> mx_qr/mx_sr, column pairs of 32-row blocks (one 32-bit LDS word per
+// row holds both columns) -> mx_qc/mx_sc. Same bytes as fp8.hip's mx_quant_dual_kernel.
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void mx_tile_out(const GemmParams& p, const bf16* Cs, int lds_s, int m0, int n0) {
+  const int tid = threadIdx.x;
+  const int rows = min(BM, p.M - m0), cols = min(BN, p.N - n0);
+  const long long M = p.M, N = p.N;
+  unsigned char* qr = (unsigned char*)p.mx_qr;
+  unsigned char* sr = (unsigned char*)p.mx_sr;
+  unsigned char* qc = (unsigned char*)p.mx_qc;
+  unsigned char* sc = (unsigned char*)p.mx_sc;
+  constexpr int NB = BN / 32, RBLK = BM * NB;
+#pragma unroll
+  for (int k0 = 0; k0 < RBLK; k0 += NT) {
+    const int k = k0 + tid, row = k / NB, blk = k - row * NB;
+    if (k < RBLK && row < rows && blk * 32 < cols) {
+      unsigned pp[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const u32x4 h = *(const u32x4*)(Cs + row * lds_s + blk * 32 + q * 8);
+        pp[4 * q] = h[0]; pp[4 * q + 1] = h[1]; pp[4 * q + 2] = h[2]; pp[4 * q + 3] = h[3];
+      }
+      unsigned w[8];
+      const int ex = mx_block_pk(pp, w);
+      unsigned char* dst = qr + (m0 + row) * N + n0 + blk * 32;
+      *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+      *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+      sr[(m0 + row) * (N / 32) + n0 / 32 + blk] = (unsigned char)(ex + 127);
+    }
+  }
+  constexpr int NP = BN / 2, CBLK = NP * (BM / 32);
+#pragma unroll
+  for (int k0 = 0; k0 < CBLK; k0 += NT) {
+    const int k = k0 + tid, rg = k / NP, col = 2 * (k - rg * NP);
+    if (k < CBLK && col < cols && rg * 32 < rows) {
+      unsigned lo[16], hi[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned a = *(const unsigned*)(Cs + (rg * 32 + 2 * r) * lds_s + col);
+        const unsigned b = *(const unsigned*)(Cs + (rg * 32 + 2 * r + 1) * lds_s + col);
+        lo[r] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+        hi[r] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+      }
+      unsigned w[8];
+      int ex = mx_block_pk(lo, w);
+      unsigned char* dst = qc + (n0 + col) * M + m0 + rg * 32;
+      *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+      *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+      sc[(n0 + col) * (M / 32) + m0 / 32 + rg] = (unsigned char)(ex + 127);
+      ex = mx_block_pk(hi, w);
+      dst += M;
+      *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+      *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+      sc[(n0 + col + 1) * (M / 32) + m0 / 32 + rg] = (unsigned char)(ex + 127);
+    }
+  }
+}
 
 // LDS the bf16 epilogues need: the padded C tile + the [2][WM][BN] f32 BN-statistics partials.
 template <int BM, int BN, int WM>
@@ -61,6 +123,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int ml = lane & 15, nl = (lane >> 4) * 4;
+  constexpr bool ext = (EPI == EPI_BF16_EXT || EPI == EPI_BF16_EXT_MX), mx = (EPI == EPI_BF16_EXT_MX);
   if constexpr (EPI == EPI_F32) {
     // split_stride < 0: every split adds its partial straight into C with hardware f32 atomics
     // (global_atomic_add_f32, -munsafe-fp-atomics) -- no slab workspace, no reduce pass.
@@ -112,7 +175,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = acc[i][j][r] * p.alpha + bv[r];
-          if constexpr (EPI != EPI_BF16_EXT) v = act_apply(v, p.act);  // EXT: in the store pass
+          if constexpr (!ext) v = act_apply(v, p.act);  // EXT: in the store pass
           csum[j][r] += v;
           csq[j][r] += v * v;
           o[r] = f2bf(v);
@@ -180,11 +243,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     // load below is from an in-bounds address: absent tensors are not loaded at all (block-uniform
     // branches), and off the residual lattice the (unused) residual load reads C.
     constexpr int GB = BNRG > 0 ? BNRG : 1;
-    constexpr int GCAP = bnr ? GB : (EPI == EPI_BF16_EXT ? 2 : 4);
+    constexpr int GCAP = bnr ? GB : (ext ? 2 : 4);
     constexpr int G = NIT < GCAP ? NIT : GCAP;
     if (tile_fast) {
       const bf16* resid_b = p.resid ? (const bf16*)p.resid : (const bf16*)p.C;
-      const bf16* dsrc_b = (EPI == EPI_BF16_EXT && p.dact_src) ? (const bf16*)p.dact_src : (const bf16*)p.C;
+      const bf16* dsrc_b = (ext && p.dact_src) ? (const bf16*)p.dact_src : (const bf16*)p.C;
       const bf16* y_b = bnr ? (const bf16*)p.bn_y : nullptr;
       const bf16* y2_b = bnr ? (p.bn_y2 ? (const bf16*)p.bn_y2 : y_b) : nullptr;
       const unsigned char* mk_b = bnr ? (p.bn_amask ? p.bn_amask : (const unsigned char*)y_b) : nullptr;
@@ -195,11 +258,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         unsigned mk[GS];
         long long off[GS];
         bool rok[GS];
-        int mlog[GS], nlog[GS];
+        int mlog[GS], nlog[GS], lofs[GS];
 #pragma unroll
         for (int g = 0; g < GS; ++g) {
           const int idx = tid + (g0 + g) * NT;
           const int row = idx / CPR, cc = idx - row * CPR;
+          lofs[g] = row * LDC_S + cc * 8;
           const int m = m0 + row, n = n0 + cc * 8;
           long long mo = m, mr = m;
           if constexpr (bnr) { mo = out_row(p, m); mr = resid_row(p, mo); }
@@ -210,7 +274,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           // off the residual's sub-sampling lattice the (unused) load reads C itself: resid is the
           // smaller lattice tensor there, so resid + off[g] could run past its allocation
           if (p.resid) rr[g] = *(const bf16x8*)(rok[g] ? resid_b + bz * p.sC + mr * p.ldc + n : (const bf16*)p.C + off[g]);
-          if constexpr (EPI == EPI_BF16_EXT) {
+          if constexpr (ext) {
             if (p.dact_src) zv[g] = *(const bf16x8*)(dsrc_b + off[g]);
           }
           if constexpr (bnr) {
@@ -222,7 +286,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
         for (int g = 0; g < GS; ++g) {
           bf16x8 v = cv[g];
-          if constexpr (EPI == EPI_BF16_EXT) {
+          if constexpr (ext) {
             // pre-activation chunk: [* act'(z)] -> [aux copy] -> act -> [dropout]
             float f[8];
 #pragma unroll
@@ -269,7 +333,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
                 if (!((keepm >> e) & 1u)) v[e] = f2bf(0.f);
             }
           }
-          *(bf16x8*)((bf16*)p.C + off[g]) = v;
+          if constexpr (mx) {
+            *(bf16x8*)(Cs + lofs[g]) = v;  // the final value, for the MX pass
+            if (!p.mx_skip_c) *(bf16x8*)((bf16*)p.C + off[g]) = v;
+          } else {
+            *(bf16x8*)((bf16*)p.C + off[g]) = v;
+          }
           if constexpr (bnr) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -304,7 +373,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       bf16* dst = C + mo * p.ldc + n;
       if (n + 7 < p.N && (p.ldc & 7) == 0) {
         const long long off = bz * p.sC + mo * p.ldc + n;
-        if constexpr (EPI == EPI_BF16_EXT) {
+        if constexpr (ext) {
           // pre-activation chunk: [* act'(z)] -> [aux copy] -> act -> [dropout]; 16-B coalesced
           float f[8];
 #pragma unroll
@@ -354,12 +423,17 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
               if (!((keepm >> e) & 1u)) v[e] = f2bf(0.f);
           }
         }
-        *(bf16x8*)dst = v;
+        if constexpr (mx) {
+          *(bf16x8*)(Cs + row * LDC_S + cc * 8) = v;
+          if (!p.mx_skip_c) *(bf16x8*)dst = v;
+        } else {
+          *(bf16x8*)dst = v;
+        }
       } else {
         for (int e = 0; e < 8 && n + e < p.N; ++e) {
           const long long off = bz * p.sC + mo * p.ldc + n + e;
           float x = bf2f(v[e]);
-          if constexpr (EPI == EPI_BF16_EXT) {
+          if constexpr (ext) {
             if (p.dact_src) x *= act_grad(bf2f(((const bf16*)p.dact_src)[off]), p.dact);
             if (p.aux) ((bf16*)p.aux)[off] = v[e];
             x = act_apply(x, p.act);
@@ -373,6 +447,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       }
     }
     }  // ragged tile
+    if constexpr (mx) {
+      __syncthreads();  // every final chunk is in the LDS tile
+      mx_tile_out<BM, BN, NT>(p, Cs, LDC_S, m0, n0);
+    }
     if constexpr (bnr) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {

@@ -618,6 +618,9 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
     const char* e = getenv("TFK_FP8_TILE");
     g_fp8_tile = e ? atoi(e) : 0;
   }
+  if (epi == EPI_BF16_EXT_MX &&
+      (splits > 1 || (p.M & 31) || (p.N & 31) || p.ldc != p.N || !p.mx_qr || !p.mx_sr || !p.mx_qc || !p.mx_sc))
+    return -2;
   const int sld = p.K / 32;
   p.K /= 2;
   p.lda /= 2;
@@ -641,6 +644,8 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
       hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_F32>), grid, block, 0, stream, p, sld);                 \
     else if (epi == EPI_BF16_EXT)                                                                               \
       hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_BF16_EXT>), grid, block, 0, stream, p, sld);            \
+    else if (epi == EPI_BF16_EXT_MX)                                                                            \
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_BF16_EXT_MX>), grid, block, 0, stream, p, sld);         \
     else                                                                                                        \
       hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_BF16>), grid, block, 0, stream, p, sld);                \
   }

@@ -65,5 +65,14 @@ struct GemmParams {
   // Q and P*Q ((umulhi(x, mul) + x) >> shift, x < 2^31), filled by the g4 host launcher
   unsigned fd_q_mul, fd_pq_mul;
   int fd_q_shift, fd_pq_shift;
+  // EPI_BF16_EXT_MX (MX-fp8 engine): MX copies of the final bf16 output C [M][N] for the next GEMMs
+  // -- row blocks (mx_qr [M][N] e4m3, mx_sr [M][N/32] e8m0) and column blocks (mx_qc [N][M],
+  // mx_sc [N][M/32]) -- quantized from the LDS C tile (M, N % 32 == 0, ldc == N). mx_skip_c: no
+  // bf16 C store (its only consumers read the MX copies).
+  void* mx_qr;
+  void* mx_sr;
+  void* mx_qc;
+  void* mx_sc;
+  int mx_skip_c;
 };
 }  // namespace tfk

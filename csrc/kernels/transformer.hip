@@ -11,6 +11,7 @@
 // every sequence) by a plain batch reduction; token-type rows (2-4 rows hit by every token) by
 // per-thread partial sums and one atomic per block -- no hot-row atomic contention.
 #include "common.h"
+#include "mx_common.h"
 
 namespace {
 constexpr int NT = 256;
@@ -64,6 +65,111 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const bf16* __restrict__ x, 
     }
   }
   if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+}
+
+// LayerNorm forward that also emits both MX-fp8 quantizations of its output (the fp8 models' LN
+// outputs feed only MX-fp8 GEMMs: the QKV / FFN-in / cross-attention projections and the tied
+// logits): a block normalizes 32 rows (8 waves x 4 rows, same math as ln_fwd_kernel) into an LDS
+// tile, then quantizes it in row blocks (qr [M][W], sr [M][W/32]) and column blocks of 32 rows
+// (qc [W][M], sc [W][M/32]) -- the bytes of fp8.hip's dual quantizer without writing + re-reading
+// the bf16 output (y may be null: no bf16 store). M % 32 == 0, W % 32 == 0, W <= 1024.
+constexpr int LNMX_ROWS = 32, LNMX_NT = 512, LNMX_WMAX = 1024;
+template <int CPL>
+__global__ __launch_bounds__(LNMX_NT) void ln_fwd_mx_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, bf16* __restrict__ y,
+                                                           float* __restrict__ mean, float* __restrict__ rstd, int M, int W,
+                                                           float eps, unsigned char* __restrict__ qr,
+                                                           unsigned char* __restrict__ sr, unsigned char* __restrict__ qc,
+                                                           unsigned char* __restrict__ sc) {
+  __shared__ __attribute__((aligned(16))) bf16 tile[LNMX_ROWS][LNMX_WMAX + 8];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * LNMX_ROWS;
+  const int nch = W >> 3;
+  constexpr int RPW = LNMX_ROWS / (LNMX_NT / 64);
+#pragma unroll 1
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int lr = wv * RPW + rr, row = r0 + lr;
+    const bf16* xr = x + (long long)row * W;
+    float v[CPL][8];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        bf16x8 t = *(const bf16x8*)(xr + c * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { v[j][e] = bf2f(t[e]); s += v[j][e]; }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[j][e] = 0.f;
+      }
+    }
+    const float mu = wave_sum(s) / W;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j)
+      if (lane + 64 * j < nch)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float d = v[j][e] - mu; q += d * d; }
+    const float rs = rsqrtf(wave_sum(q) / W + eps);
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        f32x4 g0 = *(const f32x4*)(gamma + c * 8), g1 = *(const f32x4*)(gamma + c * 8 + 4);
+        f32x4 b0 = *(const f32x4*)(beta + c * 8), b1 = *(const f32x4*)(beta + c * 8 + 4);
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = f2bf((v[j][e] - mu) * rs * g0[e] + b0[e]);
+          o[e + 4] = f2bf((v[j][e + 4] - mu) * rs * g1[e] + b1[e]);
+        }
+        *(bf16x8*)&tile[lr][c * 8] = o;
+        if (y) *(bf16x8*)(y + (long long)row * W + c * 8) = o;
+      }
+    }
+    if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+  }
+  __syncthreads();
+  const long long Ml = M;
+  const int NB = W / 32;
+  for (int k = threadIdx.x; k < LNMX_ROWS * NB; k += LNMX_NT) {
+    const int lr = k / NB, blk = k - lr * NB;
+    unsigned pp[16];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const u32x4 h = *(const u32x4*)&tile[lr][blk * 32 + q4 * 8];
+      pp[4 * q4] = h[0]; pp[4 * q4 + 1] = h[1]; pp[4 * q4 + 2] = h[2]; pp[4 * q4 + 3] = h[3];
+    }
+    unsigned w[8];
+    const int ex = tfk::mx_block_pk(pp, w);
+    unsigned char* dst = qr + (long long)(r0 + lr) * W + blk * 32;
+    *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+    *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+    sr[(long long)(r0 + lr) * NB + blk] = (unsigned char)(ex + 127);
+  }
+  for (int cp = threadIdx.x; cp < W / 2; cp += LNMX_NT) {
+    const int col = 2 * cp;
+    unsigned lo[16], hi[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const unsigned a = *(const unsigned*)&tile[2 * r][col];
+      const unsigned b = *(const unsigned*)&tile[2 * r + 1][col];
+      lo[r] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+      hi[r] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+    }
+    unsigned w[8];
+    int ex = tfk::mx_block_pk(lo, w);
+    unsigned char* dst = qc + (long long)col * Ml + r0;
+    *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+    *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+    sc[(long long)col * (Ml / 32) + r0 / 32] = (unsigned char)(ex + 127);
+    ex = tfk::mx_block_pk(hi, w);
+    dst += Ml;
+    *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
+    *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+    sc[(long long)(col + 1) * (Ml / 32) + r0 / 32] = (unsigned char)(ex + 127);
+  }
 }
 
 template <int CPL>
@@ -268,6 +374,19 @@ int tfk_layernorm_fwd(const bf16* x, const float* gamma, const float* beta, bf16
   else if (cpl <= 2) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(NT), 0, s, x, gamma, beta, y, mean, rstd, M, W, eps);
   else if (cpl <= 4) hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(NT), 0, s, x, gamma, beta, y, mean, rstd, M, W, eps);
   else return -3;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// y may be null (MX outputs only); qr/sr/qc/sc: MX row / column block outputs (ln_fwd_mx_kernel)
+int tfk_layernorm_fwd_mx(const bf16* x, const float* gamma, const float* beta, bf16* y, float* mean, float* rstd, int M,
+                         int W, float eps, void* qr, void* sr, void* qc, void* sc, hipStream_t s) {
+  if (M % LNMX_ROWS || W % 32 || W > LNMX_WMAX) return -3;
+  const int cpl = (W / 8 + 63) / 64;
+  dim3 grid(M / LNMX_ROWS);
+  auto* q0 = (unsigned char*)qr; auto* s0 = (unsigned char*)sr; auto* q1 = (unsigned char*)qc; auto* s1 = (unsigned char*)sc;
+  if (cpl <= 1)
+    hipLaunchKernelGGL(ln_fwd_mx_kernel<1>, grid, dim3(LNMX_NT), 0, s, x, gamma, beta, y, mean, rstd, M, W, eps, q0, s0, q1, s1);
+  else
+    hipLaunchKernelGGL(ln_fwd_mx_kernel<2>, grid, dim3(LNMX_NT), 0, s, x, gamma, beta, y, mean, rstd, M, W, eps, q0, s0, q1, s1);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 // dxd (optional): also write dropout(dx; drop_p, drop_seed) -- the gradient the consumer's dropout

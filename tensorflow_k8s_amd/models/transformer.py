@@ -16,6 +16,7 @@ applied in the FFN2 dgrad epilogue from the saved pre-activation.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -27,6 +28,10 @@ from ..ops.loss import softmax_xent
 from ..runtime.arena import ParamArena
 from ..runtime.layers import Embedding, FusedLinear, LayerNorm, Linear
 from .bert import _mix
+
+# fp8 training: LayerNorms and FFN GEMMs that feed only MX-fp8 GEMMs emit those GEMMs' MX operands
+# themselves (ops.fp8 _register_out); TFK_FP8_MX_PRODUCERS=0 quantizes in separate passes instead
+MX_PRODUCERS = os.environ.get("TFK_FP8_MX_PRODUCERS", "1") == "1"
 
 
 @dataclass
@@ -99,9 +104,15 @@ class EncoderLayer:
         self.ffn_ln = self.ln2
         self.saved = None
 
+    @staticmethod
+    def _mx(x, lin, training) -> bool:
+        """fp8 training with the token count on whole MX-fp8 K-tiles: a LayerNorm whose output feeds
+        only `lin` emits that GEMM's MX operands itself (no bf16 output, no quantize pass)."""
+        return MX_PRODUCERS and lin.fp8 and training and (x.numel() // x.shape[-1]) % 128 == 0
+
     def _self_attn(self, x, B, S, kv_len, causal, seed, training):
         cfg = self.cfg
-        a, st1 = self.ln1.forward(x)
+        a, st1 = self.ln1.forward(x, mx_out=self._mx(x, self.att.qkv, training))
         qkv = self.att.qkv.forward(a)
         n = self.att.names
         sp = TR.AttnSpec(B, cfg.heads, S, S, (qkv, self.att.qkv.col(n["q"])), (qkv, self.att.qkv.col(n["k"])),
@@ -128,10 +139,13 @@ class EncoderLayer:
 
     def _ffn(self, x, seed, training):
         cfg = self.cfg
-        b, st = self.ffn_ln.forward(x)
+        b, st = self.ffn_ln.forward(x, mx_out=self._mx(x, self.ff1, training))
         z = torch.empty(b.shape[0], cfg.ffn, dtype=torch.bfloat16, device=x.device)
+        # fp8 training: ff1's epilogue writes MX(f) / MX(f^T) for ff2's forward and weight gradient --
+        # f itself is never read (ff2's dgrad takes relu' from z), so its bf16 store is skipped
+        mx = MX_PRODUCERS and self.ff1.fp8 and self.ff2.fp8 and training and b.shape[0] % 128 == 0
         f = self.ff1.forward(b, act="relu", aux=z, drop_p=cfg.relu_dropout if training else 0.0,
-                             drop_seed=_mix(seed, 5))
+                             drop_seed=_mix(seed, 5), mx_out=mx, mx_skip_c=mx)
         x2 = self.ff2.forward(f, resid=x, drop_p=cfg.dropout if training else 0.0, drop_seed=_mix(seed, 6))
         return x2, (x, b, st, z, f)
 
@@ -141,7 +155,7 @@ class EncoderLayer:
         dy = din if din is not None else E.dropout(dx2, cfg.dropout if training else 0.0, _mix(seed, 6))
         # relu backward and the relu-dropout backward in the ff2 dgrad epilogue (forward mask regenerated)
         dz = self.ff2.backward(dy, f, dact_src=z, dact="relu", drop_p=cfg.relu_dropout if training else 0.0,
-                               drop_seed=_mix(seed, 5))
+                               drop_seed=_mix(seed, 5), mx_dx=MX_PRODUCERS and self.ff1.fp8)  # fp8: MX(dz) for ff1
         db = self.ff1.backward(dz, b)
         return self.ffn_ln.backward(db, x, st, dres=dx2, drop=out_drop)
 
@@ -186,7 +200,7 @@ class DecoderLayer(EncoderLayer):
     def forward(self, y, mem, B, St, Ss, src_len, seed, training):
         cfg = self.cfg
         y1, s1 = self._self_attn(y, B, St, None, True, seed, training)
-        c, st2 = self.ln2.forward(y1)
+        c, st2 = self.ln2.forward(y1, mx_out=self._mx(y1, self.xatt.q, training))
         q = self.xatt.q.forward(c)
         kv = self.xatt.kv.forward(mem)
         n = self.xatt.names
@@ -273,11 +287,15 @@ class Transformer:
         x = self._embed(src, Ss, _mix(seed, 0xE0), training)
         for i, layer in enumerate(self.enc):
             x = layer.forward(x, B, Ss, src_len, _mix(seed, 100 + i), training)
-        mem, st_m = self.enc_ln.forward(x)
+        # fp8: the encoder memory feeds only the decoders' cross-attention K/V GEMMs, the final
+        # decoder state only the tied logits GEMM -> MX outputs straight from the LayerNorm
+        mx = MX_PRODUCERS and self.cfg.fp8 and training and (x.numel() // x.shape[-1]) % 128 == 0
+        mem, st_m = self.enc_ln.forward(x, mx_out=mx and all(l.xatt.kv.fp8 for l in self.dec))
         y = self._embed(tgt_in, St, _mix(seed, 0xE1), training)
         for i, layer in enumerate(self.dec):
             y = layer.forward(y, mem, B, St, Ss, src_len, _mix(seed, 200 + i), training)
-        yo, st_y = self.dec_ln.forward(y)
+        yo, st_y = self.dec_ln.forward(y, mx_out=MX_PRODUCERS and self.cfg.fp8 and training
+                                       and (y.numel() // y.shape[-1]) % 128 == 0)
         from ..runtime.layers import linear_forward
         logits = linear_forward(yo, self.emb.table.compute, None, self.cfg.fp8)  # tied softmax weights
         return logits, (x, mem, st_m, y, yo, st_y)

@@ -122,6 +122,11 @@ class GroupQuantizer:
 _WQ: dict[int, tuple] = {}
 
 
+def _shape2(x: torch.Tensor) -> tuple:
+    """The [rows, last] view every fp8 GEMM takes of an operand (keys of the per-step caches)."""
+    return (x.numel() // x.shape[-1], x.shape[-1]) if x.dim() else (1, 1)
+
+
 # Transposed MX operands produced in the forward for the backward of the same step: the forward
 # quantizes its input x and weight w in both directions with one read each (mx_quantize_dual) and
 # parks MX(x^T) (weight-gradient operand) and MX(w^T) (dgrad operand) here, keyed by the data
@@ -138,15 +143,15 @@ def save_t(x: torch.Tensor, qt) -> None:
         _SAVED.clear()
     k = x.data_ptr()
     e = _SAVED.get(k)
-    if e is not None and e[1] == tuple(x.shape) and e[2] is qt:
+    if e is not None and e[1] == _shape2(x) and e[2] is qt:
         e[3] += 1
     else:
-        _SAVED[k] = [x, tuple(x.shape), qt, 1]
+        _SAVED[k] = [x, _shape2(x), qt, 1]
 
 
 def take_t(x: torch.Tensor):
     e = _SAVED.get(x.data_ptr())
-    if e is None or e[1] != tuple(x.shape):
+    if e is None or e[1] != _shape2(x):
         return None
     e[3] -= 1
     if e[3] <= 0:
@@ -163,13 +168,17 @@ def clear_saved() -> None:
     _SAVED.clear()
     _WQ.clear()
     _XQ.clear()
+    _NO_C.clear()
 
 
 def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
                   resid: torch.Tensor | None = None, aux: torch.Tensor | None = None, drop_p: float = 0.0,
-                  drop_seed: int = 0, wq=None, save: bool = False) -> torch.Tensor:
+                  drop_seed: int = 0, wq=None, save: bool = False, mx_out: bool = False,
+                  mx_skip_c: bool = False) -> torch.Tensor:
     """y[M,N] = dropout(act(MX(x) @ MX(w)^T + bias)) (+ resid), bf16 out. wq: pre-quantized weight.
-    save: also produce MX(x^T) / MX(w^T) for this step's backward (save_t) where it will use fp8."""
+    save: also produce MX(x^T) / MX(w^T) for this step's backward (save_t) where it will use fp8.
+    mx_out: the epilogue also writes MX(y) and MX(y^T) (registered for the next fp8 GEMM on y, see
+    _register_out); mx_skip_c: ... and no bf16 y (the caller guarantees every consumer is such a GEMM)."""
     K = x.shape[-1]
     x2 = x.reshape(-1, K)
     M, N = x2.shape[0], w.shape[0]
@@ -184,16 +193,18 @@ def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = 
                 save_t(w, e[2][1])
     # training forwards only: an input saved for this step's backward is immutable until then, so a
     # second GEMM on the same tensor (the decoders' encoder memory) reuses its quantization
-    key = (x2.data_ptr(), tuple(x2.shape))
+    key = (x2.data_ptr(), _shape2(x2))
     xe = _XQ.get(key) if save and wg_ok else None
     if xe is not None:
         (xq, xs), xt = xe[1], xe[2]
         save_t(x2, xt)
     elif save and wg_ok:
+        _check_stored(x2)
         (xq, xs), xt = mx_quantize_dual(x2)
         save_t(x2, xt)
         _XQ[key] = (x2, (xq, xs), xt)
     else:
+        _check_stored(x2)
         xq, xs = mx_quantize(x2)
     if wq is not None:
         wq_, ws_ = wq
@@ -202,6 +213,7 @@ def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = 
         save_t(w, wt)
     else:
         wq_, ws_ = mx_quantize(w)
+    mx_out = mx_out and M % MX_BLOCK == 0 and N % MX_BLOCK == 0
     if not on_gpu(x):
         y = mx_dequantize(xq, xs) @ mx_dequantize(wq_, ws_).t()
         if bias is not None:
@@ -215,11 +227,51 @@ def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = 
         y = y.to(torch.bfloat16)
         if resid is not None:
             y = (y.float() + resid.reshape(-1, N).float()).to(torch.bfloat16)
+        if mx_out:
+            _register_out(y, *mx_quantize_dual(y))
         return y
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    mo = _mx_bufs(M, N, y.device) if mx_out else None
     lib().gemm_mxfp8(xq, xs, wq_, ws_, y, M, N, K, bias, resid.reshape(-1, N) if resid is not None else None,
-                     ACT[act], aux, drop_p, drop_seed)
+                     ACT[act], aux, drop_p, drop_seed, mx_out=list(mo) if mo else None, mx_skip_c=bool(mo and mx_skip_c))
+    if mo:
+        _register_out(y, (mo[0], mo[1]), (mo[2], mo[3]))
+        if mx_skip_c:
+            mark_no_c(y)
     return y
+
+
+def _mx_bufs(M: int, N: int, dev):
+    """Epilogue MX outputs of a bf16 [M, N]: (qr [M, N], sr [M, N/32], qc [N, M], sc [N, M/32])."""
+    return (torch.empty(M, N, dtype=torch.uint8, device=dev), torch.empty(M, N // MX_BLOCK, dtype=torch.uint8, device=dev),
+            torch.empty(N, M, dtype=torch.uint8, device=dev), torch.empty(N, M // MX_BLOCK, dtype=torch.uint8, device=dev))
+
+
+def _register_out(y: torch.Tensor, rowq, colq) -> None:
+    """A GEMM output whose MX copies its producer already wrote: the next linear_fwd_mx on y (training)
+    and fp8 backward operands of y (cached_dual) take them instead of quantizing y again."""
+    _XQ[(y.data_ptr(), _shape2(y))] = (y, rowq, colq)
+
+
+# outputs whose bf16 values were never stored (mx_skip_c): only their MX copies may be used
+_NO_C: set = set()
+
+
+def mark_no_c(y: torch.Tensor) -> None:
+    """y's bf16 values were never stored (only its MX copies, _register_out)."""
+    _NO_C.add((y.data_ptr(), _shape2(y)))
+
+
+def _check_stored(x: torch.Tensor) -> None:
+    if _NO_C and (x.data_ptr(), _shape2(x)) in _NO_C:
+        raise RuntimeError("fp8: a GEMM output produced with mx_skip_c (no bf16 values) reached a consumer "
+                           "that reads bf16 -- produce it with mx_skip_c=False")
+
+
+def cached_dual(y: torch.Tensor):
+    """(MX(y), MX(y^T)) of y when its producer emitted them this step, else None."""
+    e = _XQ.get((y.data_ptr(), _shape2(y)))
+    return (e[1], e[2]) if e is not None and e[2] is not None else None
 
 
 def mx_quantize_t(x: torch.Tensor):
@@ -243,7 +295,7 @@ def mx_backward_ok(M: int, N: int, K: int) -> tuple[bool, bool]:
 
 def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None = None,
                     dact_src: torch.Tensor | None = None, dact: str | None = None, wt=None, dyq=None,
-                    drop_p: float = 0.0, drop_seed: int = 0) -> torch.Tensor:
+                    drop_p: float = 0.0, drop_seed: int = 0, mx_out: bool = False) -> torch.Tensor:
     """dx[M,K] = dropout((MX(dy) @ MX(w^T)^T) [* act'(dact_src)]) (+ resid), bf16 -- the bf16
     linear_dgrad's epilogue order. wt: pre-quantized w^T (else the one the forward saved, else
     quantized here); dyq: pre-quantized dy."""
@@ -264,10 +316,15 @@ def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | Non
         y = y.to(torch.bfloat16)
         if resid is not None:
             y = (y.float() + resid.float()).to(torch.bfloat16)
+        if mx_out and M % MX_BLOCK == 0 and K % MX_BLOCK == 0:
+            _register_out(y, *mx_quantize_dual(y))
         return y
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
+    mo = _mx_bufs(M, K, dx.device) if mx_out and M % MX_BLOCK == 0 and K % MX_BLOCK == 0 else None
     lib().gemm_mxfp8(dq, ds, wq_, ws_, dx, M, K, N, None, resid, 0, None, drop_p, drop_seed,
-                     dact_src=dact_src, dact=ACT[dact] if dact_src is not None else 0)
+                     dact_src=dact_src, dact=ACT[dact] if dact_src is not None else 0, mx_out=list(mo) if mo else None)
+    if mo:
+        _register_out(dx, (mo[0], mo[1]), (mo[2], mo[3]))
     return dx
 
 
@@ -279,6 +336,8 @@ def linear_wgrad_mx(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumul
     K = x.shape[1]
     aq, as_ = dyt if dyt is not None else mx_quantize_t(dy)
     xt = take_t(x)
+    if xt is None:
+        _check_stored(x)
     bq, bs = xt if xt is not None else mx_quantize_t(x)
     if not on_gpu(dy):
         g = mx_dequantize(aq, as_) @ mx_dequantize(bq, bs).t()

@@ -20,21 +20,37 @@ HEAD_DIM = 64
 # ----------------------------------------------------------------------------- LayerNorm
 
 
-def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12):
-    """Returns (y bf16, mean f32 [M], rstd f32 [M])."""
+def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12,
+                  mx_out: bool = False, skip_y: bool = False):
+    """Returns (y bf16, mean f32 [M], rstd f32 [M]). mx_out (fp8 training): the kernel also writes
+    MX(y) and MX(y^T), registered for the fp8 GEMMs that consume y (ops.fp8 _register_out);
+    skip_y: ... and no bf16 y (every consumer is such a GEMM; ops.fp8 guards bf16 reads)."""
     W = x.shape[-1]
     x2 = x.reshape(-1, W)
     M = x2.shape[0]
+    mx_out = mx_out and M % 32 == 0 and W % 32 == 0 and W <= 1024
     if not on_gpu(x):
         xf = x2.float()
         mu = xf.mean(1)
         var = ((xf - mu[:, None]) ** 2).mean(1)
         rs = torch.rsqrt(var + eps)
         y = ((xf - mu[:, None]) * rs[:, None] * gamma + beta).to(torch.bfloat16)
-        return y.reshape(x.shape), mu, rs
+        y = y.reshape(x.shape)
+        if mx_out:
+            from . import fp8 as F8
+            F8._register_out(y, *F8.mx_quantize_dual(y.reshape(M, W)))
+        return y, mu, rs
     y = torch.empty_like(x)
     mean = torch.empty(M, dtype=torch.float32, device=x.device)
     rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+    if mx_out:
+        from . import fp8 as F8
+        qr, sr, qc, sc = F8._mx_bufs(M, W, x.device)
+        lib().layernorm_fwd_mx(x2, gamma, beta, None if skip_y else y, mean, rstd, M, W, eps, qr, sr, qc, sc)
+        F8._register_out(y, (qr, sr), (qc, sc))
+        if skip_y:
+            F8.mark_no_c(y)
+        return y, mean, rstd
     lib().layernorm_fwd(x2, gamma, beta, y, mean, rstd, M, W, eps)
     return y, mean, rstd
 

@@ -34,6 +34,8 @@ def linear_forward(x, w, b, fp8: bool, **kw):
     if fp8 and x.shape[-1] % 128 == 0:
         from ..ops.fp8 import linear_fwd_mx
         return linear_fwd_mx(x, w, b, save=True, **kw)
+    kw.pop("mx_out", None)
+    kw.pop("mx_skip_c", None)
     return G.linear_fwd(x, w, b, **kw)
 
 
@@ -47,7 +49,9 @@ def fp8_dy(dy, K: int, fp8: bool):
     M, N = dy.shape
     dg, wg = mx_backward_ok(M, N, K)
     if dg and wg:
-        return mx_quantize_dual(dy)
+        from ..ops.fp8 import cached_dual
+        c = cached_dual(dy)  # the dgrad that produced dy already wrote its MX copies
+        return c if c is not None else mx_quantize_dual(dy)
     return None, None
 
 
@@ -67,6 +71,7 @@ def linear_dgrad(dy, w, fp8: bool, drop_p: float = 0.0, drop_seed: int = 0, dyq=
         from ..ops.fp8 import linear_dgrad_mx, mx_backward_ok
         if mx_backward_ok(dy.shape[0], dy.shape[1], w.shape[1])[0]:
             return linear_dgrad_mx(dy, w, dyq=dyq, drop_p=drop_p, drop_seed=drop_seed, **kw)
+    kw.pop("mx_out", None)
     return G.linear_dgrad(dy, w, drop_p=drop_p, drop_seed=drop_seed, **kw)
 
 
@@ -198,14 +203,19 @@ class Linear:
         self.fp8 = False  # forward, dgrad and wgrad GEMMs in MX-fp8 (ops.fp8)
         self.split_target = None  # weight-gradient split-K fill target override (ops.gemm.pick_splits)
 
-    def forward(self, x, act=None, resid=None, aux=None, drop_p: float = 0.0, drop_seed: int = 0):
+    def forward(self, x, act=None, resid=None, aux=None, drop_p: float = 0.0, drop_seed: int = 0,
+                mx_out: bool = False, mx_skip_c: bool = False):
+        """mx_out / mx_skip_c (fp8): the epilogue also emits MX(y), MX(y^T) for the next fp8 GEMM on y
+        (and skips the bf16 y when every consumer is such a GEMM; ops.fp8.linear_fwd_mx)."""
+        kw = {"mx_out": mx_out, "mx_skip_c": mx_skip_c} if mx_out else {}
         return linear_forward(x, self.w.compute, self.b.master if self.b else None, self.fp8, act=act, resid=resid,
-                              aux=aux, drop_p=drop_p, drop_seed=drop_seed)
+                              aux=aux, drop_p=drop_p, drop_seed=drop_seed, **kw)
 
     def backward(self, dy, x, need_dx: bool = True, resid=None, accumulate: bool = False, dact_src=None,
-                 dact=None, drop_p: float = 0.0, drop_seed: int = 0):
+                 dact=None, drop_p: float = 0.0, drop_seed: int = 0, mx_dx: bool = False):
         """dy: gradient of this layer's (pre-dropout, post-activation-backward) output. drop_p/drop_seed:
-        a forward dropout on this layer's input, whose backward is fused into the dgrad epilogue."""
+        a forward dropout on this layer's input, whose backward is fused into the dgrad epilogue.
+        mx_dx (fp8): the dgrad epilogue also emits MX(dx), MX(dx^T) for the producer's fp8 backward."""
         dyq, dyt = fp8_dy(dy.reshape(-1, dy.shape[-1]), self.fin, self.fp8 and need_dx)
         linear_wgrad(dy, x, self.w.grad, self.fp8, accumulate=accumulate, split_target=self.split_target, dyt=dyt)
         if self.b is not None:
@@ -215,8 +225,9 @@ class Linear:
             self.arena.grad_ready(self.w)
         if not need_dx:
             return None
+        kw = {"mx_out": True} if mx_dx else {}
         return linear_dgrad(dy, self.w.compute, self.fp8, resid=resid, dact_src=dact_src, dact=dact, drop_p=drop_p,
-                            drop_seed=drop_seed, dyq=dyq)
+                            drop_seed=drop_seed, dyq=dyq, **kw)
 
 
 class FusedLinear:
@@ -294,8 +305,9 @@ class LayerNorm:
         self.gamma = arena.add(ParamSpec(f"{name}/{names[0]}", (W,), init="ones", decay=False))
         self.beta = arena.add(ParamSpec(f"{name}/{names[1]}", (W,), init="zeros", decay=False))
 
-    def forward(self, x):
-        y, mu, rs = TR.layernorm_fwd(x, self.gamma.master, self.beta.master, self.eps)
+    def forward(self, x, mx_out: bool = False):
+        """mx_out (fp8 training): y feeds only MX-fp8 GEMMs -- emit MX(y), MX(y^T), no bf16 y."""
+        y, mu, rs = TR.layernorm_fwd(x, self.gamma.master, self.beta.master, self.eps, mx_out=mx_out, skip_y=mx_out)
         return y, (mu, rs)
 
     def backward(self, dy, x, stats, dres=None, drop=None):

@@ -219,3 +219,78 @@ def test_group_quantizer_matches_per_tensor_dual():
     torch.cuda.synchronize()
     assert torch.equal(y_pre, y_fly)
     F8.clear_saved()
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 1024, 1024), (288, 320, 256), (4096, 4096, 1024)])
+def test_mx_epilogue_outputs_equal_dual_quantizer(M, N, K):
+    """EPI_BF16_EXT_MX: the fp8 GEMM's epilogue writes MX(y) and MX(y^T) from its LDS tile -- the
+    same bytes and scales as mx_quantize_dual of the bf16 y it stores (relu + aux + dropout forward;
+    relu-backward + dropout dgrad), ragged tiles included; with mx_skip_c the MX copies are unchanged
+    and the consumers take them (no bf16 read)."""
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16).cuda()
+    b = (torch.randn(N, generator=g) * 0.1).cuda()
+    z = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    F8.clear_saved()
+    y = F8.linear_fwd_mx(x, w, b, act="relu", aux=z, drop_p=0.1, drop_seed=3, mx_out=True)
+    c = F8.cached_dual(y)
+    assert c is not None
+    (q1, s1), (qt1, st1) = F8.mx_quantize_dual(y)
+    torch.cuda.synchronize()
+    (q, s), (qt, st) = c
+    assert torch.equal(q, q1) and torch.equal(s, s1)
+    assert torch.equal(qt, qt1) and torch.equal(st, st1)
+    # same GEMM without the MX outputs: identical bf16 y and aux
+    z2 = torch.empty_like(z)
+    y2 = F8.linear_fwd_mx(x, w, b, act="relu", aux=z2, drop_p=0.1, drop_seed=3)
+    assert torch.equal(y, y2) and torch.equal(z, z2)
+    # skip-C: the MX copies are the same, the consumer's forward uses them
+    F8.clear_saved()
+    y3 = F8.linear_fwd_mx(x, w, b, act="relu", aux=z2, drop_p=0.1, drop_seed=3, mx_out=True, mx_skip_c=True)
+    (q3, s3), (qt3, st3) = F8.cached_dual(y3)
+    torch.cuda.synchronize()
+    assert torch.equal(q3, q1) and torch.equal(qt3, qt1) and torch.equal(s3, s1) and torch.equal(st3, st1)
+    if K % 128 == 0 and N % 128 == 0:
+        w2 = (torch.randn(K, N, generator=g) * 0.05).to(torch.bfloat16).cuda()
+        out_skip = F8.linear_fwd_mx(y3, w2, save=True)
+        F8.clear_saved()
+        out_ref = F8.linear_fwd_mx(y, w2, save=True)
+        torch.cuda.synchronize()
+        assert torch.equal(out_skip, out_ref)
+    F8.clear_saved()
+    # dgrad with relu' + dropout: MX(dx) from the epilogue == dual quantization of dx
+    if N % 128 == 0:
+        dy = torch.randn(M, N, generator=g).to(torch.bfloat16).cuda()
+        dx = F8.linear_dgrad_mx(dy, w, dact_src=z, dact="relu", drop_p=0.1, drop_seed=4, mx_out=True)
+        (dq, ds_), (dqt, dst) = F8.cached_dual(dx)
+        (dq1, ds1), (dqt1, dst1) = F8.mx_quantize_dual(dx)
+        dx_plain = F8.linear_dgrad_mx(dy, w, dact_src=z, dact="relu", drop_p=0.1, drop_seed=4)
+        torch.cuda.synchronize()
+        assert torch.equal(dx, dx_plain)
+        assert torch.equal(dq, dq1) and torch.equal(ds_, ds1) and torch.equal(dqt, dqt1) and torch.equal(dst, dst1)
+    F8.clear_saved()
+
+
+@pytest.mark.parametrize("M,W", [(256, 1024), (96, 768), (8192, 1024)])
+def test_layernorm_mx_outputs_equal_dual_quantizer(M, W):
+    """layernorm_fwd_mx: y, mean, rstd identical to the plain LayerNorm kernel, and its MX row /
+    column blocks identical to mx_quantize_dual(y); with skip_y the MX copies are unchanged."""
+    from tensorflow_k8s_amd.ops import transformer as T
+    g = torch.Generator().manual_seed(W)
+    x = (torch.randn(M, W, generator=g) * 3).to(torch.bfloat16).cuda()
+    gm = (torch.rand(W, generator=g) + 0.5).cuda()
+    bt = (torch.randn(W, generator=g) * 0.1).cuda()
+    F8.clear_saved()
+    y0, mu0, rs0 = T.layernorm_fwd(x, gm, bt, 1e-6)
+    y1, mu1, rs1 = T.layernorm_fwd(x, gm, bt, 1e-6, mx_out=True)
+    (q, s), (qt, st) = F8.cached_dual(y1)
+    (q0, s0), (qt0, st0) = F8.mx_quantize_dual(y0)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1) and torch.equal(mu0, mu1) and torch.equal(rs0, rs1)
+    assert torch.equal(q, q0) and torch.equal(s, s0) and torch.equal(qt, qt0) and torch.equal(st, st0)
+    y2, _, _ = T.layernorm_fwd(x, gm, bt, 1e-6, mx_out=True, skip_y=True)
+    (q2, s2), (qt2, st2) = F8.cached_dual(y2)
+    torch.cuda.synchronize()
+    assert torch.equal(q2, q0) and torch.equal(qt2, qt0) and torch.equal(s2, s0) and torch.equal(st2, st0)
+    F8.clear_saved()

@@ -90,3 +90,26 @@ def test_transformer_fp8_forward_close_to_bf16():
         res[fp8] = (float(loss.mean()), m.arena.grad.clone())
     assert abs(res[True][0] - res[False][0]) / res[False][0] < 0.02
     assert _cos(res[True][1], res[False][1]) > 0.98
+
+
+def test_transformer_fp8_mx_producers_match_separate_quantization():
+    """fp8 training with 128-token batches: LayerNorms / FFN GEMMs that emit their consumers' MX
+    operands (models.transformer MX_PRODUCERS, ops.fp8 _register_out; bf16 outputs skipped) give the
+    same loss and gradients, bit for bit, as quantizing every GEMM input in a separate pass."""
+    import tensorflow_k8s_amd.models.transformer as TM
+    from tensorflow_k8s_amd.ops import fp8 as F8
+    res = {}
+    for prod in (False, True):
+        TM.MX_PRODUCERS = prod
+        try:
+            cfg = TM.TransformerConfig(vocab_size=500, hidden=128, enc_layers=1, dec_layers=2, heads=2, ffn=256,
+                                       src_len=64, tgt_len=64, max_len=128, dropout=0.1, attn_dropout=0.1,
+                                       relu_dropout=0.1, fp8=True)
+            m = TM.Transformer(cfg).to("cpu", seed=4)
+            loss, _ = m.forward_backward(*m.synthetic_batch(2, "cpu", seed=1))
+            res[prod] = (loss.clone(), m.arena.grad.clone(), len(F8._XQ))
+        finally:
+            TM.MX_PRODUCERS = True
+    assert res[True][2] > res[False][2]  # producers registered their MX outputs
+    assert torch.equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])

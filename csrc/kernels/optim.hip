@@ -3,6 +3,7 @@
 // the bf16 compute copy refreshed in the same pass. grad_scale may be a device scalar (global-norm
 // clipping / loss-scale) so nothing synchronises with the host.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 constexpr int NT = 256;
@@ -90,6 +91,63 @@ __global__ void adamw4_kernel(float* __restrict__ w, bf16* __restrict__ wb, cons
     if (wb) {
       bf16 o[4] = {f2bf(ww[0]), f2bf(ww[1]), f2bf(ww[2]), f2bf(ww[3])};
       *(uint2*)(wb + 4 * i) = *(const uint2*)o;
+    }
+  }
+}
+
+// AdamW v2: each thread updates TWO float4s per iteration with every load of both issued before
+// any math (8 x 16-B streams in flight per thread), nontemporal (streaming) loads and stores -- the
+// optimizer touches each byte once per step, so it should not evict the GEMM working set from L2 --
+// and a resident grid (8 blocks per CU). Same arithmetic as adamw4_kernel, bit for bit.
+__device__ __forceinline__ float4 ntl(const float4* p) {
+  float4 r;
+  r.x = __builtin_nontemporal_load(&p->x); r.y = __builtin_nontemporal_load(&p->y);
+  r.z = __builtin_nontemporal_load(&p->z); r.w = __builtin_nontemporal_load(&p->w);
+  return r;
+}
+__device__ __forceinline__ void nts(float4* p, float4 v) {
+  __builtin_nontemporal_store(v.x, &p->x); __builtin_nontemporal_store(v.y, &p->y);
+  __builtin_nontemporal_store(v.z, &p->z); __builtin_nontemporal_store(v.w, &p->w);
+}
+__global__ __launch_bounds__(NT) void adamw4x2_kernel(float* __restrict__ w, bf16* __restrict__ wb,
+                                                      const float* __restrict__ g, float* __restrict__ m,
+                                                      float* __restrict__ v, long long n4, float lr_h, float b1,
+                                                      float b2, float eps, float wd, float bc1, float bc2,
+                                                      float gs_host, const float* gs_dev, const float* hp) {
+  const float gs = gscale_of(gs_host, gs_dev);
+  const float lr = hp_or(hp, 0, lr_h);
+  const float ibc1 = 1.f / hp_or(hp, 1, bc1), ibc2 = 1.f / hp_or(hp, 2, bc2);
+  const long long stride = (long long)gridDim.x * NT;
+  for (long long i0 = (long long)blockIdx.x * NT + threadIdx.x; i0 < n4; i0 += 2 * stride) {
+    const long long i1 = i0 + stride;
+    const bool two = i1 < n4;
+    float4 gr[2], mm[2], vv[2], ww[2];
+    gr[0] = ntl((const float4*)g + i0); mm[0] = ntl((const float4*)m + i0);
+    vv[0] = ntl((const float4*)v + i0); ww[0] = ntl((const float4*)w + i0);
+    if (two) {
+      gr[1] = ntl((const float4*)g + i1); mm[1] = ntl((const float4*)m + i1);
+      vv[1] = ntl((const float4*)v + i1); ww[1] = ntl((const float4*)w + i1);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k == 1 && !two) break;
+      float a[4] = {gr[k].x, gr[k].y, gr[k].z, gr[k].w}, b[4] = {mm[k].x, mm[k].y, mm[k].z, mm[k].w};
+      float c[4] = {vv[k].x, vv[k].y, vv[k].z, vv[k].w}, d[4] = {ww[k].x, ww[k].y, ww[k].z, ww[k].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float gg = a[e] * gs;
+        b[e] = b1 * b[e] + (1.f - b1) * gg;
+        c[e] = b2 * c[e] + (1.f - b2) * gg * gg;
+        d[e] -= lr * ((b[e] * ibc1) / (sqrtf(c[e] * ibc2) + eps) + wd * d[e]);
+      }
+      const long long i = k ? i1 : i0;
+      nts((float4*)m + i, make_float4(b[0], b[1], b[2], b[3]));
+      nts((float4*)v + i, make_float4(c[0], c[1], c[2], c[3]));
+      nts((float4*)w + i, make_float4(d[0], d[1], d[2], d[3]));
+      if (wb) {
+        bf16 o[4] = {f2bf(d[0]), f2bf(d[1]), f2bf(d[2]), f2bf(d[3])};
+        *(uint2*)(wb + 4 * i) = *(const uint2*)o;
+      }
     }
   }
 }
@@ -196,8 +254,17 @@ int tfk_adamw(float* w, bf16* wb, const float* g, float* m, float* v, long long 
   const bool vec = (((uintptr_t)w | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 && (((uintptr_t)wb) & 7) == 0;
   if (vec && n >= 4) {
     const long long n4 = n / 4, done = n4 * 4;
-    hipLaunchKernelGGL(adamw4_kernel, dim3(grid_for(n4)), dim3(NT), 0, s, w, wb, g, m, v, n4, lr, b1, b2, eps, wd, bc1,
-                       bc2, gs, gs_dev, hp);
+    static int v2 = -1;
+    if (v2 < 0) {
+      const char* e = getenv("TFK_ADAMW_V2");
+      v2 = e ? atoi(e) : 1;
+    }
+    if (v2)
+      hipLaunchKernelGGL(adamw4x2_kernel, dim3(grid_for(n4, 2048)), dim3(NT), 0, s, w, wb, g, m, v, n4, lr, b1, b2, eps,
+                         wd, bc1, bc2, gs, gs_dev, hp);
+    else
+      hipLaunchKernelGGL(adamw4_kernel, dim3(grid_for(n4)), dim3(NT), 0, s, w, wb, g, m, v, n4, lr, b1, b2, eps, wd, bc1,
+                         bc2, gs, gs_dev, hp);
     if (done < n)
       hipLaunchKernelGGL(adamw_kernel, dim3(1), dim3(NT), 0, s, w + done, wb ? wb + done : nullptr, g + done, m + done,
                          v + done, n - done, lr, b1, b2, eps, wd, bc1, bc2, gs, gs_dev, hp);

@@ -86,19 +86,29 @@ __global__ __launch_bounds__(LNMX_NT) void ln_fwd_mx_kernel(const bf16* __restri
   const int r0 = blockIdx.x * LNMX_ROWS;
   const int nch = W >> 3;
   constexpr int RPW = LNMX_ROWS / (LNMX_NT / 64);
-#pragma unroll 1
+  // all RPW rows' loads issued up front (RPW x CPL 16-B vectors in flight per lane), then the
+  // per-row reductions: one memory latency per wave instead of RPW
+  bf16x8 raw[RPW][CPL];
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const bf16* xr = x + (long long)(r0 + wv * RPW + rr) * W;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) raw[rr][j] = *(const bf16x8*)(xr + c * 8);
+    }
+  }
+#pragma unroll
   for (int rr = 0; rr < RPW; ++rr) {
     const int lr = wv * RPW + rr, row = r0 + lr;
-    const bf16* xr = x + (long long)row * W;
     float v[CPL][8];
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
       const int c = lane + 64 * j;
       if (c < nch) {
-        bf16x8 t = *(const bf16x8*)(xr + c * 8);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { v[j][e] = bf2f(t[e]); s += v[j][e]; }
+        for (int e = 0; e < 8; ++e) { v[j][e] = bf2f(raw[rr][j][e]); s += v[j][e]; }
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[j][e] = 0.f;

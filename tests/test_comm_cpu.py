@@ -188,8 +188,10 @@ assert (sub is None) == (rank == 2)  # non-members get no sub-communicator
 if sub is not None:
     sub.all_reduce(y)
 c.barrier()
-print(json.dumps({"rank": rank, "uid": hashlib.sha1(uid).hexdigest(), "sum": x[0].item(), "max": mx.item(),
-                  "gather": g.tolist(), "sub": y[0].item(), "backend": c.backend}), flush=True)
+# one file per rank (3 ranks printing to one pipe can interleave inside a line)
+with open(f"rank{rank}.json", "w") as f:
+    f.write(json.dumps({"rank": rank, "uid": hashlib.sha1(uid).hexdigest(), "sum": x[0].item(), "max": mx.item(),
+                        "gather": g.tolist(), "sub": y[0].item(), "backend": c.backend}))
 tfk_comm.shutdown()
 """
 
@@ -206,7 +208,7 @@ def test_tfk_comm_bootstrap_under_torchrun(tmp_path):
                         "127.0.0.1", "--master-port", str(free_port()), str(script)], env=env, capture_output=True,
                        text=True, timeout=240, cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    rows = sorted((json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"rank"')), key=lambda d: d["rank"])
+    rows = sorted((json.loads((tmp_path / f"rank{i}.json").read_text()) for i in range(3)), key=lambda d: d["rank"])
     assert len(rows) == 3 and len({d["uid"] for d in rows}) == 1
     for d in rows:
         assert d["sum"] == 6.0 and d["max"] == 2.0 and d["gather"] == [0.0, 10.0, 20.0] and d["backend"] == "gloo"

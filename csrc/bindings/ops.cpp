@@ -10,6 +10,12 @@
 #include "bind_util.h"
 #include "../kernels/gemm_params.h"
 
+// common.h drop_thr8 (8-bit dropout threshold round(256 p)), host copy in the same float arithmetic
+static inline int drop_thr8_host(float p) {
+  const int t = (int)(p * 256.f + 0.5f);
+  return t > 255 ? 255 : (t < 0 ? 0 : t);
+}
+
 extern "C" {
 int tfk_gemm_launch(tfk::GemmParams p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits, hipStream_t s);
 int tfk_gemm_splits(int K, int splits);
@@ -220,7 +226,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "drop_p");
   TORCH_CHECK(drop_p == 0.0 || (epi == 0 && ldc == N && batch == 1), "fused dropout needs bf16 out, ldc==N, batch 1");
   p.drop_p = (float)drop_p;
-  p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
+  p.drop_scale = drop_p > 0.0 ? 256.f / (float)(256 - drop_thr8_host((float)drop_p)) : 1.f;
   p.drop_seed = (unsigned long long)drop_seed;
   p.drop_seed_key = tfk_seed_key();
   const bool dense_a = amode == A_KIN || amode == A_KOUT;
@@ -356,7 +362,7 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
   p.resid = opt_ptr<const void>(resid);
   p.aux = opt_ptr<void>(aux);
   p.drop_p = (float)drop_p;
-  p.drop_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
+  p.drop_scale = drop_p > 0.0 ? 256.f / (float)(256 - drop_thr8_host((float)drop_p)) : 1.f;
   p.drop_seed = (unsigned long long)drop_seed;
   p.drop_seed_key = tfk_seed_key();
   if (dact_src.has_value() && dact_src->defined()) {

@@ -14,7 +14,7 @@ int tfk_layernorm_fwd(const void*, const float*, const float*, void*, float*, fl
 int tfk_layernorm_fwd_mx(const void*, const float*, const float*, void*, float*, float*, int, int, float, void*, void*, void*,
                          void*, hipStream_t);
 int tfk_layernorm_bwd(const void*, const void*, const float*, const float*, const float*, const void*, void*, float*,
-                      float*, int, int, void*, float, unsigned long long, hipStream_t);
+                      float*, int, int, void*, float, unsigned long long, float*, hipStream_t);
 int tfk_embedding_fwd(const int*, const void*, int, const void*, int, const int*, const void*, int, void*, long long, int,
                       float, hipStream_t);
 int tfk_embedding_bwd(const int*, const void*, int, float*, float*, int, const int*, float*, int, long long, int, float,
@@ -61,7 +61,9 @@ void layernorm_fwd_mx(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, 
 
 void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor gamma, torch::Tensor mean, torch::Tensor rstd,
                    c10::optional<torch::Tensor> dres, torch::Tensor dx, torch::Tensor dgamma, torch::Tensor dbeta,
-                   int64_t M, int W, c10::optional<torch::Tensor> dxd, double drop_p, int64_t drop_seed) {
+                   int64_t M, int W, c10::optional<torch::Tensor> dxd, double drop_p, int64_t drop_seed,
+                   c10::optional<torch::Tensor> dbias) {
+  if (dbias.has_value() && dbias->defined()) { need_f32(*dbias, "dbias"); need_numel(*dbias, W, "dbias"); }
   need_bf16(dy, "dy"); need_bf16(x, "x"); need_bf16(dx, "dx");
   for (auto* t : {&gamma, &mean, &rstd, &dgamma, &dbeta}) need_f32(*t, "ln vector");
   TORCH_CHECK(W % 8 == 0 && W <= 2048, "layernorm needs W%8==0 and W<=2048");
@@ -76,7 +78,7 @@ void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor gamma, torch
   check_rc(tfk_layernorm_bwd(dy.data_ptr(), x.data_ptr(), gamma.data_ptr<float>(), mean.data_ptr<float>(),
                              rstd.data_ptr<float>(), opt_ptr<const void>(dres), dx.data_ptr(), dgamma.data_ptr<float>(),
                              dbeta.data_ptr<float>(), (int)M, W, opt_ptr<void>(dxd), (float)drop_p,
-                             (unsigned long long)drop_seed, cur_stream()),
+                             (unsigned long long)drop_seed, opt_ptr<float>(dbias), cur_stream()),
            "layernorm_bwd");
 }
 
@@ -197,7 +199,9 @@ void attn_bwd(torch::Tensor q, int64_t qo, torch::Tensor k, int64_t ko, torch::T
 void register_transformer_ops(pybind11::module& m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_fwd_mx", &layernorm_fwd_mx);
-  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
+        py::arg("rstd"), py::arg("dres"), py::arg("dx"), py::arg("dgamma"), py::arg("dbeta"), py::arg("M"), py::arg("W"),
+        py::arg("dxd"), py::arg("drop_p"), py::arg("drop_seed"), py::arg("dbias") = py::none());
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("attn_fwd", &attn_fwd);

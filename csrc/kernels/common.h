@@ -118,12 +118,35 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   return x;
 }
 // Elementwise dropout masks (GEMM epilogues, dropout kernels, LayerNorm-backward dropout): the
-// 64-bit seed (salt + per-step key) folds once into a 32-bit stream seed, then ONE hash32 per
-// element index (indices < 2^32): ~7 VALU ops per element instead of hash_u32's ~35, which made the
-// dropout-carrying GEMM epilogues VALU-bound (ops/elementwise.py dropout_keep is the CPU copy).
+// 64-bit seed (salt + per-step key) folds once into a 32-bit stream seed; ONE hash32 per group of 4
+// consecutive elements gives 4 mask bytes -- element i is kept iff byte (i & 3) of
+// hash32(s32 ^ (i >> 2)) >= thr = round(256 p), scaled by 256 / (256 - thr) (exactly unbiased).
+// A hash per element (two quarter-rate multiplies + shifts) was the largest VALU cost of the
+// dropout-carrying GEMM epilogues (ops/elementwise.py dropout_keep is the bit-exact CPU copy).
 __device__ __forceinline__ uint32_t drop_seed32(unsigned long long s) {
   return hash32((uint32_t)s ^ hash32((uint32_t)(s >> 32) ^ 0x9E3779B9u));
 }
-__device__ __forceinline__ bool drop_keep(uint32_t s32, unsigned long long idx, float keep) {
-  return u01(hash32(s32 ^ (uint32_t)idx)) < keep;
+__host__ __device__ __forceinline__ int drop_thr8(float p) {
+  const int t = (int)(p * 256.f + 0.5f);
+  return t > 255 ? 255 : (t < 0 ? 0 : t);
+}
+__host__ __device__ __forceinline__ float drop_scale8(float p) { return 256.f / (float)(256 - drop_thr8(p)); }
+__device__ __forceinline__ bool drop_keep1(uint32_t s32, unsigned long long idx, int thr) {
+  return ((hash32(s32 ^ (uint32_t)(idx >> 2)) >> (8 * (unsigned)(idx & 3))) & 0xffu) >= (uint32_t)thr;
+}
+// keep bits (bit e) of elements base .. base+7, any base (two hashes when base % 4 == 0)
+__device__ __forceinline__ unsigned drop_keep8(uint32_t s32, unsigned long long base, int thr) {
+  unsigned m = 0;
+  if ((base & 3) == 0) {
+    const uint32_t h0 = hash32(s32 ^ (uint32_t)(base >> 2)), h1 = hash32(s32 ^ (uint32_t)((base >> 2) + 1));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      m |= ((h0 >> (8 * e)) & 0xffu) >= (uint32_t)thr ? (1u << e) : 0u;
+      m |= ((h1 >> (8 * e)) & 0xffu) >= (uint32_t)thr ? (1u << (e + 4)) : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m |= drop_keep1(s32, base + e, thr) ? (1u << e) : 0u;
+  }
+  return m;
 }

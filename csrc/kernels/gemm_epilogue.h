@@ -300,9 +300,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             for (int e = 0; e < 8; ++e) f[e] = act_apply(f[e], p.act);
             if (p.drop_p > 0.f) {
               const unsigned long long lin = (unsigned long long)mlog[g] * p.N + nlog[g];
+              const unsigned km = drop_keep8(drop_seed32(eff_seed(p.drop_seed, p.drop_seed_key)), lin, drop_thr8(p.drop_p));
 #pragma unroll
-              for (int e = 0; e < 8; ++e)
-                f[e] = drop_keep(drop_seed32(eff_seed(p.drop_seed, p.drop_seed_key)), lin + e, 1.f - p.drop_p) ? f[e] * p.drop_scale : 0.f;
+              for (int e = 0; e < 8; ++e) f[e] = (km >> e) & 1u ? f[e] * p.drop_scale : 0.f;
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = f2bf(f[e]);
@@ -388,9 +388,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           for (int e = 0; e < 8; ++e) f[e] = act_apply(f[e], p.act);
           if (p.drop_p > 0.f) {
             const unsigned long long lin = (unsigned long long)m * p.N + n;
+            const unsigned km = drop_keep8(drop_seed32(eff_seed(p.drop_seed, p.drop_seed_key)), lin, drop_thr8(p.drop_p));
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-              f[e] = drop_keep(drop_seed32(eff_seed(p.drop_seed, p.drop_seed_key)), lin + e, 1.f - p.drop_p) ? f[e] * p.drop_scale : 0.f;
+            for (int e = 0; e < 8; ++e) f[e] = (km >> e) & 1u ? f[e] * p.drop_scale : 0.f;
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = f2bf(f[e]);
@@ -438,7 +438,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             if (p.aux) ((bf16*)p.aux)[off] = v[e];
             x = act_apply(x, p.act);
             if (p.drop_p > 0.f)
-              x = drop_keep(drop_seed32(eff_seed(p.drop_seed, p.drop_seed_key)), (unsigned long long)m * p.N + n + e, 1.f - p.drop_p) ? x * p.drop_scale : 0.f;
+              x = drop_keep1(drop_seed32(eff_seed(p.drop_seed, p.drop_seed_key)), (unsigned long long)m * p.N + n + e, drop_thr8(p.drop_p)) ? x * p.drop_scale : 0.f;
             x = bf2f(f2bf(x));
           }
           if (rsrc) x += bf2f(rsrc[e]);

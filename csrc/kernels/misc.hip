@@ -232,10 +232,11 @@ __global__ void act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restri
 // Inverted dropout; mask regenerated from (seed, index) in backward -> no mask tensor stored.
 __global__ void dropout_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long long n, float p,
                                unsigned long long salt, const unsigned long long* __restrict__ key) {
-  const float keep = 1.f - p, inv = 1.f / keep;
+  const int thr = drop_thr8(p);
+  const float inv = drop_scale8(p);
   const uint32_t s32 = drop_seed32(eff_seed(salt, key));
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
-    bool k = drop_keep(s32, (unsigned long long)i, keep);
+    bool k = drop_keep1(s32, (unsigned long long)i, thr);
     y[i] = f2bf(k ? bf2f(x[i]) * inv : 0.f);
   }
 }
@@ -244,16 +245,15 @@ __global__ void dropout_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
 // form moved one bf16 per lane per iteration (19 us for a 16 MB Transformer-big residual gradient).
 __global__ void dropout8_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long long n8, float p,
                                 unsigned long long salt, const unsigned long long* __restrict__ key) {
-  const float keep = 1.f - p, inv = 1.f / keep;
+  const int thr = drop_thr8(p);
+  const float inv = drop_scale8(p);
   const uint32_t s32 = drop_seed32(eff_seed(salt, key));
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long long)gridDim.x * NT) {
     const bf16x8 v = *(const bf16x8*)(x + i * 8);
+    const unsigned km = drop_keep8(s32, (unsigned long long)i * 8, thr);
     bf16x8 o;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const bool k = drop_keep(s32, (unsigned long long)(i * 8 + e), keep);
-      o[e] = f2bf(k ? bf2f(v[e]) * inv : 0.f);
-    }
+    for (int e = 0; e < 8; ++e) o[e] = f2bf((km >> e) & 1u ? bf2f(v[e]) * inv : 0.f);
     *(bf16x8*)(y + i * 8) = o;
   }
 }

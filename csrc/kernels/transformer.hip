@@ -189,17 +189,24 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
                                                     bf16* __restrict__ dx, float* __restrict__ dgamma,
                                                     float* __restrict__ dbeta, int M, int W, bf16* __restrict__ dxd,
                                                     float drop_p, unsigned long long drop_salt,
-                                                    const unsigned long long* __restrict__ drop_key) {
-  extern __shared__ float red[];  // [NT/64][2][W]
+                                                    const unsigned long long* __restrict__ drop_key,
+                                                    float* __restrict__ dbias) {
+  // dbias (optional): += column sums of the gradient this kernel hands its consumer (dxd, else dx)
+  // -- that Linear's bias gradient, reduced with dgamma/dbeta instead of a separate column-sum pass
+  extern __shared__ float red[];  // [NT/64][2 or 3][W]
+  const int NS = dbias ? 3 : 2;
   const unsigned long long drop_seed = eff_seed(drop_salt, drop_key);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nch = W >> 3;
-  float dg[CPL][8], db[CPL][8], gm[CPL][8];
+  float dg[CPL][8], db[CPL][8], gm[CPL][8], bs[CPL][8];
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
     const int c = lane + 64 * j;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { dg[j][e] = 0.f; db[j][e] = 0.f; gm[j][e] = c < nch ? gamma[c * 8 + e] : 0.f; }
+    for (int e = 0; e < 8; ++e) {
+      dg[j][e] = 0.f; db[j][e] = 0.f; bs[j][e] = 0.f;
+      gm[j][e] = c < nch ? gamma[c * 8 + e] : 0.f;
+    }
   }
   // rows software-pipelined: the next row's dy / x / dres (and mean / rstd) are loaded before this
   // row's reductions and stores, so a wave keeps one row of loads in flight instead of paying two
@@ -268,13 +275,20 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
         if (dxd) {
           // the consumer's dropout backward on the stored dx (misc.hip dropout_kernel's mask and
           // arithmetic, index row*W + col): saves that pass's read + write of dx
-          const float keep = 1.f - drop_p, inv = 1.f / keep;
+          const float inv = drop_scale8(drop_p);
           const unsigned long long base = (unsigned long long)row * W + c * 8;
+          const unsigned km = drop_keep8(drop_seed32(drop_seed), base, drop_thr8(drop_p));
           bf16x8 od;
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
-            od[e] = f2bf(drop_keep(drop_seed32(drop_seed), base + e, keep) ? bf2f(o[e]) * inv : 0.f);
+          for (int e = 0; e < 8; ++e) od[e] = f2bf((km >> e) & 1u ? bf2f(o[e]) * inv : 0.f);
           *(bf16x8*)(dxd + base) = od;
+          if (dbias) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bs[j][e] += bf2f(od[e]);
+          }
+        } else if (dbias) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bs[j][e] += bf2f(o[e]);
         }
       }
     }
@@ -285,17 +299,23 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
     if (c < nch)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        red[(wid * 2 + 0) * W + c * 8 + e] = dg[j][e];
-        red[(wid * 2 + 1) * W + c * 8 + e] = db[j][e];
+        red[(wid * NS + 0) * W + c * 8 + e] = dg[j][e];
+        red[(wid * NS + 1) * W + c * 8 + e] = db[j][e];
+        if (dbias) red[(wid * NS + 2) * W + c * 8 + e] = bs[j][e];
       }
   }
   __syncthreads();
   for (int col = threadIdx.x; col < W; col += NT) {
-    float a = 0.f, b2 = 0.f;
+    float a = 0.f, b2 = 0.f, b3 = 0.f;
 #pragma unroll
-    for (int w = 0; w < NT / 64; ++w) { a += red[(w * 2) * W + col]; b2 += red[(w * 2 + 1) * W + col]; }
+    for (int w = 0; w < NT / 64; ++w) {
+      a += red[(w * NS) * W + col];
+      b2 += red[(w * NS + 1) * W + col];
+      if (dbias) b3 += red[(w * NS + 2) * W + col];
+    }
     atomicAdd(dgamma + col, a);
     atomicAdd(dbeta + col, b2);
+    if (dbias) atomicAdd(dbias + col, b3);
   }
 }
 
@@ -426,19 +446,19 @@ int tfk_layernorm_fwd_mx(const bf16* x, const float* gamma, const float* beta, b
 // backward would produce from dx
 int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const float* mean, const float* rstd,
                       const bf16* dres, bf16* dx, float* dgamma, float* dbeta, int M, int W, bf16* dxd, float drop_p,
-                      unsigned long long drop_seed, hipStream_t s) {
+                      unsigned long long drop_seed, float* dbias, hipStream_t s) {
   const int cpl = (W / 8 + 63) / 64;
   dim3 grid(grid_for(M, (NT / 64) * 8, 1024));
-  const size_t sh = (size_t)(NT / 64) * 2 * W * sizeof(float);
+  const size_t sh = (size_t)(NT / 64) * (dbias ? 3 : 2) * W * sizeof(float);
   if (cpl <= 1)
     hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
-                       dxd, drop_p, drop_seed, tfk_seed_key());
+                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias);
   else if (cpl <= 2)
     hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
-                       dxd, drop_p, drop_seed, tfk_seed_key());
+                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias);
   else if (cpl <= 4)
     hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
-                       dxd, drop_p, drop_seed, tfk_seed_key());
+                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias);
   else return -3;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -110,11 +110,15 @@ class BertLayer:
         h, qkv, sp, o, lse, s1, st1, h1, z, f, s2, st2, hd, s_ao, s_ff = self.saved
         self.saved = None
         # LayerNorm backward also emits the hidden-dropout backward of its gradient (one kernel)
-        ds2, dy2 = self.ln2.backward(dh2, s2, st2, drop=(hd, s_ff))
-        dz = self.ff2.backward(dy2, f, dact_src=z, dact="gelu")
+        # ... and the column sums of that gradient = the consuming Linear's bias gradient (no
+        # separate column-sum pass; only when the bias gradients were pre-zeroed for this step)
+        f2 = self.ff2.bias_sink() is not None
+        ds2, dy2 = self.ln2.backward(dh2, s2, st2, drop=(hd, s_ff), consumer=self.ff2 if f2 else None)
+        dz = self.ff2.backward(dy2, f, dact_src=z, dact="gelu", bias_done=f2)
         dh1 = self.ff1.backward(dz, h1, resid=ds2)
-        ds1, dy1 = self.ln1.backward(dh1, s1, st1, drop=(hd, s_ao))
-        do = self.ao.backward(dy1, o)
+        fa = self.ao.bias_sink() is not None
+        ds1, dy1 = self.ln1.backward(dh1, s1, st1, drop=(hd, s_ao), consumer=self.ao if fa else None)
+        do = self.ao.backward(dy1, o, bias_done=fa)
         dqkv = torch.empty_like(qkv)
         TR.attention_bwd(sp, o, do, lse, (dqkv, self.qkv.col(self.qn)), (dqkv, self.qkv.col(self.kn)),
                          (dqkv, self.qkv.col(self.vn)))

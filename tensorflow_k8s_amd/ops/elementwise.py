@@ -101,10 +101,25 @@ def eff_seed(salt: int) -> int:
     return _s64(int(salt) + int(_KEY[1]))
 
 
+def drop_thr8(p: float) -> int:
+    """common.h drop_thr8: the 8-bit drop threshold round(256 p), in the kernels' float arithmetic."""
+    import numpy as np
+    t = int(np.float32(p) * np.float32(256.0) + np.float32(0.5))
+    return max(0, min(255, t))
+
+
+def keep_scale(p: float) -> float:
+    """Inverse keep probability of the quantized mask, 256 / (256 - thr) (common.h drop_scale8)."""
+    import numpy as np
+    return float(np.float32(256.0) / np.float32(256 - drop_thr8(p)))
+
+
 def dropout_keep(seed: int, n: int, p: float) -> torch.Tensor:
-    """Keep-mask of the dropout kernel / fused GEMM dropout over a contiguous tensor of n elements."""
-    idx = torch.arange(n, dtype=torch.int64) & 0xFFFFFFFF
-    return u01(hash32(drop_seed32(seed) ^ idx)) < (1.0 - p)
+    """Keep-mask of the dropout kernel / fused GEMM dropout over a contiguous tensor of n elements:
+    element i kept iff byte (i & 3) of hash32(s32 ^ (i >> 2)) >= round(256 p) (common.h drop_keep1)."""
+    idx = torch.arange(n, dtype=torch.int64)
+    h = hash32(drop_seed32(seed) ^ ((idx >> 2) & 0xFFFFFFFF))
+    return ((h >> (8 * (idx & 3))) & 0xFF) >= drop_thr8(p)
 
 
 def act_fwd(x: torch.Tensor, act: str | None, bias: torch.Tensor | None = None) -> torch.Tensor:
@@ -131,7 +146,7 @@ def dropout(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
         return x
     if not on_gpu(x):
         keep = dropout_keep(eff_seed(seed), x.numel(), p).reshape(x.shape)
-        return (x.float() * keep / (1 - p)).to(torch.bfloat16)
+        return (x.float() * keep * keep_scale(p)).to(torch.bfloat16)
     y = torch.empty_like(x)
     lib().dropout(x, y, p, int(seed))
     return y

@@ -222,8 +222,8 @@ def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = 
             aux.view(-1, N).copy_(y)
         y = act_ref(y, act)
         if drop_p > 0:
-            from .elementwise import dropout_keep, eff_seed
-            y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) / (1 - drop_p)
+            from .elementwise import dropout_keep, eff_seed, keep_scale
+            y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) * keep_scale(drop_p)
         y = y.to(torch.bfloat16)
         if resid is not None:
             y = (y.float() + resid.reshape(-1, N).float()).to(torch.bfloat16)
@@ -311,8 +311,8 @@ def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | Non
         if dact_src is not None:
             y = y * act_grad_ref(dact_src.float(), dact)
         if drop_p > 0:
-            from .elementwise import dropout_keep, eff_seed
-            y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) / (1 - drop_p)
+            from .elementwise import dropout_keep, eff_seed, keep_scale
+            y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) * keep_scale(drop_p)
         y = y.to(torch.bfloat16)
         if resid is not None:
             y = (y.float() + resid.float()).to(torch.bfloat16)

@@ -209,8 +209,8 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
             aux.view(-1, N).copy_(y)
         y = act_ref(y, act)
         if drop_p > 0:
-            from .elementwise import dropout_keep, eff_seed
-            y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) / (1 - drop_p)
+            from .elementwise import dropout_keep, eff_seed, keep_scale
+            y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) * keep_scale(drop_p)
         y = y.to(torch.bfloat16)
         if resid is not None:
             y = (y.float() + resid.float()).to(torch.bfloat16)
@@ -254,8 +254,8 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
         if dact_src is not None:
             dx = dx * act_grad_ref(dact_src.reshape(-1, K), dact)
         if drop_p > 0:
-            from .elementwise import dropout_keep, eff_seed
-            dx = dx * dropout_keep(eff_seed(drop_seed), dx.numel(), drop_p).reshape(dx.shape) / (1 - drop_p)
+            from .elementwise import dropout_keep, eff_seed, keep_scale
+            dx = dx * dropout_keep(eff_seed(drop_seed), dx.numel(), drop_p).reshape(dx.shape) * keep_scale(drop_p)
         dx = dx.to(torch.bfloat16)
         if resid is not None:
             dx = (dx.float() + resid.reshape(-1, K).float()).to(torch.bfloat16)

@@ -70,11 +70,14 @@ def _zero_pair(a: torch.Tensor, b: torch.Tensor) -> None:
     a.zero_(); b.zero_()
 
 
-def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate: bool = False, drop=None):
+def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate: bool = False, drop=None,
+                  dbias=None):
     """dx (+ dres) bf16; dgamma/dbeta (f32, written or accumulated). drop=(p, seed): also return
-    dropout(dx, p, seed) (the consumer's dropout backward, written by the same kernel) -> (dx, dxd)."""
+    dropout(dx, p, seed) (the consumer's dropout backward, written by the same kernel) -> (dx, dxd).
+    dbias (f32 [W]): += column sums of the returned consumer gradient (dxd, else dx) -- the
+    consuming Linear's bias gradient, reduced in the same kernel."""
     if drop is not None and drop[0] <= 0.0:
-        dx = layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres, accumulate)
+        dx = layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres, accumulate, dbias=dbias)
         return dx, dx
     W = x.shape[-1]
     M = x.numel() // W
@@ -93,14 +96,20 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate
         dx = dx.to(torch.bfloat16).reshape(dy.shape)
         if drop is not None:
             from .elementwise import dropout
-            return dx, dropout(dx, drop[0], drop[1])
+            dxd = dropout(dx, drop[0], drop[1])
+            if dbias is not None:
+                dbias.add_(dxd.reshape(-1, W).float().sum(0))
+            return dx, dxd
+        if dbias is not None:
+            dbias.add_(dx.reshape(-1, W).float().sum(0))
         return dx
     if not accumulate:
         _zero_pair(dgamma, dbeta)
     dx = torch.empty_like(dy)
     dxd = torch.empty_like(dy) if drop is not None else None
     lib().layernorm_bwd(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W, dxd,
-                        float(drop[0]) if drop is not None else 0.0, int(drop[1]) if drop is not None else 0)
+                        float(drop[0]) if drop is not None else 0.0, int(drop[1]) if drop is not None else 0,
+                        dbias=dbias)
     return (dx, dxd) if drop is not None else dx
 
 

@@ -211,15 +211,20 @@ class Linear:
         return linear_forward(x, self.w.compute, self.b.master if self.b else None, self.fp8, act=act, resid=resid,
                               aux=aux, drop_p=drop_p, drop_seed=drop_seed, **kw)
 
+    def bias_sink(self):
+        """The f32 bias-gradient view a producer kernel may accumulate into (pre-zeroed this step), or None."""
+        return self.b.grad if self.b is not None and self.arena.prezeroed else None
+
     def backward(self, dy, x, need_dx: bool = True, resid=None, accumulate: bool = False, dact_src=None,
-                 dact=None, drop_p: float = 0.0, drop_seed: int = 0, mx_dx: bool = False):
+                 dact=None, drop_p: float = 0.0, drop_seed: int = 0, mx_dx: bool = False, bias_done: bool = False):
         """dy: gradient of this layer's (pre-dropout, post-activation-backward) output. drop_p/drop_seed:
         a forward dropout on this layer's input, whose backward is fused into the dgrad epilogue.
         mx_dx (fp8): the dgrad epilogue also emits MX(dx), MX(dx^T) for the producer's fp8 backward."""
         dyq, dyt = fp8_dy(dy.reshape(-1, dy.shape[-1]), self.fin, self.fp8 and need_dx)
         linear_wgrad(dy, x, self.w.grad, self.fp8, accumulate=accumulate, split_target=self.split_target, dyt=dyt)
         if self.b is not None:
-            G.bias_grad(dy, self.b.grad, accumulate=accumulate or self.arena.prezeroed)
+            if not bias_done:
+                G.bias_grad(dy, self.b.grad, accumulate=accumulate or self.arena.prezeroed)
             self.arena.grad_ready(self.w, self.b)
         else:
             self.arena.grad_ready(self.w)
@@ -310,12 +315,15 @@ class LayerNorm:
         y, mu, rs = TR.layernorm_fwd(x, self.gamma.master, self.beta.master, self.eps, mx_out=mx_out, skip_y=mx_out)
         return y, (mu, rs)
 
-    def backward(self, dy, x, stats, dres=None, drop=None):
+    def backward(self, dy, x, stats, dres=None, drop=None, consumer=None):
         """dx = LN'(x)^T dy (+ dres: gradient arriving through a residual connection). drop=(p, seed):
-        returns (dx, dropout(dx, p, seed)) from one kernel (the consumer's dropout backward)."""
+        returns (dx, dropout(dx, p, seed)) from one kernel (the consumer's dropout backward).
+        consumer: the Linear whose output gradient this is -- its bias gradient is reduced here
+        (``consumer.backward(..., bias_done=True)`` then skips its column-sum pass)."""
         mu, rs = stats
+        dbias = consumer.bias_sink() if consumer is not None else None
         dx = TR.layernorm_bwd(dy, x, self.gamma.master, mu, rs, self.gamma.grad, self.beta.grad, dres=dres,
-                              accumulate=self.arena.prezeroed, drop=drop)
+                              accumulate=self.arena.prezeroed, drop=drop, dbias=dbias)
         self.arena.grad_ready(self.gamma, self.beta)
         return dx
 

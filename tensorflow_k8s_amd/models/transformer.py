@@ -29,6 +29,12 @@ from ..runtime.arena import ParamArena
 from ..runtime.layers import Embedding, FusedLinear, LayerNorm, Linear
 from .bert import _mix
 
+def _sink(lin):
+    """lin when a LayerNorm backward may reduce its bias gradient (the gradient it hands lin is lin's
+    output gradient; runtime.layers.LayerNorm.backward consumer), else None."""
+    return lin if lin.bias_sink() is not None else None
+
+
 # fp8 training: LayerNorms and FFN GEMMs that feed only MX-fp8 GEMMs emit those GEMMs' MX operands
 # themselves (ops.fp8 _register_out); TFK_FP8_MX_PRODUCERS=0 quantizes in separate passes instead
 MX_PRODUCERS = os.environ.get("TFK_FP8_MX_PRODUCERS", "1") == "1"
@@ -128,9 +134,10 @@ class EncoderLayer:
     def _self_attn_bwd(self, dx1, saved, seed, training, din=None, out_drop=None):
         x, a, st1, qkv, sp, o, lse = saved
         n = self.att.names
+        fused = din is not None and _sink(self.att.out) is not None  # din's producer reduced our bias grad
         if din is None:
             din = E.dropout(dx1, self.cfg.dropout if training else 0.0, _mix(seed, 2))
-        do = self.att.out.backward(din, o)
+        do = self.att.out.backward(din, o, bias_done=fused)
         dqkv = torch.empty_like(qkv)
         TR.attention_bwd(sp, o, do, lse, (dqkv, self.att.qkv.col(n["q"])), (dqkv, self.att.qkv.col(n["k"])),
                          (dqkv, self.att.qkv.col(n["v"])))
@@ -152,10 +159,12 @@ class EncoderLayer:
     def _ffn_bwd(self, dx2, saved, seed, training, din=None, out_drop=None):
         cfg = self.cfg
         x, b, st, z, f = saved
+        fused = din is not None and _sink(self.ff2) is not None
         dy = din if din is not None else E.dropout(dx2, cfg.dropout if training else 0.0, _mix(seed, 6))
         # relu backward and the relu-dropout backward in the ff2 dgrad epilogue (forward mask regenerated)
         dz = self.ff2.backward(dy, f, dact_src=z, dact="relu", drop_p=cfg.relu_dropout if training else 0.0,
-                               drop_seed=_mix(seed, 5), mx_dx=MX_PRODUCERS and self.ff1.fp8)  # fp8: MX(dz) for ff1
+                               drop_seed=_mix(seed, 5), mx_dx=MX_PRODUCERS and self.ff1.fp8,  # fp8: MX(dz) for ff1
+                               bias_done=fused)
         db = self.ff1.backward(dz, b)
         return self.ffn_ln.backward(db, x, st, dres=dx2, drop=out_drop)
 
@@ -168,7 +177,7 @@ class EncoderLayer:
     def in_drop(self, training: bool, seed: int):
         """(p, seed) of the dropout whose backward consumes this layer's output gradient first (the
         FFN output dropout), for the producer's fused LayerNorm-backward output."""
-        return (self.cfg.dropout if training else 0.0, _mix(seed, 6))
+        return (self.cfg.dropout if training else 0.0, _mix(seed, 6), _sink(self.ff2))
 
     def backward(self, dx2, din=None, out_drop=None):
         """din: dropout(dx2) already produced by the caller's LayerNorm backward (None: computed
@@ -176,7 +185,7 @@ class EncoderLayer:
         s1, s2, seed, training = self.saved
         self.saved = None
         dx1, dx1d = self._ffn_bwd(dx2, s2, seed, training, din=din,
-                                  out_drop=(self.cfg.dropout if training else 0.0, _mix(seed, 2)))
+                                  out_drop=(self.cfg.dropout if training else 0.0, _mix(seed, 2), _sink(self.att.out)))
         return self._self_attn_bwd(dx1, s1, seed, training, din=dx1d, out_drop=out_drop)
 
 
@@ -219,16 +228,16 @@ class DecoderLayer(EncoderLayer):
         self.saved = None
         cfg = self.cfg
         p = cfg.dropout if training else 0.0
-        dy2, dy2d = self._ffn_bwd(dy3, s3, seed, training, din=din, out_drop=(p, _mix(seed, 4)))
+        dy2, dy2d = self._ffn_bwd(dy3, s3, seed, training, din=din, out_drop=(p, _mix(seed, 4), _sink(self.xatt.out)))
         y1, c, st2, q, kv, sp, o2, lse2 = s2
         n = self.xatt.names
-        do2 = self.xatt.out.backward(dy2d, o2)
+        do2 = self.xatt.out.backward(dy2d, o2, bias_done=_sink(self.xatt.out) is not None)
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
         TR.attention_bwd(sp, o2, do2, lse2, (dq, 0), (dkv, self.xatt.kv.col(n["k"])), (dkv, self.xatt.kv.col(n["v"])))
         dmem.copy_(self.xatt.kv.backward(dkv, mem, resid=dmem))
         dc = self.xatt.q.backward(dq, c)
-        dy1, dy1d = self.ln2.backward(dc, y1, st2, dres=dy2, drop=(p, _mix(seed, 2)))
+        dy1, dy1d = self.ln2.backward(dc, y1, st2, dres=dy2, drop=(p, _mix(seed, 2), _sink(self.att.out)))
         return self._self_attn_bwd(dy1, s1, seed, training, din=dy1d, out_drop=out_drop)
 
 

@@ -321,6 +321,8 @@ class LayerNorm:
         consumer: the Linear whose output gradient this is -- its bias gradient is reduced here
         (``consumer.backward(..., bias_done=True)`` then skips its column-sum pass)."""
         mu, rs = stats
+        if drop is not None and len(drop) > 2:  # (p, seed, consumer Linear or None)
+            drop, consumer = drop[:2], drop[2] if consumer is None else consumer
         dbias = consumer.bias_sink() if consumer is not None else None
         dx = TR.layernorm_bwd(dy, x, self.gamma.master, mu, rs, self.gamma.grad, self.beta.grad, dres=dres,
                               accumulate=self.arena.prezeroed, drop=drop, dbias=dbias)

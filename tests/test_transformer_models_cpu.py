@@ -113,3 +113,29 @@ def test_transformer_fp8_mx_producers_match_separate_quantization():
     assert res[True][2] > res[False][2]  # producers registered their MX outputs
     assert torch.equal(res[True][0], res[False][0])
     assert torch.equal(res[True][1], res[False][1])
+
+
+@pytest.mark.parametrize("which", ["bert", "transformer"])
+def test_layernorm_backward_bias_fusion_matches_column_sums(which, monkeypatch):
+    """LayerNorm backward reducing its consumer Linear's bias gradient (runtime.layers LayerNorm.backward
+    consumer) gives the same gradients as the consumers' own column-sum passes."""
+    import tensorflow_k8s_amd.runtime.layers as L
+    res = {}
+    for fused in (True, False):
+        if not fused:
+            monkeypatch.setattr(L.Linear, "bias_sink", lambda self: None)
+        if which == "bert":
+            from tensorflow_k8s_amd.models.bert import BertConfig, BertForPreTraining
+            cfg = BertConfig(vocab_size=300, hidden=128, layers=2, heads=2, intermediate=256, max_position=64,
+                             seq_len=32, max_predictions=5)
+            m = BertForPreTraining(cfg).to("cpu", seed=3)
+        else:
+            from tensorflow_k8s_amd.models.transformer import Transformer, TransformerConfig
+            cfg = TransformerConfig(vocab_size=300, hidden=128, enc_layers=2, dec_layers=2, heads=2, ffn=256,
+                                    src_len=16, tgt_len=16, max_len=32)
+            m = Transformer(cfg).to("cpu", seed=3)
+        loss, _ = m.forward_backward(*m.synthetic_batch(2, "cpu", seed=1))
+        res[fused] = (loss.clone(), m.arena.grad.clone())
+        monkeypatch.undo()
+    assert torch.equal(res[True][0], res[False][0])
+    torch.testing.assert_close(res[True][1], res[False][1], rtol=1e-5, atol=1e-6)

@@ -358,10 +358,18 @@ def linear_wgrad_mx(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumul
     lib().splitk_reduce(ws, splits, stride, N * K, gw.view(-1), None, accumulate, 1.0)
 
 
+# weight gradients whose [N, K] output already has >= this many 128x128 tiles run unsplit on 128x128
+# tiles (f32 written once, no slabs + reduce pass); TFK_FP8_WGRAD_NOSPLIT=0 restores split-K for all
+import os as _os
+WGRAD_NOSPLIT_TILES = int(_os.environ.get("TFK_FP8_WGRAD_NOSPLIT", "192"))
+
+
 def wgrad_splits(N: int, K: int, M: int) -> int:
     """Split-K slabs of an fp8 weight gradient [N, K] reduced over M tokens: fill ~one round of
     256x256 blocks (two of 128x128 when a side is < 256) with >= 8 K-tiles of 128 per split; the
     count the g4 launcher will actually run (ceil(K-tiles / per-split))."""
+    if WGRAD_NOSPLIT_TILES > 0 and (-(-N // 128)) * (-(-K // 128)) >= WGRAD_NOSPLIT_TILES:
+        return 1
     nkt = M // 128
     big = N >= 256 and K >= 256
     t = (-(-N // 256)) * (-(-K // 256)) if big else (-(-N // 128)) * (-(-K // 128))

@@ -14,7 +14,7 @@ int tfk_layernorm_fwd(const void*, const float*, const float*, void*, float*, fl
 int tfk_layernorm_fwd_mx(const void*, const float*, const float*, void*, float*, float*, int, int, float, void*, void*, void*,
                          void*, hipStream_t);
 int tfk_layernorm_bwd(const void*, const void*, const float*, const float*, const float*, const void*, void*, float*,
-                      float*, int, int, void*, float, unsigned long long, float*, hipStream_t);
+                      float*, int, int, void*, float, unsigned long long, float*, void*, void*, void*, void*, hipStream_t);
 int tfk_embedding_fwd(const int*, const void*, int, const void*, int, const int*, const void*, int, void*, long long, int,
                       float, hipStream_t);
 int tfk_embedding_bwd(const int*, const void*, int, float*, float*, int, const int*, float*, int, long long, int, float,
@@ -62,8 +62,18 @@ void layernorm_fwd_mx(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, 
 void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor gamma, torch::Tensor mean, torch::Tensor rstd,
                    c10::optional<torch::Tensor> dres, torch::Tensor dx, torch::Tensor dgamma, torch::Tensor dbeta,
                    int64_t M, int W, c10::optional<torch::Tensor> dxd, double drop_p, int64_t drop_seed,
-                   c10::optional<torch::Tensor> dbias) {
+                   c10::optional<torch::Tensor> dbias, c10::optional<std::vector<torch::Tensor>> mx_out) {
   if (dbias.has_value() && dbias->defined()) { need_f32(*dbias, "dbias"); need_numel(*dbias, W, "dbias"); }
+  void* mxp[4] = {nullptr, nullptr, nullptr, nullptr};
+  if (mx_out.has_value()) {
+    const auto& o = *mx_out;
+    TORCH_CHECK(o.size() == 4 && M % 32 == 0 && W % 32 == 0 && W <= 1024, "layernorm_bwd mx_out: 4 tensors, M, W % 32 == 0, W <= 1024");
+    for (const auto& t : o) need(t, at::kByte, "mx_out");
+    need_numel(o[0], M * W, "mx qr"); need_numel(o[1], M * W / 32, "mx sr");
+    need_numel(o[2], M * W, "mx qc"); need_numel(o[3], M * W / 32, "mx sc");
+    need_aligned(o[0], 16, "mx qr"); need_aligned(o[2], 16, "mx qc");
+    for (int i = 0; i < 4; ++i) mxp[i] = o[i].data_ptr();
+  }
   need_bf16(dy, "dy"); need_bf16(x, "x"); need_bf16(dx, "dx");
   for (auto* t : {&gamma, &mean, &rstd, &dgamma, &dbeta}) need_f32(*t, "ln vector");
   TORCH_CHECK(W % 8 == 0 && W <= 2048, "layernorm needs W%8==0 and W<=2048");
@@ -78,7 +88,8 @@ void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor gamma, torch
   check_rc(tfk_layernorm_bwd(dy.data_ptr(), x.data_ptr(), gamma.data_ptr<float>(), mean.data_ptr<float>(),
                              rstd.data_ptr<float>(), opt_ptr<const void>(dres), dx.data_ptr(), dgamma.data_ptr<float>(),
                              dbeta.data_ptr<float>(), (int)M, W, opt_ptr<void>(dxd), (float)drop_p,
-                             (unsigned long long)drop_seed, opt_ptr<float>(dbias), cur_stream()),
+                             (unsigned long long)drop_seed, opt_ptr<float>(dbias), mxp[0], mxp[1], mxp[2], mxp[3],
+                             cur_stream()),
            "layernorm_bwd");
 }
 
@@ -201,7 +212,8 @@ void register_transformer_ops(pybind11::module& m) {
   m.def("layernorm_fwd_mx", &layernorm_fwd_mx);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
         py::arg("rstd"), py::arg("dres"), py::arg("dx"), py::arg("dgamma"), py::arg("dbeta"), py::arg("M"), py::arg("W"),
-        py::arg("dxd"), py::arg("drop_p"), py::arg("drop_seed"), py::arg("dbias") = py::none());
+        py::arg("dxd"), py::arg("drop_p"), py::arg("drop_seed"), py::arg("dbias") = py::none(),
+        py::arg("mx_out") = py::none());
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("attn_fwd", &attn_fwd);

@@ -141,45 +141,7 @@ __global__ __launch_bounds__(LNMX_NT) void ln_fwd_mx_kernel(const bf16* __restri
     if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
   }
   __syncthreads();
-  const long long Ml = M;
-  const int NB = W / 32;
-  for (int k = threadIdx.x; k < LNMX_ROWS * NB; k += LNMX_NT) {
-    const int lr = k / NB, blk = k - lr * NB;
-    unsigned pp[16];
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      const u32x4 h = *(const u32x4*)&tile[lr][blk * 32 + q4 * 8];
-      pp[4 * q4] = h[0]; pp[4 * q4 + 1] = h[1]; pp[4 * q4 + 2] = h[2]; pp[4 * q4 + 3] = h[3];
-    }
-    unsigned w[8];
-    const int ex = tfk::mx_block_pk(pp, w);
-    unsigned char* dst = qr + (long long)(r0 + lr) * W + blk * 32;
-    *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
-    *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
-    sr[(long long)(r0 + lr) * NB + blk] = (unsigned char)(ex + 127);
-  }
-  for (int cp = threadIdx.x; cp < W / 2; cp += LNMX_NT) {
-    const int col = 2 * cp;
-    unsigned lo[16], hi[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const unsigned a = *(const unsigned*)&tile[2 * r][col];
-      const unsigned b = *(const unsigned*)&tile[2 * r + 1][col];
-      lo[r] = __builtin_amdgcn_perm(b, a, 0x05040100u);
-      hi[r] = __builtin_amdgcn_perm(b, a, 0x07060302u);
-    }
-    unsigned w[8];
-    int ex = tfk::mx_block_pk(lo, w);
-    unsigned char* dst = qc + (long long)col * Ml + r0;
-    *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
-    *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
-    sc[(long long)col * (Ml / 32) + r0 / 32] = (unsigned char)(ex + 127);
-    ex = tfk::mx_block_pk(hi, w);
-    dst += Ml;
-    *(u32x4*)dst = u32x4{w[0], w[1], w[2], w[3]};
-    *(u32x4*)(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
-    sc[(long long)(col + 1) * (Ml / 32) + r0 / 32] = (unsigned char)(ex + 127);
-  }
+  tfk::mx_rows32_out<LNMX_NT>(&tile[0][0], LNMX_WMAX + 8, W, M, r0, qr, sr, qc, sc);
 }
 
 template <int CPL>
@@ -190,7 +152,9 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
                                                     float* __restrict__ dbeta, int M, int W, bf16* __restrict__ dxd,
                                                     float drop_p, unsigned long long drop_salt,
                                                     const unsigned long long* __restrict__ drop_key,
-                                                    float* __restrict__ dbias) {
+                                                    float* __restrict__ dbias, unsigned char* __restrict__ mq,
+                                                    unsigned char* __restrict__ ms, unsigned char* __restrict__ mqt,
+                                                    unsigned char* __restrict__ mst) {
   // dbias (optional): += column sums of the gradient this kernel hands its consumer (dxd, else dx)
   // -- that Linear's bias gradient, reduced with dgamma/dbeta instead of a separate column-sum pass
   extern __shared__ float red[];  // [NT/64][2 or 3][W]
@@ -211,8 +175,14 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
   // rows software-pipelined: the next row's dy / x / dres (and mean / rstd) are loaded before this
   // row's reductions and stores, so a wave keeps one row of loads in flight instead of paying two
   // dependent memory latencies per row (measured 2.2 TB/s on Transformer-big's 8192 x 1024 rows)
-  const int rstep = gridDim.x * (NT / 64);
-  int row = blockIdx.x * (NT / 64) + wid;
+  // MX mode (mq != null: emit MX-fp8 row + column blocks of the consumer gradient): a block owns 32
+  // consecutive rows (8 per wave), stages their final values in an LDS tile behind `red` and
+  // quantizes the tile after the row loop (the consumer's fp8 backward then skips its quantize pass)
+  const bool mxo = mq != nullptr;
+  const int rstep = mxo ? 1 : gridDim.x * (NT / 64);
+  int row = mxo ? blockIdx.x * 32 + wid * 8 : blockIdx.x * (NT / 64) + wid;
+  const int rend = mxo ? row + 8 : M;
+  bf16* mtile = (bf16*)(red + (NT / 64) * NS * W);  // [32][W + 8] (MX mode only)
   bf16x8 ndv[CPL], nxv[CPL], nrv[CPL];
   float nmu = 0.f, nrs = 0.f;
   auto fetch = [&](int r) {
@@ -228,13 +198,13 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
       }
     }
   };
-  if (row < M) fetch(row);
-  for (; row < M; row += rstep) {
+  if (row < rend) fetch(row);
+  for (; row < rend; row += rstep) {
     const float mu = nmu, rs = nrs;
     bf16x8 cdv[CPL], cxv[CPL], crv[CPL];
 #pragma unroll
     for (int j = 0; j < CPL; ++j) { cdv[j] = ndv[j]; cxv[j] = nxv[j]; crv[j] = nrv[j]; }
-    if (row + rstep < M) fetch(row + rstep);
+    if (row + rstep < rend) fetch(row + rstep);
     float g[CPL][8], xh[CPL][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -286,9 +256,13 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
 #pragma unroll
             for (int e = 0; e < 8; ++e) bs[j][e] += bf2f(od[e]);
           }
-        } else if (dbias) {
+          if (mxo) *(bf16x8*)(mtile + (row - blockIdx.x * 32) * (W + 8) + c * 8) = od;
+        } else {
+          if (dbias) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) bs[j][e] += bf2f(o[e]);
+            for (int e = 0; e < 8; ++e) bs[j][e] += bf2f(o[e]);
+          }
+          if (mxo) *(bf16x8*)(mtile + (row - blockIdx.x * 32) * (W + 8) + c * 8) = o;
         }
       }
     }
@@ -317,6 +291,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
     atomicAdd(dbeta + col, b2);
     if (dbias) atomicAdd(dbias + col, b3);
   }
+  if (mxo) tfk::mx_rows32_out<NT>(mtile, W + 8, W, M, blockIdx.x * 32, mq, ms, mqt, mst);  // tile complete: barrier above
 }
 
 __global__ void embed_fwd_kernel(const int* __restrict__ ids, const bf16* __restrict__ word, int V,
@@ -446,19 +421,25 @@ int tfk_layernorm_fwd_mx(const bf16* x, const float* gamma, const float* beta, b
 // backward would produce from dx
 int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const float* mean, const float* rstd,
                       const bf16* dres, bf16* dx, float* dgamma, float* dbeta, int M, int W, bf16* dxd, float drop_p,
-                      unsigned long long drop_seed, float* dbias, hipStream_t s) {
+                      unsigned long long drop_seed, float* dbias, void* mq, void* ms, void* mqt, void* mst,
+                      hipStream_t s) {
   const int cpl = (W / 8 + 63) / 64;
-  dim3 grid(grid_for(M, (NT / 64) * 8, 1024));
-  const size_t sh = (size_t)(NT / 64) * (dbias ? 3 : 2) * W * sizeof(float);
+  const bool mxo = mq != nullptr;
+  if (mxo && (M % 32 || W % 32 || W > 1024)) return -3;
+  dim3 grid(mxo ? (unsigned)(M / 32) : grid_for(M, (NT / 64) * 8, 1024));
+  const size_t sh = (size_t)(NT / 64) * (dbias ? 3 : 2) * W * sizeof(float) + (mxo ? (size_t)32 * (W + 8) * 2 : 0);
   if (cpl <= 1)
     hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
-                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias);
+                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
+                       (unsigned char*)mqt, (unsigned char*)mst);
   else if (cpl <= 2)
     hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
-                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias);
+                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
+                       (unsigned char*)mqt, (unsigned char*)mst);
   else if (cpl <= 4)
     hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
-                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias);
+                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
+                       (unsigned char*)mqt, (unsigned char*)mst);
   else return -3;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -358,10 +358,11 @@ def linear_wgrad_mx(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumul
     lib().splitk_reduce(ws, splits, stride, N * K, gw.view(-1), None, accumulate, 1.0)
 
 
-# weight gradients whose [N, K] output already has >= this many 128x128 tiles run unsplit on 128x128
-# tiles (f32 written once, no slabs + reduce pass); TFK_FP8_WGRAD_NOSPLIT=0 restores split-K for all
+# opt-in: weight gradients whose [N, K] output has >= this many 128x128 tiles run unsplit on 128x128
+# tiles (f32 written once, no slabs + reduce pass). Measured slower on Transformer-big (threshold
+# 128 / 192 / 256: 19.03 / 18.97 / 19.10 ms vs 18.86 ms split-K, profiles/perf_log_r3c.md): off (0)
 import os as _os
-WGRAD_NOSPLIT_TILES = int(_os.environ.get("TFK_FP8_WGRAD_NOSPLIT", "192"))
+WGRAD_NOSPLIT_TILES = int(_os.environ.get("TFK_FP8_WGRAD_NOSPLIT", "0"))
 
 
 def wgrad_splits(N: int, K: int, M: int) -> int:

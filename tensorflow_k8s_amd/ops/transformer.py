@@ -71,13 +71,15 @@ def _zero_pair(a: torch.Tensor, b: torch.Tensor) -> None:
 
 
 def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate: bool = False, drop=None,
-                  dbias=None):
+                  dbias=None, mx_out: bool = False):
     """dx (+ dres) bf16; dgamma/dbeta (f32, written or accumulated). drop=(p, seed): also return
     dropout(dx, p, seed) (the consumer's dropout backward, written by the same kernel) -> (dx, dxd).
     dbias (f32 [W]): += column sums of the returned consumer gradient (dxd, else dx) -- the
-    consuming Linear's bias gradient, reduced in the same kernel."""
+    consuming Linear's bias gradient, reduced in the same kernel. mx_out (fp8 training): the kernel
+    also writes MX row / column blocks of that consumer gradient (ops.fp8 _register_out), which the
+    consumer's fp8 backward takes instead of quantizing it."""
     if drop is not None and drop[0] <= 0.0:
-        dx = layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres, accumulate, dbias=dbias)
+        dx = layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres, accumulate, dbias=dbias, mx_out=mx_out)
         return dx, dx
     W = x.shape[-1]
     M = x.numel() // W
@@ -94,22 +96,35 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dgamma, dbeta, dres=None, accumulate
         else:
             dgamma.copy_(dg); dbeta.copy_(db)
         dx = dx.to(torch.bfloat16).reshape(dy.shape)
+        mx_out = mx_out and M % 32 == 0 and W % 32 == 0 and W <= 1024
         if drop is not None:
             from .elementwise import dropout
             dxd = dropout(dx, drop[0], drop[1])
             if dbias is not None:
                 dbias.add_(dxd.reshape(-1, W).float().sum(0))
+            if mx_out:
+                from . import fp8 as F8
+                F8._register_out(dxd, *F8.mx_quantize_dual(dxd.reshape(M, W)))
             return dx, dxd
         if dbias is not None:
             dbias.add_(dx.reshape(-1, W).float().sum(0))
+        if mx_out:
+            from . import fp8 as F8
+            F8._register_out(dx, *F8.mx_quantize_dual(dx.reshape(M, W)))
         return dx
     if not accumulate:
         _zero_pair(dgamma, dbeta)
     dx = torch.empty_like(dy)
     dxd = torch.empty_like(dy) if drop is not None else None
+    mo = None
+    if mx_out and M % 32 == 0 and W % 32 == 0 and W <= 1024:
+        from . import fp8 as F8
+        mo = F8._mx_bufs(M, W, dy.device)
     lib().layernorm_bwd(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W, dxd,
                         float(drop[0]) if drop is not None else 0.0, int(drop[1]) if drop is not None else 0,
-                        dbias=dbias)
+                        dbias=dbias, mx_out=list(mo) if mo else None)
+    if mo:
+        F8._register_out(dxd if drop is not None else dx, (mo[0], mo[1]), (mo[2], mo[3]))
     return (dx, dxd) if drop is not None else dx
 
 

@@ -302,6 +302,13 @@ def weight_quantizer(model, lins: list, extra: list | None = None):
     return model._wq
 
 
+def _mx_producers() -> bool:
+    """models.transformer.MX_PRODUCERS (TFK_FP8_MX_PRODUCERS): producers emit fp8 consumers' MX operands."""
+    import sys
+    m = sys.modules.get("tensorflow_k8s_amd.models.transformer")
+    return bool(getattr(m, "MX_PRODUCERS", True)) if m is not None else True
+
+
 class LayerNorm:
     """TF variables <name>/gamma, <name>/beta (f32, no weight decay)."""
 
@@ -324,8 +331,11 @@ class LayerNorm:
         if drop is not None and len(drop) > 2:  # (p, seed, consumer Linear or None)
             drop, consumer = drop[:2], drop[2] if consumer is None else consumer
         dbias = consumer.bias_sink() if consumer is not None else None
+        # an fp8 consumer whose gradient rows tile the MX-fp8 K-tile takes MX operands from this kernel
+        rows = dy.numel() // dy.shape[-1]
+        mx = consumer is not None and getattr(consumer, "fp8", False) and rows % 128 == 0 and _mx_producers()
         dx = TR.layernorm_bwd(dy, x, self.gamma.master, mu, rs, self.gamma.grad, self.beta.grad, dres=dres,
-                              accumulate=self.arena.prezeroed, drop=drop, dbias=dbias)
+                              accumulate=self.arena.prezeroed, drop=drop, dbias=dbias, mx_out=mx)
         self.arena.grad_ready(self.gamma, self.beta)
         return dx
 

@@ -101,8 +101,9 @@ def test_mx_dgrad_wgrad(M, N, K):
 
 def test_fp8_training_tracks_bf16_200_steps():
     """A tiny Transformer with every linear GEMM on MX-fp8 (fwd + dgrad + wgrad) trains like the
-    bf16 model: 200 Adam steps on a fixed batch, loss curves within 5 % (mean over the last 20
-    steps) and both converge."""
+    bf16 model: 200 Adam steps on a fixed batch, loss curves within 3 % (mean over the last 20
+    steps) and both converge. The fp8 run takes every producer-emitted MX path (LayerNorm+MX,
+    EXT_MX epilogues, grouped weight quantization: 256 tokens tile every GEMM)."""
     from tensorflow_k8s_amd.models.transformer import Transformer, TransformerConfig
     from tensorflow_k8s_amd.runtime.optimizer import AdamW
     curves = {}
@@ -124,7 +125,8 @@ def test_fp8_training_tracks_bf16_200_steps():
     assert all(v == v for v in f), "fp8 loss went NaN"
     assert b[-1] < 0.5 * b[0] and f[-1] < 0.5 * f[0], (b[::20], f[::20])
     mb, mf = sum(b[-20:]) / 20, sum(f[-20:]) / 20
-    assert abs(mf - mb) <= 0.05 * mb + 0.02, (b[::20], f[::20])
+    print(f"fp8 vs bf16 loss, mean of last 20 steps: {mf:.4f} vs {mb:.4f} (gap {abs(mf - mb) / mb:.2%})")
+    assert abs(mf - mb) <= 0.03 * mb + 0.02, (b[::20], f[::20])
 
 
 @pytest.mark.parametrize("tile", [128, 256])
@@ -293,4 +295,37 @@ def test_layernorm_mx_outputs_equal_dual_quantizer(M, W):
     (q2, s2), (qt2, st2) = F8.cached_dual(y2)
     torch.cuda.synchronize()
     assert torch.equal(q2, q0) and torch.equal(qt2, qt0) and torch.equal(s2, s0) and torch.equal(st2, st0)
+    F8.clear_saved()
+
+
+@pytest.mark.parametrize("M,W,drop", [(256, 1024, 0.1), (96, 768, 0.0), (8192, 1024, 0.3)])
+def test_layernorm_bwd_mx_outputs(M, W, drop):
+    """layernorm_bwd mx_out: dx / dropout(dx) identical to the plain kernel, dgamma / dbeta / consumer
+    bias gradient equal up to the f32 summation order (rows are blocked differently), and the MX row /
+    column blocks identical to mx_quantize_dual of the consumer gradient."""
+    from tensorflow_k8s_amd.ops import transformer as T
+    g = torch.Generator().manual_seed(M + W)
+    x = (torch.randn(M, W, generator=g) * 2).to(torch.bfloat16).cuda()
+    dy = torch.randn(M, W, generator=g).to(torch.bfloat16).cuda()
+    dres = torch.randn(M, W, generator=g).to(torch.bfloat16).cuda()
+    gm = (torch.rand(W, generator=g) + 0.5).cuda()
+    bt = torch.zeros(W).cuda()
+    _, mu, rs = T.layernorm_fwd(x, gm, bt, 1e-6)
+    outs = {}
+    for mx in (False, True):
+        F8.clear_saved()
+        dg, db, dbias = torch.zeros(W).cuda(), torch.zeros(W).cuda(), torch.zeros(W).cuda()
+        r = T.layernorm_bwd(dy, x, gm, mu, rs, dg, db, dres=dres, accumulate=True,
+                            drop=(drop, 7) if drop > 0 else None, dbias=dbias, mx_out=mx)
+        cons = r[1] if drop > 0 else r
+        outs[mx] = (r, dg, db, dbias, F8.cached_dual(cons) if mx else None, cons)
+    torch.cuda.synchronize()
+    (r0, dg0, db0, bs0, _, c0), (r1, dg1, db1, bs1, mxq, c1) = outs[False], outs[True]
+    assert torch.equal(c0, c1)
+    for a, b in ((dg0, dg1), (db0, db1), (bs0, bs1)):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)
+    (q, s), (qt, st) = mxq
+    (q1, s1), (qt1, st1) = F8.mx_quantize_dual(c1)
+    torch.cuda.synchronize()
+    assert torch.equal(q, q1) and torch.equal(s, s1) and torch.equal(qt, qt1) and torch.equal(st, st1)
     F8.clear_saved()

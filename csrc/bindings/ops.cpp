@@ -72,6 +72,7 @@ int tfk_stem_fwd_launch(const void*, const void*, void*, float*, int, int, int, 
 int tfk_stem_wgrad_launch(const void*, const void*, float*, int, int, int, int, hipStream_t);
 int tfk_hwgrad_launch(const void*, const void*, float*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int tfk_transpose_arb(const void*, void*, int, int, int, int, hipStream_t);
+int tfk_transpose_group(const void*, int, int, hipStream_t);
 int tfk_transpose_f32(const float*, float*, int, int, hipStream_t);
 int tfk_cast_f32_bf16(const float*, void*, long long, hipStream_t);
 int tfk_cast_bf16_f32(const void*, float*, long long, hipStream_t);
@@ -699,6 +700,15 @@ void stem_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::optional<t
   }
   check_rc(tfk_stem_fwd_launch(x.data_ptr(), w.data_ptr(), y.data_ptr(), st, shards, N, H, W, cur_stream()), "stem_fwd");
 }
+// Grouped transpose_arb: table int64 [n][6] on the device (in, out, A | R << 32, B | flip << 32,
+// t0 | tb << 32, ta), built and validated by ops/gemm.py FlipTransposeGroup.
+void transpose_group(torch::Tensor table, int64_t n, int64_t total) {
+  need(table, at::kLong, "transpose group table");
+  TORCH_CHECK(table.is_cuda() && table.is_contiguous() && table.numel() == n * 6 && n > 0 && total > 0,
+              "transpose_group: table must be a contiguous device int64 [n][6]");
+  check_rc(tfk_transpose_group(table.data_ptr(), (int)n, (int)total, cur_stream()), "transpose_group");
+}
+
 void transpose_arb(torch::Tensor in, torch::Tensor out, int A, int R, int B, int flip) {
   need_bf16(in, "in"); need_bf16(out, "out");
   need_numel(in, (long long)A * R * B, "in"); need_numel(out, (long long)A * R * B, "out");
@@ -824,6 +834,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("stem_wgrad", &stem_wgrad);
   m.def("stem_fwd_ok", &stem_fwd_ok);
   m.def("stem_fwd", &stem_fwd);
+  m.def("transpose_group", &transpose_group);
   m.def("transpose_arb", &transpose_arb, py::arg("in"), py::arg("out"), py::arg("A"), py::arg("R"), py::arg("B"),
         py::arg("flip") = 0);
   m.def("transpose_f32", &transpose_f32);

@@ -185,6 +185,7 @@ class ResNet:
     # ------------------------------------------------------------------ setup
     def to(self, device, seed: int = 1234) -> "ResNet":
         self.arena.finalize(device, seed)
+        self._flip = None
         return self
 
     def batchnorms(self):
@@ -233,6 +234,22 @@ class ResNet:
     def forward_backward(self, x, labels, loss_scale: float = 1.0):
         """One training forward + backward. Returns (loss_sum f32[N] per-row, correct f32[N]).
         Gradients land in arena.grad (mean over the local batch)."""
+        from ..ops import gemm as G
+        # the flipped 3x3 dgrad weights of this step in ONE grouped transpose up front (the first
+        # step records which convs need them); cache scoped to this step
+        flip = getattr(self, "_flip", None)
+        if x.is_cuda and flip is None:
+            G._FLIP_RECORD = []
+        G._FLIP_ACTIVE = flip.run() if flip is not None else None
+        try:
+            return self._forward_backward(x, labels, loss_scale)
+        finally:
+            G._FLIP_ACTIVE = None
+            if G._FLIP_RECORD:
+                self._flip = G.FlipTransposeGroup(G._FLIP_RECORD)
+            G._FLIP_RECORD = None
+
+    def _forward_backward(self, x, labels, loss_scale: float = 1.0):
         f = self._features(x)
         logits = self.fc.forward(f)
         B = logits.shape[0]

@@ -393,6 +393,42 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
     return y
 
 
+# Flipped dgrad weights of a training step, produced up front by ONE grouped launch
+# (FlipTransposeGroup.run; the model sets _FLIP_ACTIVE for the duration of its step, so a cache can
+# never outlive the weights it was computed from). _FLIP_RECORD collects (w, g) of the convs that
+# needed one, for the model to build its group after the first step.
+_FLIP_ACTIVE: dict | None = None
+_FLIP_RECORD: list | None = None
+
+
+class FlipTransposeGroup:
+    """conv_weight_t(w, g, flip=True) of many convs in one launch (misc.hip transpose_group_kernel):
+    a ResNet-50 step's 16 flipped 3x3 weights were 16 latency-bound launches (~16 us each) on the
+    dgrad critical path. Outputs are allocated once (fixed addresses: graph-capturable)."""
+
+    def __init__(self, items: list):
+        self.items, self.out, rows, t0 = [], [], [], 0
+        seen = set()
+        for w, g in items:
+            if w.data_ptr() in seen:
+                continue
+            seen.add(w.data_ptr())
+            o = torch.empty(g.C, g.R, g.S, g.K, dtype=w.dtype, device=w.device)
+            A, R, B = g.K, g.R * g.S, g.C
+            tb, ta = -(-B // 32), -(-A // 32)
+            rows.append([w.data_ptr(), o.data_ptr(), A | (R << 32), B | (1 << 32), t0 | (tb << 32), ta])
+            t0 += tb * ta * R
+            self.items.append(w)
+            self.out.append(o)
+        self.total = t0
+        self.table = torch.tensor(rows, dtype=torch.int64).to(self.items[0].device) if rows else None
+
+    def run(self) -> dict:
+        if self.table is not None:
+            lib().transpose_group(self.table, len(self.items), self.total)
+        return {w.data_ptr(): o for w, o in zip(self.items, self.out)}
+
+
 def conv_weight_t(w: torch.Tensor, g: ConvGeom, out: torch.Tensor | None = None, flip: bool = False) -> torch.Tensor:
     """OHWI [K][R][S][C] -> [C][R][S][K] (dgrad B operand); flip: taps reversed,
     out[c][r][s][k] = w[k][R-1-r][S-1-s][c] (the stride-1 dgrad as a forward conv)."""
@@ -531,7 +567,11 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
     if f is not None and g.C < DGRAD_AS_FWD_MIN_C and not halo_ok(f):
         f = None
     if f is not None:
-        wf = conv_weight_t(w, g, flip=True)  # [C][R][S][K]: the forward conv's OHWI weight
+        wf = _FLIP_ACTIVE.get(w.data_ptr()) if _FLIP_ACTIVE else None
+        if wf is None or tuple(wf.shape) != (g.C, g.R, g.S, g.K):
+            wf = conv_weight_t(w, g, flip=True)  # [C][R][S][K]: the forward conv's OHWI weight
+            if _FLIP_RECORD is not None:
+                _FLIP_RECORD.append((w, g))
         Kd = g.R * g.S * g.K
         _gemm(dy, wf, dx, M, g.C, Kd, 0, Kd, g.C, A_CONV_FWD, B_KIN, EPI_BF16,
               _conv_tile("dgrad_fwd", g, lambda: pick_tile(M, g.C, K=Kd, mid_ok=False, g4=True), flags),

@@ -29,6 +29,8 @@ SIDE_SHORTCUT = os.environ.get("TFK_SIDE_SHORTCUT", "1") == "1"
 # BN-backward apply then reads no mask and an identity block's residual gradient is dz itself (no
 # second output pass). TFK_BN_PREMASK=0 restores the unmasked dA + separate dres for A/B.
 PREMASK = os.environ.get("TFK_BN_PREMASK", "1") == "1"
+# flipped 3x3 dgrad weights from one grouped transpose per step (TFK_FLIP_GROUP=0: per conv)
+FLIP_GROUP = os.environ.get("TFK_FLIP_GROUP", "1") == "1"
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
 
@@ -238,7 +240,7 @@ class ResNet:
         # the flipped 3x3 dgrad weights of this step in ONE grouped transpose up front (the first
         # step records which convs need them); cache scoped to this step
         flip = getattr(self, "_flip", None)
-        if x.is_cuda and flip is None:
+        if x.is_cuda and flip is None and FLIP_GROUP:
             G._FLIP_RECORD = []
         G._FLIP_ACTIVE = flip.run() if flip is not None else None
         try:

@@ -29,8 +29,10 @@ SIDE_SHORTCUT = os.environ.get("TFK_SIDE_SHORTCUT", "1") == "1"
 # BN-backward apply then reads no mask and an identity block's residual gradient is dz itself (no
 # second output pass). TFK_BN_PREMASK=0 restores the unmasked dA + separate dres for A/B.
 PREMASK = os.environ.get("TFK_BN_PREMASK", "1") == "1"
-# flipped 3x3 dgrad weights from one grouped transpose per step (TFK_FLIP_GROUP=0: per conv)
-FLIP_GROUP = os.environ.get("TFK_FLIP_GROUP", "1") == "1"
+# opt-in: flipped 3x3 dgrad weights from one grouped transpose at the start of the step instead of
+# per conv right before its dgrad. Measured slower (ResNet-50 bs256 same box: 22.29 vs 22.05 ms/step,
+# profiles/perf_log_r3c.md): the per-conv transposes are not on the critical path after all.
+FLIP_GROUP = os.environ.get("TFK_FLIP_GROUP", "0") == "1"
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
 

@@ -632,9 +632,22 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
   p.kt_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
   const bool big = g_fp8_tile == 256 || (g_fp8_tile == 0 && p.M >= 256 && p.N >= 256 && t256 * splits >= 240);
+  // 256 x 128 (8 waves, one block per CU): narrow outputs with many rows -- the Transformer's
+  // [tokens, 1024] GEMMs get 256 blocks (one round) with each B column panel shared by 256 A rows
+  // instead of two co-resident 128 x 128 blocks. TFK_FP8_TILE=2561 forces it, =0 picks by shape
+  // (g_fp8_wide: TFK_FP8_WIDE=0 disables the shape rule, for A/B).
+  static int g_fp8_wide = -1;
+  if (g_fp8_wide < 0) {
+    const char* e = getenv("TFK_FP8_WIDE");
+    g_fp8_wide = e ? atoi(e) : 1;
+  }
+  const long long t256x128 = (long long)((p.M + 255) / 256) * ((p.N + 127) / 128);
+  const bool wide = !big && (g_fp8_tile == 2561 || (g_fp8_tile == 0 && g_fp8_wide && p.M >= 4096 && p.N >= 128 &&
+                                                     t256x128 * splits >= 240));
   const int T = big ? 256 : 128;
+  const int TM = wide ? 256 : T;
   p.tiles_n = (p.N + T - 1) / T;
-  const int tiles = ((p.M + T - 1) / T) * p.tiles_n;
+  const int tiles = ((p.M + TM - 1) / TM) * p.tiles_n;
   if (p.stats_shards < 1) p.stats_shards = 1;
   const dim3 grid(tiles, 1, splits);
 #define TFK_FP8_G4(BT)                                                                                          \
@@ -649,10 +662,21 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
     else                                                                                                        \
       hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_BF16>), grid, block, 0, stream, p, sld);                \
   }
-  if (big)
+  if (big) {
     TFK_FP8_G4(256)
-  else
+  } else if (wide) {
+    const dim3 block(g4::nwaves<256, 128>() * 64);
+    if (epi == EPI_F32)
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<256, 128, EPI_F32>), grid, block, 0, stream, p, sld);
+    else if (epi == EPI_BF16_EXT)
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<256, 128, EPI_BF16_EXT>), grid, block, 0, stream, p, sld);
+    else if (epi == EPI_BF16_EXT_MX)
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<256, 128, EPI_BF16_EXT_MX>), grid, block, 0, stream, p, sld);
+    else
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<256, 128, EPI_BF16>), grid, block, 0, stream, p, sld);
+  } else {
     TFK_FP8_G4(128)
+  }
 #undef TFK_FP8_G4
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

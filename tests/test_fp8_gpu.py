@@ -129,13 +129,14 @@ def test_fp8_training_tracks_bf16_200_steps():
     assert abs(mf - mb) <= 0.03 * mb + 0.02, (b[::20], f[::20])
 
 
-@pytest.mark.parametrize("tile", [128, 256])
+@pytest.mark.parametrize("tile", [128, 256, 2561])
 @pytest.mark.parametrize("M,N,K", [(512, 1024, 1024), (300, 200, 256), (1000, 520, 384)])
 def test_g4_fp8_engine_matches_register_engine(M, N, K, tile):
     """The LDS-DMA (g4) MX-fp8 kernel and the register-staged one run the same quantized operands
     through the same scaled MFMAs in the same K order: results agree to f32 rounding, for the bf16
     (bias/relu/residual), EXT (GELU-backward) and f32 (accumulate) epilogues, incl. ragged M/N, on
-    both g4 tiles (128x128 4-wave and 256x256 16-wave blocks; scales staged by LDS-DMA)."""
+    every g4 tile (128x128 4-wave, 256x256 16-wave and 256x128 8-wave blocks -- tile code 2561;
+    scales staged by LDS-DMA)."""
     from tensorflow_k8s_amd.ops._lib import lib
     g = torch.Generator().manual_seed(7)
     x = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()

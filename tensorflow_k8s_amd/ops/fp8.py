@@ -363,6 +363,9 @@ def linear_wgrad_mx(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumul
 # 128 / 192 / 256: 19.03 / 18.97 / 19.10 ms vs 18.86 ms split-K, profiles/perf_log_r3c.md): off (0)
 import os as _os
 WGRAD_NOSPLIT_TILES = int(_os.environ.get("TFK_FP8_WGRAD_NOSPLIT", "0"))
+# split-K fill target (256x256 blocks; 2x for 128x128) and minimum K-tiles per split (A/B knobs)
+WGRAD_TARGET = int(_os.environ.get("TFK_FP8_WGRAD_TARGET", "256"))
+WGRAD_MIN_KT = int(_os.environ.get("TFK_FP8_WGRAD_MIN_KT", "8"))
 
 
 def wgrad_splits(N: int, K: int, M: int) -> int:
@@ -374,6 +377,7 @@ def wgrad_splits(N: int, K: int, M: int) -> int:
     nkt = M // 128
     big = N >= 256 and K >= 256
     t = (-(-N // 256)) * (-(-K // 256)) if big else (-(-N // 128)) * (-(-K // 128))
-    s = max(1, min(-(-(256 if big else 512) // t), max(1, nkt // 8)))
+    target = WGRAD_TARGET if big else 2 * WGRAD_TARGET
+    s = max(1, min(-(-target // t), max(1, nkt // WGRAD_MIN_KT)))
     per = -(-nkt // s)
     return -(-nkt // per)

@@ -35,13 +35,17 @@ def main():
     ap.add_argument("--ps-transport", default="rccl", choices=["rccl", "gloo"],
                     help="rccl: ps ranks own a GPU (bucketed bf16 reduce/broadcast); gloo: ps ranks on the CPU")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
-    ap.add_argument("--comm-dtype", default="bf16", choices=["bf16", "f32"],
-                    help="gradient wire dtype (bf16: half the xGMI bytes; f32 master update either way)")
+    ap.add_argument("--comm-dtype", default="f32", choices=["bf16", "f32"],
+                    help="gradient wire dtype (f32 default: exact f32 aggregation like TF's; bf16: half the xGMI "
+                         "bytes, opt-in like TF's CommunicationOptions; f32 master update either way)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a hipGraph (default: on, at every world size, unless the model has host-side per-step state)")
     ap.add_argument("--rccl-algo", default="", help="RCCL algorithm (Ring|Tree|...), see parallel/comm.py")
     ap.add_argument("--rccl-proto", default="", help="RCCL protocol (Simple|LL|LL128)")
     ap.add_argument("--rccl-channels", type=int, default=0, help="minimum RCCL channels (concurrent rings)")
+    ap.add_argument("--watchdog-timeout", type=float, default=-1.0,
+                    help="abort the communicators and exit 143 after this many seconds without progress, or at "
+                         "once on an RCCL async error (default: 300 s when the step has collectives, else off)")
     ap.add_argument("--force-comm", action="store_true",
                     help="1 GPU: still run the RCCL gradient all-reduce (world-size-1 tfk_comm communicator)")
     ap.add_argument("--fp8", type=int, default=0, help="transformer models: MX-fp8 linear GEMMs (fwd, dgrad, wgrad)")
@@ -73,13 +77,16 @@ def main():
     # roles: parameter servers are the last ranks (TF_CONFIG order: chief, workers, ps)
     if info is not None:
         ps_ranks, worker_ranks = list(info.ps_ranks), list(info.worker_ranks)
+    elif args.strategy == "ps" and args.force_comm and world == 1:
+        # colocated: worker 0 also owns the only shard -- the collective PS path on one GPU
+        ps_ranks, worker_ranks = [0], [0]
     else:
         nps = args.ps if args.strategy == "ps" else 0
         ps_ranks, worker_ranks = list(range(world - nps, world)), list(range(world - nps))
     use_ps = args.strategy == "ps" or bool(ps_ranks)
     if use_ps and (not ps_ranks or not worker_ranks):
         sys.exit(f"--strategy ps needs at least one worker and one ps rank (world {world}, --ps {args.ps})")
-    is_ps = rank in ps_ranks
+    is_ps = rank in ps_ranks and rank not in worker_ranks
     ps_on_cpu = (use_ps and args.ps_transport == "gloo") or args.cpu_rehearsal
     if (is_ps and ps_on_cpu) or args.cpu_rehearsal:
         dev = torch.device("cpu")
@@ -105,8 +112,23 @@ def main():
     elif args.force_comm:
         import torch.distributed as dist
         world_comm = tfk_comm.init(dist.HashStore(), 0, 1, dev)
+    # failure detection from here on: heartbeat + ncclCommGetAsyncError polling; a hung or failed
+    # collective aborts every communicator and exits 143 (retryable) instead of wedging the node
+    wd = None
+    wd_s = args.watchdog_timeout if args.watchdog_timeout >= 0 else (300.0 if world_comm is not None else 0.0)
+    if wd_s > 0:
+        from tensorflow_k8s_amd.runtime.watchdog import StepWatchdog
+        wd = StepWatchdog(wd_s, name=f"bench-rank{rank}", comm_checks=True).start()
+        wd.beat(phase="comm self-test")
+    guards = {}
+    if world_comm is not None:
+        # the interconnect is checked before any model work: exact all-reduce + broadcast results
+        from tensorflow_k8s_amd.runtime.guard import comm_self_test
+        guards["comm_self_test"] = comm_self_test(world_comm)
     # barrier / timing group: the workers (parameter servers serve on their own schedule)
     wcomm = world_comm.split(worker_ranks, "workers") if (use_ps and world_comm is not None) else world_comm
+    if wd is not None:
+        wd.beat(phase="setup")
 
     from tensorflow_k8s_amd.models import build_model, synthetic_batch
     from tensorflow_k8s_amd.runtime.optimizer import LAMB, SGD, AdamW
@@ -136,14 +158,20 @@ def main():
         # parameter-server rank: holds one shard (f32 master + slots), serves every worker step
         from tensorflow_k8s_amd.parallel.ps import ParameterServer
         server = ParameterServer(model.arena, opt, ps_ranks.index(rank), ps_ranks, worker_ranks, "sync")
+        if wd is not None:
+            wd.beat(phase="serve")
         if args.ps_transport == "gloo":
             server.serve()
         else:
             server.setup_collective(args.bucket_mb, world_comm, wire)
-            server.serve_steps(0, args.warmup + args.steps)
+            server.serve_steps(0, args.warmup + args.steps, beat=wd.beat if wd is not None else None)
             sync()
         _gather_times(world_comm, cdev, world, 0.0)  # (the workers' clock defines the result)
+        if wd is not None:
+            wd.exit_code = 0
         tfk_comm.shutdown()
+        if wd is not None:
+            wd.stop()
         return 0
 
     if use_ps:
@@ -163,7 +191,22 @@ def main():
     # world size; only a model with host-side per-step state (graph_hazards) runs eager
     from tensorflow_k8s_amd.runtime.trainer import graph_hazards
     use_graph = (not graph_hazards(model)) if args.graph < 0 else bool(args.graph)
-    runner = StepRunner(model, opt, strat, batch, use_graph=use_graph)
+    agree = None
+    if wcomm is not None:
+        # graph-or-eager is decided unanimously by the ranks that share the step's collectives: a
+        # probe capture of fork -> all_reduce -> join first, then a vote on the real step's capture
+        from tensorflow_k8s_amd.runtime.guard import Agreement, capture_probe
+        agree = Agreement(wcomm.store, rank, worker_ranks)
+        if use_graph:
+            if wd is not None:
+                wd.beat(phase="capture probe")
+            ok, why = capture_probe(wcomm, agree, rank)
+            guards["capture_probe"] = why
+            use_graph = ok
+        else:
+            guards["capture_probe"] = "off"
+    runner = StepRunner(model, opt, strat, batch, use_graph=use_graph, agree=agree, rank=rank)
+    beat = (lambda i, ph="train": wd.beat(i, ph)) if wd is not None else (lambda i, ph="train": None)
 
     def barrier():
         sync()
@@ -171,8 +214,9 @@ def main():
             wcomm.barrier()
         sync()
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         runner.step()
+        beat(i, "warmup")
     barrier()
     # per-step device timestamps (no host sync inside the timed loop) for the median / p90
     gpu = dev.type == "cuda"
@@ -184,6 +228,7 @@ def main():
         runner.step()
         if gpu:
             evs[i + 1].record()
+        beat(args.warmup + i)
     barrier()
     dt = time.perf_counter() - t0
     mine_ms = dt / args.steps * 1000.0
@@ -212,6 +257,11 @@ def main():
         comm_cfg["rccl_transport"] = comm.transport_summary()
         comm_cfg["rccl_config"] = rccl_cfg
     loss = runner.last_loss()
+    if runner.fallback:
+        guards["capture_fallback"] = runner.fallback
+    if wd is not None:
+        guards["watchdog_s"] = wd.timeout_s
+    comm_cfg["guards"] = guards
     par = f"ps{len(ps_ranks)}+worker{nworkers}" if use_ps else f"dp{world}"
     if rank == worker_ranks[0] and not is_cnn:
         seq = model.cfg.seq_len if args.model.startswith("bert") else model.cfg.tgt_len
@@ -244,7 +294,11 @@ def main():
                        "optimizer": opt_name, "hipgraph": runner.use_graph, "comm": comm_cfg},
             "loss": loss,
         }), flush=True)
+    if wd is not None:
+        wd.exit_code = 0  # the result is out: a hung teardown must not turn the run into a failure
     tfk_comm.shutdown()
+    if wd is not None:
+        wd.stop()
 
 
 def _rccl_version() -> str:

@@ -72,6 +72,11 @@ int version() {
   return v;
 }
 
+// The rccl.h this binding was compiled against (ROCm 7.2) is newer than the librccl torch loads
+// (ROCm 7.0.x); parallel/tfk_comm.py checks at import that both are the same major family and that
+// the runtime has every entry point used here (ncclCommSplit / ncclCommFinalize: >= 2.18).
+int header_version() { return NCCL_VERSION_CODE; }
+
 class RcclComm {
  public:
   // Blocks until all nranks have joined (ncclCommInitRank); the GIL is released meanwhile.
@@ -108,9 +113,12 @@ class RcclComm {
     need_comm_tensor(in, device_, "input");
     need_comm_tensor(out, device_, "output");
     TORCH_CHECK(in.numel() == out.numel() && in.scalar_type() == out.scalar_type(), "all_reduce: in/out mismatch");
-    nccl_check(ncclAllReduce(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), nccl_dtype(in), nccl_op(op), comm_,
-                             pick_stream(stream)),
-               "ncclAllReduce");
+    ncclResult_t r;
+    {
+      py::gil_scoped_release nogil;  // RCCL may block (lazy peer connect): keep the watchdog thread runnable
+      r = ncclAllReduce(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), nccl_dtype(in), nccl_op(op), comm_, pick_stream(stream));
+    }
+    nccl_check(r, "ncclAllReduce");
   }
   void reduce(torch::Tensor in, torch::Tensor out, int root, const std::string& op, uint64_t stream) {
     live();
@@ -118,17 +126,23 @@ class RcclComm {
     need_comm_tensor(out, device_, "output");
     TORCH_CHECK(in.numel() == out.numel() && in.scalar_type() == out.scalar_type(), "reduce: in/out mismatch");
     check_peer(root);
-    nccl_check(ncclReduce(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), nccl_dtype(in), nccl_op(op), root, comm_,
-                          pick_stream(stream)),
-               "ncclReduce");
+    ncclResult_t r;
+    {
+      py::gil_scoped_release nogil;  // RCCL may block (lazy peer connect): keep the watchdog thread runnable
+      r = ncclReduce(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), nccl_dtype(in), nccl_op(op), root, comm_, pick_stream(stream));
+    }
+    nccl_check(r, "ncclReduce");
   }
   void broadcast(torch::Tensor t, int root, uint64_t stream) {
     live();
     need_comm_tensor(t, device_, "tensor");
     check_peer(root);
-    nccl_check(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), nccl_dtype(t), root, comm_,
-                             pick_stream(stream)),
-               "ncclBroadcast");
+    ncclResult_t r;
+    {
+      py::gil_scoped_release nogil;  // RCCL may block (lazy peer connect): keep the watchdog thread runnable
+      r = ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), nccl_dtype(t), root, comm_, pick_stream(stream));
+    }
+    nccl_check(r, "ncclBroadcast");
   }
   // out holds size() * in.numel() elements (rank-major)
   void all_gather(torch::Tensor out, torch::Tensor in, uint64_t stream) {
@@ -137,9 +151,12 @@ class RcclComm {
     need_comm_tensor(out, device_, "output");
     TORCH_CHECK(out.numel() == in.numel() * nranks_ && in.scalar_type() == out.scalar_type(),
                 "all_gather: output must hold world * input elements");
-    nccl_check(ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), nccl_dtype(in), comm_,
-                             pick_stream(stream)),
-               "ncclAllGather");
+    ncclResult_t r;
+    {
+      py::gil_scoped_release nogil;  // RCCL may block (lazy peer connect): keep the watchdog thread runnable
+      r = ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), nccl_dtype(in), comm_, pick_stream(stream));
+    }
+    nccl_check(r, "ncclAllGather");
   }
   // in holds size() * out.numel() elements; rank r receives the reduced r-th slice
   void reduce_scatter(torch::Tensor out, torch::Tensor in, const std::string& op, uint64_t stream) {
@@ -148,9 +165,12 @@ class RcclComm {
     need_comm_tensor(out, device_, "output");
     TORCH_CHECK(in.numel() == out.numel() * nranks_ && in.scalar_type() == out.scalar_type(),
                 "reduce_scatter: input must hold world * output elements");
-    nccl_check(ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), nccl_dtype(in), nccl_op(op), comm_,
-                                 pick_stream(stream)),
-               "ncclReduceScatter");
+    ncclResult_t r;
+    {
+      py::gil_scoped_release nogil;  // RCCL may block (lazy peer connect): keep the watchdog thread runnable
+      r = ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), nccl_dtype(in), nccl_op(op), comm_, pick_stream(stream));
+    }
+    nccl_check(r, "ncclReduceScatter");
   }
   void all_to_all(torch::Tensor out, torch::Tensor in, uint64_t stream) {
     live();
@@ -158,21 +178,34 @@ class RcclComm {
     need_comm_tensor(out, device_, "output");
     TORCH_CHECK(in.numel() == out.numel() && in.numel() % nranks_ == 0 && in.scalar_type() == out.scalar_type(),
                 "all_to_all: equal in/out, divisible by world");
-    nccl_check(ncclAllToAll(in.data_ptr(), out.data_ptr(), (size_t)(in.numel() / nranks_), nccl_dtype(in), comm_,
-                            pick_stream(stream)),
-               "ncclAllToAll");
+    ncclResult_t r;
+    {
+      py::gil_scoped_release nogil;  // RCCL may block (lazy peer connect): keep the watchdog thread runnable
+      r = ncclAllToAll(in.data_ptr(), out.data_ptr(), (size_t)(in.numel() / nranks_), nccl_dtype(in), comm_, pick_stream(stream));
+    }
+    nccl_check(r, "ncclAllToAll");
   }
   void send(torch::Tensor t, int peer, uint64_t stream) {
     live();
     need_comm_tensor(t, device_, "tensor");
     check_peer(peer);
-    nccl_check(ncclSend(t.data_ptr(), (size_t)t.numel(), nccl_dtype(t), peer, comm_, pick_stream(stream)), "ncclSend");
+    ncclResult_t r;
+    {
+      py::gil_scoped_release nogil;  // RCCL may block (lazy peer connect): keep the watchdog thread runnable
+      r = ncclSend(t.data_ptr(), (size_t)t.numel(), nccl_dtype(t), peer, comm_, pick_stream(stream));
+    }
+    nccl_check(r, "ncclSend");
   }
   void recv(torch::Tensor t, int peer, uint64_t stream) {
     live();
     need_comm_tensor(t, device_, "tensor");
     check_peer(peer);
-    nccl_check(ncclRecv(t.data_ptr(), (size_t)t.numel(), nccl_dtype(t), peer, comm_, pick_stream(stream)), "ncclRecv");
+    ncclResult_t r;
+    {
+      py::gil_scoped_release nogil;  // RCCL may block (lazy peer connect): keep the watchdog thread runnable
+      r = ncclRecv(t.data_ptr(), (size_t)t.numel(), nccl_dtype(t), peer, comm_, pick_stream(stream));
+    }
+    nccl_check(r, "ncclRecv");
   }
 
   // Sub-communicator (ncclCommSplit): every rank of this communicator must call it, in the same
@@ -237,6 +270,7 @@ void group_end() {
 void register_comm_ops(py::module& m) {
   m.def("rccl_unique_id", &unique_id);
   m.def("rccl_version", &version);
+  m.def("rccl_header_version", &header_version);
   m.def("rccl_group_start", &group_start);
   m.def("rccl_group_end", &group_end);
   py::class_<RcclComm>(m, "RcclComm")

@@ -14,7 +14,9 @@ runs at every world size.
 * Launch order is the bucket order on every rank (a bucket that completes early waits for its
   predecessors), so all ranks issue the same collective sequence whatever the readiness callbacks
   do -- a mismatched order would pair different buckets in the ring and hang or corrupt.
-* ``comm_dtype=torch.bfloat16`` puts bf16 on the wire: the bucket is packed f32->bf16 by a HIP
+* The default wire is f32 (RCCL sums exactly what TF's f32 gradient aggregation sums).
+  ``comm_dtype=torch.bfloat16`` (opt-in, like TF's CommunicationOptions) puts bf16 on the wire:
+  the bucket is packed f32->bf16 by a HIP
   cast kernel on the compute stream (the RCCL stream waits on it), all-reduced in bf16 (half the
   xGMI bytes of f32: 51 MB instead of 102 MB per ResNet-50 step) and unpacked into the f32 arena
   right after the wait; the 1/world mean stays in the fused optimizer's grad_scale.
@@ -59,7 +61,7 @@ class Bucket:
 class MultiWorkerMirroredStrategy:
     name = "mwms"
 
-    def __init__(self, arena: ParamArena, comm=None, bucket_mb: float = 32.0, comm_dtype=torch.bfloat16,
+    def __init__(self, arena: ParamArena, comm=None, bucket_mb: float = 32.0, comm_dtype=torch.float32,
                  force: bool = False):
         self.arena = arena
         self.comm = comm if comm is not None else tfk_comm.world()

@@ -28,7 +28,7 @@ Two transports:
     sub-communicators (ncclCommSplit) over {its owner} + workers -- one for gradient ``reduce``, one
     for parameter ``broadcast`` -- so a bucket's broadcast does not queue behind later buckets'
     reduces, and no other ps task contributes zeros to s's traffic;
-  - bf16 on the wire in both directions: workers pack each gradient bucket f32->bf16 and ``reduce``
+  - f32 on the wire by default; with ``wire_dtype=torch.bfloat16`` (opt-in) bf16 in both directions: workers pack each gradient bucket f32->bf16 and ``reduce``
     it to the owner; the owner ships back the bf16 COMPUTE copy of weight-decayed buckets (what the
     workers' GEMMs read; the f32 master never leaves the owner) and the small f32 no-decay buckets
     (biases, BN/LayerNorm gamma+beta, which kernels read in f32). Per BERT-base step that is
@@ -43,6 +43,13 @@ Two transports:
     buckets are updated and shipped back while later ones are still being reduced.
   The schedule is identical on every rank (steps and checkpoint steps are known), so no control
   messages are needed; for a checkpoint the owners ``send`` f32 master + slots to the chief.
+  The owner loop is host-driven; its run-ahead is bounded (``RUN_AHEAD`` steps, an event ring),
+  so a stalled peer shows up as a stalled heartbeat instead of an ever-growing launch queue.
+* colocated owners: a shard whose owner is also a worker (``ps_ranks`` ∩ ``worker_ranks``, e.g.
+  ``bench.py --strategy ps --force-comm`` at world size 1, where worker 0 owns the only shard) is
+  updated inside that worker's own step: its reduce is the worker's reduce, and the unpack ->
+  ``step_region`` -> broadcast run in ``apply_gradients`` -- so the whole collective PS path,
+  including its hipGraph capture, runs on one GPU.
 """
 from __future__ import annotations
 
@@ -53,6 +60,7 @@ from ..runtime.arena import ALIGN, ParamArena
 from . import tfk_comm
 
 PUSH, DONE, FETCH, LOAD, PULL = 1, 2, 3, 4, 5
+RUN_AHEAD = 2  # owner loop: at most this many global steps enqueued ahead of the device
 
 
 def shard_bounds(numel: int, nshards: int, param_spans: list[tuple[int, int]] | None = None) -> list[tuple[int, int]]:
@@ -105,7 +113,7 @@ class ParameterServerStrategy:
     name = "ps"
 
     def __init__(self, arena: ParamArena, ps_ranks: list[int], worker_ranks: list[int], mode: str = "sync",
-                 group=None, transport: str = "gloo", bucket_mb: float = 32.0, comm=None, wire_dtype=torch.bfloat16):
+                 group=None, transport: str = "gloo", bucket_mb: float = 32.0, comm=None, wire_dtype=torch.float32):
         if mode not in ("sync", "async"):
             raise ValueError(f"ps mode must be sync|async, got {mode}")
         if transport not in ("gloo", "rccl"):
@@ -129,6 +137,10 @@ class ParameterServerStrategy:
         self.step_count = 0
         self._next = 0
         self._red = []
+        # shards this rank owns while also being a worker (colocated owner)
+        self.owned = [s for s, owner in enumerate(self.ps_ranks) if owner == self.rank and owner in self.worker_ranks]
+        if self.owned and transport != "rccl":
+            raise ValueError("a colocated parameter-server shard needs the rccl (collective) transport")
 
     @property
     def capturable(self) -> bool:
@@ -193,6 +205,8 @@ class ParameterServerStrategy:
         a = self.arena
         if self.transport == "rccl":
             self.finish_step()  # (no-op when the runner already called it)
+            if self.owned:
+                self._update_owned(opt if opt is not None else self.opt)
             works = [self.plan.broadcast(i) for i in range(len(self.plan.buckets))]
             for w in self._red + works:
                 w.wait()  # stream waits: the next forward is ordered after the pulled parameters
@@ -213,6 +227,19 @@ class ParameterServerStrategy:
         self.step_count += 1
         if opt is not None:
             opt.step_count = self.step_count
+
+    def _update_owned(self, opt) -> None:
+        """Colocated owner: per owned bucket, wait for its reduce, unpack, update (one global step)."""
+        plan, k = self.plan, 0
+        for s in self.owned:
+            for i in plan.buckets_of(s):
+                self._red[i].wait()
+                plan.unpack(i)
+                lo, hi, _ = plan.buckets[i]
+                opt.region = (lo, hi)
+                opt.step_region(advance=k == 0)
+                k += 1
+        opt.region = None
 
     def pull(self) -> None:
         """Initial (or resync) read of every variable from the ps tasks."""
@@ -273,7 +300,7 @@ class CollectivePlan:
     ratio included), listed in arena order = backward-completion order."""
 
     def __init__(self, arena: ParamArena, shards, ps_ranks, worker_ranks, bucket_mb: float = 32.0, comm=None,
-                 wire_dtype=torch.bfloat16):
+                 wire_dtype=torch.float32):
         self.arena, self.shards, self.ps_ranks = arena, list(shards), list(ps_ranks)
         self.comm = comm if comm is not None else tfk_comm.world()
         self.me = self.comm.rank
@@ -462,16 +489,16 @@ class ParameterServer:
     # ------------------------------------------------------------------ rccl transport
     def serve_collective(self, start_step: int, total_steps: int, checkpoint_every: int = 0,
                          chief: int = 0, final_checkpoint: bool = True, bucket_mb: float = 32.0, comm=None,
-                         wire_dtype=torch.bfloat16) -> int:
+                         wire_dtype=torch.float32, beat=None) -> int:
         """Mirror of the workers' step schedule over tfk_comm (CollectivePlan): initial broadcast,
         then per step: zero the own shard's gradient, post the own buckets' reduces, and per bucket
         stream-wait -> unpack -> fused optimizer on that bucket -> post its broadcast. The global step
         (host counter or device schedule) advances once per step. Ships f32 master + slots to the
         chief at its checkpoint steps."""
         self.setup_collective(bucket_mb, comm, wire_dtype)
-        return self.serve_steps(start_step, total_steps, checkpoint_every, chief, final_checkpoint)
+        return self.serve_steps(start_step, total_steps, checkpoint_every, chief, final_checkpoint, beat=beat)
 
-    def setup_collective(self, bucket_mb: float = 32.0, comm=None, wire_dtype=torch.bfloat16) -> None:
+    def setup_collective(self, bucket_mb: float = 32.0, comm=None, wire_dtype=torch.float32) -> None:
         """Create the per-shard sub-communicators (in the same order as the workers'
         ParameterServerStrategy) and serve the initial parameter pull."""
         a = self.arena
@@ -480,13 +507,19 @@ class ParameterServer:
         self._plan.pull_master()
 
     def serve_steps(self, start_step: int, end_step: int, checkpoint_every: int = 0, chief: int = 0,
-                    final_checkpoint: bool = False, total_steps: int | None = None) -> int:
-        """Serve global steps start_step+1 .. end_step (after setup_collective)."""
+                    final_checkpoint: bool = False, total_steps: int | None = None, beat=None) -> int:
+        """Serve global steps start_step+1 .. end_step (after setup_collective). ``beat(step)`` is
+        the watchdog heartbeat; the host runs at most RUN_AHEAD steps ahead of the device."""
         a, plan, comm, opt = self.arena, self._plan, self._comm, self.opt
         total = end_step if total_steps is None else total_steps
         me = self.ps_ranks.index(comm.rank)
         mine = plan.buckets_of(me)
+        ring = []
         for step in range(start_step + 1, end_step + 1):
+            if len(ring) >= RUN_AHEAD:
+                ring.pop(0).synchronize()  # bounded run-ahead: step - RUN_AHEAD has completed
+            if beat is not None:
+                beat(step)
             a.grad[self.lo:self.hi].zero_()  # the owner's own (zero) contribution to its reduces
             if plan.wire is not None:
                 plan.wire[self.lo:self.hi].zero_()
@@ -503,6 +536,10 @@ class ParameterServer:
                 w.wait()
             opt.region = (self.lo, self.hi)
             self.updates += 1
+            if a.master.is_cuda:
+                ev = torch.cuda.Event()
+                ev.record()
+                ring.append(ev)
             ckpt = (checkpoint_every and step % checkpoint_every == 0 and step < total) or \
                 (final_checkpoint and step == total)
             if ckpt:

@@ -44,6 +44,33 @@ def abort_all() -> int:
     return n
 
 
+def async_errors() -> str:
+    """The first asynchronous RCCL error of any live communicator ("" while all are healthy); the
+    step watchdog polls this every tick (ncclCommGetAsyncError is thread-safe)."""
+    with _LIVE_LOCK:
+        comms = list(_LIVE)
+    for c in comms:
+        try:
+            e = c.async_error()
+        except Exception as ex:  # pragma: no cover - a broken communicator is an error too
+            e = str(ex)
+        if e:
+            return f"{getattr(c, 'tag', '?')}: {e}"
+    return ""
+
+
+MIN_RCCL = 21800  # ncclCommSplit / ncclCommFinalize
+
+
+def check_rccl_version(header: int, runtime: int) -> None:
+    """The binding compiles against /opt/rocm's rccl.h but runs on the librccl torch loads: refuse a
+    runtime of another major family, or one older than the entry points the binding calls."""
+    if header // 10000 != runtime // 10000:
+        raise RuntimeError(f"tfk_comm: librccl {runtime} is not the major family of rccl.h {header}")
+    if runtime < MIN_RCCL:
+        raise RuntimeError(f"tfk_comm: librccl {runtime} predates ncclCommSplit/ncclCommFinalize ({MIN_RCCL})")
+
+
 def exchange_unique_id(store, rank: int, tag: str, make_uid, timeout_s: float = 300.0) -> bytes:
     """Rank 0 draws the communicator's unique id and publishes it under ``tfk_comm/<tag>/uid`` in the
     job store; every other rank waits for the key and reads it."""
@@ -100,6 +127,7 @@ class RcclComm:
         # comm stream: RCCL kernels of this communicator; priority -1 = high on ROCm, so bucket
         # all-reduces are not starved behind the backward grids queued on the compute stream
         self.stream = torch.cuda.Stream(device=device, priority=-1)
+        self.store = None  # the job store the communicator was bootstrapped from (agreements)
         self._aborted = False
         with _LIVE_LOCK:
             _LIVE.add(self)
@@ -110,16 +138,23 @@ class RcclComm:
                    timeout_s: float = 300.0) -> "RcclComm":
         """Chief publishes the unique id under ``tfk_comm/<tag>/uid``; all ranks init."""
         from .. import _C
+        check_rccl_version(_C.rccl_header_version(), _C.rccl_version())
         uid = exchange_unique_id(store, rank, tag, _C.rccl_unique_id, timeout_s)
         native = _C.RcclComm(uid, world, rank, device.index if device.index is not None else torch.cuda.current_device())
-        return cls(native, device, tag)
+        c = cls(native, device, tag)
+        c.store = store
+        return c
 
     def split(self, ranks: list[int], tag: str) -> "RcclComm | None":
         """Sub-communicator over ``ranks`` (ncclCommSplit; every rank must call, in order)."""
         color = 0 if self.rank in ranks else -1
         key = sorted(ranks).index(self.rank) if self.rank in ranks else 0
         nc = self._c.split(color, key)
-        return RcclComm(nc, self.device, tag) if nc is not None else None
+        if nc is None:
+            return None
+        c = RcclComm(nc, self.device, tag)
+        c.store = self.store
+        return c
 
     # ------------------------------------------------------------------ stream plumbing
     def _fork(self):
@@ -234,10 +269,12 @@ class _DistGroup:
 class TorchDistComm:
     """CPU tier: a torch.distributed process group (gloo) behind the tfk_comm interface."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, store=None):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
+        self.store = store
+        self.tag = "gloo"
         self.backend = str(dist.get_backend(group))
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -254,7 +291,7 @@ class TorchDistComm:
 
     def split(self, ranks: list[int], tag: str) -> "TorchDistComm | None":
         g = self.dist.new_group([self._global[r] for r in sorted(ranks)])
-        return TorchDistComm(g) if self.rank in ranks else None
+        return TorchDistComm(g, self.store) if self.rank in ranks else None
 
     def all_reduce(self, t, op="sum", async_op=False, out=None):
         if out is not None and out.data_ptr() != t.data_ptr():
@@ -340,7 +377,7 @@ def init(store, rank: int, world_size: int, device: torch.device, timeout_s: flo
         if not dist.is_initialized():
             dist.init_process_group("gloo", store=store, rank=rank, world_size=world_size,
                                     timeout=datetime.timedelta(seconds=timeout_s))
-        c = TorchDistComm()
+        c = TorchDistComm(store=store)
     set_world(c)
     return c
 

@@ -5,7 +5,7 @@ This is the program a TFJob replica runs (the reference's pods run a TF script t
 the operator-injected TF_CONFIG). Per role:
 
 * chief / worker: one process per GPU (HIP_VISIBLE_DEVICES set by the node agent), a tfk_comm RCCL
-  world over all workers (MWMS; bf16 gradient wire, the whole step captured in a hipGraph) or the
+  world over all workers (MWMS; f32 gradient wire by default, the whole step captured in a hipGraph) or the
   ps tasks (PS strategy: collective RCCL transport, or gloo point-to-point to CPU ps tasks); restore-or-init, train
   ``--steps`` global steps on synthetic data of the model's shape, chief writes TF-bundle
   checkpoints every ``--checkpoint-every`` steps and at the end, JSON-lines metrics on stdout;
@@ -66,8 +66,9 @@ def parse_args(argv=None):
     ap.add_argument("--ps-transport", default="gloo", choices=["gloo", "rccl"],
                     help="gloo: ps tasks on CPU (sync/async); rccl: ps tasks own a GPU, RCCL reduce/broadcast (sync)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
-    ap.add_argument("--comm-dtype", default="bf16", choices=["f32", "bf16"],
-                    help="gradient wire dtype (MWMS all-reduce, collective PS push/pull)")
+    ap.add_argument("--comm-dtype", default="f32", choices=["f32", "bf16"],
+                    help="gradient wire dtype (MWMS all-reduce, collective PS push/pull); f32 default = exact f32 "
+                         "aggregation, bf16 = half the xGMI bytes (opt-in, like TF's CommunicationOptions)")
     ap.add_argument("--device", default="auto", choices=["auto", "cpu", "cuda"])
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a hipGraph (default: on for GPU workers at any world size, unless the "
@@ -84,8 +85,9 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--step-sleep", type=float, default=0.0, help="seconds to pause after each step (paces demo/test jobs)")
     ap.add_argument("--rendezvous-timeout", type=float, default=300.0)
-    ap.add_argument("--watchdog-timeout", type=float, default=0.0,
-                    help="exit 143 (retryable) when no step completes for this many seconds (0 = off)")
+    ap.add_argument("--watchdog-timeout", type=float, default=-1.0,
+                    help="abort the communicators and exit 143 (retryable) when no step completes for this many "
+                         "seconds or RCCL reports an async error (default: 300 s at world size > 1; 0 = off)")
     ap.add_argument("--trace-file", default="", help="Chrome-trace step timeline (+ roctx ranges); {rank} expands")
     # evaluator
     ap.add_argument("--eval-batches", type=int, default=4)
@@ -154,7 +156,7 @@ def maybe_fault(step: int, rank: int):
     os._exit(code)
 
 
-def run_ps(args, info, dev, world_comm) -> int:
+def run_ps(args, info, dev, world_comm, watchdog=None) -> int:
     from ..models import build_model
     from ..parallel import tfk_comm
     from ..parallel.ps import ParameterServer
@@ -174,7 +176,8 @@ def run_ps(args, info, dev, world_comm) -> int:
     if args.ps_transport == "rccl":
         n = server.serve_collective(start, args.steps, args.checkpoint_every if args.checkpoint_dir else 0,
                                     chief=0, final_checkpoint=bool(args.checkpoint_dir), bucket_mb=args.bucket_mb,
-                                    comm=world_comm, wire_dtype=_wire(args))
+                                    comm=world_comm, wire_dtype=_wire(args),
+                                    beat=watchdog.beat if watchdog is not None else None)
     else:
         n = server.serve()
     _log({"event": "done", "role": "ps", "index": info.task_index, "updates": n})
@@ -186,7 +189,7 @@ def _wire(args):
     return torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32
 
 
-def run_worker(args, info, dev, world_comm) -> int:
+def run_worker(args, info, dev, world_comm, watchdog=None) -> int:
     from ..models import build_model, synthetic_batch
     from ..parallel import tfk_comm
     from .checkpoint import CheckpointManager
@@ -229,21 +232,30 @@ def run_worker(args, info, dev, world_comm) -> int:
     static = tuple(t.clone() for t in batches[0])
     from .trainer import graph_hazards
     use_graph = dev.type == "cuda" and (not graph_hazards(model) if args.graph < 0 else bool(args.graph))
-    runner = StepRunner(model, opt, strat, static, use_graph=use_graph)
+    agree, probe = None, "off"
+    if world_comm is not None and world_comm.backend == "rccl":
+        # graph-or-eager decided unanimously by the workers (runtime/guard.py): probe capture of
+        # fork -> all_reduce -> join (MWMS), then a vote on the real step's capture
+        from .guard import Agreement, capture_probe
+        agree = Agreement(world_comm.store, info.rank, info.worker_ranks, timeout_s=args.rendezvous_timeout)
+        if use_graph and not use_ps:
+            if watchdog is not None:
+                watchdog.beat(phase="capture probe")
+            use_graph, probe = capture_probe(world_comm, agree, info.rank)
+    runner = StepRunner(model, opt, strat, static, use_graph=use_graph, agree=agree, rank=info.rank)
     metrics_fh = open(args.metrics_file, "a") if (args.metrics_file and info.is_chief) else None
     gb = args.batch * nworkers
     _log({"event": "start", "rank": info.rank, "world": info.world_size, "workers": nworkers, "model": model.name,
           "params": model.arena.num_parameters(), "device": str(dev), "strategy": strat.name, "start_step": start,
           "wire_mb_per_step": round(strat.wire_bytes() / 2**20, 3) if hasattr(strat, "wire_bytes") else 0.0,
-          "hipgraph": runner.use_graph,
+          "hipgraph": runner.use_graph, "capture_probe": probe,
           "global_batch": gb, "restart_generation": int(os.environ.get("TFK_RESTART_GENERATION", "0"))})
     from ..utils.tracing import NULL_TRACER, Tracer
     tracer = Tracer(rank=info.rank, device_events=dev.type == "cuda") if args.trace_file else NULL_TRACER
-    watchdog = None
-    if args.watchdog_timeout > 0:
-        from .watchdog import StepWatchdog
-        watchdog = StepWatchdog(args.watchdog_timeout, name=f"rank{info.rank}").start()
+    if watchdog is not None:
+        watchdog.beat(start, phase="train")
     t_last, n_last = time.perf_counter(), 0
+    fell_back = False
     step = start
     while step < args.steps:
         with tracer.span("step", cat="train", step=step):
@@ -253,6 +265,9 @@ def run_worker(args, info, dev, world_comm) -> int:
         n_last += 1
         if watchdog is not None:
             watchdog.beat(step)
+        if runner.fallback and not fell_back:
+            fell_back = True
+            _log({"event": "graph_fallback", "rank": info.rank, "step": step, "reason": runner.fallback[:500]})
         if step % max(1, args.log_every) == 0 or step == args.steps:
             m = torch.tensor([runner.last_loss() or 0.0, runner.last_accuracy() or 0.0], dtype=torch.float32,
                              device=dev if strat.name == "mwms" else "cpu")
@@ -278,8 +293,6 @@ def run_worker(args, info, dev, world_comm) -> int:
         maybe_fault(step, info.rank)
         if args.step_sleep > 0:
             time.sleep(args.step_sleep)
-    if watchdog is not None:
-        watchdog.stop()
     if args.trace_file:
         _log({"event": "trace", "path": tracer.dump(args.trace_file.format(rank=info.rank))})
     if ckpt is not None and info.is_chief:
@@ -300,6 +313,11 @@ def run_worker(args, info, dev, world_comm) -> int:
     return EXIT_OK
 
 
+def _guard_error():
+    from .guard import CommSelfTestError
+    return CommSelfTestError
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     from ..parallel import cluster
@@ -314,14 +332,32 @@ def main(argv=None) -> int:
             # co-located CPU replicas: split the cores instead of oversubscribing them
             torch.set_num_threads(max(1, (os.cpu_count() or 1) // info.world_size))
         world_comm = None
+        watchdog = None
+        wd_s = args.watchdog_timeout if args.watchdog_timeout >= 0 else (300.0 if info.world_size > 1 else 0.0)
+        if wd_s > 0:
+            # failure detection: heartbeat + ncclCommGetAsyncError polling from the
+            # first collective on; a hung/failed peer aborts the communicators and exits 143
+            from .watchdog import StepWatchdog
+            watchdog = StepWatchdog(wd_s, name=f"rank{info.rank}", comm_checks=True).start()
+            watchdog.beat(phase="rendezvous")
         if info.world_size > 1:
             use_ps = args.strategy == "ps" or (args.strategy == "auto" and info.ps_ranks)
             backend = "rccl" if (dev.type == "cuda" and (not use_ps or args.ps_transport == "rccl")) else "gloo"
             world_comm = cluster.init_comm(info, dev, backend, timeout_s=args.rendezvous_timeout,
                                            retries=int(os.environ.get("TFK_RENDEZVOUS_RETRIES", "5")))
-        if info.is_ps:
-            return run_ps(args, info, dev, world_comm)
-        return run_worker(args, info, dev, world_comm)
+            if watchdog is not None:
+                watchdog.beat(phase="comm self-test")
+            from .guard import comm_self_test
+            _log({"event": "comm_self_test", "rank": info.rank, **comm_self_test(world_comm)})
+            if watchdog is not None:
+                watchdog.beat(phase="setup")
+        try:
+            if info.is_ps:
+                return run_ps(args, info, dev, world_comm, watchdog)
+            return run_worker(args, info, dev, world_comm, watchdog)
+        finally:
+            if watchdog is not None:
+                watchdog.stop()
     except torch.cuda.OutOfMemoryError as e:
         _termination_message("OOMKilled")
         _log({"event": "error", "kind": "oom", "message": str(e)[:500]})
@@ -331,7 +367,7 @@ def main(argv=None) -> int:
         _termination_message(f"CheckpointWriteFailed: {e}"[:2000])
         _log({"event": "error", "kind": "checkpoint", "message": str(e)[:500]})
         return EXIT_USER
-    except cluster.RendezvousError as e:
+    except (cluster.RendezvousError, _guard_error()) as e:
         _termination_message(str(e))
         _log({"event": "error", "kind": "rendezvous", "message": str(e)[:500]})
         return EXIT_RETRY

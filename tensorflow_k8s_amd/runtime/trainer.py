@@ -11,6 +11,11 @@ Everything a replay must see change per step lives on the device: the optimizer'
 schedule, step counter and Adam bias corrections (Optimizer.enable_device_schedule) and the models'
 dropout RNG state (ops.elementwise.rng_advance/rng_key). Host-side per-step values that would
 freeze inside a graph make capture refuse (GraphUnsafe) instead of silently training wrong.
+
+Multi-rank safety (runtime/guard.py): with an ``agree`` (guard.Agreement over the ranks that share
+the step's collectives) the capture result is voted on before the first replay; if any rank failed
+to capture, every rank drops its graph and the step runs eagerly from then on (``fallback`` holds
+the reason) -- nobody is left waiting in a replayed collective its peer never issues.
 """
 from __future__ import annotations
 
@@ -35,7 +40,8 @@ def graph_hazards(model) -> list[str]:
 
 
 class StepRunner:
-    def __init__(self, model, opt, strategy, batch, use_graph: bool = False, warmup_eager: int = 2):
+    def __init__(self, model, opt, strategy, batch, use_graph: bool = False, warmup_eager: int = 2,
+                 agree=None, rank: int = 0):
         self.model, self.opt, self.strategy = model, opt, strategy
         self.batch = batch
         # a parameter-server strategy is capturable only on its collective (RCCL) transport
@@ -48,6 +54,8 @@ class StepRunner:
             if opt is not None and hasattr(opt, "enable_device_schedule"):
                 opt.enable_device_schedule()
         self.warmup_eager = warmup_eager
+        self.agree, self.rank = agree, rank
+        self.fallback = ""  # why the step runs eager after a failed (agreed) capture
         self.graph = None
         self.n = 0
         self._loss = None
@@ -85,14 +93,38 @@ class StepRunner:
                     self._loss, self._corr = self._step_body()
                 torch.cuda.current_stream().wait_stream(side)
                 return
-            self.graph = torch.cuda.CUDAGraph()
-            torch.cuda.synchronize()
-            # thread-local capture: RCCL's process-group watchdog thread polls its work events while
-            # this thread captures; under the default global mode that poll fails the capture
-            # ("operation not permitted when stream is capturing")
-            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-                self._loss, self._corr = self._step_body()
+            if not self._capture():
+                self._loss, self._corr = self._step_body()  # agreed fallback: this step runs eager
+                return
         self.graph.replay()
+
+    def _capture(self) -> bool:
+        from .guard import Agreement, capture_fault
+        err = ""
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        try:
+            capture_fault("step", self.rank)
+            # thread-local capture: a watchdog thread polling RCCL / events while this thread
+            # captures must not invalidate the capture (the default global mode would)
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._loss, self._corr = self._step_body()
+        except Exception as e:  # noqa: BLE001 -- every failure votes no
+            err = f"{type(e).__name__}: {e}"[:600]
+            if self.agree is None:
+                raise
+        ok = not err
+        if self.agree is not None:
+            ok, bad = self.agree.decide("step_capture", not err, err)
+            if not ok:
+                err = Agreement.summary(bad)
+        if not ok:
+            self.graph, self.use_graph, self.fallback = None, False, err
+            del g
+            torch.cuda.synchronize()
+            return False
+        self.graph = g
+        return True
 
     def last_loss(self):
         if self._loss is None:

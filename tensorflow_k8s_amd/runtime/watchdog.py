@@ -8,6 +8,11 @@ event, aborts every live tfk_comm RCCL communicator (``ncclCommAbort``: the rank
 kernels exit instead of spinning on a dead peer) and exits with 143, the retryable code of the operator's ExitCode restart policy: the
 operator bumps the restart generation, every rank re-rendezvouses and training resumes from the
 latest checkpoint (runtime/train.py, runtime/checkpoint.py).
+
+Besides the heartbeat, every tick polls the registered health checks -- by default
+``tfk_comm.async_errors()`` (ncclCommGetAsyncError of every live communicator): a peer that RCCL has
+already declared lost fires the watchdog at once instead of after the heartbeat timeout. The
+multi-rank runtimes (bench.py, runtime/train.py) arm it by default at world size > 1.
 """
 from __future__ import annotations
 
@@ -21,13 +26,21 @@ EXIT_RETRY = 143
 
 
 class StepWatchdog:
-    def __init__(self, timeout_s: float, on_timeout=None, poll_s: float | None = None, name: str = "train"):
+    def __init__(self, timeout_s: float, on_timeout=None, poll_s: float | None = None, name: str = "train",
+                 checks=None, comm_checks: bool = False):
         if timeout_s <= 0:
             raise ValueError("watchdog timeout must be > 0")
         self.timeout_s = float(timeout_s)
         self.poll_s = float(poll_s) if poll_s else min(1.0, self.timeout_s / 4)
         self.name = name
         self.on_timeout = on_timeout or self._default_timeout
+        # health checks polled every tick: callables returning "" (healthy) or an error message
+        self.checks = list(checks or [])
+        if comm_checks:
+            self.checks.append(comm_async_error)
+        self.exit_code = EXIT_RETRY  # set to 0 once the job's result is out (a hung teardown is not a failure)
+        self.phase = "train"
+        self.error = ""
         self.last_step = -1
         self._last = time.monotonic()
         self._stop = threading.Event()
@@ -42,11 +55,13 @@ class StepWatchdog:
         self._thread.start()
         return self
 
-    def beat(self, step: int | None = None) -> None:
+    def beat(self, step: int | None = None, phase: str | None = None) -> None:
         with self._lock:
             self._last = time.monotonic()
             if step is not None:
                 self.last_step = step
+            if phase is not None:
+                self.phase = phase
 
     def stop(self) -> None:
         self._stop.set()
@@ -70,13 +85,26 @@ class StepWatchdog:
             with self._lock:
                 idle = time.monotonic() - self._last
                 step = self.last_step
-            if idle > self.timeout_s:
+            err = ""
+            for chk in self.checks:
+                try:
+                    err = chk() or ""
+                except Exception as e:  # a failing check is itself an error signal
+                    err = f"{getattr(chk, '__name__', 'check')}: {e}"
+                if err:
+                    break
+            if err or idle > self.timeout_s:
+                self.error = err
                 self._fired.set()
                 self.on_timeout(step, idle)
                 return
 
     def _default_timeout(self, step: int, idle: float) -> None:
-        msg = f"watchdog: no training progress for {idle:.1f}s after step {step} (peer lost or collective hung)"
+        if self.error:
+            msg = f"watchdog: communicator error during {self.phase} after step {step}: {self.error}"
+        else:
+            msg = (f"watchdog: no progress for {idle:.1f}s during {self.phase} after step {step} "
+                   "(peer lost or collective hung)")
         path = os.environ.get("TFK_TERMINATION_LOG")
         if path:
             try:
@@ -84,20 +112,38 @@ class StepWatchdog:
                     f.write(msg)
             except OSError:
                 pass
-        print(json.dumps({"event": "error", "kind": "watchdog", "step": step, "idle_s": round(idle, 2),
-                          "message": msg}, sort_keys=True), flush=True)
+        print(json.dumps({"event": "error", "kind": "comm_error" if self.error else "watchdog", "step": step,
+                          "phase": self.phase, "idle_s": round(idle, 2), "message": msg,
+                          "rccl_transport": _transport()}, sort_keys=True), flush=True)
         n = abort_communicators()
         print(json.dumps({"event": "comm_aborted", "communicators": n}, sort_keys=True), flush=True)
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(EXIT_RETRY)
+        os._exit(self.exit_code)
+
+
+def _comm_module():
+    return sys.modules.get(__name__.rsplit(".", 2)[0] + ".parallel.tfk_comm")
+
+
+def comm_async_error() -> str:
+    """ncclCommGetAsyncError over every live tfk_comm communicator ("" = healthy)."""
+    mod = _comm_module()
+    return mod.async_errors() if mod is not None else ""
+
+
+def _transport() -> dict:
+    mod = sys.modules.get(__name__.rsplit(".", 2)[0] + ".parallel.comm")
+    try:
+        return mod.transport_summary() if mod is not None else {}
+    except Exception:  # pragma: no cover
+        return {}
 
 
 def abort_communicators() -> int:
     """ncclCommAbort every live RCCL communicator of this process (parallel/tfk_comm). gloo groups
     of the CPU tier need no abort: os._exit closes their sockets and the peers' pending ops fail."""
-    import sys
-    mod = sys.modules.get(__name__.rsplit(".", 2)[0] + ".parallel.tfk_comm")
+    mod = _comm_module()
     if mod is None:  # never imported -> no communicator exists; do not pay a torch import here
         return 0
     try:

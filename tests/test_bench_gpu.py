@@ -43,3 +43,43 @@ def test_bench_force_comm_reports_rccl(tmp_path):
     c = d["config"]
     assert c["hipgraph"] is True and c["comm"]["wire_mb_per_step"] > 0
     assert c["comm"]["backend"].startswith("tfk_comm RCCL")
+    g = c["comm"]["guards"]
+    assert g["comm_self_test"]["ok"] is True and g["capture_probe"] == "ok" and "capture_fallback" not in g
+    assert g["watchdog_s"] == 300.0
+
+
+def _run_bench(tmp_path, extra, env_extra=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, **(env_extra or {}))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "resnet50", "--batch", "32",
+                        "--steps", "2", "--warmup", "3", "--force-comm"] + extra,
+                       env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return _bench_line(r.stdout)
+
+
+def test_bench_injected_capture_failures_fall_back_to_eager(tmp_path):
+    """First-N-GPU-run guards on the GPU (runtime/guard.py): an injected capture-probe failure and
+    an injected failure of the real step's capture both make the run fall back to eager steps
+    in-process; the JSON says why, and the loss equals a plain eager run's (same data, same init)."""
+    eager = _run_bench(tmp_path, ["--graph", "0"])
+    assert eager["config"]["hipgraph"] is False and eager["config"]["comm"]["guards"]["capture_probe"] == "off"
+    probe = _run_bench(tmp_path, [], {"TFK_FAULT_CAPTURE": "1"})
+    gp = probe["config"]["comm"]["guards"]
+    assert probe["config"]["hipgraph"] is False and "injected probe capture failure" in gp["capture_probe"]
+    step = _run_bench(tmp_path, [], {"TFK_FAULT_CAPTURE": "step"})
+    gs = step["config"]["comm"]["guards"]
+    assert gs["capture_probe"] == "ok" and "injected step capture failure" in gs["capture_fallback"]
+    assert step["config"]["hipgraph"] is False
+    for d in (probe, step):
+        assert abs(d["loss"] - eager["loss"]) <= 1e-3 * abs(eager["loss"]), (d["loss"], eager["loss"])
+
+
+def test_bench_collective_ps_colocated_one_gpu(tmp_path):
+    """The collective (RCCL) parameter-server transport on one GPU: worker 0 owns the only shard
+    (colocated owner), so the bucketed reduce -> unpack -> step_region -> broadcast path runs on GPU
+    tensors inside the captured worker step."""
+    d = _run_bench(tmp_path, ["--strategy", "ps", "--ps-transport", "rccl"])
+    c = d["config"]
+    assert c["parallelism"] == "ps1+worker1" and c["comm"]["transport"] == "rccl"
+    assert c["comm"]["wire_mb_per_step"] > 0 and c["comm"]["buckets"] > 0
+    assert c["hipgraph"] is True and d["loss"] is not None and d["loss"] == d["loss"]

@@ -70,3 +70,59 @@ def test_rccl_mwms_eager_and_graph_match_nocomm(tmp_path):
         assert abs(out[mode]["loss"] - out["nocomm"]["loss"]) < 0.05 * abs(out["nocomm"]["loss"]), out
     wg, we = (torch.load(str(tmp_path / f"w.{m}"), weights_only=True) for m in ("graph", "eager"))
     assert (wg - we).norm() / we.norm() < 2e-3
+
+
+PS_SCRIPT = r"""
+import os, sys, json, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["TFK_ROOT"])
+from tensorflow_k8s_amd.models.resnet import ResNet, synthetic_imagenet
+from tensorflow_k8s_amd.parallel import tfk_comm
+from tensorflow_k8s_amd.parallel.mwms import MultiWorkerMirroredStrategy
+from tensorflow_k8s_amd.parallel.ps import ParameterServerStrategy
+from tensorflow_k8s_amd.runtime.optimizer import SGD
+from tensorflow_k8s_amd.runtime.trainer import StepRunner
+dev = torch.device("cuda", 0); torch.cuda.set_device(dev)
+comm = tfk_comm.init(dist.HashStore(), 0, 1, dev)
+out = {}
+for mode in ("mwms", "ps_eager", "ps_graph"):
+    m = ResNet(50, stages=[1, 1, 1, 1], num_classes=100).to(dev, seed=7)
+    opt = SGD(m.arena, lr=0.05, momentum=0.9)
+    if mode == "mwms":
+        s = MultiWorkerMirroredStrategy(m.arena, comm=comm, bucket_mb=2.0, comm_dtype="bf16", force=True)
+    else:
+        s = ParameterServerStrategy(m.arena, [0], [0], "sync", transport="rccl", bucket_mb=2.0, comm=comm,
+                                    wire_dtype=torch.bfloat16)
+    s.configure_optimizer(opt)
+    s.broadcast_parameters()
+    x, y = synthetic_imagenet(16, dev, num_classes=100, seed=3)
+    r = StepRunner(m, opt, s, (x, y), use_graph=mode != "ps_eager")
+    for _ in range(6):
+        r.step()
+    torch.cuda.synchronize()
+    out[mode] = {"loss": r.last_loss(), "graph": r.use_graph,
+                 "buckets": len(s.plan.buckets) if mode != "mwms" else len(s.buckets)}
+    torch.save(m.arena.master.cpu(), os.environ["TFK_OUT"] + "." + mode)
+tfk_comm.shutdown()
+print(json.dumps(out))
+"""
+
+
+def test_colocated_collective_ps_matches_forced_mwms(tmp_path):
+    """the collective PS transport on GPU tensors -- bucketed bf16 reduce to the owner,
+    unpack, per-bucket fused optimizer (step_region), broadcast of the bf16 compute copy -- with the
+    owner colocated on worker 0 of a world-size-1 RCCL communicator, eager and hipGraph-captured,
+    tracks forced-comm MWMS over 6 steps within bf16 wire tolerance."""
+    env = dict(os.environ, TFK_ROOT=ROOT, TFK_OUT=str(tmp_path / "w"))
+    r = subprocess.run([sys.executable, "-c", PS_SCRIPT], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    import json
+
+    import torch
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["ps_graph"]["graph"] is True and out["ps_eager"]["graph"] is False and out["ps_eager"]["buckets"] > 3
+    ref = torch.load(str(tmp_path / "w.mwms"), weights_only=True)
+    for mode in ("ps_eager", "ps_graph"):
+        w = torch.load(str(tmp_path / f"w.{mode}"), weights_only=True)
+        rel = (w - ref).norm() / ref.norm()
+        assert rel < 3e-3, (mode, float(rel))
+        assert abs(out[mode]["loss"] - out["mwms"]["loss"]) < 0.05 * abs(out["mwms"]["loss"]), out

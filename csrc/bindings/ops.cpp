@@ -22,7 +22,6 @@ int tfk_gemm_splits(int K, int splits);
 void tfk_gemm_set_persist(int on);
 void tfk_gemm_set_engine(int e);
 void tfk_g4_set_shortk(int on);
-void tfk_g4_set_persist(int on);
 extern "C" void tfk_fp8_set_engine(int e);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_quant_t(const void*, void*, void*, int, int, hipStream_t);
@@ -34,7 +33,6 @@ const unsigned long long* tfk_seed_key();
 void tfk_set_seed_key(const unsigned long long* k);
 int tfk_rng_advance(unsigned long long* st, unsigned long long stream, hipStream_t s);
 void tfk_halo_set(int on);
-void tfk_w128_set(int v);
 void tfk_fp8_set_tile(int t);
 int tfk_bn_finalize(float*, int, int, float, const float*, const float*, float, float, float*, float*, float*, float*,
                     float*, float*, hipStream_t);
@@ -72,7 +70,6 @@ int tfk_stem_fwd_launch(const void*, const void*, void*, float*, int, int, int, 
 int tfk_stem_wgrad_launch(const void*, const void*, float*, int, int, int, int, hipStream_t);
 int tfk_hwgrad_launch(const void*, const void*, float*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int tfk_transpose_arb(const void*, void*, int, int, int, int, hipStream_t);
-int tfk_transpose_group(const void*, int, int, hipStream_t);
 int tfk_transpose_f32(const float*, float*, int, int, hipStream_t);
 int tfk_cast_f32_bf16(const float*, void*, long long, hipStream_t);
 int tfk_cast_bf16_f32(const void*, float*, long long, hipStream_t);
@@ -277,7 +274,6 @@ int64_t gemm_splits(int K, int splits) { return tfk_gemm_splits(K, splits); }
 void gemm_set_persist(int on) { tfk_gemm_set_persist(on); }
 void gemm_set_engine(int e) { tfk_gemm_set_engine(e); }
 void gemm_set_shortk(int on) { tfk_g4_set_shortk(on); }
-void gemm_set_g4_persist(int on) { tfk_g4_set_persist(on); }
 void fp8_set_engine(int e) { tfk_fp8_set_engine(e); }
 
 void mx_probe(torch::Tensor X, torch::Tensor Y, torch::Tensor sx, torch::Tensor sy, torch::Tensor D) {
@@ -700,15 +696,6 @@ void stem_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::optional<t
   }
   check_rc(tfk_stem_fwd_launch(x.data_ptr(), w.data_ptr(), y.data_ptr(), st, shards, N, H, W, cur_stream()), "stem_fwd");
 }
-// Grouped transpose_arb: table int64 [n][6] on the device (in, out, A | R << 32, B | flip << 32,
-// t0 | tb << 32, ta), built and validated by ops/gemm.py FlipTransposeGroup.
-void transpose_group(torch::Tensor table, int64_t n, int64_t total) {
-  need(table, at::kLong, "transpose group table");
-  TORCH_CHECK(table.is_cuda() && table.is_contiguous() && table.numel() == n * 6 && n > 0 && total > 0,
-              "transpose_group: table must be a contiguous device int64 [n][6]");
-  check_rc(tfk_transpose_group(table.data_ptr(), (int)n, (int)total, cur_stream()), "transpose_group");
-}
-
 void transpose_arb(torch::Tensor in, torch::Tensor out, int A, int R, int B, int flip) {
   need_bf16(in, "in"); need_bf16(out, "out");
   need_numel(in, (long long)A * R * B, "in"); need_numel(out, (long long)A * R * B, "out");
@@ -798,7 +785,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_persist", &gemm_set_persist);
   m.def("gemm_set_engine", &gemm_set_engine);
   m.def("gemm_set_shortk", &gemm_set_shortk);
-  m.def("gemm_set_g4_persist", &gemm_set_g4_persist);
   m.def("fp8_set_engine", &fp8_set_engine);
   m.def("mx_quant", &mx_quant);
   m.def("mx_quant_t", &mx_quant_t);
@@ -834,7 +820,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("stem_wgrad", &stem_wgrad);
   m.def("stem_fwd_ok", &stem_fwd_ok);
   m.def("stem_fwd", &stem_fwd);
-  m.def("transpose_group", &transpose_group);
   m.def("transpose_arb", &transpose_arb, py::arg("in"), py::arg("out"), py::arg("A"), py::arg("R"), py::arg("B"),
         py::arg("flip") = 0);
   m.def("transpose_f32", &transpose_f32);
@@ -849,8 +834,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("dropout", &dropout);
   m.def("set_rng_key", &set_rng_key);
   m.def("halo_set", &tfk_halo_set);
-  m.def("w128_set", &tfk_w128_set);
-  m.def("fp8_set_tile", &tfk_fp8_set_tile);  // fp8 g4 tile: 0 by shape, 128 / 256 forced, -1 -> TFK_FP8_TILE  // 0: g4 256x256, 1..4: w128 variant, -1: back to TFK_W128  // 1/0: halo-tile 3x3 conv on/off, -1: back to TFK_HALO
+  m.def("fp8_set_tile", &tfk_fp8_set_tile);  // fp8 g4 tile: 0 by shape, 128 / 256 forced, -1 -> TFK_FP8_TILE
   m.def("rng_advance", &rng_advance);
   m.def("add", &add);
   register_transformer_ops(m);

@@ -138,17 +138,11 @@ void embedding_bwd(torch::Tensor ids, torch::Tensor dy, torch::Tensor dword, c10
     TORCH_CHECK(T >= 1 && T <= 4, "at most 4 token types");
   }
   // row-bucketed word gradient (no f32 atomics): int32 scratch [3 V + ntok] from the caching allocator
-  // (graph-capture safe); TFK_EMB_ATOMIC=1 keeps the scattered-atomic kernel
-  static int atomic_only = -1;
-  if (atomic_only < 0) {
-    const char* e = getenv("TFK_EMB_ATOMIC");
-    atomic_only = (e && e[0] == '1') ? 1 : 0;
-  }
-  torch::Tensor scratch;
-  if (!atomic_only) scratch = torch::empty({3 * (long long)V + ntok}, ids.options());
+  // (graph-capture safe); rows that are not 16-B aligned fall back to the scattered-atomic kernel
+  torch::Tensor scratch = torch::empty({3 * (long long)V + ntok}, ids.options());
   check_rc(tfk_embedding_bwd(ids.data_ptr<int>(), dy.data_ptr(), V, dword.data_ptr<float>(), opt_ptr<float>(dpos),
                              (int)S, opt_ptr<const int>(tt), opt_ptr<float>(dtype), T, ntok, (int)W, (float)scale,
-                             atomic_only ? nullptr : scratch.data_ptr<int>(), cur_stream()),
+                             scratch.data_ptr<int>(), cur_stream()),
            "embedding_bwd");
 }
 

@@ -167,136 +167,6 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
 }
 
 // ---------------------------------------------------------------------------------------------
-// Persistent g4: a resident grid walks the tiles (t = blockIdx.x, += gridDim.x; gridDim.x % 8 == 0
-// keeps each block's tiles on one XCD, so the XCD-contiguous tile order still applies). The next
-// tile's first K-tile is DMA'd into stage 0 while the current tile's epilogue runs in an LDS region
-// placed after stage 0 -- the one-shot kernel's unhidden prologue load and epilogue stores overlap.
-// 128x128: 2 x 32 KiB stages, epilogue image at +32 KiB (36 KiB) -> 68 KiB, still 2 blocks/CU.
-template <int BM, int BN, int AM, int BMD, int EPI>
-__global__ __launch_bounds__((nwaves<BM, BN>() * 64), (occ_default<BM, BN>())) void g4p_kernel(GemmParams p,
-                                                                                              int total_tiles) {
-  constexpr int NW = nwaves<BM, BN>(), NTH = NW * 64, WGM = BM / 64, WGN = BN / 64;
-  constexpr int LBM = BMD == 2 ? CONV_WGRAD : BMD;
-  constexpr bool AKO = (AM == KOUT), BKO = (LBM == KOUT || LBM == CONV_WGRAD);
-  constexpr int WTM = 64, WTN = 64, FM = 4, FN = 4;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int EPIB = epi_lds_bytes<BM, BN, WGM>();
-  constexpr int SMEM = (2 * STAGE > STAGE + EPIB) ? 2 * STAGE : STAGE + EPIB;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w / WGN, wn = w % WGN;
-  const int bz = blockIdx.y;
-  const int tiles_m = (p.M + BM - 1) / BM;
-  constexpr int GM = 4;
-  auto coords = [&](int t, int& m0, int& n0) {
-    const int tile = xcd_remap(t, total_tiles);
-    const int grp = tile / (GM * p.tiles_n), first_m = grp * GM;
-    const int gm = min(GM, tiles_m - first_m), inr = tile - grp * GM * p.tiles_n;
-    m0 = (first_m + inr % gm) * BM;
-    n0 = (inr / gm) * BN;
-  };
-  const int nkt = (p.K + BK - 1) / BK;
-  const int kt0 = blockIdx.z * p.kt_per_split;
-  const int kt1 = min(nkt, kt0 + p.kt_per_split);
-  const long long a_step = AKO ? (long long)BK * p.lda * 2 : BK * 2;
-  const long long b_step = BKO ? (long long)BK * p.ldb * 2 : BK * 2;
-  auto a_base = [&](int m0) -> const char* {
-    if constexpr (AM == CONV_FWD) return (const char*)p.A + (long long)bz * p.sA * 2;
-    else return (const char*)p.A + (long long)bz * p.sA * 2 + (AKO ? (long long)m0 * 2 : (long long)m0 * p.lda * 2);
-  };
-  auto b_base = [&](int n0) -> const char* {
-    return (const char*)p.B + (long long)bz * p.sB * 2 +
-           (LBM == CONV_WGRAD ? 0LL : BKO ? (long long)n0 * 2 : (long long)n0 * p.ldb * 2);
-  };
-  auto stage_ptr = [&](int st) { return smem + st * STAGE; };
-
-  int t = blockIdx.x;
-  int m0, n0;
-  coords(t, m0, n0);
-  const char* Ab = a_base(m0);
-  const char* Bb = b_base(n0);
-  int lim_a = p.M - m0, lim_b = p.N - n0;
-  Loader<BM, AM, NW> la;
-  Loader<BN, LBM, NW> lb;
-  la.init(p, lane, w, p.lda, m0, p.M);
-  lb.init(p, lane, w, p.ldb, n0, p.N);
-  la.issue(p, Ab, a_step, kt0, lim_a, stage_ptr(0), w, lane);
-  lb.issue(p, Bb, b_step, kt0, lim_b, stage_ptr(0) + A_BYTES, w, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  const int ar = wm * WTM, bc = wn * WTN;
-
-#pragma unroll 1
-  while (true) {
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 b0[FN], b1[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) b0[j] = frag<BKO>(stage_ptr(0) + A_BYTES, bc + j * 16, 0);
-#pragma unroll 1
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const int st = (kt - kt0) & 1;
-      const char* As = stage_ptr(st);
-      const char* Bs = As + A_BYTES;
-      const bool more = kt + 1 < kt1;
-      if (more) {
-        char* nx = stage_ptr(st ^ 1);
-        la.issue(p, Ab, a_step, kt + 1, lim_a, nx, w, lane);
-        lb.issue(p, Bb, b_step, kt + 1, lim_b, nx + A_BYTES, w, lane);
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) b1[j] = frag<BKO>(Bs, bc + j * 16, 1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const bf16x8 a = frag<AKO>(As, ar + i * 16, 0);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a, acc[i][j], 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const bf16x8 a = frag<AKO>(As, ar + i * 16, 1);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a, acc[i][j], 0, 0, 0);
-      }
-      if (more) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        const char* Bn = stage_ptr(st ^ 1) + A_BYTES;
-#pragma unroll
-        for (int j = 0; j < FN; ++j) b0[j] = frag<BKO>(Bn, bc + j * 16, 0);
-      }
-    }
-    __syncthreads();  // every wave is done reading both stages
-    const int next = t + gridDim.x;  // block-uniform
-    const int cm0 = m0, cn0 = n0;
-    if (next < total_tiles) {
-      // prefetch the next tile's first K-tile into stage 0 (the epilogue image starts after it)
-      t = next;
-      coords(t, m0, n0);
-      Ab = a_base(m0);
-      Bb = b_base(n0);
-      lim_a = p.M - m0;
-      lim_b = p.N - n0;
-      la.init(p, lane, w, p.lda, m0, p.M);
-      lb.init(p, lane, w, p.ldb, n0, p.N);
-      la.issue(p, Ab, a_step, kt0, lim_a, stage_ptr(0), w, lane);
-      lb.issue(p, Bb, b_step, kt0, lim_b, stage_ptr(0) + A_BYTES, w, lane);
-    }
-    gemm_epilogue<BM, BN, NTH, WGM, EPI, 0, true>(p, acc, smem + STAGE, cm0, cn0, bz);
-    if (next >= total_tiles) break;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // prefetch landed for every wave; the epilogue image is free again
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // MX-fp8 on the g4 engine: A [M][K] and B [N][K] e4m3 bytes (both K-inner), e8m0 scales [rows][K/32].
 // A K-tile is 128 fp8 bytes per row -- byte-for-byte the 128-B row image of a bf16 BK=64 tile, so
 // the LDS-DMA Loader and the XOR-swizzled image are reused unchanged (driven with bf16-equivalent
@@ -458,45 +328,6 @@ extern "C" int tfk_g4_ok(const GemmParams& p, int amode, int bmode) {
     return hipGetLastError() == hipSuccess ? 0 : -2;                                                \
   }
 
-// Persistent launch: grid = resident blocks (occupancy query, cached per instantiation, rounded
-// down to a multiple of 8), only when there are more tiles than that.
-template <int BM_, int BN_, int AM_, int BM2_, int EPI_>
-static int launch_g4p(const GemmParams& p, int tiles, int batch, int splits, hipStream_t stream) {
-  static int resident = 0;
-  if (resident == 0) {
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, g4::g4p_kernel<BM_, BN_, AM_, BM2_, EPI_>,
-                                                     g4::nwaves<BM_, BN_>() * 64, 0) == hipSuccess &&
-        cus > 0 && per_cu > 0)
-      resident = (cus * per_cu) & ~7;
-    else
-      resident = -1;
-  }
-  if (resident < 8 || tiles <= resident) return -1;  // one-shot grid instead
-  hipLaunchKernelGGL((g4::g4p_kernel<BM_, BN_, AM_, BM2_, EPI_>), dim3(resident, batch, splits),
-                     dim3(g4::nwaves<BM_, BN_>() * 64), 0, stream, p, tiles);
-  return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-#define TFK_G4P_CASE(BM_, BN_, AM_, BM2_, EPI_)                                                    \
-  if (bm == BM_ && bn == BN_ && amode == AM_ && bmode == BM2_ && epi == EPI_) {                   \
-    const int r = launch_g4p<BM_, BN_, AM_, BM2_, EPI_>(p, tiles, batch, splits, stream);         \
-    if (r != -1) return r;                                                                        \
-  }
-// 128x128 only: a 256x256 tile's 143 KiB epilogue image cannot sit beside a 64 KiB stage in LDS
-#define TFK_G4P_TILES(AM_, BM2_, EPI_) TFK_G4P_CASE(128, 128, AM_, BM2_, EPI_)
-
-static int g_persist = -1;
-static bool persist_on() {
-  if (g_persist < 0) {
-    const char* e = getenv("TFK_G4_PERSIST");
-    g_persist = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_persist == 1;
-}
-extern "C" void tfk_g4_set_persist(int on) { g_persist = on ? 1 : 0; }
-
 #ifndef G4_SHORTK_DEFAULT_KT
 #define G4_SHORTK_DEFAULT_KT 8  // measured ResNet-50 bs256: 2 -> 27.42, 4 -> 27.04, 8 -> 26.71, 16 -> 26.67 ms
 #endif
@@ -522,8 +353,6 @@ static void fast_div(unsigned d, unsigned* mul, int* shift) {
 
 // p.tiles_n / p.kt_per_split set by the caller (tfk_gemm_launch). Returns -1 if not instantiated.
 extern "C" int tfk_halo_launch(const GemmParams& p, int epi, int batch, int splits, hipStream_t stream);
-extern "C" int tfk_w128_launch(const GemmParams& p, int amode, int bmode, int epi, int tiles, int batch, int splits,
-                               hipStream_t stream);
 
 extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, int bmode, int epi, int batch,
                              int splits, hipStream_t stream) {
@@ -542,23 +371,6 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
   if (amode == 2 && p.Cin < 64) {
     fast_div((unsigned)p.S, &p.fd_q_mul, &p.fd_q_shift);
     fast_div((unsigned)p.Cin, &p.fd_pq_mul, &p.fd_pq_shift);
-  }
-  // dense 256x256: the 1-wave-per-SIMD 128x128-wave-tile engine when selected (gemm_w128.h)
-  if (bm == 256 && bn == 256) {
-    const int r = tfk_w128_launch(p, amode, bmode, epi, tiles, batch, splits, stream);
-    if (r != -1) return r;
-  }
-  // many tiles: the persistent kernel on a resident grid (opt-in TFK_G4_PERSIST=1; measured slower
-  // than the one-shot grid: sq4096 fwd 814 vs 854 TF, tfm_ffn1 772 vs 840, ResNet-50 29.01 vs
-  // 28.81 ms -- its 165-200 VGPRs and the drain before the epilogue's loads eat the overlap)
-  if (persist_on() && p.kt_per_split > 1 && bm == 128 && bn == 128) {
-    TFK_G4P_TILES(0, 0, EPI_BF16)
-    TFK_G4P_TILES(0, 0, EPI_BF16_EXT)
-    TFK_G4P_TILES(0, 1, EPI_BF16)
-    TFK_G4P_TILES(0, 1, EPI_BF16_EXT)
-    TFK_G4P_TILES(0, 1, EPI_BF16_BNR)
-    TFK_G4P_TILES(2, 0, EPI_BF16)
-    TFK_G4P_TILES(2, 0, EPI_BF16_BNR)
   }
   // few K-tiles per block: the 4-blocks-per-CU single-stage instantiations (TFK_G4_SHORTK=0: off;
   // one K-tile measured ResNet-50 bs256: 30.40 -> 29.72 ms/step)
@@ -632,22 +444,9 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
   p.kt_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
   const bool big = g_fp8_tile == 256 || (g_fp8_tile == 0 && p.M >= 256 && p.N >= 256 && t256 * splits >= 240);
-  // 256 x 128 (8 waves, one block per CU): narrow outputs with many rows -- the Transformer's
-  // [tokens, 1024] GEMMs get 256 blocks (one round) with each B column panel shared by 256 A rows
-  // instead of two co-resident 128 x 128 blocks. TFK_FP8_TILE=2561 forces it, =0 picks by shape
-  // (g_fp8_wide: TFK_FP8_WIDE=0 disables the shape rule, for A/B).
-  static int g_fp8_wide = -1;
-  if (g_fp8_wide < 0) {
-    const char* e = getenv("TFK_FP8_WIDE");
-    g_fp8_wide = e ? atoi(e) : 0;  // measured slower on Transformer-big (19.44 vs 18.94 ms): opt-in
-  }
-  const long long t256x128 = (long long)((p.M + 255) / 256) * ((p.N + 127) / 128);
-  const bool wide = !big && (g_fp8_tile == 2561 || (g_fp8_tile == 0 && g_fp8_wide && p.M >= 4096 && p.N >= 128 &&
-                                                     t256x128 * splits >= 240));
   const int T = big ? 256 : 128;
-  const int TM = wide ? 256 : T;
   p.tiles_n = (p.N + T - 1) / T;
-  const int tiles = ((p.M + TM - 1) / TM) * p.tiles_n;
+  const int tiles = ((p.M + T - 1) / T) * p.tiles_n;
   if (p.stats_shards < 1) p.stats_shards = 1;
   const dim3 grid(tiles, 1, splits);
 #define TFK_FP8_G4(BT)                                                                                          \
@@ -664,16 +463,6 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
   }
   if (big) {
     TFK_FP8_G4(256)
-  } else if (wide) {
-    const dim3 block(g4::nwaves<256, 128>() * 64);
-    if (epi == EPI_F32)
-      hipLaunchKernelGGL((g4::g4_fp8_kernel<256, 128, EPI_F32>), grid, block, 0, stream, p, sld);
-    else if (epi == EPI_BF16_EXT)
-      hipLaunchKernelGGL((g4::g4_fp8_kernel<256, 128, EPI_BF16_EXT>), grid, block, 0, stream, p, sld);
-    else if (epi == EPI_BF16_EXT_MX)
-      hipLaunchKernelGGL((g4::g4_fp8_kernel<256, 128, EPI_BF16_EXT_MX>), grid, block, 0, stream, p, sld);
-    else
-      hipLaunchKernelGGL((g4::g4_fp8_kernel<256, 128, EPI_BF16>), grid, block, 0, stream, p, sld);
   } else {
     TFK_FP8_G4(128)
   }

@@ -107,42 +107,6 @@ __global__ void transpose_arb_kernel(const bf16* __restrict__ in, bf16* __restri
   }
 }
 
-// Many transpose_arb's in ONE launch (descriptor table): a ResNet step's flipped 3x3 dgrad weights
-// ([K][RS][C] -> [C][RS'][K]) were 16 latency-bound launches of ~16 us on the critical path. Each
-// block walks (tensor, 32x32 tile, r) work items: t = blockIdx.x, += gridDim.x.
-struct TDesc {
-  const bf16* in;
-  bf16* out;
-  int A, R, B, flip;
-  int t0, tb, ta, pad;  // first work item; tiles along B and A
-};
-__global__ __launch_bounds__(256) void transpose_group_kernel(const TDesc* __restrict__ tab, int n, int total) {
-  __shared__ bf16 tile[32][33];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int t = blockIdx.x; t < total; t += gridDim.x) {
-    int lo = 0, hi = n - 1;  // last descriptor with t0 <= t (block-uniform)
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (tab[mid].t0 <= t) lo = mid; else hi = mid - 1;
-    }
-    const TDesc d = tab[lo];
-    int w = t - d.t0;
-    const int bt = w % d.tb; w /= d.tb;
-    const int at = w % d.ta, r = w / d.ta;
-    const int b0 = bt * 32, a0 = at * 32;
-    __syncthreads();  // the previous item's tile reads are done
-    for (int i = ty; i < 32; i += 8) {
-      const int a = a0 + i, b = b0 + tx;
-      tile[i][tx] = (a < d.A && b < d.B) ? d.in[((long long)a * d.R + r) * d.B + b] : f2bf(0.f);
-    }
-    __syncthreads();
-    for (int i = ty; i < 32; i += 8) {
-      const int b = b0 + i, a = a0 + tx;
-      if (a < d.A && b < d.B) d.out[((long long)b * d.R + (d.flip ? d.R - 1 - r : r)) * d.A + a] = tile[tx][i];
-    }
-  }
-}
-
 // 2D transpose [rows][cols] -> [cols][rows] for f32 (weight layout conversions for checkpoints).
 __global__ void transpose_f32_kernel(const float* __restrict__ in, float* __restrict__ out, int rows, int cols) {
   __shared__ float tile[32][33];
@@ -324,12 +288,6 @@ int tfk_splitk_reduce(const float* slabs, int S, long long stride, long long n, 
 int tfk_transpose_arb(const bf16* in, bf16* out, int A, int R, int B, int flip, hipStream_t s) {
   dim3 grid((B + 31) / 32, (A + 31) / 32, R);
   hipLaunchKernelGGL(transpose_arb_kernel, grid, dim3(NT), 0, s, in, out, A, R, B, flip);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-int tfk_transpose_group(const void* tab, int n, int total, hipStream_t s) {
-  if (n <= 0 || total <= 0) return -1;
-  const int grid = total < 2048 ? total : 2048;
-  hipLaunchKernelGGL(transpose_group_kernel, dim3(grid), dim3(NT), 0, s, (const TDesc*)tab, n, total);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_transpose_f32(const float* in, float* out, int rows, int cols, hipStream_t s) {

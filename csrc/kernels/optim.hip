@@ -63,42 +63,11 @@ __global__ void adamw_kernel(float* __restrict__ w, bf16* __restrict__ wb, const
   }
 }
 
-// Vector form: 4 parameters per lane per iteration (16-B f32 loads/stores, 8-B bf16 shadow store);
-// the update is HBM-bound (~30 B/param), so the wide accesses are what sets its speed.
-// Requires w, g, m, v 16-B aligned and wb 8-B aligned; n4 = n / 4 (the tail runs the scalar kernel).
-__global__ void adamw4_kernel(float* __restrict__ w, bf16* __restrict__ wb, const float* __restrict__ g,
-                              float* __restrict__ m, float* __restrict__ v, long long n4, float lr_h, float b1, float b2,
-                              float eps, float wd, float bc1, float bc2, float gs_host, const float* gs_dev,
-                              const float* hp) {
-  const float gs = gscale_of(gs_host, gs_dev);
-  const float lr = hp_or(hp, 0, lr_h);
-  const float ibc1 = 1.f / hp_or(hp, 1, bc1), ibc2 = 1.f / hp_or(hp, 2, bc2);
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long long)gridDim.x * NT) {
-    const float4 gr4 = ((const float4*)g)[i];
-    float4 m4 = ((float4*)m)[i], v4 = ((float4*)v)[i], w4 = ((float4*)w)[i];
-    float gr[4] = {gr4.x, gr4.y, gr4.z, gr4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w};
-    float vv[4] = {v4.x, v4.y, v4.z, v4.w}, ww[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float gg = gr[e] * gs;
-      mm[e] = b1 * mm[e] + (1.f - b1) * gg;
-      vv[e] = b2 * vv[e] + (1.f - b2) * gg * gg;
-      ww[e] -= lr * ((mm[e] * ibc1) / (sqrtf(vv[e] * ibc2) + eps) + wd * ww[e]);
-    }
-    ((float4*)m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
-    ((float4*)v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-    ((float4*)w)[i] = make_float4(ww[0], ww[1], ww[2], ww[3]);
-    if (wb) {
-      bf16 o[4] = {f2bf(ww[0]), f2bf(ww[1]), f2bf(ww[2]), f2bf(ww[3])};
-      *(uint2*)(wb + 4 * i) = *(const uint2*)o;
-    }
-  }
-}
-
-// AdamW v2: each thread updates TWO float4s per iteration with every load of both issued before
-// any math (8 x 16-B streams in flight per thread), nontemporal (streaming) loads and stores -- the
-// optimizer touches each byte once per step, so it should not evict the GEMM working set from L2 --
-// and a resident grid (8 blocks per CU). Same arithmetic as adamw4_kernel, bit for bit.
+// Vector AdamW: each thread updates TWO float4s per iteration with every load of both issued
+// before any math (8 x 16-B streams in flight per thread; the update is HBM-bound, ~30 B/param),
+// nontemporal (streaming) loads and stores -- the optimizer touches each byte once per step, so it
+// should not evict the GEMM working set from L2 -- and a resident grid (8 blocks per CU). Same
+// arithmetic as the scalar adamw_kernel, bit for bit. Needs w, g, m, v 16-B and wb 8-B aligned.
 __device__ __forceinline__ float4 ntl(const float4* p) {
   float4 r;
   r.x = __builtin_nontemporal_load(&p->x); r.y = __builtin_nontemporal_load(&p->y);
@@ -254,17 +223,8 @@ int tfk_adamw(float* w, bf16* wb, const float* g, float* m, float* v, long long 
   const bool vec = (((uintptr_t)w | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 && (((uintptr_t)wb) & 7) == 0;
   if (vec && n >= 4) {
     const long long n4 = n / 4, done = n4 * 4;
-    static int v2 = -1;
-    if (v2 < 0) {
-      const char* e = getenv("TFK_ADAMW_V2");
-      v2 = e ? atoi(e) : 1;
-    }
-    if (v2)
-      hipLaunchKernelGGL(adamw4x2_kernel, dim3(grid_for(n4, 2048)), dim3(NT), 0, s, w, wb, g, m, v, n4, lr, b1, b2, eps,
-                         wd, bc1, bc2, gs, gs_dev, hp);
-    else
-      hipLaunchKernelGGL(adamw4_kernel, dim3(grid_for(n4)), dim3(NT), 0, s, w, wb, g, m, v, n4, lr, b1, b2, eps, wd, bc1,
-                         bc2, gs, gs_dev, hp);
+    hipLaunchKernelGGL(adamw4x2_kernel, dim3(grid_for(n4, 2048)), dim3(NT), 0, s, w, wb, g, m, v, n4, lr, b1, b2, eps,
+                       wd, bc1, bc2, gs, gs_dev, hp);
     if (done < n)
       hipLaunchKernelGGL(adamw_kernel, dim3(1), dim3(NT), 0, s, w + done, wb ? wb + done : nullptr, g + done, m + done,
                          v + done, n - done, lr, b1, b2, eps, wd, bc1, bc2, gs, gs_dev, hp);

@@ -8,8 +8,6 @@ fc1000) so checkpoints line up with TF-era tooling.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from ..ops import norm as BN
@@ -19,20 +17,12 @@ from ..runtime import streams
 from ..runtime.arena import ParamArena
 from ..runtime.layers import BatchNorm, Conv2d, Linear
 
-# stem BN's backward channel sums inside the max-pool backward (opt-in TFK_FUSE_POOL_BNR=1): measured
-# neutral on MI355X (ResNet-50 bs256, same box: fused 26.71/26.76 ms vs standalone reduce 26.67/26.69) --
-# the gather-form pool backward is latency-bound and absorbs the saved pass in its own time
-FUSE_POOL_BNR = os.environ.get("TFK_FUSE_POOL_BNR", "0") == "1"
 # projection shortcut (forward conv, lattice dgrad) on the side stream (runtime/streams.py)
-SIDE_SHORTCUT = os.environ.get("TFK_SIDE_SHORTCUT", "1") == "1"
+SIDE_SHORTCUT = True
 # the dgrad epilogues that feed a BN backward store dz = dA * relu-mask (BNReduce premask): the
 # BN-backward apply then reads no mask and an identity block's residual gradient is dz itself (no
-# second output pass). TFK_BN_PREMASK=0 restores the unmasked dA + separate dres for A/B.
-PREMASK = os.environ.get("TFK_BN_PREMASK", "1") == "1"
-# opt-in: flipped 3x3 dgrad weights from one grouped transpose at the start of the step instead of
-# per conv right before its dgrad. Measured slower (ResNet-50 bs256 same box: 22.29 vs 22.05 ms/step,
-# profiles/perf_log_r3c.md): the per-conv transposes are not on the critical path after all.
-FLIP_GROUP = os.environ.get("TFK_FLIP_GROUP", "0") == "1"
+# second output pass).
+PREMASK = True
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
 
@@ -189,7 +179,6 @@ class ResNet:
     # ------------------------------------------------------------------ setup
     def to(self, device, seed: int = 1234) -> "ResNet":
         self.arena.finalize(device, seed)
-        self._flip = None
         return self
 
     def batchnorms(self):
@@ -238,22 +227,6 @@ class ResNet:
     def forward_backward(self, x, labels, loss_scale: float = 1.0):
         """One training forward + backward. Returns (loss_sum f32[N] per-row, correct f32[N]).
         Gradients land in arena.grad (mean over the local batch)."""
-        from ..ops import gemm as G
-        # the flipped 3x3 dgrad weights of this step in ONE grouped transpose up front (the first
-        # step records which convs need them); cache scoped to this step
-        flip = getattr(self, "_flip", None)
-        if x.is_cuda and flip is None and FLIP_GROUP:
-            G._FLIP_RECORD = []
-        G._FLIP_ACTIVE = flip.run() if flip is not None else None
-        try:
-            return self._forward_backward(x, labels, loss_scale)
-        finally:
-            G._FLIP_ACTIVE = None
-            if G._FLIP_RECORD:
-                self._flip = G.FlipTransposeGroup(G._FLIP_RECORD)
-            G._FLIP_RECORD = None
-
-    def _forward_backward(self, x, labels, loss_scale: float = 1.0):
         f = self._features(x)
         logits = self.fc.forward(f)
         B = logits.shape[0]
@@ -267,11 +240,9 @@ class ResNet:
         for i in range(nb - 1, -1, -1):
             nxt = self.blocks[i - 1].tail_reduce() if i > 0 else None
             dh = self.blocks[i].backward(dh, dout_reduced=i < nb - 1, next_bnr=nxt)
-        # the stem BN's backward channel sums accumulate inside the max-pool backward
-        fuse = FUSE_POOL_BNR and y0.shape[-1] % 8 == 0 and 256 % (y0.shape[-1] // 8) == 0
-        da0 = PL.maxpool_bwd(dh, idx, a0.shape, 3, 2, 1, bnr=BN.BNReduce(y0, self.bn1.st) if fuse else None)
+        da0 = PL.maxpool_bwd(dh, idx, a0.shape, 3, 2, 1)
         dy0, _, _ = BN.bn_backward(da0, None, y0, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
-                                   self.bn1.beta.grad, y0.numel() // y0.shape[-1], relu_from_y=True, reduced=fuse)
+                                   self.bn1.beta.grad, y0.numel() // y0.shape[-1], relu_from_y=True)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
         self.conv1.backward(dy0, x0, need_dx=False)
         streams.join()  # side-stream weight gradients complete before anyone reads arena.grad

@@ -16,7 +16,6 @@ applied in the FFN2 dgrad epilogue from the saved pre-activation.
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 
 import torch
@@ -36,8 +35,8 @@ def _sink(lin):
 
 
 # fp8 training: LayerNorms and FFN GEMMs that feed only MX-fp8 GEMMs emit those GEMMs' MX operands
-# themselves (ops.fp8 _register_out); TFK_FP8_MX_PRODUCERS=0 quantizes in separate passes instead
-MX_PRODUCERS = os.environ.get("TFK_FP8_MX_PRODUCERS", "1") == "1"
+# themselves (ops.fp8 _register_out) instead of separate quantize passes (measured 19.21 -> 18.86 ms)
+MX_PRODUCERS = True
 
 
 @dataclass

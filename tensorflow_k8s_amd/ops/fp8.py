@@ -358,22 +358,17 @@ def linear_wgrad_mx(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumul
     lib().splitk_reduce(ws, splits, stride, N * K, gw.view(-1), None, accumulate, 1.0)
 
 
-# opt-in: weight gradients whose [N, K] output has >= this many 128x128 tiles run unsplit on 128x128
-# tiles (f32 written once, no slabs + reduce pass). Measured slower on Transformer-big (threshold
-# 128 / 192 / 256: 19.03 / 18.97 / 19.10 ms vs 18.86 ms split-K, profiles/perf_log_r3c.md): off (0)
-import os as _os
-WGRAD_NOSPLIT_TILES = int(_os.environ.get("TFK_FP8_WGRAD_NOSPLIT", "0"))
-# split-K fill target (256x256 blocks; 2x for 128x128) and minimum K-tiles per split (A/B knobs)
-WGRAD_TARGET = int(_os.environ.get("TFK_FP8_WGRAD_TARGET", "256"))
-WGRAD_MIN_KT = int(_os.environ.get("TFK_FP8_WGRAD_MIN_KT", "8"))
+# split-K fill target (256x256 blocks; 2x for 128x128) and minimum K-tiles per split. (Unsplit
+# 128x128 weight gradients were measured slower on Transformer-big -- 19.0 vs 18.86 ms,
+# profiles/perf_log_r3c.md -- and removed.)
+WGRAD_TARGET = 256
+WGRAD_MIN_KT = 8
 
 
 def wgrad_splits(N: int, K: int, M: int) -> int:
     """Split-K slabs of an fp8 weight gradient [N, K] reduced over M tokens: fill ~one round of
     256x256 blocks (two of 128x128 when a side is < 256) with >= 8 K-tiles of 128 per split; the
     count the g4 launcher will actually run (ceil(K-tiles / per-split))."""
-    if WGRAD_NOSPLIT_TILES > 0 and (-(-N // 128)) * (-(-K // 128)) >= WGRAD_NOSPLIT_TILES:
-        return 1
     nkt = M // 128
     big = N >= 256 and K >= 256
     t = (-(-N // 256)) * (-(-K // 256)) if big else (-(-N // 128)) * (-(-K // 128))

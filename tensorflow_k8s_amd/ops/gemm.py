@@ -35,12 +35,10 @@ def act_ref(y: torch.Tensor, act) -> torch.Tensor:
 NO_CONV = [0] * 15
 TARGET_BLOCKS = int(os.environ.get("TFK_TARGET_BLOCKS", 1024))  # split-K fill target: ~4 blocks per CU on 256 CUs
 SPLIT_MIN_KTILES = int(os.environ.get("TFK_SPLIT_MIN_KTILES", 4))  # min 64-deep K tiles per split
-# Split-K for f32 outputs (weight gradients): "slab" (default) = per-split workspace slabs +
-# splitk_reduce (two passes, bitwise deterministic); "atomic" = splits accumulate into the output
-# with f32 atomics from the GEMM epilogue (one pass). Measured on MI355X, ResNet-50 bs256 step:
-# slab 32.1 ms, atomic 39.4 ms -- hundreds of splits hammering one small [K][RSC] gradient from all
-# 8 XCDs serialise on the atomics, far costlier than the extra streaming pass. TFK_SPLITK=atomic.
-SPLITK_ATOMIC = os.environ.get("TFK_SPLITK", "slab") == "atomic"
+# Split-K for f32 outputs (weight gradients): per-split workspace slabs + splitk_reduce (two
+# passes, bitwise deterministic). (f32 atomics from the epilogue were measured slower on MI355X,
+# ResNet-50 bs256 step 39.4 vs 32.1 ms: hundreds of splits hammering one small gradient from all
+# 8 XCDs serialise on the atomics.)
 
 
 @dataclass(frozen=True)
@@ -90,12 +88,12 @@ _G4_TILES = {(256, 256): (256, 0.95), (128, 128): (512, 0.80), (128, 64): (768, 
 # 4-wave 64x256 / 256x64 blocks of the g4 engine for dense weight gradients with a narrow side
 # (rect_ok): the register engine's 64x64 tile ran these at ~300 TF/s (ResNet-50 1x1 wgrads)
 _G4_RECT = {(64, 256): (512, 0.80), (256, 64): (512, 0.80)}
-G4_RECT = os.environ.get("TFK_G4_RECT", "1") == "1"
+G4_RECT = True
 G4_BIG_MIN_K = 512  # one 16-wave block per CU: shorter K cannot amortise its prologue/epilogue
 # 64x256 tile for Cout<=64 conv weight gradients whose B gather changes (r,s) every chunk (C <= 16,
 # i.e. the 7x7 stem on C padded to 8). Measured on MI355X (ResNet-50 bs256, rocprofv3): stem wgrad
 # 673 -> 644 us; the stage-1 3x3 (C=64) got slower on it (236 -> 249 us), so it keeps 64x64.
-WIDE_WGRAD = os.environ.get("TFK_WIDE_WGRAD", "1") == "1"
+WIDE_WGRAD = True
 WIDE_WGRAD_MAX_C = 16
 BIG_TILE_MIN_K = 2048  # register engine: one 8-wave block per CU, needs a long K loop
 G4_ENABLED = os.environ.get("TFK_GEMM_ENGINE", "g4") != "reg"
@@ -178,12 +176,6 @@ def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, 
     ns = int(lib().gemm_splits(K, splits))
     if ns == 1:
         run(out, 1, 0, 1.0 if accumulate else 0.0)
-        return
-    if SPLITK_ATOMIC:
-        # each split adds its partial into `out` with f32 atomics from the GEMM epilogue
-        if not accumulate:
-            out.zero_()
-        run(out, splits, -1, 0.0)
         return
     stride = ((M * N + 3) // 4) * 4
     ws = workspace(device, ns * stride, slot=slot)
@@ -349,8 +341,8 @@ def _conv_tile(kind: str, g: ConvGeom, default, flags=()):
 
 
 # ResNet stem (7x7/s2/p3, RGB padded to 8 channels -> 64) forward on the direct halo kernel
-# (csrc/kernels/conv_stem.hip); TFK_STEM=0 restores the implicit-GEMM gather.
-STEM = os.environ.get("TFK_STEM", "1") == "1"
+# (csrc/kernels/conv_stem.hip).
+STEM = True
 
 
 def stem_fwd_ok(g: ConvGeom, cin_used: int | None) -> bool:
@@ -393,42 +385,6 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
     return y
 
 
-# Flipped dgrad weights of a training step, produced up front by ONE grouped launch
-# (FlipTransposeGroup.run; the model sets _FLIP_ACTIVE for the duration of its step, so a cache can
-# never outlive the weights it was computed from). _FLIP_RECORD collects (w, g) of the convs that
-# needed one, for the model to build its group after the first step.
-_FLIP_ACTIVE: dict | None = None
-_FLIP_RECORD: list | None = None
-
-
-class FlipTransposeGroup:
-    """conv_weight_t(w, g, flip=True) of many convs in one launch (misc.hip transpose_group_kernel):
-    a ResNet-50 step's 16 flipped 3x3 weights were 16 latency-bound launches (~16 us each) on the
-    dgrad critical path. Outputs are allocated once (fixed addresses: graph-capturable)."""
-
-    def __init__(self, items: list):
-        self.items, self.out, rows, t0 = [], [], [], 0
-        seen = set()
-        for w, g in items:
-            if w.data_ptr() in seen:
-                continue
-            seen.add(w.data_ptr())
-            o = torch.empty(g.C, g.R, g.S, g.K, dtype=w.dtype, device=w.device)
-            A, R, B = g.K, g.R * g.S, g.C
-            tb, ta = -(-B // 32), -(-A // 32)
-            rows.append([w.data_ptr(), o.data_ptr(), A | (R << 32), B | (1 << 32), t0 | (tb << 32), ta])
-            t0 += tb * ta * R
-            self.items.append(w)
-            self.out.append(o)
-        self.total = t0
-        self.table = torch.tensor(rows, dtype=torch.int64).to(self.items[0].device) if rows else None
-
-    def run(self) -> dict:
-        if self.table is not None:
-            lib().transpose_group(self.table, len(self.items), self.total)
-        return {w.data_ptr(): o for w, o in zip(self.items, self.out)}
-
-
 def conv_weight_t(w: torch.Tensor, g: ConvGeom, out: torch.Tensor | None = None, flip: bool = False) -> torch.Tensor:
     """OHWI [K][R][S][C] -> [C][R][S][K] (dgrad B operand); flip: taps reversed,
     out[c][r][s][k] = w[k][R-1-r][S-1-s][c] (the stride-1 dgrad as a forward conv)."""
@@ -454,11 +410,11 @@ def dgrad_as_fwd_geom(g: ConvGeom) -> ConvGeom | None:
 
 
 # Stride-1 dgrads go through the LDS-DMA engine's conv-forward gather (its Cin = the conv's Cout
-# must be a multiple of 64) for outputs of >= 128 channels. TFK_DGRAD_AS_FWD=0 restores the
-# register-engine gather (measured ResNet-50 step: 31.13 -> 30.81 ms with it on).
-DGRAD_AS_FWD = os.environ.get("TFK_DGRAD_AS_FWD", "1") == "1"
-# 64-channel dx: the 2-wave 128x64 BN epilogue measured slower (0.28 vs 0.22 ms); TFK_DGRAD_AS_FWD_MIN_C
-DGRAD_AS_FWD_MIN_C = int(os.environ.get("TFK_DGRAD_AS_FWD_MIN_C", 128))
+# must be a multiple of 64) for outputs of >= 128 channels (measured ResNet-50 step: 31.13 -> 30.81
+# ms against the register-engine gather).
+DGRAD_AS_FWD = True
+# 64-channel dx: the 2-wave 128x64 BN epilogue measured slower (0.28 vs 0.22 ms)
+DGRAD_AS_FWD_MIN_C = 128
 # 3x3 / stride-1 / pad-1 convs of ResNet stage 1 (56x56x64) run on the halo-tile direct conv
 # (csrc/kernels/conv_halo.hip; the C++ g4 launcher picks it for these shapes), forward and -- as a
 # forward conv over dY -- dgrad. TFK_HALO=0 restores the implicit-GEMM gather; TFK_HALO=2 also
@@ -475,17 +431,14 @@ def halo_ok(f: ConvGeom) -> bool:
 
 
 # Strided-conv dgrad phases (BN-reduce epilogue with the phase out-map) as forward convs over dY on
-# the LDS-DMA gather (needs the conv's Cout % 64 == 0); TFK_PHASES_AS_FWD=0: register-engine gather.
-PHASES_AS_FWD = os.environ.get("TFK_PHASES_AS_FWD", "1") == "1"
-# scale on the measured (isolated-kernel) split-K counts of conv weight gradients, for A/B under the
-# side-stream overlap (runtime/streams.py), where fewer, larger slabs may pay off
-WGRAD_SPLIT_SCALE = float(os.environ.get("TFK_WGRAD_SPLIT_SCALE", "1.0"))
+# the LDS-DMA gather (needs the conv's Cout % 64 == 0).
+PHASES_AS_FWD = True
 # Non-pointwise weight gradients on the LDS-DMA engine's im2col gather (B_CONV_WGRAD, C % 8 == 0).
-G4_WGRAD = os.environ.get("TFK_G4_WGRAD", "1") == "1"
+G4_WGRAD = True
 # 3x3 / pad-1 / stride-1|2 weight gradients on the halo-tile direct kernel (csrc/kernels/conv_hwgrad.hip:
 # one L2->LDS load of each band's input halo + dY for all nine taps, per-block f32 slabs + one
-# splitk_reduce). TFK_HWGRAD=0 restores the im2col gather on the g4 engine.
-HWGRAD = os.environ.get("TFK_HWGRAD", "1") == "1"
+# splitk_reduce).
+HWGRAD = True
 
 
 def hwgrad_slabs(g: ConvGeom) -> int:
@@ -567,11 +520,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
     if f is not None and g.C < DGRAD_AS_FWD_MIN_C and not halo_ok(f):
         f = None
     if f is not None:
-        wf = _FLIP_ACTIVE.get(w.data_ptr()) if _FLIP_ACTIVE else None
-        if wf is None or tuple(wf.shape) != (g.C, g.R, g.S, g.K):
-            wf = conv_weight_t(w, g, flip=True)  # [C][R][S][K]: the forward conv's OHWI weight
-            if _FLIP_RECORD is not None:
-                _FLIP_RECORD.append((w, g))
+        wf = conv_weight_t(w, g, flip=True)  # [C][R][S][K]: the forward conv's OHWI weight
         Kd = g.R * g.S * g.K
         _gemm(dy, wf, dx, M, g.C, Kd, 0, Kd, g.C, A_CONV_FWD, B_KIN, EPI_BF16,
               _conv_tile("dgrad_fwd", g, lambda: pick_tile(M, g.C, K=Kd, mid_ok=False, g4=True), flags),
@@ -651,8 +600,6 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
     tuned = tuning.wgrad_config(g.K, Nn, Kp) if (g.pointwise and g.K % 8 == 0 and g.C % 8 == 0) else None
     if splits is None and tuned is not None:
         tile, splits = tuned
-        if WGRAD_SPLIT_SCALE != 1.0:
-            splits = max(1, int(round(splits * WGRAD_SPLIT_SCALE)))
     else:
         tile = pick_tile(g.K, Nn, splits_ok=True, big_ok=g.pointwise, K=Kp,
                          wide_ok=WIDE_WGRAD and not g.pointwise and g.C <= WIDE_WGRAD_MAX_C,

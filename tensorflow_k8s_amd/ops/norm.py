@@ -6,17 +6,16 @@ residual add of the same pass (dual form). Backward is reduce -> finalize -> app
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
 from ._lib import lib, on_gpu
 
 # f32 atomic shards of the BN statistics / backward sums (GEMM epilogues spread their per-block
-# partial sums over SHARDS copies; finalize kernels reduce them). TFK_BN_SHARDS overrides. Measured
+# partial sums over SHARDS copies; finalize kernels reduce them). Measured
 # (ResNet-50 bs256 step, same box): 8 -> 25.21, 12 -> 25.33, 16 -> 25.15-25.19, 32 -> 25.25-25.41,
 # 64 -> 25.70 ms -- the finalize kernels sit on the critical path and read every shard
-SHARDS = int(os.environ.get("TFK_BN_SHARDS", "16"))
+SHARDS = 16
 
 
 class BNState:

@@ -33,7 +33,7 @@ MODE = os.environ.get("TFK_CONCURRENT_WGRAD", "auto")
 # side streams used round-robin (each with its own split-K workspace slot): a weight gradient's slab
 # reduce then overlaps the next weight gradient's GEMM. Measured (ResNet-50 bs256, same box):
 # 1 -> 25.64 ms, 2 -> 25.41 ms, 3 -> 25.76 ms
-NSIDE = int(os.environ.get("TFK_WGRAD_STREAMS", "2"))
+NSIDE = 2
 _side: dict[tuple[int, int], torch.cuda.Stream] = {}
 _keep: list[torch.Tensor] = []
 _rr = 0

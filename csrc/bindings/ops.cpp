@@ -81,6 +81,8 @@ int tfk_act_fwd(const void*, const float*, int, void*, long long, int, hipStream
 int tfk_act_bwd(const void*, const void*, void*, long long, int, hipStream_t);
 int tfk_dropout(const void*, void*, long long, float, unsigned long long, hipStream_t);
 int tfk_add(const void*, const void*, void*, long long, float, float, hipStream_t);
+int tfk_gather_rows(const void*, const int*, int, int, int, long long, void*, hipStream_t);
+int tfk_scatter_add_rows(void*, const void*, const int*, int, int, int, int, hipStream_t);
 }
 
 namespace {
@@ -236,7 +238,9 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
                   (bm == 256 && bn == 64 && dense_a && !(amode == A_KOUT && bmode == B_KOUT && epi == 0)) ||
                   (bm == 256 && bn == 64 && amode == A_CONV_FWD && bmode == B_KIN) ||
                   (bm == 64 && bn == 256 && amode == A_KOUT && bmode == B_CONV_WGRAD && epi == 1) ||
-                  (bm == 64 && bn == 256 && amode == A_KOUT && bmode == B_KOUT && epi == 1),
+                  (bm == 64 && bn == 256 && amode == A_KOUT && bmode == B_KOUT && epi == 1) ||
+                  // 8-wave 3-stage g4 tiles (the launcher falls back to 128x128 where g4 declines)
+                  ((bm == 256 && bn == 128) || (bm == 128 && bn == 256)),
               "unsupported tile ", bm, "x", bn, " for operand modes ", amode, "/", bmode);
   // row maps: [om_hp, om_wp, om_h, om_w, om_sh, om_sw, om_a, om_b, rs_h, rs_w, rs_p, rs_q, rs_sh, rs_sw]
   if (!rowmap.empty()) {
@@ -767,6 +771,30 @@ void dropout(torch::Tensor x, torch::Tensor y, double p, int64_t seed) {
   need_bf16(x, "x"); need_bf16(y, "y"); need_numel(y, x.numel(), "y");
   check_rc(tfk_dropout(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (unsigned long long)seed, cur_stream()), "dropout");
 }
+// Head rows of a [B*S][W] activation: row r -> (r / P) * S + pos[r] (pos int32 [B*P]) or the
+// first row of each sequence (pos = None, P = 1).
+void gather_rows(torch::Tensor src, c10::optional<torch::Tensor> pos, int64_t P, int64_t S, torch::Tensor dst) {
+  need_bf16(src, "src"); need_bf16(dst, "dst");
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && src.size(1) == dst.size(1), "gather_rows: [rows][W] operands");
+  const long long n = dst.size(0);
+  TORCH_CHECK(n % P == 0 && (n / P) * S <= src.size(0), "gather_rows: ", n, " rows of ", P, " per sequence exceed src");
+  const int* pp = nullptr;
+  if (pos.has_value() && pos->defined()) { need(*pos, at::kInt, "pos"); need_numel(*pos, n, "pos"); pp = pos->data_ptr<int>(); }
+  else TORCH_CHECK(P == 1, "gather_rows: without pos, one row (the first) per sequence");
+  check_rc(tfk_gather_rows(src.data_ptr(), pp, (int)P, (int)S, (int)src.size(1), n, dst.data_ptr(), cur_stream()), "gather_rows");
+}
+void scatter_add_rows(torch::Tensor dst, torch::Tensor src, c10::optional<torch::Tensor> pos, int64_t P, int64_t S) {
+  need_bf16(src, "src"); need_bf16(dst, "dst");
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && src.size(1) == dst.size(1), "scatter_add_rows: [rows][W] operands");
+  const long long n = src.size(0);
+  TORCH_CHECK(n % P == 0 && (n / P) * S <= dst.size(0), "scatter_add_rows: rows exceed dst");
+  const int* pp = nullptr;
+  if (pos.has_value() && pos->defined()) { need(*pos, at::kInt, "pos"); need_numel(*pos, n, "pos"); pp = pos->data_ptr<int>(); }
+  else TORCH_CHECK(P == 1, "scatter_add_rows: without pos, one row (the first) per sequence");
+  check_rc(tfk_scatter_add_rows(dst.data_ptr(), src.data_ptr(), pp, (int)P, (int)S, (int)src.size(1), (int)(n / P),
+                                cur_stream()), "scatter_add_rows");
+}
+
 void add(torch::Tensor a, torch::Tensor b, torch::Tensor y, double alpha, double beta) {
   need_bf16(a, "a"); need_bf16(b, "b"); need_bf16(y, "y");
   need_numel(b, a.numel(), "b"); need_numel(y, a.numel(), "y");
@@ -837,6 +865,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("fp8_set_tile", &tfk_fp8_set_tile);  // fp8 g4 tile: 0 by shape, 128 / 256 forced, -1 -> TFK_FP8_TILE
   m.def("rng_advance", &rng_advance);
   m.def("add", &add);
+  m.def("gather_rows", &gather_rows);
+  m.def("scatter_add_rows", &scatter_add_rows);
   register_transformer_ops(m);
   register_ckpt_ops(m);
   register_comm_ops(m);

@@ -121,6 +121,8 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
 // 64-bit seed (salt + per-step key) folds once into a 32-bit stream seed; ONE hash32 per group of 4
 // consecutive elements gives 4 mask bytes -- element i is kept iff byte (i & 3) of
 // hash32(s32 ^ (i >> 2)) >= thr = round(256 p), scaled by 256 / (256 - thr) (exactly unbiased).
+// The effective drop rate is thr / 256 (p = 0.1 -> 0.1016); rates 0 < p < 1/512 and p > 255.5/256
+// are not representable and are rejected by the Python layer (ops/elementwise.py check_rate).
 // A hash per element (two quarter-rate multiplies + shifts) was the largest VALU cost of the
 // dropout-carrying GEMM epilogues (ops/elementwise.py dropout_keep is the bit-exact CPU copy).
 __device__ __forceinline__ uint32_t drop_seed32(unsigned long long s) {

@@ -11,6 +11,11 @@
 //   s_waitcnt vmcnt(0) lgkmcnt(0); barrier               (tile t+1 landed; every read of s retired)
 //   read the k-half-0 fragments of tile t+1 from stage s^1
 // so HBM/L2 latency hides under one K-tile of MFMAs and each K-tile costs one barrier.
+// NST = 3 (one-block-per-CU 8-wave 256x128 / 128x256 tiles, 3 x 48 KiB stages): K-tile t+2 is
+// issued at the top of tile t into the stage tile t-1 vacated (its reads retired before the
+// barrier that closed t-1), and the end-of-tile wait is the COUNTED s_waitcnt vmcnt(LNI) -- tile
+// t+1 landed, tile t+2's LNI DMA instructions per lane still in flight across the raw s_barrier --
+// so two K-tiles of MFMAs cover each DMA (cdna_hip_programming.md §5 "Pipelining across barriers").
 //
 // Operand images (cdna_hip_programming.md §2 T2 / T10; one __shared__ array):
 //   K-inner [rows][64 k] bf16, 128-B rows, chunk c of row r at r*128 + ((c ^ (r>>1 & 7)) << 4)
@@ -49,7 +54,7 @@ constexpr int nwaves() { return (BM / 64) * (BN / 64); }
 template <int BM, int BN>
 constexpr int occ_default() { return (BM * BN <= 128 * 128) ? 2 : 1; }
 
-template <int BM, int BN, int AM, int BMD, int EPI, int OCC = occ_default<BM, BN>()>
+template <int BM, int BN, int AM, int BMD, int EPI, int OCC = occ_default<BM, BN>(), int NST = 2>
 __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmParams p) {
   constexpr int NW = nwaves<BM, BN>(), NTH = NW * 64, WGM = BM / 64, WGN = BN / 64;
   constexpr int LBM = BMD == 2 ? CONV_WGRAD : BMD;  // B_CONV_WGRAD (= 2 in the B-mode numbering)
@@ -59,7 +64,8 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
   // SHORTK: one LDS stage, no intra-block double buffering (the host launches it for blocks of
   // <= g_shortk K-tiles); co-resident blocks hide the DMA latency instead
   constexpr bool SHORTK = OCC > occ_default<BM, BN>();
-  constexpr int MAIN = (SHORTK ? 1 : 2) * STAGE, EPIB = epi_lds_bytes<BM, BN, WGM>();
+  static_assert(NST == 2 || (NST == 3 && !SHORTK), "stages: 2, or 3 without SHORTK");
+  constexpr int MAIN = (SHORTK ? 1 : NST) * STAGE, EPIB = epi_lds_bytes<BM, BN, WGM>();
   __shared__ __attribute__((aligned(16))) char smem[MAIN > EPIB ? MAIN : EPIB];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -101,9 +107,22 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
 
   auto stage_ptr = [&](int s) { return smem + s * STAGE; };
 
+  // DMA instructions per lane per K-tile (the counted wait of the 3-stage pipeline)
+  constexpr int LNI = Loader<BM, AM, NW, !SHORTK>::NI + Loader<BN, LBM, NW>::NI;
+  static_assert(LNI <= 60, "vmcnt field");
   la.issue(p, Ab, a_step, kt0, lim_a, stage_ptr(0), w, lane);
   lb.issue(p, Bb, b_step, kt0, lim_b, stage_ptr(0) + A_BYTES, w, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (NST == 3) {
+    if (kt0 + 1 < kt1) {
+      la.issue(p, Ab, a_step, kt0 + 1, lim_a, stage_ptr(1), w, lane);
+      lb.issue(p, Bb, b_step, kt0 + 1, lim_b, stage_ptr(1) + A_BYTES, w, lane);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LNI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
@@ -118,13 +137,20 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
     for (int j = 0; j < FN; ++j) b0[j] = frag<BKO>(As + A_BYTES, bc + j * 16, 0);
   }
 
+  int s3 = 0;  // NST = 3: stage of tile kt (kt - kt0) % 3, carried without a division
 #pragma unroll 1
   for (int kt = kt0; kt < kt1; ++kt) {
-    const int s = SHORTK ? 0 : (kt - kt0) & 1;
+    const int s = NST == 3 ? s3 : SHORTK ? 0 : (kt - kt0) & 1;
     const char* As = stage_ptr(s);
     const char* Bs = As + A_BYTES;
     const bool more = kt + 1 < kt1;
-    if (!SHORTK && more) {
+    if constexpr (NST == 3) {
+      if (kt + 2 < kt1) {
+        char* nx = stage_ptr(s == 0 ? 2 : s - 1);  // = (s + 2) % 3: tile kt-1's stage
+        la.issue(p, Ab, a_step, kt + 2, lim_a, nx, w, lane);
+        lb.issue(p, Bb, b_step, kt + 2, lim_b, nx + A_BYTES, w, lane);
+      }
+    } else if (!SHORTK && more) {
       char* nx = stage_ptr(s ^ 1);
       la.issue(p, Ab, a_step, kt + 1, lim_a, nx, w, lane);
       lb.issue(p, Bb, b_step, kt + 1, lim_b, nx + A_BYTES, w, lane);
@@ -152,10 +178,21 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
         la.issue(p, Ab, a_step, kt + 1, lim_a, stage_ptr(0), w, lane);
         lb.issue(p, Bb, b_step, kt + 1, lim_b, stage_ptr(0) + A_BYTES, w, lane);
       }
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      int nxs;
+      if constexpr (NST == 3) {
+        nxs = s == 2 ? 0 : s + 1;
+        s3 = nxs;
+        if (kt + 2 < kt1)
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(LNI) : "memory");  // tile kt+1 landed
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      } else {
+        nxs = SHORTK ? 0 : s ^ 1;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      const char* Bn = stage_ptr(SHORTK ? 0 : s ^ 1) + A_BYTES;
+      const char* Bn = stage_ptr(nxs) + A_BYTES;
 #pragma unroll
       for (int j = 0; j < FN; ++j) b0[j] = frag<BKO>(Bn, bc + j * 16, 0);
     }
@@ -321,6 +358,15 @@ extern "C" int tfk_g4_ok(const GemmParams& p, int amode, int bmode) {
 // 2-wave tiles for 64-wide operands (Cout = 64 weight gradients, 64-channel dgrads)
 #define TFK_G4_NARROW(AM_, BM2_, EPI_) TFK_G4_CASE(128, 64, AM_, BM2_, EPI_) TFK_G4_CASE(64, 128, AM_, BM2_, EPI_)
 
+// 8-wave one-block-per-CU tiles with the 3-stage LDS ring (NST = 3)
+#define TFK_G4_DEEP_CASE(BM_, BN_, AM_, BM2_, EPI_)                                                  \
+  if (bm == BM_ && bn == BN_ && amode == AM_ && bmode == BM2_ && epi == EPI_) {                     \
+    hipLaunchKernelGGL((g4::g4_kernel<BM_, BN_, AM_, BM2_, EPI_, 1, 3>), dim3(tiles, batch, splits),  \
+                       dim3(g4::nwaves<BM_, BN_>() * 64), 0, stream, p);                            \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                                \
+  }
+#define TFK_G4_DEEP(AM_, BM2_, EPI_) TFK_G4_DEEP_CASE(256, 128, AM_, BM2_, EPI_) TFK_G4_DEEP_CASE(128, 256, AM_, BM2_, EPI_)
+
 #define TFK_G4_SHORTK(AM_, BM2_, EPI_)                                                               \
   if (amode == AM_ && bmode == BM2_ && epi == EPI_) {                                               \
     hipLaunchKernelGGL((g4::g4_kernel<128, 128, AM_, BM2_, EPI_, 4>), dim3(tiles, batch, splits),    \
@@ -381,6 +427,15 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
     TFK_G4_SHORTK(2, 0, EPI_BF16)
     TFK_G4_SHORTK(2, 0, EPI_BF16_BNR)
   }
+  TFK_G4_DEEP(0, 0, EPI_BF16)
+  TFK_G4_DEEP(0, 0, EPI_BF16_EXT)
+  TFK_G4_DEEP(0, 1, EPI_BF16)
+  TFK_G4_DEEP(0, 1, EPI_BF16_EXT)
+  TFK_G4_DEEP(0, 1, EPI_BF16_BNR)
+  TFK_G4_DEEP(1, 1, EPI_F32)
+  TFK_G4_DEEP(2, 0, EPI_BF16)
+  TFK_G4_DEEP(2, 0, EPI_BF16_BNR)
+  TFK_G4_DEEP(1, 2, EPI_F32)
   TFK_G4_TILES(0, 0, EPI_BF16)
   TFK_G4_TILES(0, 0, EPI_F32)
   TFK_G4_TILES(0, 0, EPI_BF16_EXT)

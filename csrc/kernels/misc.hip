@@ -263,9 +263,54 @@ __global__ void add_kernel(const bf16* __restrict__ a, const bf16* __restrict__ 
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
     y[i] = f2bf(alpha * bf2f(a[i]) + beta * bf2f(b[i]));
 }
+
+// Row gather / scatter-add of BERT's prediction heads (the MLM positions and the [CLS] rows of a
+// [B*S][W] activation): GEMM-row r of the head is activation row (r / P) * S + (pos ? pos[r] : 0).
+// One 16-B chunk (8 bf16) per lane, rows of W % 8 == 0.
+__global__ void gather_rows_kernel(const bf16* __restrict__ src, const int* __restrict__ pos, int P, int S, int W,
+                                   long long n_rows, bf16* __restrict__ dst) {
+  const int cpr = W / 8;
+  const long long total = n_rows * cpr;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const long long r = i / cpr;
+    const int c = (int)(i - r * cpr);
+    const long long b = r / P;
+    const long long row = b * S + (pos ? pos[r] : 0);
+    *(bf16x8*)(dst + r * W + c * 8) = *(const bf16x8*)(src + row * W + c * 8);
+  }
+}
+// dst[row(r)] += src[r] in f32, rounded to bf16. Block b owns sequence b: its P rows are added one
+// after the other (barrier between), so repeated positions inside a sequence accumulate correctly
+// and no two blocks ever touch the same destination row (no atomics).
+__global__ void scatter_add_rows_kernel(bf16* __restrict__ dst, const bf16* __restrict__ src, const int* __restrict__ pos,
+                                        int P, int S, int W) {
+  const long long b = blockIdx.x;
+  for (int q = 0; q < P; ++q) {
+    const long long r = b * P + q;
+    const long long row = b * S + (pos ? pos[r] : 0);
+    for (int c = threadIdx.x; c < W / 8; c += NT) {
+      bf16x8 d = *(const bf16x8*)(dst + row * W + c * 8);
+      const bf16x8 v = *(const bf16x8*)(src + r * W + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = f2bf(bf2f(d[e]) + bf2f(v[e]));
+      *(bf16x8*)(dst + row * W + c * 8) = d;
+    }
+    __syncthreads();  // the next position of this sequence may be the same row
+  }
+}
 }  // namespace
 
 extern "C" {
+int tfk_gather_rows(const bf16* src, const int* pos, int P, int S, int W, long long n_rows, bf16* dst, hipStream_t s) {
+  if (W % 8 || P < 1 || (((uintptr_t)src | (uintptr_t)dst) & 15)) return -1;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(n_rows * (W / 8))), dim3(NT), 0, s, src, pos, P, S, W, n_rows, dst);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int tfk_scatter_add_rows(bf16* dst, const bf16* src, const int* pos, int P, int S, int W, int B, hipStream_t s) {
+  if (W % 8 || P < 1 || B < 1 || (((uintptr_t)src | (uintptr_t)dst) & 15)) return -1;
+  hipLaunchKernelGGL(scatter_add_rows_kernel, dim3(B), dim3(NT), 0, s, dst, src, pos, P, S, W);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 int tfk_splitk_reduce(const float* slabs, int S, long long stride, long long n, float* out, bf16* outb, int accumulate,
                       float alpha, hipStream_t s) {
   if (S < 1 || n < 1) return 0;

@@ -49,6 +49,11 @@ class BertConfig:
     # on MI355X, base bs64x128: 512 -> 15.44 ms/step vs 16.17 at 1024 (profiles/splitk_sweep_*).
     wgrad_split_target: int | None = 512
 
+    def __post_init__(self):
+        from ..ops.elementwise import check_rate
+        check_rate(self.hidden_dropout)  # representable by the kernels' 8-bit mask threshold
+        check_rate(self.attn_dropout)
+
     @classmethod
     def base(cls):
         return cls()
@@ -192,19 +197,16 @@ class BertForPreTraining:
         return h, (e, st, hd, s_emb)
 
     def _heads(self, h, B, S, mlm_pos):
-        P = mlm_pos.shape[1]
-        rows = (mlm_pos.long() + torch.arange(B, device=h.device)[:, None] * S).reshape(-1)
-        hm = h.index_select(0, rows)
+        hm = TR.gather_rows(h, mlm_pos, S)  # the MLM positions' rows (HIP gather)
         zt = torch.empty_like(hm)
         t = self.mlm_dense.forward(hm, act="gelu", aux=zt)
         tl, stt = self.mlm_ln.forward(t)
         logits = G.linear_fwd(tl, self.word.table.compute, self.mlm_bias.master)  # tied decoder
-        cls_rows = torch.arange(B, device=h.device) * S
-        hc = h.index_select(0, cls_rows)
+        hc = TR.gather_rows(h, None, S)  # the [CLS] rows
         zp = torch.empty(B, self.cfg.hidden, dtype=torch.bfloat16, device=h.device)
         pooled = self.pooler.forward(hc, act="tanh", aux=zp)
         nsp_logits = self.nsp.forward(pooled)
-        return logits, nsp_logits, (rows, hm, zt, t, tl, stt, cls_rows, hc, zp, pooled)
+        return logits, nsp_logits, (mlm_pos, hm, zt, t, tl, stt, None, hc, zp, pooled)
 
     def forward_backward(self, ids, tt, mlm_pos, mlm_ids, nsp_labels, loss_scale: float = 1.0):
         """One training step's forward + backward (see _forward_backward). The no-decay gradients
@@ -221,6 +223,9 @@ class BertForPreTraining:
                 return self._forward_backward(ids, tt, mlm_pos, mlm_ids, nsp_labels, loss_scale)
         finally:
             self.arena.prezeroed = False
+            if self.cfg.fp8:
+                from ..ops.fp8 import clear_saved
+                clear_saved()  # nothing quantized in this step may leak into a later forward
 
     def _forward_backward(self, ids, tt, mlm_pos, mlm_ids, nsp_labels, loss_scale: float = 1.0):
         """One pretraining step's forward + backward. Returns (loss f32 [B], mlm-correct f32 [B*P])."""
@@ -249,8 +254,8 @@ class BertForPreTraining:
         dzp = E.act_bwd(dpooled, zp, "tanh")
         dhc = self.pooler.backward(dzp, hc)
         dh = torch.zeros_like(h)
-        dh.index_add_(0, rows, dhm)
-        dh.index_add_(0, cls_rows, dhc)
+        TR.scatter_add_rows(dh, dhm, rows, S)  # rows = the MLM positions
+        TR.scatter_add_rows(dh, dhc, None, S)  # the [CLS] rows
         # ---- encoder backward
         for layer in reversed(self.layers):
             dh = layer.backward(dh)

@@ -57,6 +57,11 @@ class TransformerConfig:
     max_len: int = 1024
     fp8: bool = False  # all linear GEMMs (fwd, dgrad, wgrad) in MX-fp8 (e4m3 + e8m0 block scales)
 
+    def __post_init__(self):
+        from ..ops.elementwise import check_rate
+        for k in ("dropout", "attn_dropout", "relu_dropout"):
+            check_rate(getattr(self, k))  # representable by the kernels' 8-bit mask threshold
+
     @classmethod
     def big(cls):
         return cls()
@@ -324,6 +329,9 @@ class Transformer:
                 return self._forward_backward(src, tgt_in, tgt_out, src_len, loss_scale)
         finally:
             self.arena.prezeroed = False
+            if self.cfg.fp8:
+                from ..ops.fp8 import clear_saved
+                clear_saved()  # nothing quantized in this step may leak into a later forward
 
     def _forward_backward(self, src, tgt_in, tgt_out, src_len, loss_scale: float = 1.0):
         cfg = self.cfg

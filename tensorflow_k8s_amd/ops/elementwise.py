@@ -108,6 +108,27 @@ def drop_thr8(p: float) -> int:
     return max(0, min(255, t))
 
 
+def check_rate(p: float) -> float:
+    """Dropout rates the 8-bit mask threshold represents: the kernels drop an element iff a hash
+    byte < thr = round(256 p), so the EFFECTIVE rate is thr / 256 (p = 0.1 runs at 0.1016,
+    p = 0.3 at 0.3008; the 256 / (256 - thr) keep scale keeps it unbiased). Rejected: 0 < p < 1/512
+    (thr = 0: nothing would be dropped) and p > 255.5/256 (thr caps at 255: 1/256 of the elements
+    would survive, scaled by 256, instead of all being dropped). Returns p."""
+    p = float(p)
+    if p < 0.0 or p >= 1.0:
+        raise ValueError(f"dropout rate must be in [0, 1), got {p}")
+    if p > 0.0 and drop_thr8(p) == 0:
+        raise ValueError(f"dropout rate {p} < 1/512 rounds to no dropout in the 8-bit mask; use 0 or >= 1/512")
+    if p > 255.5 / 256.0:
+        raise ValueError(f"dropout rate {p} > 255.5/256 is not representable by the 8-bit mask")
+    return p
+
+
+def effective_rate(p: float) -> float:
+    """The drop probability the kernels actually apply for nominal rate p (thr / 256)."""
+    return drop_thr8(p) / 256.0
+
+
 def keep_scale(p: float) -> float:
     """Inverse keep probability of the quantized mask, 256 / (256 - thr) (common.h drop_scale8)."""
     import numpy as np
@@ -144,6 +165,7 @@ def dropout(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
     """Inverted dropout; the mask is a hash of (seed, index), so backward = dropout(dy, p, seed)."""
     if p <= 0.0:
         return x
+    check_rate(p)
     if not on_gpu(x):
         keep = dropout_keep(eff_seed(seed), x.numel(), p).reshape(x.shape)
         return (x.float() * keep * keep_scale(p)).to(torch.bfloat16)

@@ -185,7 +185,9 @@ def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = 
     if K % 128:
         raise ValueError(f"MX-fp8 GEMM needs K % 128 == 0, got {K}")
     dg_ok, wg_ok = mx_backward_ok(M, N, K)
-    if wq is None:
+    if wq is None and save:
+        # this step's pre-quantized weights are valid only inside the training step that quantized
+        # them (an evaluation forward after the optimizer update must not see last step's MX(w))
         e = _WQ.get(w.data_ptr())
         if e is not None and e[1] == tuple(w.shape):
             wq = e[2][0]

@@ -164,6 +164,39 @@ def embedding_bwd(ids, dy, dword, dpos=None, seq_len: int = 1, type_ids=None, dt
 
 # ----------------------------------------------------------------------------- attention
 
+def gather_rows(src: torch.Tensor, pos: torch.Tensor | None, S: int) -> torch.Tensor:
+    """Prediction-head rows of a [B*S, W] activation: row (r // P) * S + pos[b, r % P] for pos int32
+    [B, P] (BERT's MLM positions), or the first row of every sequence (pos None: the [CLS] rows)."""
+    W = src.shape[-1]
+    src2 = src.reshape(-1, W)
+    B = src2.shape[0] // S
+    P = pos.shape[-1] if pos is not None else 1
+    if not on_gpu(src):
+        rows = torch.arange(B, device=src.device)[:, None] * S
+        rows = (rows + pos.long().reshape(B, P)) if pos is not None else rows
+        return src2.index_select(0, rows.reshape(-1))
+    out = torch.empty(B * P, W, dtype=src.dtype, device=src.device)
+    lib().gather_rows(src2, pos.reshape(-1) if pos is not None else None, P, S, out)
+    return out
+
+
+def scatter_add_rows(dst: torch.Tensor, src: torch.Tensor, pos: torch.Tensor | None, S: int) -> None:
+    """dst[(r // P) * S + pos[b, r % P]] += src[r] (the backward of gather_rows; repeated positions
+    inside a sequence accumulate). dst [B*S, W] bf16, summed in f32 per add."""
+    W = src.shape[-1]
+    dst2 = dst.reshape(-1, W)
+    P = pos.shape[-1] if pos is not None else 1
+    B = src.shape[0] // P
+    if not on_gpu(dst):
+        rows = torch.arange(B, device=dst.device)[:, None] * S
+        rows = (rows + pos.long().reshape(B, P)) if pos is not None else rows
+        acc = dst2.float()
+        acc.index_add_(0, rows.reshape(-1), src.reshape(-1, W).float())
+        dst2.copy_(acc.to(dst.dtype))
+        return
+    lib().scatter_add_rows(dst2, src.reshape(-1, W), pos.reshape(-1) if pos is not None else None, P, S)
+
+
 def _hash32(x: torch.Tensor) -> torch.Tensor:
     """Bit-exact torch (int64 holding uint32) copy of common.h hash32 (lowbias32)."""
     m = 0xFFFFFFFF

@@ -593,72 +593,6 @@ def test_shortk_single_stage_blocks(shape):
         assert rel(res[8][i], res[0][i]) < 1e-4, i
 
 
-@pytest.mark.parametrize("case", ["fwd_relu", "dgrad_resid", "ext_gelu_drop", "conv_stats", "bnr_dgrad"])
-def test_g4_persistent_matches_one_shot(case):
-    """The persistent g4 kernel (resident grid walking > 512 tiles of 128x128, next tile's first
-    K-tile prefetched during the epilogue) computes every tile exactly like the one-shot grid."""
-    L = lib()
-    M, N, K = 70000, 256, 320  # 547 x 2 = 1094 tiles > resident blocks; K=320: 5 K-tiles
-    x, w = bf(M, K, seed=1).cuda(), bf(N, K, scale=0.05, seed=2).cuda()
-    dy, r = bf(M, N, seed=3).cuda(), bf(M, K, seed=4).cuda()
-    t = (128, 128)
-
-    def run():
-        if case == "fwd_relu":
-            y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-            G._gemm(x, w, y, M, N, K, K, K, N, G.A_KIN, G.B_KIN, G.EPI_BF16, t, act=1)
-            return (y,)
-        if case == "dgrad_resid":
-            dx = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
-            G._gemm(dy, w, dx, M, K, N, N, K, K, G.A_KIN, G.B_KOUT, G.EPI_BF16, t, resid=r)
-            return (dx,)
-        if case == "ext_gelu_drop":
-            y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-            z = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-            G._gemm(x, w, y, M, N, K, K, K, N, G.A_KIN, G.B_KIN, G.EPI_BF16, t, act=2, aux=z, drop_p=0.1, drop_seed=9)
-            return (y, z)
-        if case == "conv_stats":
-            g = G.ConvGeom(16, 40, 40, 64, 256, 3, 3, 1, 1, 1, 1)
-            xc = bf(16, 40, 40, 64, seed=5).cuda()
-            wc = bf(256, 3, 3, 64, scale=0.05, seed=6).cuda()
-            st = torch.zeros(8 * 2 * 256, device=DEV)
-            G.FORCE_TILE = t
-            try:
-                y = G.conv_fwd(xc, wc, g, st, 8)
-            finally:
-                G.FORCE_TILE = None
-            return (y, st.view(8, 2, 256).sum(0))
-        st = BN.BNState(K, DEV)
-        gen = torch.Generator().manual_seed(11)  # identical statistics in both runs
-        st.mean.copy_(torch.rand(K, generator=gen) * 0.2 - 0.1)
-        st.invstd.copy_(torch.rand(K, generator=gen) + 0.5)
-        y2, a2 = bf(M, K, seed=7).cuda(), bf(M, K, seed=8).cuda()
-        spec = BN.BNReduce(y2.view(M, 1, 1, K), st, a=a2.view(M, 1, 1, K))
-        g = G.ConvGeom(M, 1, 1, K, N, 1, 1)
-        G.FORCE_TILE = t
-        try:
-            dx = G.conv_dgrad(dy.view(M, 1, 1, N), w.view(N, 1, 1, K), g, resid=r.view(M, 1, 1, K), bnr=spec)
-        finally:
-            G.FORCE_TILE = None
-        return (dx, st.sums.view(st.shards, 3, K).sum(0))
-
-    res = {}
-    try:
-        for flag in (0, 1):
-            L.gemm_set_g4_persist(flag)
-            res[flag] = [v.clone() for v in run()]
-            torch.cuda.synchronize()
-    finally:
-        L.gemm_set_g4_persist(0)
-    a, b = res[1], res[0]
-    assert torch.equal(a[0], b[0]), case
-    for u, v in zip(a[1:], b[1:]):
-        if u.dtype == torch.bfloat16:
-            assert torch.equal(u, v), case
-        else:
-            assert rel(u, v) < 1e-5, case
-
-
 @pytest.mark.parametrize("S,n", [(1, 1000), (3, 4096), (8, 1048576), (256, 16384), (126, 65536), (502, 4100), (5, 1001),
                                  (7, 2359296)])
 @pytest.mark.parametrize("acc", [False, True])

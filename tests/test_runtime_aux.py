@@ -105,3 +105,21 @@ def test_tracer_disabled_is_noop(tmp_path):
     with tr.span("x"):
         pass
     assert tr.events == []
+
+
+def test_dropout_rate_quantization_is_validated():
+    """the kernels' 8-bit mask threshold applies round(256 p) / 256; unrepresentable
+    rates are rejected instead of silently changing meaning."""
+    import pytest
+    from tensorflow_k8s_amd.models.bert import BertConfig
+    from tensorflow_k8s_amd.models.transformer import TransformerConfig
+    from tensorflow_k8s_amd.ops.elementwise import check_rate, effective_rate
+    assert abs(effective_rate(0.1) - 26 / 256) < 1e-12 and check_rate(0.1) == 0.1
+    assert effective_rate(0.0) == 0.0 and check_rate(0.0) == 0.0
+    for bad in (1e-4, 0.999, 1.0, -0.1):
+        with pytest.raises(ValueError):
+            check_rate(bad)
+    with pytest.raises(ValueError):
+        TransformerConfig(dropout=0.9995)
+    with pytest.raises(ValueError):
+        BertConfig(attn_dropout=1e-3)

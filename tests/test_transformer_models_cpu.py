@@ -99,6 +99,13 @@ def test_transformer_fp8_mx_producers_match_separate_quantization():
     import tensorflow_k8s_amd.models.transformer as TM
     from tensorflow_k8s_amd.ops import fp8 as F8
     res = {}
+    orig = F8.clear_saved
+    seen = []
+
+    def clear_and_count():  # the step clears its caches on exit: count the MX registrations first
+        seen.append(len(F8._XQ))
+        orig()
+    F8.clear_saved = clear_and_count
     for prod in (False, True):
         TM.MX_PRODUCERS = prod
         try:
@@ -106,10 +113,13 @@ def test_transformer_fp8_mx_producers_match_separate_quantization():
                                        src_len=64, tgt_len=64, max_len=128, dropout=0.1, attn_dropout=0.1,
                                        relu_dropout=0.1, fp8=True)
             m = TM.Transformer(cfg).to("cpu", seed=4)
+            seen.clear()
             loss, _ = m.forward_backward(*m.synthetic_batch(2, "cpu", seed=1))
-            res[prod] = (loss.clone(), m.arena.grad.clone(), len(F8._XQ))
+            res[prod] = (loss.clone(), m.arena.grad.clone(), max(seen))
         finally:
             TM.MX_PRODUCERS = True
+            F8.clear_saved = orig if prod else clear_and_count
+    assert not F8._XQ and not F8._SAVED and not F8._WQ  # nothing survives the step
     assert res[True][2] > res[False][2]  # producers registered their MX outputs
     assert torch.equal(res[True][0], res[False][0])
     assert torch.equal(res[True][1], res[False][1])

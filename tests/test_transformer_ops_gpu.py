@@ -166,3 +166,27 @@ def test_linear_gelu_aux_and_dact():
         out[dev] = dict(a=a, z=z, dz=dz, ad=ad, th=th)
     for k in out["cpu"]:
         assert rel(out[DEV][k], out["cpu"][k]) < 1e-2, k
+
+
+def test_head_row_gather_scatter_match_index_ops():
+    """BERT's prediction-head rows (misc.hip gather_rows / scatter_add_rows) against torch's
+    index_select / index_add_ in f32: MLM positions (with a repeated position inside a sequence, which
+    must accumulate) and the [CLS] rows."""
+    B, S, W, P = 6, 40, 768, 7
+    g = torch.Generator().manual_seed(5)
+    h = torch.randn(B * S, W, generator=g).to(torch.bfloat16)
+    pos = torch.randint(1, S, (B, P), generator=g, dtype=torch.int32)
+    pos[2, 3] = pos[2, 1]  # repeated position
+    rows = (torch.arange(B)[:, None] * S + pos.long()).reshape(-1)
+    got = T.gather_rows(h.to(DEV), pos.to(DEV), S)
+    assert torch.equal(got.cpu(), h.index_select(0, rows))
+    assert torch.equal(T.gather_rows(h.to(DEV), None, S).cpu(), h.index_select(0, torch.arange(B) * S))
+    dm = torch.randn(B * P, W, generator=g).to(torch.bfloat16)
+    dc = torch.randn(B, W, generator=g).to(torch.bfloat16)
+    dh = torch.zeros(B * S, W, dtype=torch.bfloat16, device=DEV)
+    T.scatter_add_rows(dh, dm.to(DEV), pos.to(DEV), S)
+    T.scatter_add_rows(dh, dc.to(DEV), None, S)
+    ref = torch.zeros(B * S, W)
+    ref.index_add_(0, rows, dm.float())
+    ref.index_add_(0, torch.arange(B) * S, dc.float())
+    assert rel(dh.cpu().float(), ref) < 5e-3

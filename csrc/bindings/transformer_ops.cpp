@@ -14,7 +14,9 @@ int tfk_layernorm_fwd(const void*, const float*, const float*, void*, float*, fl
 int tfk_layernorm_fwd_mx(const void*, const float*, const float*, void*, float*, float*, int, int, float, void*, void*, void*,
                          void*, hipStream_t);
 int tfk_layernorm_bwd(const void*, const void*, const float*, const float*, const float*, const void*, void*, float*,
-                      float*, int, int, void*, float, unsigned long long, float*, void*, void*, void*, void*, hipStream_t);
+                      float*, int, int, void*, float, unsigned long long, float*, void*, void*, void*, void*, float*,
+                      hipStream_t);
+int tfk_ln_bwd_blocks(int M, int mxo);
 int tfk_embedding_fwd(const int*, const void*, int, const void*, int, const int*, const void*, int, void*, long long, int,
                       float, hipStream_t);
 int tfk_embedding_bwd(const int*, const void*, int, float*, float*, int, const int*, float*, int, long long, int, float,
@@ -85,11 +87,15 @@ void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor gamma, torch
     need_bf16(*dxd, "dxd"); need_numel(*dxd, M * W, "dxd");
     TORCH_CHECK(drop_p > 0.0 && drop_p < 1.0, "dxd needs 0 < drop_p < 1");
   }
+  // per-block column partials (caching allocator: graph-capture safe), reduced by a second launch
+  const int NS = (dbias.has_value() && dbias->defined()) ? 3 : 2;
+  torch::Tensor part = torch::empty({(long long)tfk_ln_bwd_blocks((int)M, mxp[0] != nullptr) * NS * W},
+                                    dgamma.options());
   check_rc(tfk_layernorm_bwd(dy.data_ptr(), x.data_ptr(), gamma.data_ptr<float>(), mean.data_ptr<float>(),
                              rstd.data_ptr<float>(), opt_ptr<const void>(dres), dx.data_ptr(), dgamma.data_ptr<float>(),
                              dbeta.data_ptr<float>(), (int)M, W, opt_ptr<void>(dxd), (float)drop_p,
                              (unsigned long long)drop_seed, opt_ptr<float>(dbias), mxp[0], mxp[1], mxp[2], mxp[3],
-                             cur_stream()),
+                             part.data_ptr<float>(), cur_stream()),
            "layernorm_bwd");
 }
 

@@ -114,7 +114,10 @@ __device__ __forceinline__ long long resid_row(const GemmParams& p, long long mo
 // DRAIN: the caller has LDS-DMA loads in flight (persistent g4: the next tile's prefetch), which
 // the compiler's vmcnt bookkeeping does not model -- wait for all of them before the store pass
 // issues its own global loads (residual, BN-reduce inputs), so those waits stay exact.
-template <int BM, int BN, int NT, int WM, int EPI, int BNRG = 0, bool DRAIN = false>
+// QUAD: the 8-phase engine's wave layout (gemm_g8.hip): wave (wm, wn) owns the four quadrant
+// sub-tiles rows {q*BM/2 + wm*64 + [0,64)} x cols {q'*BN/2 + wn*32 + [0,32)}; row fragment i covers
+// rows (i>>2)*BM/2 + wm*64 + (i&3)*16, column fragment j cols (j>>1)*BN/2 + wn*32 + (j&1)*16.
+template <int BM, int BN, int NT, int WM, int EPI, int BNRG = 0, bool DRAIN = false, bool QUAD = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[BM / WM / 16][BN / (NT / 64 / WM) / 16],
                                               char* smem, int m0, int n0, int bz) {
   constexpr int NW = NT / 64, WN = NW / WM;
@@ -123,6 +126,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int ml = lane & 15, nl = (lane >> 4) * 4;
+  static_assert(!QUAD || (FM == 8 && FN == 4), "QUAD: 8 row x 4 column fragments per wave");
+  auto frow = [&](int i) { return QUAD ? (i >> 2) * (BM / 2) + wm * 64 + (i & 3) * 16 : wm * TM + i * 16; };
+  auto fcol = [&](int j) { return QUAD ? (j >> 1) * (BN / 2) + wn * 32 + (j & 1) * 16 : wn * TN + j * 16; };
   constexpr bool ext = (EPI == EPI_BF16_EXT || EPI == EPI_BF16_EXT_MX), mx = (EPI == EPI_BF16_EXT_MX);
   if constexpr (EPI == EPI_F32) {
     // split_stride < 0: every split adds its partial straight into C with hardware f32 atomics
@@ -131,11 +137,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     float* C = (float*)p.C + bz * p.sC + (atomic ? 0LL : (long long)blockIdx.z * p.split_stride);
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * TM + i * 16 + ml;
+      const int m = m0 + frow(i) + ml;
       if (m >= p.M) continue;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wn * TN + j * 16 + nl;
+        const int n = n0 + fcol(j) + nl;
         float* dst = C + (long long)m * p.ldc + n;
         f32x4 v = acc[i][j] * p.alpha;
         if (atomic) {
@@ -162,7 +168,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       for (int r = 0; r < 4; ++r) { csum[j][r] = 0.f; csq[j][r] = 0.f; }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int nloc = wn * TN + j * 16 + nl;
+      const int nloc = fcol(j) + nl;
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
       if (p.bias) {
 #pragma unroll
@@ -170,7 +176,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int mloc = wm * TM + i * 16 + ml;
+        const int mloc = frow(i) + ml;
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -194,7 +200,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         for (int r = 0; r < 4; ++r) {
           const float s = row16_sum(csum[j][r]), q = row16_sum(csq[j][r]);
           if (ml == 0) {
-            const int nloc = wn * TN + j * 16 + nl + r;
+            const int nloc = fcol(j) + nl + r;
             red[wm * BN + nloc] = s;
             red[(WM + wm) * BN + nloc] = q;
           }

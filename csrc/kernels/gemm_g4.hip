@@ -399,12 +399,19 @@ static void fast_div(unsigned d, unsigned* mul, int* shift) {
 
 // p.tiles_n / p.kt_per_split set by the caller (tfk_gemm_launch). Returns -1 if not instantiated.
 extern "C" int tfk_halo_launch(const GemmParams& p, int epi, int batch, int splits, hipStream_t stream);
+extern "C" int tfk_g8_launch(const GemmParams& p, int amode, int bmode, int epi, int batch, int splits,
+                             hipStream_t stream);
 
 extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, int bmode, int epi, int batch,
                              int splits, hipStream_t stream) {
   // 3x3 / stride-1 convs of the supported shapes: the halo-tile direct conv (conv_halo.hip)
   if (amode == 2 && bmode == 0) {
     const int r = tfk_halo_launch(p_in, epi, batch, splits, stream);
+    if (r != -1) return r;
+  }
+  // dense 256x256: the 8-phase engine when enabled (gemm_g8.hip)
+  if (bm == 256 && bn == 256) {
+    const int r = tfk_g8_launch(p_in, amode, bmode, epi, batch, splits, stream);
     if (r != -1) return r;
   }
   GemmParams p = p_in;

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
                                                     const unsigned long long* __restrict__ drop_key,
                                                     float* __restrict__ dbias, unsigned char* __restrict__ mq,
                                                     unsigned char* __restrict__ ms, unsigned char* __restrict__ mqt,
-                                                    unsigned char* __restrict__ mst) {
+                                                    unsigned char* __restrict__ mst, float* __restrict__ part) {
   // dbias (optional): += column sums of the gradient this kernel hands its consumer (dxd, else dx)
   // -- that Linear's bias gradient, reduced with dgamma/dbeta instead of a separate column-sum pass
   extern __shared__ float red[];  // [NT/64][2 or 3][W]
@@ -279,6 +279,10 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
       }
   }
   __syncthreads();
+  // block partials: plain stores into this block's slab row (part), reduced by ln_part_reduce_kernel
+  // -- every block adding atomically into the same 2-3 x W floats serialised on those few lines at
+  // the kernel's tail (256 adders per address on Transformer-big's 8192 rows)
+  float* prow = part ? part + (long long)blockIdx.x * NS * W : nullptr;
   for (int col = threadIdx.x; col < W; col += NT) {
     float a = 0.f, b2 = 0.f, b3 = 0.f;
 #pragma unroll
@@ -287,11 +291,32 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
       b2 += red[(w * NS + 1) * W + col];
       if (dbias) b3 += red[(w * NS + 2) * W + col];
     }
-    atomicAdd(dgamma + col, a);
-    atomicAdd(dbeta + col, b2);
-    if (dbias) atomicAdd(dbias + col, b3);
+    if (prow) {
+      prow[col] = a;
+      prow[W + col] = b2;
+      if (dbias) prow[2 * W + col] = b3;
+    } else {
+      atomicAdd(dgamma + col, a);
+      atomicAdd(dbeta + col, b2);
+      if (dbias) atomicAdd(dbias + col, b3);
+    }
   }
   if (mxo) tfk::mx_rows32_out<NT>(mtile, W + 8, W, M, blockIdx.x * 32, mq, ms, mqt, mst);  // tile complete: barrier above
+}
+
+// Column sums of the ln_bwd block partials part[nblk][NS][W] into dgamma / dbeta / dbias (added):
+// grid.y row groups of the slabs each sum their share and add it with one atomic per column
+// (LN_PART_GROUPS adders per address instead of one per block).
+constexpr int LN_PART_GROUPS = 8;
+__global__ void ln_part_reduce_kernel(const float* __restrict__ part, int nblk, int NS, int W, float* __restrict__ dgamma,
+                                      float* __restrict__ dbeta, float* __restrict__ dbias) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= NS * W) return;
+  const int per = (nblk + gridDim.y - 1) / gridDim.y, b0 = blockIdx.y * per, b1 = min(nblk, b0 + per);
+  float v = 0.f;
+  for (int b = b0; b < b1; ++b) v += part[(long long)b * NS * W + c];
+  const int which = c / W, col = c - which * W;
+  atomicAdd((which == 0 ? dgamma : which == 1 ? dbeta : dbias) + col, v);
 }
 
 __global__ void embed_fwd_kernel(const int* __restrict__ ids, const bf16* __restrict__ word, int V,
@@ -474,28 +499,37 @@ int tfk_layernorm_fwd_mx(const bf16* x, const float* gamma, const float* beta, b
 }
 // dxd (optional): also write dropout(dx; drop_p, drop_seed) -- the gradient the consumer's dropout
 // backward would produce from dx
+// blocks of the LayerNorm-backward grid (the binding sizes the partials workspace with it)
+int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (NT / 64) * 8, 1024); }
+static unsigned ln_bwd_blocks(int M, bool mxo) { return (unsigned)tfk_ln_bwd_blocks(M, mxo ? 1 : 0); }
+// part (optional): f32 workspace [blocks][2 or 3][W] for the column partials (no tail atomics)
 int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const float* mean, const float* rstd,
                       const bf16* dres, bf16* dx, float* dgamma, float* dbeta, int M, int W, bf16* dxd, float drop_p,
                       unsigned long long drop_seed, float* dbias, void* mq, void* ms, void* mqt, void* mst,
-                      hipStream_t s) {
+                      float* part, hipStream_t s) {
   const int cpl = (W / 8 + 63) / 64;
   const bool mxo = mq != nullptr;
   if (mxo && (M % 32 || W % 32 || W > 1024)) return -3;
-  dim3 grid(mxo ? (unsigned)(M / 32) : grid_for(M, (NT / 64) * 8, 1024));
+  dim3 grid(ln_bwd_blocks(M, mxo));
   const size_t sh = (size_t)(NT / 64) * (dbias ? 3 : 2) * W * sizeof(float) + (mxo ? (size_t)32 * (W + 8) * 2 : 0);
   if (cpl <= 1)
     hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
                        dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
-                       (unsigned char*)mqt, (unsigned char*)mst);
+                       (unsigned char*)mqt, (unsigned char*)mst, part);
   else if (cpl <= 2)
     hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
                        dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
-                       (unsigned char*)mqt, (unsigned char*)mst);
+                       (unsigned char*)mqt, (unsigned char*)mst, part);
   else if (cpl <= 4)
     hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
                        dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
-                       (unsigned char*)mqt, (unsigned char*)mst);
+                       (unsigned char*)mqt, (unsigned char*)mst, part);
   else return -3;
+  if (part) {
+    const int NS = dbias ? 3 : 2;
+    hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((NS * W + NT - 1) / NT, LN_PART_GROUPS), dim3(NT), 0, s, part,
+                       (int)grid.x, NS, W, dgamma, dbeta, dbias);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_embedding_fwd(const int* ids, const bf16* word, int V, const bf16* pos, int S, const int* tt, const bf16* type,

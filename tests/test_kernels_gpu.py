@@ -481,14 +481,20 @@ G4_SHAPES = [(256, 256, 64), (512, 768, 1024), (300, 264, 200), (1000, 520, 72),
              (4200, 4104, 200)]  # last: 289 tiles > 256 resident blocks -> persistent multi-item walk
 
 
-@pytest.mark.parametrize("tile", [(256, 256), (128, 128)])
+@pytest.mark.parametrize("tile", [(256, 256), (128, 128), (256, 128), (128, 256), "g8"])
 @pytest.mark.parametrize("M,N,K", G4_SHAPES)
 def test_lds_dma_gemm_modes(M, N, K, tile):
-    """The LDS-DMA GEMM engine (gemm_g4.hip: 64x64 wave tiles; 256x256 = 16 waves, 128x128 = 4) in
-    every dense mode it serves: NT bf16 (bias+relu), NN bf16 (residual), TN f32 (beta accumulate;
-    split-K slabs), on interior and ragged M/N/K (zero-filled out-of-range DMA), against the fp32
-    reference AND the register-staged engine (TFK_GEMM_ENGINE=reg)."""
+    """The LDS-DMA GEMM engines in every dense mode they serve: NT bf16 (bias+relu), NN bf16
+    (residual), TN f32 (beta accumulate; split-K slabs), on interior and ragged M/N/K (zero-filled
+    out-of-range DMA), against the fp32 reference AND the register-staged engine: gemm_g4.hip's
+    64x64 wave tiles (256x256 = 16 waves, 128x128 = 4; the 8-wave 3-stage 256x128 / 128x256) and
+    "g8", gemm_g8.hip's 8-phase 256x256 schedule (quadrant wave layout, counted vmcnt)."""
     L = lib()
+    if tile == "g8":
+        L.g8_set(1)
+        tile = (256, 256)
+    else:
+        L.g8_set(0)
     x, w = bf(M, K, seed=1), bf(N, K, seed=2, scale=0.05)
     dy, r = bf(M, N, seed=3), bf(M, K, seed=4)
     b = torch.randn(N) * 0.1
@@ -515,6 +521,7 @@ def test_lds_dma_gemm_modes(M, N, K, tile):
             res[eng] = dict(y=y, dx=dx, gw=gw, gws=gws)
     finally:
         L.gemm_set_engine(1)
+        L.g8_set(0)
     ref = dict(y=torch.relu(x.float() @ w.float().t() + b),
                dx=(dy.float() @ w.float()).to(torch.bfloat16).float() + r.float(),
                gw=gw0 + dy.float().t() @ x.float(), gws=dy.float().t() @ x.float())

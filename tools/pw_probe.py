@@ -1,11 +1,18 @@
 #!/usr/bin/env python3
-"""Driver for rocprofv3 PMC passes on ResNet-50's memory-bound pointwise GEMMs (bs256 shapes):
-the forward 1x1 conv with fused BN statistics, the 1x1 dgrad with the fused BN-backward reduction
-(mask + residual), and a stage-3 3x3 forward conv. Runs each a few times on random data.
+"""ResNet-50 (bs256) memory-bound pointwise GEMMs, each with and without its fused BN epilogue
+work, timed with device events (interleaved rounds) -- and the driver for rocprofv3 PMC passes
+on them (--reps N, no timing). Variants:
+  fwd1x1        a2[M,64] @ w3 -> y3[M,256]            (+stats: BN batch statistics in the epilogue)
+  dgrad1x1      dy[M,64] @ w1 -> dx[M,256]            (+bnr: mask, residual, BN-backward sums, dz store)
+  conv3x3_s3    28x28x128 -> 128 3x3 forward          (+stats)
 
-    rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES ... -- python3 tools/pw_probe.py
+    python tools/pw_probe.py [--iters 20] [--rounds 3]      -> JSON lines
+    rocprofv3 --pmc ... -- python3 tools/pw_probe.py --reps 5
 """
+import argparse
+import json
 import os
+import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -20,27 +27,59 @@ def r(*shape):
     return (torch.rand(*shape, device="cuda") * 2 - 1).to(torch.bfloat16)
 
 
-def main(reps: int = 5):
-    M = 256 * 56 * 56
-    # forward 1x1 conv a2[M,64] -> y3[M,256] + BN stats
+def variants():
     g = G.ConvGeom(256, 56, 56, 64, 256, 1, 1)
     x, w = r(256, 56, 56, 64), r(256, 1, 1, 64) * 0.1
     st = BN.BNState(256, "cuda")
-    # 1x1 dgrad dy[M,64] @ w1[64,256] -> dx[M,256] + BN3 reduce of the previous block (mask, resid)
     gd = G.ConvGeom(256, 56, 56, 256, 64, 1, 1)
     dy, w1 = r(256, 56, 56, 64), r(64, 1, 1, 256) * 0.1
     y3, res = r(256, 56, 56, 256), r(256, 56, 56, 256)
     st3 = BN.BNState(256, "cuda")
     mk = BN.pack_relu_mask(r(256, 56, 56, 256))
-    # 3x3 stage 3
     g3 = G.ConvGeom(256, 28, 28, 128, 128, 3, 3, 1, 1, 1, 1)
     x3, w3 = r(256, 28, 28, 128), r(128, 3, 3, 128) * 0.05
-    for _ in range(reps):
-        G.conv_fwd(x, w, g, st.stats, st.shards)
-        G.conv_dgrad(dy, w1, gd, resid=res, bnr=BN.BNReduce(y3, st3, a=mk, premask=True))
-        G.conv_fwd(x3, w3, g3)
-    torch.cuda.synchronize()
-    print("pw_probe done", M)
+    st33 = BN.BNState(128, "cuda")
+    M = 256 * 56 * 56
+    return {
+        "fwd1x1": (lambda: G.conv_fwd(x, w, g), (M * 64 + M * 256) * 2),
+        "fwd1x1+stats": (lambda: G.conv_fwd(x, w, g, st.stats, st.shards), (M * 64 + M * 256) * 2),
+        "dgrad1x1": (lambda: G.conv_dgrad(dy, w1, gd), (M * 64 + M * 256) * 2),
+        "dgrad1x1+resid": (lambda: G.conv_dgrad(dy, w1, gd, resid=res), (M * 64 + 2 * M * 256) * 2),
+        "dgrad1x1+bnr": (lambda: G.conv_dgrad(dy, w1, gd, resid=res, bnr=BN.BNReduce(y3, st3, a=mk, premask=True)),
+                         (M * 64 + 3 * M * 256) * 2 + M * 256 // 8),
+        "conv3x3_s3": (lambda: G.conv_fwd(x3, w3, g3), (200704 * 128 * 2) * 2),
+        "conv3x3_s3+stats": (lambda: G.conv_fwd(x3, w3, g3, st33.stats, st33.shards), (200704 * 128 * 2) * 2),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=0, help="profiler driver mode: run each variant N times, no timing")
+    args = ap.parse_args()
+    vs = variants()
+    if args.reps:
+        for _ in range(args.reps):
+            for fn, _ in vs.values():
+                fn()
+        torch.cuda.synchronize()
+        print("pw_probe done")
+        return
+    res = {k: [] for k in vs}
+    for _ in range(args.rounds):
+        for k, (fn, _) in vs.items():
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            res[k].append(e0.elapsed_time(e1) / args.iters * 1000.0)
+    for k, (fn, nbytes) in vs.items():
+        us = statistics.median(res[k])
+        print(json.dumps({"variant": k, "us": round(us, 1), "TB_s": round(nbytes / us / 1e6, 2)}), flush=True)
 
 
 if __name__ == "__main__":

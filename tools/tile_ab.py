@@ -19,6 +19,22 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from tensorflow_k8s_amd.ops import gemm as G  # noqa: E402
+from tensorflow_k8s_amd.ops._lib import lib  # noqa: E402
+
+
+def _g8(fn, t):
+    """Run fn on tile t; "g8" = the 256x256 tile with the 8-phase engine switched on."""
+    if t != "g8":
+        return fn(t)
+    lib().g8_set(1)
+    try:
+        return fn((256, 256))
+    finally:
+        lib().g8_set(0)
+
+
+def tname(t):
+    return t if isinstance(t, str) else f"t{t[0]}x{t[1]}"
 
 DENSE = {  # name: (M, N, K)
     "sq4096": (4096, 4096, 4096),
@@ -36,7 +52,7 @@ CONV = {  # ResNet-50 bs256 3x3 convs (N, H, W, C, K): stride 1
     "r50_3x3_s4": (256, 14, 14, 256, 256),
     "r50_3x3_s5": (256, 7, 7, 512, 512),
 }
-TILES = [(256, 256), (128, 128), (256, 128), (128, 256)]
+TILES = [(256, 256), (128, 128), (256, 128), (128, 256), "g8"]  # "g8": 256x256 on the 8-phase engine
 
 
 def timeit(fn, iters):
@@ -70,13 +86,14 @@ def main():
         fl = 2.0 * M * N * K
         runs = {}
         if "fwd" in dirs:
-            runs["fwd"] = ({t: (lambda t=t: G._gemm(x, w, y, M, N, K, K, K, N, G.A_KIN, G.B_KIN, G.EPI_BF16, t))
-                            for t in TILES}, lambda: x @ w.t())
+            runs["fwd"] = ({t: (lambda t=t: _g8(lambda tt: G._gemm(x, w, y, M, N, K, K, K, N, G.A_KIN, G.B_KIN,
+                                                                   G.EPI_BF16, tt), t)) for t in TILES}, lambda: x @ w.t())
         if "dgrad" in dirs:
-            runs["dgrad"] = ({t: (lambda t=t: G._gemm(dy, w, dx, M, K, N, N, K, K, G.A_KIN, G.B_KOUT, G.EPI_BF16, t))
-                              for t in TILES}, lambda: dy @ w)
+            runs["dgrad"] = ({t: (lambda t=t: _g8(lambda tt: G._gemm(dy, w, dx, M, K, N, N, K, K, G.A_KIN, G.B_KOUT,
+                                                                     G.EPI_BF16, tt), t)) for t in TILES}, lambda: dy @ w)
         if "wgrad" in dirs:
-            runs["wgrad"] = ({t: (lambda t=t: G._gemm(dy, x, gw, N, K, M, N, K, K, G.A_KOUT, G.B_KOUT, G.EPI_F32, t))
+            runs["wgrad"] = ({t: (lambda t=t: G._gemm(dy, x, gw, N, K, M, N, K, K, G.A_KOUT, G.B_KOUT, G.EPI_F32,
+                                                      (256, 256) if t == "g8" else t))
                               for t in TILES}, lambda: dy.t() @ x)
         ref = (x.float() @ w.float().t())
         for d, (fns, blas) in runs.items():
@@ -88,12 +105,12 @@ def main():
                 res["blas"].append(fl / timeit(blas, args.iters) / 1e12)
             out = {"shape": name, "dir": d, "M": M, "N": N, "K": K}
             for k, v in res.items():
-                out["blas" if k == "blas" else f"t{k[0]}x{k[1]}"] = round(statistics.median(v), 1)
+                out["blas" if k == "blas" else tname(k)] = round(statistics.median(v), 1)
             if d == "fwd":  # correctness of every tile against fp32
                 errs = {}
                 for t, fn in fns.items():
                     fn()
-                    errs[f"t{t[0]}x{t[1]}"] = round(float((y.float() - ref).norm() / ref.norm()), 5)
+                    errs[tname(t)] = round(float((y.float() - ref).norm() / ref.norm()), 5)
                 out["rel_err"] = errs
             print(json.dumps(out), flush=True)
         del x, w, dy, y, dx, gw, ref
@@ -101,16 +118,17 @@ def main():
     if "conv" not in dirs:
         return
     for name, (Nn, H, W, C, Kc) in CONV.items():
+        TILES_C = [t for t in TILES if t != "g8"]
         if args.only and args.only not in name:
             continue
         g = G.ConvGeom(Nn, H, W, C, Kc, 3, 3, 1, 1, 1, 1)
         x = (torch.rand(Nn, H, W, C, device=dev) * 2 - 1).to(torch.bfloat16)
         w = ((torch.rand(Kc, 3, 3, C, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
         fl = float(g.flops())
-        res = {t: [] for t in TILES}
+        res = {t: [] for t in TILES_C}
         outs = {}
         for _ in range(args.rounds):
-            for t in TILES:
+            for t in TILES_C:
                 G.FORCE_TILE = t
                 try:
                     res[t].append(fl / timeit(lambda: G.conv_fwd(x, w, g), args.iters) / 1e12)
@@ -119,9 +137,9 @@ def main():
                     G.FORCE_TILE = None
         ref = G._ref_conv(x, w, g)
         out = {"shape": name, "dir": "conv_fwd", "M": Nn * H * W, "N": Kc, "K": 9 * C}
-        for t in TILES:
-            out[f"t{t[0]}x{t[1]}"] = round(statistics.median(res[t]), 1)
-        out["rel_err"] = {f"t{t[0]}x{t[1]}": round(float((outs[t].float() - ref).norm() / ref.norm()), 5) for t in TILES}
+        for t in TILES_C:
+            out[tname(t)] = round(statistics.median(res[t]), 1)
+        out["rel_err"] = {tname(t): round(float((outs[t].float() - ref).norm() / ref.norm()), 5) for t in TILES_C}
         print(json.dumps(out), flush=True)
 
 

@@ -28,6 +28,7 @@ namespace tfk {
 namespace g8 {
 
 using g4::BK;
+using g4::CONV_FWD;
 using g4::frag;
 using g4::KIN;
 using g4::KOUT;
@@ -43,7 +44,9 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
-template <int BMD, int EPI>
+// AM: KIN (dense A [M][K]) or CONV_FWD (implicit-GEMM gather of NHWC x, Cin % 64 == 0: a K-tile
+// is one (r, s) tap x 64 channels); BMD: KIN or KOUT.
+template <int AM, int BMD, int EPI>
 __global__ __launch_bounds__(NT, 1) void g8_kernel(GemmParams p) {
   constexpr bool BKO = (BMD == KOUT);
   constexpr int MAIN = 2 * BUF, EPIB = epi_lds_bytes<BM, BN, 2>();
@@ -68,14 +71,15 @@ __global__ __launch_bounds__(NT, 1) void g8_kernel(GemmParams p) {
   // one loader per half-image (its rows are the half's 128 rows)
   const char* Abase = (const char*)p.A + (long long)bz * p.sA * 2;
   const char* Bbase = (const char*)p.B + (long long)bz * p.sB * 2;
-  const char* Ah[2] = {Abase + (long long)m0 * p.lda * 2, Abase + (long long)(m0 + HALF) * p.lda * 2};
+  const char* Ah[2] = {AM == CONV_FWD ? Abase : Abase + (long long)m0 * p.lda * 2,
+                       AM == CONV_FWD ? Abase : Abase + (long long)(m0 + HALF) * p.lda * 2};
   const char* Bh[2] = {Bbase + (BKO ? (long long)n0 * 2 : (long long)n0 * p.ldb * 2),
                        Bbase + (BKO ? (long long)(n0 + HALF) * 2 : (long long)(n0 + HALF) * p.ldb * 2)};
   const long long a_step = BK * 2;
   const long long b_step = BKO ? (long long)BK * p.ldb * 2 : BK * 2;
   const int lim_a[2] = {p.M - m0, p.M - m0 - HALF};
   const int lim_b[2] = {p.N - n0, p.N - n0 - HALF};
-  Loader<HALF, KIN, NW> la0, la1;
+  Loader<HALF, AM, NW, false> la0, la1;
   Loader<HALF, BMD, NW> lb0, lb1;
   la0.init(p, lane, w, p.lda, m0, p.M);
   la1.init(p, lane, w, p.lda, m0 + HALF, p.M);
@@ -192,25 +196,32 @@ static bool g8_on() {
   return g_g8 > 0;
 }
 
-// 256x256 dense GEMMs with K-inner A (fwd: B K-inner; dgrad: B K-outer). -1: not handled here.
+// 256x256 GEMMs with K-inner A (fwd: B K-inner; dgrad: B K-outer) and the Cin % 64 == 0 conv
+// forward gather (fwd, and stride-1 dgrad run as a forward conv with the BN-reduce epilogue).
+// -1: not handled here.
 extern "C" int tfk_g8_launch(const GemmParams& p_in, int amode, int bmode, int epi, int batch, int splits,
                              hipStream_t stream) {
-  if (!g8_on() || amode != g4::KIN || (bmode != g4::KIN && bmode != g4::KOUT)) return -1;
-  if (epi != EPI_BF16 && epi != EPI_BF16_EXT && epi != EPI_F32) return -1;
+  if (!g8_on()) return -1;
+  const bool dense = amode == g4::KIN && (bmode == g4::KIN || bmode == g4::KOUT);
+  const bool conv = amode == g4::CONV_FWD && bmode == g4::KIN && (p_in.Cin & 63) == 0;
+  if (!dense && !conv) return -1;
   GemmParams p = p_in;
   p.tiles_n = (p.N + g8::BN - 1) / g8::BN;
   const int tiles = ((p.M + g8::BM - 1) / g8::BM) * p.tiles_n;
   const dim3 grid(tiles, batch, splits), block(g8::NT);
-#define TFK_G8(BMD_, EPI_)                                                                         \
-  if (bmode == BMD_ && epi == EPI_) {                                                              \
-    hipLaunchKernelGGL((g8::g8_kernel<BMD_, EPI_>), grid, block, 0, stream, p);                    \
+#define TFK_G8(AM_, BMD_, EPI_)                                                                    \
+  if (amode == AM_ && bmode == BMD_ && epi == EPI_) {                                              \
+    hipLaunchKernelGGL((g8::g8_kernel<AM_, BMD_, EPI_>), grid, block, 0, stream, p);               \
     return hipGetLastError() == hipSuccess ? 0 : -2;                                               \
   }
-  TFK_G8(g4::KIN, EPI_BF16)
-  TFK_G8(g4::KIN, EPI_BF16_EXT)
-  TFK_G8(g4::KIN, EPI_F32)
-  TFK_G8(g4::KOUT, EPI_BF16)
-  TFK_G8(g4::KOUT, EPI_BF16_EXT)
+  TFK_G8(g4::KIN, g4::KIN, EPI_BF16)
+  TFK_G8(g4::KIN, g4::KIN, EPI_BF16_EXT)
+  TFK_G8(g4::KIN, g4::KIN, EPI_F32)
+  TFK_G8(g4::KIN, g4::KOUT, EPI_BF16)
+  TFK_G8(g4::KIN, g4::KOUT, EPI_BF16_EXT)
+  TFK_G8(g4::KIN, g4::KOUT, EPI_BF16_BNR)
+  TFK_G8(g4::CONV_FWD, g4::KIN, EPI_BF16)
+  TFK_G8(g4::CONV_FWD, g4::KIN, EPI_BF16_BNR)
 #undef TFK_G8
   return -1;
 }

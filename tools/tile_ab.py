@@ -118,7 +118,7 @@ def main():
     if "conv" not in dirs:
         return
     for name, (Nn, H, W, C, Kc) in CONV.items():
-        TILES_C = [t for t in TILES if t != "g8"]
+        TILES_C = list(TILES)
         if args.only and args.only not in name:
             continue
         g = G.ConvGeom(Nn, H, W, C, Kc, 3, 3, 1, 1, 1, 1)
@@ -129,12 +129,14 @@ def main():
         outs = {}
         for _ in range(args.rounds):
             for t in TILES_C:
-                G.FORCE_TILE = t
+                G.FORCE_TILE = (256, 256) if t == "g8" else t
+                lib().g8_set(1 if t == "g8" else 0)
                 try:
                     res[t].append(fl / timeit(lambda: G.conv_fwd(x, w, g), args.iters) / 1e12)
                     outs[t] = G.conv_fwd(x, w, g)
                 finally:
                     G.FORCE_TILE = None
+                    lib().g8_set(0)
         ref = G._ref_conv(x, w, g)
         out = {"shape": name, "dir": "conv_fwd", "M": Nn * H * W, "N": Kc, "K": 9 * C}
         for t in TILES_C:

@@ -536,7 +536,7 @@ def test_lds_dma_gemm_modes(M, N, K, tile):
                                  # Cin < 64: several taps per K-tile (stem 7x7/2 on 8 channels, ragged K)
                                  (2, 20, 20, 8, 64, 7, 7, 2, 3), (1, 15, 17, 16, 72, 3, 3, 1, 1),
                                  (2, 9, 9, 32, 64, 5, 5, 2, 2)])
-@pytest.mark.parametrize("tile", [(256, 256), (128, 128), (256, 64)])
+@pytest.mark.parametrize("tile", [(256, 256), (128, 128), (256, 64), "g8"])
 def test_g4_conv_fwd_gather(cfg, tile):
     """g4's implicit-GEMM conv-forward gather (Cin % 64 == 0: a K-tile is one tap x 64 channels;
     Cin % 8 == 0 below 64: 64/Cin taps per K-tile; zero padding from out-of-range DMA) against the
@@ -548,8 +548,13 @@ def test_g4_conv_fwd_gather(cfg, tile):
     Kd = R * S * C
     y = torch.empty(N, g.P, g.Q, K, dtype=torch.bfloat16, device=DEV)
     st_ = torch.zeros(2, K, device=DEV)
-    G._gemm(x.to(DEV), w.to(DEV), y, M, K, Kd, 0, Kd, K, G.A_CONV_FWD, G.B_KIN, G.EPI_BF16, tile, stats=st_,
-            shards=1, conv=g.vec())
+    g8 = tile == "g8"  # gemm_g8.hip's 8-phase engine (Cin % 64 == 0 convs; others fall back to g4)
+    lib().g8_set(1 if g8 else 0)
+    try:
+        G._gemm(x.to(DEV), w.to(DEV), y, M, K, Kd, 0, Kd, K, G.A_CONV_FWD, G.B_KIN, G.EPI_BF16,
+                (256, 256) if g8 else tile, stats=st_, shards=1, conv=g.vec())
+    finally:
+        lib().g8_set(0)
     ref = G._ref_conv(x, w, g)
     assert rel(y, ref) < 1e-2
     assert rel(st_[0], ref.reshape(-1, K).sum(0)) < 1e-2

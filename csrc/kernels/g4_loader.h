@@ -99,7 +99,9 @@ struct Loader {
         const int n = m / PQ, rem = m - n * PQ, pp = rem / p.Q, qq = rem - pp * p.Q;
         ch[i] = pp * p.sh - p.ph;
         cw[i] = qq * p.sw - p.pw;
-        off[i] = (unsigned)n;
+        // input pixel index of tap (0, 0) (may be negative in the padding: only used when in range;
+        // x < 2^30 elements, checked by tfk_g4_ok, so 32-bit pixel / element math suffices)
+        off[i] = (unsigned)((n * p.H + ch[i]) * p.W + cw[i]);
       }
     }
   }
@@ -126,15 +128,18 @@ struct Loader {
     } else if constexpr (MODE == CONV_FWD) {
       __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, NREC, 0x00020000);
       if (!SMALLC || p.Cin >= BK) {
-        // K-tile kt covers tap (r, s) = divmod(kt*64 / Cin, S) and channels c0..c0+63 (Cin % 64 == 0)
+        // K-tile kt covers tap (r, s) = divmod(kt*64 / Cin, S) and channels c0..c0+63 (Cin % 64 == 0);
+        // the tap's pixel shift and channel offset are block-uniform (scalar), per lane: 2 adds,
+        // the bounds test and one 32-bit multiply-add
         const int k0 = kt * BK, rs = k0 / p.Cin, c0 = k0 - rs * p.Cin;
         const int r = rs / p.S, s = rs - r * p.S;
+        const int rdh = r * p.dh, sdw = s * p.dw, tap = rdh * p.W + sdw;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-          const int h = ch[i] + r * p.dh, wq = cw[i] + s * p.dw;
+          const int h = ch[i] + rdh, wq = cw[i] + sdw;
           const bool ok = (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
-          const long long pix = ((long long)off[i] * p.H + h) * p.W + wq;
-          const unsigned vo = ok ? (unsigned)((pix * p.Cin + c0 + k_of(i, w, lane)) * 2) : OOB;
+          const int pix = (int)off[i] + tap;
+          const unsigned vo = ok ? (unsigned)(pix * p.Cin + c0 + k_of(i, w, lane)) * 2u : OOB;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
         }
       } else {
@@ -149,8 +154,8 @@ struct Loader {
           const int h = ch[i] + (int)r * p.dh, wq = cw[i] + (int)sx * p.dw;
           const bool ok = (int)k < p.K && (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H &&
                           (unsigned)wq < (unsigned)p.W;
-          const long long pix = ((long long)off[i] * p.H + h) * p.W + wq;
-          const unsigned vo = ok ? (unsigned)((pix * p.Cin + c) * 2) : OOB;
+          const int pix = (int)off[i] + (int)r * p.dh * p.W + (int)sx * p.dw;
+          const unsigned vo = ok ? (unsigned)(pix * p.Cin + (int)c) * 2u : OOB;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
         }
       }

@@ -54,16 +54,18 @@ __device__ __forceinline__ int arow(int b, int g, int r) { return 32 * (b >> 1) 
 // ---- global tile <-> registers <-> LDS (64 rows x 64 bf16; 2 x 16 B per thread)
 struct TileRegs {
   u32x4 v[2];
+  bool ok[2];
 };
+// Loads are unconditional (rows past nvalid re-read the last valid row, or row 0) and the padding zeros
+// are applied when the registers are stored: no exec-masked branch around the loads, so the
+// compiler's wait for them stays at the store, a whole tile later.
 template <int NTH>  // NTH <= 512: a 64 x 64 tile is 512 16-B chunks
 __device__ __forceinline__ void tile_load(TileRegs& t, const bf16* base, int rs, int row0, int nvalid) {
 #pragma unroll
   for (int it = 0; it < 512 / NTH; ++it) {
     const int c = threadIdx.x + it * NTH, row = c >> 3, col = (c & 7) * 8;
-    if (row0 + row < nvalid)
-      t.v[it] = *(const u32x4*)(base + (long long)(row0 + row) * rs + col);
-    else
-      t.v[it] = u32x4{0u, 0u, 0u, 0u};
+    t.ok[it] = row0 + row < nvalid;
+    t.v[it] = *(const u32x4*)(base + (long long)max(min(row0 + row, nvalid - 1), 0) * rs + col);
   }
 }
 template <int NTH>
@@ -71,7 +73,8 @@ __device__ __forceinline__ void tile_store(const TileRegs& t, bf16* lds) {
 #pragma unroll
   for (int it = 0; it < 512 / NTH; ++it) {
     const int c = threadIdx.x + it * NTH, row = c >> 3, col = (c & 7) * 8;
-    *(u32x4*)(lds + row * LS + col) = t.v[it];
+    const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+    *(u32x4*)(lds + row * LS + col) = t.ok[it] ? t.v[it] : z;
   }
 }
 // row fragment: lane -> row `row`, k-slots = columns kk*32 + 8g .. +7
@@ -91,16 +94,14 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16* lds, int kbase, int cbase)
   r.hi = hi;
   return r;
 }
-// register row fragment straight from global (rows of this wave): row `row` (global), k-slots kk
+// register row fragment straight from global (rows of this wave): row `row` (global), k-slots kk;
+// unconditional load of a clamped row, zeroed past nvalid
 __device__ __forceinline__ bf16x8 frag_global(const bf16* base, int rs, int row, int nvalid, int kk) {
   const int g = (threadIdx.x & 63) >> 4;
-  if (row >= nvalid) {
-    bf16x8 z;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) z[e] = f2bf(0.f);
-    return z;
-  }
-  return *(const bf16x8*)(base + (long long)row * rs + kk * 32 + 8 * g);
+  const bf16x8 v = *(const bf16x8*)(base + (long long)max(min(row, nvalid - 1), 0) * rs + kk * 32 + 8 * g);
+  const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+  const u32x4 r = row < nvalid ? __builtin_bit_cast(u32x4, v) : z;
+  return __builtin_bit_cast(bf16x8, r);
 }
 __device__ __forceinline__ bf16x8 pack2(const f32x4& a, const f32x4& b) {
   bf16x8 r;
@@ -150,13 +151,32 @@ __device__ __forceinline__ void store_rowvec4(bf16* dst, const f32x4& v, float s
   *(bf16x4*)dst = o;
 }
 
+// v_exp_f32 without the libm denormal fix-up (exp2f adds a compare, two selects, an add and an
+// ldexp): softmax terms below 2^-126 of the row maximum flush to 0
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+// LDS-only block barrier. __syncthreads() is a workgroup release/acquire fence around s_barrier and
+// drains EVERY outstanding global load (vmcnt(0)) -- including the next tile's register prefetch,
+// which must stay in flight across the barrier. The tiles only communicate through LDS, so waiting
+// for this wave's LDS ops (lgkmcnt(0)) is enough.
+__device__ __forceinline__ void lds_bar() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Every kernel stages its streamed 64-row tiles global -> registers -> LDS through a DOUBLE-buffered
+// LDS ring with one barrier per tile: tile t+1 (loaded into registers during tile t-1) is stored
+// into the idle buffer after tile t's math, and tile t+2's global loads are issued right behind it,
+// so a whole tile of MFMA work covers each load. The per-element softmax / mask / dropout math is
+// branch-free (wave-uniform `full` selects the unmasked form; masked elements get a -inf exponent).
+
 // =============================================================================== forward
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
-  constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; query (key) rows per block
-  __shared__ __attribute__((aligned(16))) bf16 Ks[TILE * LS];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[TILE * LS];
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
+  constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; query rows per block
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][TILE * LS];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[2][TILE * LS];
+  const int l = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = l >> 4, li = l & 15;
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * RB;
   const int bh = b * p.H + h;
   const uint32_t hs = head_seed(p, bh);
@@ -165,6 +185,13 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   const bf16* Vb = p.v + b * p.v_bs + h * D;
   const int kvl = p.kv_len ? min(p.kv_len[b], p.Sk) : p.Sk;
   const int qrow = q0 + 16 * w + li;  // this lane's query
+  int kend = kvl;
+  if (p.causal) kend = min(kend, q0 + RB);
+  const int ntiles = (kend + TILE - 1) / TILE;
+  TileRegs kr, vr;
+  // prologue (unconditional: the tile-0 store's wait then covers every prologue load on all paths)
+  tile_load<NTH>(kr, Kb, p.k_rs, 0, kvl);
+  tile_load<NTH>(vr, Vb, p.v_rs, 0, kvl);
   const bf16x8 qf0 = frag_global(Qb, p.q_rs, qrow, p.Sq, 0), qf1 = frag_global(Qb, p.q_rs, qrow, p.Sq, 1);
   const float sl2 = p.scale * LOG2E;
   const int thr = drop_thr(p.p_drop);
@@ -174,63 +201,49 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   f32x4 oacc[4];
 #pragma unroll
   for (int db = 0; db < 4; ++db) oacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int kend = kvl;
-  if (p.causal) kend = min(kend, q0 + RB);
-  const int ntiles = (kend + TILE - 1) / TILE;
-  TileRegs kr, vr;
-  if (ntiles > 0) { tile_load<NTH>(kr, Kb, p.k_rs, 0, kvl); tile_load<NTH>(vr, Vb, p.v_rs, 0, kvl); }
+  tile_store<NTH>(kr, Ks[0]);
+  tile_store<NTH>(vr, Vs[0]);
+  tile_load<NTH>(kr, Kb, p.k_rs, TILE, kvl);
+  tile_load<NTH>(vr, Vb, p.v_rs, TILE, kvl);
+  lds_bar();
   for (int t = 0; t < ntiles; ++t) {
     const int k0 = t * TILE;
-    __syncthreads();
-    tile_store<NTH>(kr, Ks);
-    tile_store<NTH>(vr, Vs);
-    __syncthreads();
-    if (t + 1 < ntiles) { tile_load<NTH>(kr, Kb, p.k_rs, k0 + TILE, kvl); tile_load<NTH>(vr, Vb, p.v_rs, k0 + TILE, kvl); }
+    const bf16* K_ = Ks[t & 1];
+    const bf16* V_ = Vs[t & 1];
     // S^T blocks: lane (g, r) of block bb = score(key k0 + arow(bb,g,r), query qrow)
     f32x4 s[4];
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
       const int kr_ = prow(bb, li);
       f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
-      a = mfma(frag_row(Ks, kr_, 0), qf0, a);
-      a = mfma(frag_row(Ks, kr_, 1), qf1, a);
+      a = mfma(frag_row(K_, kr_, 0), qf0, a);
+      a = mfma(frag_row(K_, kr_, 1), qf1, a);
       s[bb] = a;
     }
-    float mx = -INFINITY;
     // wave-uniform: every (query, key) of this wave's tile valid -> no per-element mask
     const bool full = k0 + TILE <= kvl && (!p.causal || k0 + TILE - 1 <= q0 + 16 * w);
-    if (full) {
+    float mx = -INFINITY;
 #pragma unroll
-      for (int bb = 0; bb < 4; ++bb)
+    for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s[bb][r] *= sl2;
-          mx = fmaxf(mx, s[bb][r]);
-        }
-    } else {
-#pragma unroll
-      for (int bb = 0; bb < 4; ++bb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + arow(bb, g, r);
-          float v = s[bb][r] * sl2;
-          if (key >= kvl || (p.causal && key > qrow)) v = -INFINITY;
-          s[bb][r] = v;
-          mx = fmaxf(mx, v);
-        }
-    }
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + arow(bb, g, r);
+        float v = s[bb][r] * sl2;
+        if (!full) v = (key >= kvl || (p.causal && key > qrow)) ? -INFINITY : v;
+        s[bb][r] = v;
+        mx = fmaxf(mx, v);
+      }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mnew = fmaxf(m, mx);
     const float muse = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = exp2f(m - muse);
+    const float alpha = ex2(m - muse);
     float rs = 0.f;
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float e = exp2f(s[bb][r] - muse);
+        const float e = ex2(s[bb][r] - muse);
         rs += e;
         s[bb][r] = e;
       }
@@ -251,9 +264,15 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
     const bf16x8 pf0 = pack2(s[0], s[1]), pf1 = pack2(s[2], s[3]);
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
-      oacc[db] = mfma(frag_tr(Vs, 0, db * 16), pf0, oacc[db]);
-      oacc[db] = mfma(frag_tr(Vs, 32, db * 16), pf1, oacc[db]);
+      oacc[db] = mfma(frag_tr(V_, 0, db * 16), pf0, oacc[db]);
+      oacc[db] = mfma(frag_tr(V_, 32, db * 16), pf1, oacc[db]);
     }
+    // unconditional: past the end these stage clamped rows into the idle buffer, never read
+    tile_store<NTH>(kr, Ks[(t + 1) & 1]);
+    tile_store<NTH>(vr, Vs[(t + 1) & 1]);
+    tile_load<NTH>(kr, Kb, p.k_rs, k0 + 2 * TILE, kvl);
+    tile_load<NTH>(vr, Vb, p.v_rs, k0 + 2 * TILE, kvl);
+    lds_bar();
   }
   if (qrow < p.Sq) {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
@@ -268,10 +287,10 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
 // =============================================================================== dQ pass
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
-  constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; query (key) rows per block
-  __shared__ __attribute__((aligned(16))) bf16 Ks[TILE * LS];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[TILE * LS];
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
+  constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; query rows per block
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][TILE * LS];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[2][TILE * LS];
+  const int l = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = l >> 4, li = l & 15;
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * RB;
   const int bh = b * p.H + h;
   const uint32_t hs = head_seed(p, bh);
@@ -281,13 +300,19 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   const bf16* dOb = p.dout + b * p.o_bs + h * D;
   const int kvl = p.kv_len ? min(p.kv_len[b], p.Sk) : p.Sk;
   const int qrow = q0 + 16 * w + li;
+  int kend = kvl;
+  if (p.causal) kend = min(kend, q0 + RB);
+  const int ntiles = (kend + TILE - 1) / TILE;
+  TileRegs kr, vr;
+  tile_load<NTH>(kr, Kb, p.k_rs, 0, kvl);
+  tile_load<NTH>(vr, Vb, p.v_rs, 0, kvl);
   const bf16x8 qf0 = frag_global(Qb, p.q_rs, qrow, p.Sq, 0), qf1 = frag_global(Qb, p.q_rs, qrow, p.Sq, 1);
   const bf16x8 df0 = frag_global(dOb, p.o_rs, qrow, p.Sq, 0), df1 = frag_global(dOb, p.o_rs, qrow, p.Sq, 1);
   const float sl2 = p.scale * LOG2E;
   const int thr = drop_thr(p.p_drop);
   const float keep_scale = p.p_drop > 0.f ? 256.f / (float)(256 - thr) : 1.f;
   const int qgbase = (qrow >> 2) * p.Sk;
-  const float lse2 = qrow < p.Sq ? p.lse[(long long)bh * p.Sq + qrow] * LOG2E : INFINITY;
+  const float lse2 = qrow < p.Sq ? p.lse[(long long)bh * p.Sq + min(qrow, p.Sq - 1)] * LOG2E : INFINITY;
   // delta = rowsum(dO * O) of this lane's query, from the dO fragments already in registers + the
   // same fragments of O (4 lane groups x 16 of the 64 dims); written for the dK/dV pass, which
   // runs after this kernel -- no separate delta kernel (a strided 128-B-per-lane pass)
@@ -306,35 +331,39 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   f32x4 acc[4];
 #pragma unroll
   for (int db = 0; db < 4; ++db) acc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int kend = kvl;
-  if (p.causal) kend = min(kend, q0 + RB);
-  const int ntiles = (kend + TILE - 1) / TILE;
-  TileRegs kr, vr;
-  if (ntiles > 0) { tile_load<NTH>(kr, Kb, p.k_rs, 0, kvl); tile_load<NTH>(vr, Vb, p.v_rs, 0, kvl); }
+  tile_store<NTH>(kr, Ks[0]);
+  tile_store<NTH>(vr, Vs[0]);
+  tile_load<NTH>(kr, Kb, p.k_rs, TILE, kvl);
+  tile_load<NTH>(vr, Vb, p.v_rs, TILE, kvl);
+  lds_bar();
   for (int t = 0; t < ntiles; ++t) {
     const int k0 = t * TILE;
-    __syncthreads();
-    tile_store<NTH>(kr, Ks);
-    tile_store<NTH>(vr, Vs);
-    __syncthreads();
-    if (t + 1 < ntiles) { tile_load<NTH>(kr, Kb, p.k_rs, k0 + TILE, kvl); tile_load<NTH>(vr, Vb, p.v_rs, k0 + TILE, kvl); }
+    const bf16* K_ = Ks[t & 1];
+    const bf16* V_ = Vs[t & 1];
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int kr_ = prow(bb, li);
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
+      a = mfma(frag_row(K_, kr_, 0), qf0, a);
+      c = mfma(frag_row(V_, kr_, 0), df0, c);
+      a = mfma(frag_row(K_, kr_, 1), qf1, a);
+      c = mfma(frag_row(V_, kr_, 1), df1, c);
+      s[bb] = a;
+      dp[bb] = c;
+    }
     const bool full = k0 + TILE <= kvl && (!p.causal || k0 + TILE - 1 <= q0 + 16 * w);
     f32x4 ds[4];
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
-      const int kr_ = prow(bb, li);
-      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-      s = mfma(frag_row(Ks, kr_, 0), qf0, s);
-      s = mfma(frag_row(Ks, kr_, 1), qf1, s);
-      dp = mfma(frag_row(Vs, kr_, 0), df0, dp);
-      dp = mfma(frag_row(Vs, kr_, 1), df1, dp);
       const unsigned kp = p.p_drop > 0.f ? keep4_rows(hs, qgbase, k0 + arow(bb, g, 0), li & 3, thr) : 0xfu;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + arow(bb, g, r);
-        const bool valid = full || (key < kvl && !(p.causal && key > qrow));
-        const float pr = valid ? exp2f(s[r] * sl2 - lse2) : 0.f;
-        float dpv = dp[r];
+        float x = s[bb][r] * sl2 - lse2;
+        if (!full) x = (key >= kvl || (p.causal && key > qrow)) ? -INFINITY : x;
+        const float pr = ex2(x);
+        float dpv = dp[bb][r];
         if (p.p_drop > 0.f) dpv = (kp >> r) & 1u ? dpv * keep_scale : 0.f;
         ds[bb][r] = pr * (dpv - dlt);
       }
@@ -342,9 +371,15 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
     const bf16x8 sf0 = pack2(ds[0], ds[1]), sf1 = pack2(ds[2], ds[3]);
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
-      acc[db] = mfma(frag_tr(Ks, 0, db * 16), sf0, acc[db]);
-      acc[db] = mfma(frag_tr(Ks, 32, db * 16), sf1, acc[db]);
+      acc[db] = mfma(frag_tr(K_, 0, db * 16), sf0, acc[db]);
+      acc[db] = mfma(frag_tr(K_, 32, db * 16), sf1, acc[db]);
     }
+    // unconditional: past the end these stage clamped rows into the idle buffer, never read
+    tile_store<NTH>(kr, Ks[(t + 1) & 1]);
+    tile_store<NTH>(vr, Vs[(t + 1) & 1]);
+    tile_load<NTH>(kr, Kb, p.k_rs, k0 + 2 * TILE, kvl);
+    tile_load<NTH>(vr, Vb, p.v_rs, k0 + 2 * TILE, kvl);
+    lds_bar();
   }
   if (qrow < p.Sq) {
     bf16* dQ = p.dq + b * p.dq_bs + (long long)qrow * p.dq_rs + h * D;
@@ -356,11 +391,12 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
 // =============================================================================== dK/dV pass
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(AttnParams p) {
-  constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; query (key) rows per block
-  __shared__ __attribute__((aligned(16))) bf16 Qs[TILE * LS];
-  __shared__ __attribute__((aligned(16))) bf16 dOs[TILE * LS];
-  __shared__ float lse_s[TILE], dlt_s[TILE];
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
+  constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; key rows per block
+  __shared__ __attribute__((aligned(16))) bf16 Qs[2][TILE * LS];
+  __shared__ __attribute__((aligned(16))) bf16 dOs[2][TILE * LS];
+  __shared__ __attribute__((aligned(16))) float lse_s[2][TILE];
+  __shared__ __attribute__((aligned(16))) float dlt_s[2][TILE];
+  const int l = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = l >> 4, li = l & 15;
   const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * RB;
   const int bh = b * p.H + h;
   const uint32_t hs = head_seed(p, bh);
@@ -368,8 +404,29 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(AttnParams p) {
   const bf16* Kb = p.k + b * p.k_bs + h * D;
   const bf16* Vb = p.v + b * p.v_bs + h * D;
   const bf16* dOb = p.dout + b * p.o_bs + h * D;
+  const float* lseb = p.lse + (long long)bh * p.Sq;
+  const float* dltb = p.delta + (long long)bh * p.Sq;
   const int kvl = p.kv_len ? min(p.kv_len[b], p.Sk) : p.Sk;
   const int krow = k0 + 16 * w + li;  // this lane's key
+  const int qstart = p.causal ? (k0 / TILE) * TILE : 0;
+  const int ntiles = k0 < kvl ? (p.Sq - qstart + TILE - 1) / TILE : 0;
+  // row statistics of the staged query tile: thread i < TILE carries query q0 + i
+  // (unconditional loads, clamped row; padded rows get lse = +inf -> P = 0, delta = 0 at the store)
+  auto stat_load = [&](int q0, float& ls, float& dl) {
+    const int qq = min(q0 + (int)(threadIdx.x & (TILE - 1)), p.Sq - 1);
+    ls = lseb[qq];
+    dl = dltb[qq];
+  };
+  auto stat_store = [&](int q0, int buf, float ls, float dl) {
+    const bool ok = q0 + (int)threadIdx.x < p.Sq;
+    lse_s[buf][threadIdx.x] = ok ? ls * LOG2E : INFINITY;
+    dlt_s[buf][threadIdx.x] = ok ? dl : 0.f;
+  };
+  TileRegs qr, dr;
+  float nls = 0.f, ndl = 0.f;
+  tile_load<NTH>(qr, Qb, p.q_rs, qstart, p.Sq);
+  tile_load<NTH>(dr, dOb, p.o_rs, qstart, p.Sq);
+  stat_load(qstart, nls, ndl);
   const bf16x8 kf0 = frag_global(Kb, p.k_rs, krow, kvl, 0), kf1 = frag_global(Kb, p.k_rs, krow, kvl, 1);
   const bf16x8 vf0 = frag_global(Vb, p.v_rs, krow, kvl, 0), vf1 = frag_global(Vb, p.v_rs, krow, kvl, 1);
   const float sl2 = p.scale * LOG2E;
@@ -378,58 +435,72 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(AttnParams p) {
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int db = 0; db < 4; ++db) { dk[db] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[db] = f32x4{0.f, 0.f, 0.f, 0.f}; }
-  const int qstart = p.causal ? (k0 / TILE) * TILE : 0;
-  const int ntiles = k0 < kvl ? (p.Sq - qstart + TILE - 1) / TILE : 0;
-  TileRegs qr, dr;
-  if (ntiles > 0) { tile_load<NTH>(qr, Qb, p.q_rs, qstart, p.Sq); tile_load<NTH>(dr, dOb, p.o_rs, qstart, p.Sq); }
+  tile_store<NTH>(qr, Qs[0]);
+  tile_store<NTH>(dr, dOs[0]);
+  if (threadIdx.x < TILE) stat_store(qstart, 0, nls, ndl);
+  tile_load<NTH>(qr, Qb, p.q_rs, qstart + TILE, p.Sq);
+  tile_load<NTH>(dr, dOb, p.o_rs, qstart + TILE, p.Sq);
+  stat_load(qstart + TILE, nls, ndl);
+  lds_bar();
+  // wave-uniform: this wave's 16 keys all valid (padded query rows are handled by lse = +inf)
+  const bool keys_ok = k0 + 16 * w + 15 < kvl;
   for (int t = 0; t < ntiles; ++t) {
     const int q0 = qstart + t * TILE;
-    __syncthreads();
-    tile_store<NTH>(qr, Qs);
-    tile_store<NTH>(dr, dOs);
-    if (threadIdx.x < TILE) {
-      const int qq = q0 + threadIdx.x;
-      lse_s[threadIdx.x] = qq < p.Sq ? p.lse[(long long)bh * p.Sq + qq] * LOG2E : INFINITY;
-      dlt_s[threadIdx.x] = qq < p.Sq ? p.delta[(long long)bh * p.Sq + qq] : 0.f;
-    }
-    __syncthreads();
-    if (t + 1 < ntiles) { tile_load<NTH>(qr, Qb, p.q_rs, q0 + TILE, p.Sq); tile_load<NTH>(dr, dOb, p.o_rs, q0 + TILE, p.Sq); }
-    f32x4 pp[4], ds[4];
-    // wave-uniform: this wave's 16 keys valid against every query of the tile
-    const bool full = k0 + 16 * w + 15 < kvl && q0 + TILE <= p.Sq && (!p.causal || k0 + 16 * w + 15 <= q0);
+    const int cur = t & 1;
+    const bf16* Q_ = Qs[cur];
+    const bf16* O_ = dOs[cur];
+    f32x4 s[4], dp[4];
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
       const int qr_ = prow(bb, li);
-      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-      s = mfma(frag_row(Qs, qr_, 0), kf0, s);
-      s = mfma(frag_row(Qs, qr_, 1), kf1, s);
-      dp = mfma(frag_row(dOs, qr_, 0), vf0, dp);
-      dp = mfma(frag_row(dOs, qr_, 1), vf1, dp);
-      const unsigned kp = p.p_drop > 0.f ? keep4_cols(hs, (q0 + arow(bb, g, 0)) >> 2, p.Sk, krow, thr) : 0xfu;
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
+      a = mfma(frag_row(Q_, qr_, 0), kf0, a);
+      c = mfma(frag_row(O_, qr_, 0), vf0, c);
+      a = mfma(frag_row(Q_, qr_, 1), kf1, a);
+      c = mfma(frag_row(O_, qr_, 1), vf1, c);
+      s[bb] = a;
+      dp[bb] = c;
+    }
+    const bool full = keys_ok && (!p.causal || k0 + 16 * w + 15 <= q0);
+    f32x4 pp[4], ds[4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int rb = 32 * (bb >> 1) + 8 * g + 4 * (bb & 1);  // tile rows arow(bb, g, 0..3)
+      const f32x4 L = *(const f32x4*)&lse_s[cur][rb];
+      const f32x4 Dl = *(const f32x4*)&dlt_s[cur][rb];
+      const unsigned kp = p.p_drop > 0.f ? keep4_cols(hs, (q0 + rb) >> 2, p.Sk, krow, thr) : 0xfu;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int qt = arow(bb, g, r), qq = q0 + qt;
-        const bool valid = full || (krow < kvl && qq < p.Sq && !(p.causal && krow > qq));
-        const float pr = valid ? exp2f(s[r] * sl2 - lse_s[qt]) : 0.f;
-        float pd = pr, dpv = dp[r];
+        float x = s[bb][r] * sl2 - L[r];
+        if (!full) x = (krow >= kvl || (p.causal && krow > q0 + rb + r)) ? -INFINITY : x;
+        const float pr = ex2(x);
+        float pd = pr, dpv = dp[bb][r];
         if (p.p_drop > 0.f) {
           const bool keep = (kp >> r) & 1u;
           pd = keep ? pr * keep_scale : 0.f;
           dpv = keep ? dpv * keep_scale : 0.f;
         }
         pp[bb][r] = pd;
-        ds[bb][r] = pr * (dpv - dlt_s[qt]);
+        ds[bb][r] = pr * (dpv - Dl[r]);
       }
     }
     const bf16x8 pf0 = pack2(pp[0], pp[1]), pf1 = pack2(pp[2], pp[3]);
     const bf16x8 sf0 = pack2(ds[0], ds[1]), sf1 = pack2(ds[2], ds[3]);
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
-      dv[db] = mfma(frag_tr(dOs, 0, db * 16), pf0, dv[db]);
-      dv[db] = mfma(frag_tr(dOs, 32, db * 16), pf1, dv[db]);
-      dk[db] = mfma(frag_tr(Qs, 0, db * 16), sf0, dk[db]);
-      dk[db] = mfma(frag_tr(Qs, 32, db * 16), sf1, dk[db]);
+      dv[db] = mfma(frag_tr(O_, 0, db * 16), pf0, dv[db]);
+      dk[db] = mfma(frag_tr(Q_, 0, db * 16), sf0, dk[db]);
+      dv[db] = mfma(frag_tr(O_, 32, db * 16), pf1, dv[db]);
+      dk[db] = mfma(frag_tr(Q_, 32, db * 16), sf1, dk[db]);
     }
+    // unconditional: past the end these stage clamped rows into the idle buffer, never read
+    tile_store<NTH>(qr, Qs[cur ^ 1]);
+    tile_store<NTH>(dr, dOs[cur ^ 1]);
+    if (threadIdx.x < TILE) stat_store(q0 + TILE, cur ^ 1, nls, ndl);
+    tile_load<NTH>(qr, Qb, p.q_rs, q0 + 2 * TILE, p.Sq);
+    tile_load<NTH>(dr, dOb, p.o_rs, q0 + 2 * TILE, p.Sq);
+    stat_load(q0 + 2 * TILE, nls, ndl);
+    lds_bar();
   }
   if (krow < p.Sk) {
     bf16* dK = p.dk + b * p.dk_bs + (long long)krow * p.dk_rs + h * D;

@@ -164,6 +164,8 @@ __device__ __forceinline__ void lds_bar() {
   asm volatile("" ::: "memory");
 }
 
+// Occupancy: the 8-wave kernels are held to <= 128 VGPRs (waves_per_eu 4) so two 512-thread blocks
+// share a CU (2 x 37 KiB of LDS); the backward kernels work on 32-row halves of each tile to fit.
 // Every kernel stages its streamed 64-row tiles global -> registers -> LDS through a DOUBLE-buffered
 // LDS ring with one barrier per tile: tile t+1 (loaded into registers during tile t-1) is stored
 // into the idle buffer after tile t's math, and tile t+2's global loads are issued right behind it,
@@ -172,7 +174,7 @@ __device__ __forceinline__ void lds_bar() {
 
 // =============================================================================== forward
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(AttnParams p) {
   constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; query rows per block
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][TILE * LS];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][TILE * LS];
@@ -286,7 +288,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
 
 // =============================================================================== dQ pass
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; query rows per block
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][TILE * LS];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][TILE * LS];
@@ -340,39 +342,40 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
     const int k0 = t * TILE;
     const bf16* K_ = Ks[t & 1];
     const bf16* V_ = Vs[t & 1];
-    f32x4 s[4], dp[4];
-#pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-      const int kr_ = prow(bb, li);
-      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
-      a = mfma(frag_row(K_, kr_, 0), qf0, a);
-      c = mfma(frag_row(V_, kr_, 0), df0, c);
-      a = mfma(frag_row(K_, kr_, 1), qf1, a);
-      c = mfma(frag_row(V_, kr_, 1), df1, c);
-      s[bb] = a;
-      dp[bb] = c;
-    }
     const bool full = k0 + TILE <= kvl && (!p.causal || k0 + TILE - 1 <= q0 + 16 * w);
-    f32x4 ds[4];
+    // two 32-key halves: S/dP of blocks 2hh, 2hh+1 -> dS -> its dQ MFMAs (k-slots 32hh..32hh+31)
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-      const unsigned kp = p.p_drop > 0.f ? keep4_rows(hs, qgbase, k0 + arow(bb, g, 0), li & 3, thr) : 0xfu;
+    for (int hh = 0; hh < 2; ++hh) {
+      f32x4 s[2], dp[2], ds[2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + arow(bb, g, r);
-        float x = s[bb][r] * sl2 - lse2;
-        if (!full) x = (key >= kvl || (p.causal && key > qrow)) ? -INFINITY : x;
-        const float pr = ex2(x);
-        float dpv = dp[bb][r];
-        if (p.p_drop > 0.f) dpv = (kp >> r) & 1u ? dpv * keep_scale : 0.f;
-        ds[bb][r] = pr * (dpv - dlt);
+      for (int j = 0; j < 2; ++j) {
+        const int kr_ = prow(2 * hh + j, li);
+        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
+        a = mfma(frag_row(K_, kr_, 0), qf0, a);
+        c = mfma(frag_row(V_, kr_, 0), df0, c);
+        a = mfma(frag_row(K_, kr_, 1), qf1, a);
+        c = mfma(frag_row(V_, kr_, 1), df1, c);
+        s[j] = a;
+        dp[j] = c;
       }
-    }
-    const bf16x8 sf0 = pack2(ds[0], ds[1]), sf1 = pack2(ds[2], ds[3]);
 #pragma unroll
-    for (int db = 0; db < 4; ++db) {
-      acc[db] = mfma(frag_tr(K_, 0, db * 16), sf0, acc[db]);
-      acc[db] = mfma(frag_tr(K_, 32, db * 16), sf1, acc[db]);
+      for (int j = 0; j < 2; ++j) {
+        const int bb = 2 * hh + j;
+        const unsigned kp = p.p_drop > 0.f ? keep4_rows(hs, qgbase, k0 + arow(bb, g, 0), li & 3, thr) : 0xfu;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + arow(bb, g, r);
+          float x = s[j][r] * sl2 - lse2;
+          if (!full) x = (key >= kvl || (p.causal && key > qrow)) ? -INFINITY : x;
+          const float pr = ex2(x);
+          float dpv = dp[j][r];
+          if (p.p_drop > 0.f) dpv = (kp >> r) & 1u ? dpv * keep_scale : 0.f;
+          ds[j][r] = pr * (dpv - dlt);
+        }
+      }
+      const bf16x8 sf = pack2(ds[0], ds[1]);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) acc[db] = mfma(frag_tr(K_, 32 * hh, db * 16), sf, acc[db]);
     }
     // unconditional: past the end these stage clamped rows into the idle buffer, never read
     tile_store<NTH>(kr, Ks[(t + 1) & 1]);
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
 
 // =============================================================================== dK/dV pass
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(AttnParams p) {
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dkv_kernel(AttnParams p) {
   constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; key rows per block
   __shared__ __attribute__((aligned(16))) bf16 Qs[2][TILE * LS];
   __shared__ __attribute__((aligned(16))) bf16 dOs[2][TILE * LS];
@@ -449,49 +452,51 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(AttnParams p) {
     const int cur = t & 1;
     const bf16* Q_ = Qs[cur];
     const bf16* O_ = dOs[cur];
-    f32x4 s[4], dp[4];
-#pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-      const int qr_ = prow(bb, li);
-      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
-      a = mfma(frag_row(Q_, qr_, 0), kf0, a);
-      c = mfma(frag_row(O_, qr_, 0), vf0, c);
-      a = mfma(frag_row(Q_, qr_, 1), kf1, a);
-      c = mfma(frag_row(O_, qr_, 1), vf1, c);
-      s[bb] = a;
-      dp[bb] = c;
-    }
     const bool full = keys_ok && (!p.causal || k0 + 16 * w + 15 <= q0);
-    f32x4 pp[4], ds[4];
+    // two 32-query halves: S/dP of blocks 2hh, 2hh+1 -> P, dS -> their dV / dK MFMAs (k-slots
+    // 32hh..32hh+31); half the live score registers of a whole-tile pass
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-      const int rb = 32 * (bb >> 1) + 8 * g + 4 * (bb & 1);  // tile rows arow(bb, g, 0..3)
-      const f32x4 L = *(const f32x4*)&lse_s[cur][rb];
-      const f32x4 Dl = *(const f32x4*)&dlt_s[cur][rb];
-      const unsigned kp = p.p_drop > 0.f ? keep4_cols(hs, (q0 + rb) >> 2, p.Sk, krow, thr) : 0xfu;
+    for (int hh = 0; hh < 2; ++hh) {
+      f32x4 s[2], dp[2], pp[2], ds[2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float x = s[bb][r] * sl2 - L[r];
-        if (!full) x = (krow >= kvl || (p.causal && krow > q0 + rb + r)) ? -INFINITY : x;
-        const float pr = ex2(x);
-        float pd = pr, dpv = dp[bb][r];
-        if (p.p_drop > 0.f) {
-          const bool keep = (kp >> r) & 1u;
-          pd = keep ? pr * keep_scale : 0.f;
-          dpv = keep ? dpv * keep_scale : 0.f;
-        }
-        pp[bb][r] = pd;
-        ds[bb][r] = pr * (dpv - Dl[r]);
+      for (int j = 0; j < 2; ++j) {
+        const int qr_ = prow(2 * hh + j, li);
+        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
+        a = mfma(frag_row(Q_, qr_, 0), kf0, a);
+        c = mfma(frag_row(O_, qr_, 0), vf0, c);
+        a = mfma(frag_row(Q_, qr_, 1), kf1, a);
+        c = mfma(frag_row(O_, qr_, 1), vf1, c);
+        s[j] = a;
+        dp[j] = c;
       }
-    }
-    const bf16x8 pf0 = pack2(pp[0], pp[1]), pf1 = pack2(pp[2], pp[3]);
-    const bf16x8 sf0 = pack2(ds[0], ds[1]), sf1 = pack2(ds[2], ds[3]);
 #pragma unroll
-    for (int db = 0; db < 4; ++db) {
-      dv[db] = mfma(frag_tr(O_, 0, db * 16), pf0, dv[db]);
-      dk[db] = mfma(frag_tr(Q_, 0, db * 16), sf0, dk[db]);
-      dv[db] = mfma(frag_tr(O_, 32, db * 16), pf1, dv[db]);
-      dk[db] = mfma(frag_tr(Q_, 32, db * 16), sf1, dk[db]);
+      for (int j = 0; j < 2; ++j) {
+        const int bb = 2 * hh + j;
+        const int rb = 32 * (bb >> 1) + 8 * g + 4 * (bb & 1);  // tile rows arow(bb, g, 0..3)
+        const f32x4 L = *(const f32x4*)&lse_s[cur][rb];
+        const f32x4 Dl = *(const f32x4*)&dlt_s[cur][rb];
+        const unsigned kp = p.p_drop > 0.f ? keep4_cols(hs, (q0 + rb) >> 2, p.Sk, krow, thr) : 0xfu;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = s[j][r] * sl2 - L[r];
+          if (!full) x = (krow >= kvl || (p.causal && krow > q0 + rb + r)) ? -INFINITY : x;
+          const float pr = ex2(x);
+          float pd = pr, dpv = dp[j][r];
+          if (p.p_drop > 0.f) {
+            const bool keep = (kp >> r) & 1u;
+            pd = keep ? pr * keep_scale : 0.f;
+            dpv = keep ? dpv * keep_scale : 0.f;
+          }
+          pp[j][r] = pd;
+          ds[j][r] = pr * (dpv - Dl[r]);
+        }
+      }
+      const bf16x8 pf = pack2(pp[0], pp[1]), sf = pack2(ds[0], ds[1]);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        dv[db] = mfma(frag_tr(O_, 32 * hh, db * 16), pf, dv[db]);
+        dk[db] = mfma(frag_tr(Q_, 32 * hh, db * 16), sf, dk[db]);
+      }
     }
     // unconditional: past the end these stage clamped rows into the idle buffer, never read
     tile_store<NTH>(qr, Qs[cur ^ 1]);

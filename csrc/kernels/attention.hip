@@ -19,6 +19,7 @@
 // Backward = two kernels (no atomics, deterministic): dQ pass (grid over query tiles, recompute
 // P and dP, dQ = dS K) and dK/dV pass (grid over key tiles, dV = P^T dO, dK = dS^T Q).
 #include "common.h"
+#include <type_traits>
 
 namespace {
 constexpr int D = 64;
@@ -65,7 +66,10 @@ __device__ __forceinline__ void tile_load(TileRegs& t, const bf16* base, int rs,
   for (int it = 0; it < 512 / NTH; ++it) {
     const int c = threadIdx.x + it * NTH, row = c >> 3, col = (c & 7) * 8;
     t.ok[it] = row0 + row < nvalid;
-    t.v[it] = *(const u32x4*)(base + (long long)max(min(row0 + row, nvalid - 1), 0) * rs + col);
+    // 32-bit byte offset from the block-uniform base: the SGPR-base + VGPR-offset load form (a
+    // head's rows span < 4 GiB), no 64-bit per-lane address pairs held across the loop
+    const unsigned off = (unsigned)(max(min(row0 + row, nvalid - 1), 0) * rs + col) * 2u;
+    t.v[it] = *(const u32x4*)((const char*)base + off);
   }
 }
 template <int NTH>
@@ -169,11 +173,19 @@ __device__ __forceinline__ void lds_bar() {
 // Every kernel stages its streamed 64-row tiles global -> registers -> LDS through a DOUBLE-buffered
 // LDS ring with one barrier per tile: tile t+1 (loaded into registers during tile t-1) is stored
 // into the idle buffer after tile t's math, and tile t+2's global loads are issued right behind it,
-// so a whole tile of MFMA work covers each load. The per-element softmax / mask / dropout math is
-// branch-free (wave-uniform `full` selects the unmasked form; masked elements get a -inf exponent).
+// so a whole tile of MFMA work covers each load.
+//
+// The kernels are VALU-issue bound (one v_exp and ~5-10 other VALU ops per score element against
+// 1/16 of a 16x16x32 MFMA), so the element math is specialised: DROP (template: p_drop > 0) and
+// FULL (per tile, wave-uniform: no mask needed) pick one of four straight-line bodies, instead of
+// one body that evaluates the masks and both dropout arms for every element. The dropout keep
+// scale is applied once per output row / accumulator instead of per element (O and dV are linear
+// in the kept P; dS = P (dP_kept * scale - delta) is one FMA).
+template <bool B>
+using bconst = std::integral_constant<bool, B>;
 
 // =============================================================================== forward
-template <int NW>
+template <int NW, bool DROP>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(AttnParams p) {
   constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; query rows per block
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][TILE * LS];
@@ -197,9 +209,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(Attn
   const bf16x8 qf0 = frag_global(Qb, p.q_rs, qrow, p.Sq, 0), qf1 = frag_global(Qb, p.q_rs, qrow, p.Sq, 1);
   const float sl2 = p.scale * LOG2E;
   const int thr = drop_thr(p.p_drop);
-  const float keep_scale = p.p_drop > 0.f ? 256.f / (float)(256 - thr) : 1.f;
+  const float keep_scale = DROP ? 256.f / (float)(256 - thr) : 1.f;
   const int qgbase = (qrow >> 2) * p.Sk;
-  float m = -INFINITY, lsum = 0.f;
+  float m = -INFINITY, lsum = 0.f;  // running max (log2 units) and row sum of the UNdropped P
   f32x4 oacc[4];
 #pragma unroll
   for (int db = 0; db < 4; ++db) oacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -224,45 +236,51 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(Attn
     }
     // wave-uniform: every (query, key) of this wave's tile valid -> no per-element mask
     const bool full = k0 + TILE <= kvl && (!p.causal || k0 + TILE - 1 <= q0 + 16 * w);
-    float mx = -INFINITY;
+    auto body = [&](auto FULL) {
+      constexpr bool F = decltype(FULL)::value;
+      // max over the RAW scores (scale > 0), masked ones -inf; exp2(s * sl2 - m) is one FMA + v_exp
+      float mx = -INFINITY;
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb)
+      for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + arow(bb, g, r);
-        float v = s[bb][r] * sl2;
-        if (!full) v = (key >= kvl || (p.causal && key > qrow)) ? -INFINITY : v;
-        s[bb][r] = v;
-        mx = fmaxf(mx, v);
+        for (int r = 0; r < 4; ++r) {
+          if (!F) {
+            const int key = k0 + arow(bb, g, r);
+            if (key >= kvl || (p.causal && key > qrow)) s[bb][r] = -INFINITY;
+          }
+          mx = fmaxf(mx, s[bb][r]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx * sl2);
+      const float muse = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = ex2(m - muse);
+      float rs = 0.f;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = ex2(fmaf(s[bb][r], sl2, -muse));
+          rs += e;
+          s[bb][r] = e;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      lsum = lsum * alpha + rs;
+      m = mnew;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) oacc[db] *= alpha;
+      if (DROP) {
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const unsigned kp = keep4_rows(hs, qgbase, k0 + arow(bb, g, 0), li & 3, thr);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[bb][r] = (kp & (1u << r)) ? s[bb][r] : 0.f;
+        }
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx);
-    const float muse = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = ex2(m - muse);
-    float rs = 0.f;
-#pragma unroll
-    for (int bb = 0; bb < 4; ++bb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = ex2(s[bb][r] - muse);
-        rs += e;
-        s[bb][r] = e;
-      }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    lsum = lsum * alpha + rs;
-    m = mnew;
-#pragma unroll
-    for (int db = 0; db < 4; ++db) oacc[db] *= alpha;
-    if (p.p_drop > 0.f) {
-#pragma unroll
-      for (int bb = 0; bb < 4; ++bb) {
-        const unsigned kp = keep4_rows(hs, qgbase, k0 + arow(bb, g, 0), li & 3, thr);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s[bb][r] = (kp >> r) & 1u ? s[bb][r] * keep_scale : 0.f;
-      }
-    }
+    };
+    if (full) body(bconst<true>{});
+    else body(bconst<false>{});
     const bf16x8 pf0 = pack2(s[0], s[1]), pf1 = pack2(s[2], s[3]);
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
@@ -277,7 +295,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(Attn
     lds_bar();
   }
   if (qrow < p.Sq) {
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    const float inv = lsum > 0.f ? keep_scale / lsum : 0.f;
     bf16* O = p.out + b * p.o_bs + (long long)qrow * p.o_rs + h * D;
 #pragma unroll
     for (int db = 0; db < 4; ++db) store_rowvec4(O + db * 16 + 4 * g, oacc[db], inv);
@@ -287,7 +305,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(Attn
 }
 
 // =============================================================================== dQ pass
-template <int NW>
+template <int NW, bool DROP>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; query rows per block
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][TILE * LS];
@@ -312,7 +330,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dq_kernel(A
   const bf16x8 df0 = frag_global(dOb, p.o_rs, qrow, p.Sq, 0), df1 = frag_global(dOb, p.o_rs, qrow, p.Sq, 1);
   const float sl2 = p.scale * LOG2E;
   const int thr = drop_thr(p.p_drop);
-  const float keep_scale = p.p_drop > 0.f ? 256.f / (float)(256 - thr) : 1.f;
+  const float keep_scale = DROP ? 256.f / (float)(256 - thr) : 1.f;
   const int qgbase = (qrow >> 2) * p.Sk;
   const float lse2 = qrow < p.Sq ? p.lse[(long long)bh * p.Sq + min(qrow, p.Sq - 1)] * LOG2E : INFINITY;
   // delta = rowsum(dO * O) of this lane's query, from the dO fragments already in registers + the
@@ -358,21 +376,32 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dq_kernel(A
         s[j] = a;
         dp[j] = c;
       }
+      auto body = [&](auto FULL) {
+        constexpr bool F = decltype(FULL)::value;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int bb = 2 * hh + j;
-        const unsigned kp = p.p_drop > 0.f ? keep4_rows(hs, qgbase, k0 + arow(bb, g, 0), li & 3, thr) : 0xfu;
+        for (int j = 0; j < 2; ++j) {
+          const int bb = 2 * hh + j;
+          unsigned kp = 0xfu;
+          if (DROP) kp = keep4_rows(hs, qgbase, k0 + arow(bb, g, 0), li & 3, thr);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + arow(bb, g, r);
-          float x = s[j][r] * sl2 - lse2;
-          if (!full) x = (key >= kvl || (p.causal && key > qrow)) ? -INFINITY : x;
-          const float pr = ex2(x);
-          float dpv = dp[j][r];
-          if (p.p_drop > 0.f) dpv = (kp >> r) & 1u ? dpv * keep_scale : 0.f;
-          ds[j][r] = pr * (dpv - dlt);
+          for (int r = 0; r < 4; ++r) {
+            float x = fmaf(s[j][r], sl2, -lse2);
+            if (!F) {
+              const int key = k0 + arow(bb, g, r);
+              if (key >= kvl || (p.causal && key > qrow)) x = -INFINITY;
+            }
+            const float pr = ex2(x);
+            if (DROP) {
+              const float dpk = (kp & (1u << r)) ? dp[j][r] : 0.f;
+              ds[j][r] = pr * fmaf(dpk, keep_scale, -dlt);
+            } else {
+              ds[j][r] = pr * (dp[j][r] - dlt);
+            }
+          }
         }
-      }
+      };
+      if (full) body(bconst<true>{});
+      else body(bconst<false>{});
       const bf16x8 sf = pack2(ds[0], ds[1]);
 #pragma unroll
       for (int db = 0; db < 4; ++db) acc[db] = mfma(frag_tr(K_, 32 * hh, db * 16), sf, acc[db]);
@@ -392,7 +421,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dq_kernel(A
 }
 
 // =============================================================================== dK/dV pass
-template <int NW>
+template <int NW, bool DROP>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dkv_kernel(AttnParams p) {
   constexpr int NTH = NW * 64, RB = 16 * NW;  // threads; key rows per block
   __shared__ __attribute__((aligned(16))) bf16 Qs[2][TILE * LS];
@@ -434,7 +463,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dkv_kernel(
   const bf16x8 vf0 = frag_global(Vb, p.v_rs, krow, kvl, 0), vf1 = frag_global(Vb, p.v_rs, krow, kvl, 1);
   const float sl2 = p.scale * LOG2E;
   const int thr = drop_thr(p.p_drop);
-  const float keep_scale = p.p_drop > 0.f ? 256.f / (float)(256 - thr) : 1.f;
+  const float keep_scale = DROP ? 256.f / (float)(256 - thr) : 1.f;
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int db = 0; db < 4; ++db) { dk[db] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[db] = f32x4{0.f, 0.f, 0.f, 0.f}; }
@@ -469,28 +498,34 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dkv_kernel(
         s[j] = a;
         dp[j] = c;
       }
+      auto body = [&](auto FULL) {
+        constexpr bool F = decltype(FULL)::value;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int bb = 2 * hh + j;
-        const int rb = 32 * (bb >> 1) + 8 * g + 4 * (bb & 1);  // tile rows arow(bb, g, 0..3)
-        const f32x4 L = *(const f32x4*)&lse_s[cur][rb];
-        const f32x4 Dl = *(const f32x4*)&dlt_s[cur][rb];
-        const unsigned kp = p.p_drop > 0.f ? keep4_cols(hs, (q0 + rb) >> 2, p.Sk, krow, thr) : 0xfu;
+        for (int j = 0; j < 2; ++j) {
+          const int bb = 2 * hh + j;
+          const int rb = 32 * (bb >> 1) + 8 * g + 4 * (bb & 1);  // tile rows arow(bb, g, 0..3)
+          const f32x4 L = *(const f32x4*)&lse_s[cur][rb];
+          const f32x4 Dl = *(const f32x4*)&dlt_s[cur][rb];
+          unsigned kp = 0xfu;
+          if (DROP) kp = keep4_cols(hs, (q0 + rb) >> 2, p.Sk, krow, thr);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float x = s[j][r] * sl2 - L[r];
-          if (!full) x = (krow >= kvl || (p.causal && krow > q0 + rb + r)) ? -INFINITY : x;
-          const float pr = ex2(x);
-          float pd = pr, dpv = dp[j][r];
-          if (p.p_drop > 0.f) {
-            const bool keep = (kp >> r) & 1u;
-            pd = keep ? pr * keep_scale : 0.f;
-            dpv = keep ? dpv * keep_scale : 0.f;
+          for (int r = 0; r < 4; ++r) {
+            float x = fmaf(s[j][r], sl2, -L[r]);
+            if (!F && (krow >= kvl || (p.causal && krow > q0 + rb + r))) x = -INFINITY;
+            const float pr = ex2(x);
+            if (DROP) {
+              const bool keep = kp & (1u << r);
+              pp[j][r] = keep ? pr : 0.f;  // dV is scaled by keep_scale once at the store
+              ds[j][r] = pr * fmaf(keep ? dp[j][r] : 0.f, keep_scale, -Dl[r]);
+            } else {
+              pp[j][r] = pr;
+              ds[j][r] = pr * (dp[j][r] - Dl[r]);
+            }
           }
-          pp[j][r] = pd;
-          ds[j][r] = pr * (dpv - Dl[r]);
         }
-      }
+      };
+      if (full) body(bconst<true>{});
+      else body(bconst<false>{});
       const bf16x8 pf = pack2(pp[0], pp[1]), sf = pack2(ds[0], ds[1]);
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
@@ -513,7 +548,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dkv_kernel(
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
       store_rowvec4(dK + db * 16 + 4 * g, dk[db], p.scale);
-      store_rowvec4(dV + db * 16 + 4 * g, dv[db], 1.f);
+      store_rowvec4(dV + db * 16 + 4 * g, dv[db], keep_scale);
     }
   }
 }
@@ -545,10 +580,14 @@ int tfk_attn_fwd(const void* q, const void* k, const void* v, void* out, float* 
   p.q_bs = strides[0]; p.q_rs = (int)strides[1]; p.k_bs = strides[2]; p.k_rs = (int)strides[3];
   p.v_bs = strides[4]; p.v_rs = (int)strides[5]; p.o_bs = strides[6]; p.o_rs = (int)strides[7];
   p.kv_len = kv_len; p.scale = scale; p.causal = causal; p.p_drop = p_drop; p.seed = seed; p.seed_key = tfk_seed_key();
+  const bool drop = p_drop > 0.f;
+  const dim3 g8((p.Sq + 127) / 128, p.H, p.B), g4((p.Sq + 63) / 64, p.H, p.B);
   if (attn_waves() == 8) {
-    hipLaunchKernelGGL(attn_fwd_kernel<8>, dim3((p.Sq + 127) / 128, p.H, p.B), dim3(512), 0, s, p);
+    if (drop) hipLaunchKernelGGL((attn_fwd_kernel<8, true>), g8, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((attn_fwd_kernel<8, false>), g8, dim3(512), 0, s, p);
   } else {
-    hipLaunchKernelGGL(attn_fwd_kernel<4>, dim3((p.Sq + 63) / 64, p.H, p.B), dim3(256), 0, s, p);
+    if (drop) hipLaunchKernelGGL((attn_fwd_kernel<4, true>), g4, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((attn_fwd_kernel<4, false>), g4, dim3(256), 0, s, p);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -567,13 +606,18 @@ int tfk_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
   p.dv_bs = gstrides[4]; p.dv_rs = (int)gstrides[5];
   p.kv_len = kv_len; p.scale = scale; p.causal = causal; p.p_drop = p_drop; p.seed = seed; p.seed_key = tfk_seed_key();
   // delta = rowsum(dO * O) is computed and stored by the dQ kernel's prologue
+  const bool drop = p_drop > 0.f;
+  const dim3 q8((p.Sq + 127) / 128, p.H, p.B), k8((p.Sk + 127) / 128, p.H, p.B);
+  const dim3 q4((p.Sq + 63) / 64, p.H, p.B), k4((p.Sk + 63) / 64, p.H, p.B);
+#define TFK_ATTN_BWD(NW_, DROP_, GQ, GK)                                                       \
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<NW_, DROP_>), GQ, dim3(NW_ * 64), 0, s, p);          \
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<NW_, DROP_>), GK, dim3(NW_ * 64), 0, s, p);
   if (attn_waves() == 8) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<8>, dim3((p.Sq + 127) / 128, p.H, p.B), dim3(512), 0, s, p);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<8>, dim3((p.Sk + 127) / 128, p.H, p.B), dim3(512), 0, s, p);
+    if (drop) { TFK_ATTN_BWD(8, true, q8, k8) } else { TFK_ATTN_BWD(8, false, q8, k8) }
   } else {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<4>, dim3((p.Sq + 63) / 64, p.H, p.B), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<4>, dim3((p.Sk + 63) / 64, p.H, p.B), dim3(256), 0, s, p);
+    if (drop) { TFK_ATTN_BWD(4, true, q4, k4) } else { TFK_ATTN_BWD(4, false, q4, k4) }
   }
+#undef TFK_ATTN_BWD
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }

@@ -19,6 +19,16 @@
 // u+1's four halves landed, the three halves issued since stay in flight across the raw barrier)
 // and tile u+1 is read from the next phase on ("read a staged buffer one phase after the wait
 // that retires it").
+//
+// Ping-pong: the two wave groups (wr = 0: waves 0-3, wr = 1: waves 4-7) run ONE BARRIER APART --
+// group 1 passes an extra barrier before the loop, group 0 one after it -- so each barrier pairs
+// group 0's "MFMAs done" with group 1's "fragments read", and one group's 16-MFMA cluster runs
+// while the other issues its ds_reads and DMA. Under the stagger a wave may pass the barrier that
+// closes phase p-1 while the other group has only ISSUED its phase p-1 reads, so each phase retires
+// its own ds_reads (lgkmcnt(0)) BEFORE its first barrier: a half-image restaged in phase p (one
+// phase after its last read) is then never overwritten under an in-flight read.
+// (Lockstep form, no stagger: 1046 / 999 TF/s sq4096 fwd / dgrad vs the g4 256x256 tile's
+// 1217 / 1156, profiles/tile_ab_r4b.jsonl.)
 #include "common.h"
 #include "gemm_params.h"
 #include "gemm_epilogue.h"
@@ -133,9 +143,13 @@ __global__ __launch_bounds__(NT, 1) void g8_kernel(GemmParams p) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) rb[kk][j] = frag<BKO>(img, wc * 32 + j * 16, kk);
   };
-  auto quad = [&](int qm, int qn, const bf16x8 (&rb)[2][2]) {
+  // close a phase's load section: own ds_reads retired, then the barrier (see header)
+  auto ready = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    bar();
+  };
+  auto quad = [&](int qm, int qn, const bf16x8 (&rb)[2][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -148,6 +162,7 @@ __global__ __launch_bounds__(NT, 1) void g8_kernel(GemmParams p) {
     __builtin_amdgcn_s_setprio(0);
   };
 
+  if (wr == 1) bar();  // group 1 runs one barrier behind group 0
 #pragma unroll 1
   for (int u = kt0; u < kt1; ++u) {
     const int buf = u & 1;
@@ -155,19 +170,19 @@ __global__ __launch_bounds__(NT, 1) void g8_kernel(GemmParams p) {
     read_a(buf, A0);
     read_b(buf, B0, rb0);
     if (u + 1 < kt1) issue(B0, u + 1);
-    bar();
+    ready();
     quad(0, 0, rb0);
     bar();
     // phase 1: Q(0,1) -- B1; restage A0(u+2)
     read_b(buf, B1, rb1);
     if (u + 2 < kt1) issue(A0, u + 2);
-    bar();
+    ready();
     quad(0, 1, rb1);
     bar();
     // phase 2: Q(1,1) -- A1; restage B1(u+2)
     read_a(buf, A1);
     if (u + 2 < kt1) issue(B1, u + 2);
-    bar();
+    ready();
     quad(1, 1, rb1);
     bar();
     // phase 3: Q(1,0) -- B0 again; restage A1(u+2); tile u+1 must be complete after this phase
@@ -178,10 +193,11 @@ __global__ __launch_bounds__(NT, 1) void g8_kernel(GemmParams p) {
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    bar();
+    ready();
     quad(1, 0, rb0);
     bar();
   }
+  if (wr == 0) bar();  // re-align the groups: every wave has passed the same barrier count
   __syncthreads();
   constexpr int WPS = 2;  // waves per SIMD
   gemm_epilogue<BM, BN, NT, 2, EPI, (512 / WPS >= 256 ? 4 : 2), false, true>(p, acc, smem, m0, n0, bz);

@@ -54,11 +54,12 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
-// AM: KIN (dense A [M][K]) or CONV_FWD (implicit-GEMM gather of NHWC x, Cin % 64 == 0: a K-tile
-// is one (r, s) tap x 64 channels); BMD: KIN or KOUT.
+// AM: KIN (dense A [M][K]), KOUT (dense A stored [K][M]: weight gradients dY^T X) or CONV_FWD
+// (implicit-GEMM gather of NHWC x, Cin % 64 == 0: a K-tile is one (r, s) tap x 64 channels);
+// BMD: KIN or KOUT.
 template <int AM, int BMD, int EPI>
 __global__ __launch_bounds__(NT, 1) void g8_kernel(GemmParams p) {
-  constexpr bool BKO = (BMD == KOUT);
+  constexpr bool AKO = (AM == KOUT), BKO = (BMD == KOUT);
   constexpr int MAIN = 2 * BUF, EPIB = epi_lds_bytes<BM, BN, 2>();
   __shared__ __attribute__((aligned(16))) char smem[MAIN > EPIB ? MAIN : EPIB];
 
@@ -81,11 +82,12 @@ __global__ __launch_bounds__(NT, 1) void g8_kernel(GemmParams p) {
   // one loader per half-image (its rows are the half's 128 rows)
   const char* Abase = (const char*)p.A + (long long)bz * p.sA * 2;
   const char* Bbase = (const char*)p.B + (long long)bz * p.sB * 2;
-  const char* Ah[2] = {AM == CONV_FWD ? Abase : Abase + (long long)m0 * p.lda * 2,
-                       AM == CONV_FWD ? Abase : Abase + (long long)(m0 + HALF) * p.lda * 2};
+  const char* Ah[2] = {AM == CONV_FWD ? Abase : Abase + (AKO ? (long long)m0 * 2 : (long long)m0 * p.lda * 2),
+                       AM == CONV_FWD ? Abase
+                                      : Abase + (AKO ? (long long)(m0 + HALF) * 2 : (long long)(m0 + HALF) * p.lda * 2)};
   const char* Bh[2] = {Bbase + (BKO ? (long long)n0 * 2 : (long long)n0 * p.ldb * 2),
                        Bbase + (BKO ? (long long)(n0 + HALF) * 2 : (long long)(n0 + HALF) * p.ldb * 2)};
-  const long long a_step = BK * 2;
+  const long long a_step = AKO ? (long long)BK * p.lda * 2 : BK * 2;
   const long long b_step = BKO ? (long long)BK * p.ldb * 2 : BK * 2;
   const int lim_a[2] = {p.M - m0, p.M - m0 - HALF};
   const int lim_b[2] = {p.N - n0, p.N - n0 - HALF};
@@ -134,7 +136,7 @@ __global__ __launch_bounds__(NT, 1) void g8_kernel(GemmParams p) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ra[kk][i] = frag<false>(img, wr * 64 + i * 16, kk);
+      for (int i = 0; i < 4; ++i) ra[kk][i] = frag<AKO>(img, wr * 64 + i * 16, kk);
   };
   auto read_b = [&](int buf, int h, bf16x8 (&rb)[2][2]) {
     const char* img = himg(buf, h);
@@ -218,7 +220,8 @@ static bool g8_on() {
 extern "C" int tfk_g8_launch(const GemmParams& p_in, int amode, int bmode, int epi, int batch, int splits,
                              hipStream_t stream) {
   if (!g8_on()) return -1;
-  const bool dense = amode == g4::KIN && (bmode == g4::KIN || bmode == g4::KOUT);
+  const bool dense = (amode == g4::KIN && (bmode == g4::KIN || bmode == g4::KOUT)) ||
+                     (amode == g4::KOUT && bmode == g4::KOUT && epi == EPI_F32);
   const bool conv = amode == g4::CONV_FWD && bmode == g4::KIN && (p_in.Cin & 63) == 0;
   if (!dense && !conv) return -1;
   GemmParams p = p_in;
@@ -236,6 +239,7 @@ extern "C" int tfk_g8_launch(const GemmParams& p_in, int amode, int bmode, int e
   TFK_G8(g4::KIN, g4::KOUT, EPI_BF16)
   TFK_G8(g4::KIN, g4::KOUT, EPI_BF16_EXT)
   TFK_G8(g4::KIN, g4::KOUT, EPI_BF16_BNR)
+  TFK_G8(g4::KOUT, g4::KOUT, EPI_F32)  // weight gradients dY^T X (split-K slabs by blockIdx.z)
   TFK_G8(g4::CONV_FWD, g4::KIN, EPI_BF16)
   TFK_G8(g4::CONV_FWD, g4::KIN, EPI_BF16_BNR)
 #undef TFK_G8

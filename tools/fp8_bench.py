@@ -19,7 +19,10 @@ from tensorflow_k8s_amd.ops import gemm as G  # noqa: E402
 from tensorflow_k8s_amd.ops._lib import lib  # noqa: E402
 
 SHAPES = {"tfm_ffn1": (16384, 4096, 1024), "tfm_ffn2": (16384, 1024, 4096), "tfm_qkv": (16384, 3072, 1024),
-          "tfm_logits": (8192, 33728, 1024), "bert_ffn1": (8192, 3072, 768), "sq8192": (8192, 8192, 8192)}
+          "tfm_logits": (8192, 33728, 1024), "bert_ffn1": (8192, 3072, 768), "sq8192": (8192, 8192, 8192),
+          # Transformer-big bs32 x 256 tokens: the shapes the benchmark step runs
+          "tb_o": (8192, 1024, 1024), "tb_kv": (8192, 2048, 1024), "tb_qkv": (8192, 3072, 1024),
+          "tb_ffn1": (8192, 4096, 1024), "tb_ffn2": (8192, 1024, 4096)}
 
 
 def tflops(f, fl, iters):

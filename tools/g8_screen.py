@@ -34,7 +34,7 @@ def main():
     args = ap.parse_args()
     bad_total = 0
     for M, N, K in SHAPES:
-        for d in ("fwd", "dgrad"):
+        for d in ("fwd", "dgrad", "wgrad"):
             bad = 0
             for r in range(args.reps):
                 g = torch.Generator(device="cuda").manual_seed(r)
@@ -43,11 +43,18 @@ def main():
                     w = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
                     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
                     fn = lambda: (G._gemm(x, w, y, M, N, K, K, K, N, G.A_KIN, G.B_KIN, G.EPI_BF16, (256, 256)), y.clone())[1]
-                else:
+                elif d == "dgrad":
                     dy = (torch.rand(M, N, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
                     w = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
                     y = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
                     fn = lambda: (G._gemm(dy, w, y, M, K, N, N, K, K, G.A_KIN, G.B_KOUT, G.EPI_BF16, (256, 256)), y.clone())[1]
+                else:  # weight gradient gw[N][K] = dy^T x over the M rows, 4 split-K f32 slabs
+                    dy = (torch.rand(M, N, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+                    x = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+                    ns = int(G.lib().gemm_splits(M, 4))
+                    ws = torch.empty(ns * N * K, device="cuda", dtype=torch.float32)
+                    fn = lambda: (G._gemm(dy, x, ws, N, K, M, N, K, K, G.A_KOUT, G.B_KOUT, G.EPI_F32, (256, 256),
+                                          splits=4, split_stride=N * K), ws.clone())[1]
                 ref = run(fn, False)
                 out = run(fn, True)
                 torch.cuda.synchronize()

@@ -92,9 +92,9 @@ def main():
             runs["dgrad"] = ({t: (lambda t=t: _g8(lambda tt: G._gemm(dy, w, dx, M, K, N, N, K, K, G.A_KIN, G.B_KOUT,
                                                                      G.EPI_BF16, tt), t)) for t in TILES}, lambda: dy @ w)
         if "wgrad" in dirs:
-            runs["wgrad"] = ({t: (lambda t=t: G._gemm(dy, x, gw, N, K, M, N, K, K, G.A_KOUT, G.B_KOUT, G.EPI_F32,
-                                                      (256, 256) if t == "g8" else t))
-                              for t in TILES}, lambda: dy.t() @ x)
+            runs["wgrad"] = ({t: (lambda t=t: _g8(lambda tt: G._gemm(dy, x, gw, N, K, M, N, K, K, G.A_KOUT, G.B_KOUT,
+                                                                     G.EPI_F32, tt), t)) for t in TILES},
+                             lambda: dy.t() @ x)
         ref = (x.float() @ w.float().t())
         for d, (fns, blas) in runs.items():
             res = {t: [] for t in TILES}

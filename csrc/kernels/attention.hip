@@ -14,7 +14,7 @@
 // of the "X" operand are read with the row permutation  i -> 8*(i>>2) + 4*half + (i&3)  so that
 // the P / dS accumulators of two blocks, packed to bf16, are directly the k-slots 8g..8g+7 of the
 // next MFMA (P*V, dS*K, ...) whose other operand is a transposed LDS read (ds_read_b64_tr_b16).
-// LDS tiles are [64 rows][72] bf16 (144-B rows: conflict-free 16-B row reads and tr reads).
+// LDS tiles are [64 rows][64] bf16 with XOR-swizzled 16-B chunks (aswz: conflict-free row and tr reads).
 //
 // Backward = two kernels (no atomics, deterministic): dQ pass (grid over query tiles, recompute
 // P and dP, dQ = dS K) and dK/dV pass (grid over key tiles, dV = P^T dO, dK = dS^T Q).
@@ -24,7 +24,14 @@
 namespace {
 constexpr int D = 64;
 constexpr int TILE = 64;
-constexpr int LS = 72;  // LDS row stride (elements)
+constexpr int LS = 64;  // LDS row stride (elements): 128-B rows, 16-B chunks XOR-swizzled (aswz)
+// chunk c of tile row r sits at chunk position c ^ aswz(r). With gfx950's ds_read_b128 lane groups
+// ({0-3,12-15,20-27}, ...) and the permuted rows of frag_row, and the 32-lane groups of
+// ds_read_b64_tr_b16 in frag_tr, this is conflict-free for both reads (a 144-B padded row -- the r3
+// layout -- costs 2x: SQ_LDS_BANK_CONFLICT 2.1e6 / 3.1e6 / 4.2e6 cycles per fwd / dQ / dKV call).
+// (independent of row bit 2, so rows r and r + 4 share it: the +4-row fragment reads are immediate
+// offsets of the same per-lane base)
+__device__ __forceinline__ int aswz(int r) { return (((r >> 2) & 6) ^ ((r & 3) << 1)) & 7; }
 constexpr int NT = 256;
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -78,21 +85,41 @@ __device__ __forceinline__ void tile_store(const TileRegs& t, bf16* lds) {
   for (int it = 0; it < 512 / NTH; ++it) {
     const int c = threadIdx.x + it * NTH, row = c >> 3, col = (c & 7) * 8;
     const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-    *(u32x4*)(lds + row * LS + col) = t.ok[it] ? t.v[it] : z;
+    *(u32x4*)(lds + row * LS + (((col >> 3) ^ aswz(row)) << 3)) = t.ok[it] ? t.v[it] : z;
   }
 }
-// row fragment: lane -> row `row`, k-slots = columns kk*32 + 8g .. +7
-__device__ __forceinline__ bf16x8 frag_row(const bf16* lds, int row, int kk) {
-  const int g = (threadIdx.x & 63) >> 4;
-  return *(const bf16x8*)(lds + row * LS + kk * 32 + 8 * g);
+// Per-lane LDS byte offsets of the fragment reads, computed once per kernel (the swizzle is a
+// lane-dependent XOR, so the compile-time parts -- k-half, block parity, column block -- select one
+// of a few precomputed offsets and the remaining row shifts are immediate offsets):
+//  frag_row (row prow(bb, l&15), k-slots kk*32 + 8g..+7): row[kk] + 4*(bb&1) + 32*(bb>>1) rows,
+//    since aswz(r + 4) == aswz(r + 32) == aswz(r);
+//  frag_tr (column cbase + (l&15), k-slots = tile rows kbase + 8g..+7, two 4-row reads): tr[cbase/16]
+//    + kbase rows (+ 4 rows for the second read; kbase in {0, 32}).
+struct FragOffs {
+  int row[2];
+  int tr[4];
+  __device__ __forceinline__ void init() {
+    const int l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+    const int R0 = 8 * (li >> 2) + (li & 3);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) row[kk] = R0 * 128 + (((kk * 4 + g) ^ aswz(R0)) << 4);
+    const int qq = li >> 2, pc = li & 3, r = 8 * g + qq;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int col = cb * 16 + 4 * pc;
+      tr[cb] = r * 128 + (((col >> 3) ^ aswz(r)) << 4) + (col & 7) * 2;
+    }
+  }
+};
+// row fragment of block bb: lane -> tile row prow(bb, l&15), k-slots kk*32 + 8g .. +7
+__device__ __forceinline__ bf16x8 frag_row(const bf16* lds, const FragOffs& o, int bb, int kk) {
+  return *(const bf16x8*)((const char*)lds + o.row[kk] + ((bb & 1) * 4 + (bb >> 1) * 32) * 128);
 }
 // transposed fragment: lane -> column cbase + (l&15), k-slots = tile rows kbase + 8g .. +7
-__device__ __forceinline__ bf16x8 frag_tr(const bf16* lds, int kbase, int cbase) {
-  const int l = threadIdx.x & 63, g = l >> 4, i = l & 15, qq = i >> 2, pc = i & 3;
-  const bf16* p0 = lds + (kbase + 8 * g + qq) * LS + cbase + 4 * pc;
-  const bf16* p1 = p0 + 4 * LS;
-  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p0);
-  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p1);
+__device__ __forceinline__ bf16x8 frag_tr(const bf16* lds, const FragOffs& o, int kbase, int cbase) {
+  const char* b = (const char*)lds + kbase * 128;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)(b + o.tr[cbase >> 4]));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)(b + o.tr[cbase >> 4] + 4 * 128));
   bf16x8 r;
   r.lo = lo;
   r.hi = hi;
@@ -158,6 +185,21 @@ __device__ __forceinline__ void store_rowvec4(bf16* dst, const f32x4& v, float s
 // v_exp_f32 without the libm denormal fix-up (exp2f adds a compare, two selects, an add and an
 // ldexp): softmax terms below 2^-126 of the row maximum flush to 0
 __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+// Butterfly reductions over the 4 lane rows (lanes l, l^16, l^32, l^48: the 4 k-groups of one
+// query) with gfx950's v_permlane16/32_swap -- plain VALU, where __shfl_xor is an LDS bpermute plus
+// an lgkmcnt(0) wait (4 per tile in the forward). swap(x, x) leaves (x[l], x[partner]) in the pair.
+__device__ __forceinline__ float rows_max(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float rows_sum(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 // LDS-only block barrier. __syncthreads() is a workgroup release/acquire fence around s_barrier and
 // drains EVERY outstanding global load (vmcnt(0)) -- including the next tile's register prefetch,
 // which must stay in flight across the barrier. The tiles only communicate through LDS, so waiting
@@ -191,6 +233,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(Attn
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][TILE * LS];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][TILE * LS];
   const int l = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = l >> 4, li = l & 15;
+  FragOffs fo;
+  fo.init();
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * RB;
   const int bh = b * p.H + h;
   const uint32_t hs = head_seed(p, bh);
@@ -228,10 +272,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(Attn
     f32x4 s[4];
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
-      const int kr_ = prow(bb, li);
       f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
-      a = mfma(frag_row(K_, kr_, 0), qf0, a);
-      a = mfma(frag_row(K_, kr_, 1), qf1, a);
+      a = mfma(frag_row(K_, fo, bb, 0), qf0, a);
+      a = mfma(frag_row(K_, fo, bb, 1), qf1, a);
       s[bb] = a;
     }
     // wave-uniform: every (query, key) of this wave's tile valid -> no per-element mask
@@ -250,8 +293,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(Attn
           }
           mx = fmaxf(mx, s[bb][r]);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = rows_max(mx);
       const float mnew = fmaxf(m, mx * sl2);
       const float muse = mnew == -INFINITY ? 0.f : mnew;
       const float alpha = ex2(m - muse);
@@ -264,8 +306,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(Attn
           rs += e;
           s[bb][r] = e;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs = rows_sum(rs);
       lsum = lsum * alpha + rs;
       m = mnew;
 #pragma unroll
@@ -284,8 +325,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_fwd_kernel(Attn
     const bf16x8 pf0 = pack2(s[0], s[1]), pf1 = pack2(s[2], s[3]);
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
-      oacc[db] = mfma(frag_tr(V_, 0, db * 16), pf0, oacc[db]);
-      oacc[db] = mfma(frag_tr(V_, 32, db * 16), pf1, oacc[db]);
+      oacc[db] = mfma(frag_tr(V_, fo, 0, db * 16), pf0, oacc[db]);
+      oacc[db] = mfma(frag_tr(V_, fo, 32, db * 16), pf1, oacc[db]);
     }
     // unconditional: past the end these stage clamped rows into the idle buffer, never read
     tile_store<NTH>(kr, Ks[(t + 1) & 1]);
@@ -311,6 +352,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dq_kernel(A
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][TILE * LS];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][TILE * LS];
   const int l = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = l >> 4, li = l & 15;
+  FragOffs fo;
+  fo.init();
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * RB;
   const int bh = b * p.H + h;
   const uint32_t hs = head_seed(p, bh);
@@ -343,8 +386,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dq_kernel(A
     float d = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) d += bf2f(df0[e]) * bf2f(of0[e]) + bf2f(df1[e]) * bf2f(of1[e]);
-    d += __shfl_xor(d, 16, 64);
-    d += __shfl_xor(d, 32, 64);
+    d = rows_sum(d);
     dlt = d;
     if (g == 0 && qrow < p.Sq) p.delta[(long long)bh * p.Sq + qrow] = d;
   }
@@ -367,12 +409,11 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dq_kernel(A
       f32x4 s[2], dp[2], ds[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int kr_ = prow(2 * hh + j, li);
         f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
-        a = mfma(frag_row(K_, kr_, 0), qf0, a);
-        c = mfma(frag_row(V_, kr_, 0), df0, c);
-        a = mfma(frag_row(K_, kr_, 1), qf1, a);
-        c = mfma(frag_row(V_, kr_, 1), df1, c);
+        a = mfma(frag_row(K_, fo, 2 * hh + j, 0), qf0, a);
+        c = mfma(frag_row(V_, fo, 2 * hh + j, 0), df0, c);
+        a = mfma(frag_row(K_, fo, 2 * hh + j, 1), qf1, a);
+        c = mfma(frag_row(V_, fo, 2 * hh + j, 1), df1, c);
         s[j] = a;
         dp[j] = c;
       }
@@ -404,7 +445,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dq_kernel(A
       else body(bconst<false>{});
       const bf16x8 sf = pack2(ds[0], ds[1]);
 #pragma unroll
-      for (int db = 0; db < 4; ++db) acc[db] = mfma(frag_tr(K_, 32 * hh, db * 16), sf, acc[db]);
+      for (int db = 0; db < 4; ++db) acc[db] = mfma(frag_tr(K_, fo, 32 * hh, db * 16), sf, acc[db]);
     }
     // unconditional: past the end these stage clamped rows into the idle buffer, never read
     tile_store<NTH>(kr, Ks[(t + 1) & 1]);
@@ -429,6 +470,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dkv_kernel(
   __shared__ __attribute__((aligned(16))) float lse_s[2][TILE];
   __shared__ __attribute__((aligned(16))) float dlt_s[2][TILE];
   const int l = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = l >> 4, li = l & 15;
+  FragOffs fo;
+  fo.init();
   const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * RB;
   const int bh = b * p.H + h;
   const uint32_t hs = head_seed(p, bh);
@@ -489,12 +532,11 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dkv_kernel(
       f32x4 s[2], dp[2], pp[2], ds[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int qr_ = prow(2 * hh + j, li);
         f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = f32x4{0.f, 0.f, 0.f, 0.f};
-        a = mfma(frag_row(Q_, qr_, 0), kf0, a);
-        c = mfma(frag_row(O_, qr_, 0), vf0, c);
-        a = mfma(frag_row(Q_, qr_, 1), kf1, a);
-        c = mfma(frag_row(O_, qr_, 1), vf1, c);
+        a = mfma(frag_row(Q_, fo, 2 * hh + j, 0), kf0, a);
+        c = mfma(frag_row(O_, fo, 2 * hh + j, 0), vf0, c);
+        a = mfma(frag_row(Q_, fo, 2 * hh + j, 1), kf1, a);
+        c = mfma(frag_row(O_, fo, 2 * hh + j, 1), vf1, c);
         s[j] = a;
         dp[j] = c;
       }
@@ -529,8 +571,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void attn_bwd_dkv_kernel(
       const bf16x8 pf = pack2(pp[0], pp[1]), sf = pack2(ds[0], ds[1]);
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
-        dv[db] = mfma(frag_tr(O_, 32 * hh, db * 16), pf, dv[db]);
-        dk[db] = mfma(frag_tr(Q_, 32 * hh, db * 16), sf, dk[db]);
+        dv[db] = mfma(frag_tr(O_, fo, 32 * hh, db * 16), pf, dv[db]);
+        dk[db] = mfma(frag_tr(Q_, fo, 32 * hh, db * 16), sf, dk[db]);
       }
     }
     // unconditional: past the end these stage clamped rows into the idle buffer, never read

@@ -19,15 +19,59 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
 
+// Wave-wide reductions without the LDS: DPP within each 16-lane row (quad_perm xor 1, xor 2, then
+// half-row mirror and row mirror -- every lane of a group already holds the group's value, so any
+// cross-group pairing completes the butterfly) and gfx950's v_permlane16/32_swap across rows.
+// (__shfl_xor is a ds_bpermute plus an lgkmcnt(0) wait per step: 6 LDS round trips per reduction.)
+// Every lane ends with the bitwise-same value (each step adds the same two operands on both sides).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_swap16(float v, float& other) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  other = __uint_as_float(a[1]);
+  return __uint_as_float(a[0]);
+}
+__device__ __forceinline__ float lane_swap32(float v, float& other) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  other = __uint_as_float(a[1]);
+  return __uint_as_float(a[0]);
+}
+// sum over the lane pair (l, l ^ O), O in {8, 16, 32}: row_ror 8 within a 16-lane row, or a
+// permlane swap across rows (both lanes get the same operands in the same order)
+template <int O>
+__device__ __forceinline__ float xor_sum(float v) {
+  static_assert(O == 8 || O == 16 || O == 32, "xor_sum: O in {8, 16, 32}");
+  if constexpr (O == 8) {
+    return v + dpp_f<0x128>(v);
+  } else {
+    float o;
+    const float a = O == 16 ? lane_swap16(v, o) : lane_swap32(v, o);
+    return a + o;
+  }
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  float o;
+  float a = lane_swap16(v, o);
+  v = a + o;
+  a = lane_swap32(v, o);
+  return a + o;
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  float o;
+  float a = lane_swap16(v, o);
+  v = fmaxf(a, o);
+  a = lane_swap32(v, o);
+  return fmaxf(a, o);
 }
 
 // Block-wide sum for blockDim.x == NT (multiple of 64). `red` needs NT/64 floats.

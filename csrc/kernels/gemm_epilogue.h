@@ -465,14 +465,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         if (p.bn_y2) r2[e] = (r2[e] - p.bn_mean2[n] * r0[e]) * p.bn_invstd2[n];
       }
       // lanes sharing a column chunk: tid % CPR equal -> xor over the bits above log2(CPR)
+      // (DPP / permlane-swap butterflies: no LDS round trip per step)
+      static_assert(CPR >= 8, "BN-reduce lane butterfly needs >= 8 chunks per row");
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-#pragma unroll
-        for (int o = CPR; o < 64; o <<= 1) {
-          r0[e] += __shfl_xor(r0[e], o, 64);
-          r1[e] += __shfl_xor(r1[e], o, 64);
-          r2[e] += __shfl_xor(r2[e], o, 64);
-        }
+      for (int e = 0; e < 8; ++e) {
+        if constexpr (CPR <= 8) { r0[e] = xor_sum<8>(r0[e]); r1[e] = xor_sum<8>(r1[e]); r2[e] = xor_sum<8>(r2[e]); }
+        if constexpr (CPR <= 16) { r0[e] = xor_sum<16>(r0[e]); r1[e] = xor_sum<16>(r1[e]); r2[e] = xor_sum<16>(r2[e]); }
+        if constexpr (CPR <= 32) { r0[e] = xor_sum<32>(r0[e]); r1[e] = xor_sum<32>(r1[e]); r2[e] = xor_sum<32>(r2[e]); }
+      }
       __syncthreads();  // C tile no longer needed: reuse LDS for the cross-wave reduction
       float* red = (float*)smem;  // [NW waves][3][CPR*8]
       if (lane < CPR) {

@@ -503,7 +503,11 @@ int tfk_layernorm_fwd_mx(const bf16* x, const float* gamma, const float* beta, b
 // dxd (optional): also write dropout(dx; drop_p, drop_seed) -- the gradient the consumer's dropout
 // backward would produce from dx
 // blocks of the LayerNorm-backward grid (the binding sizes the partials workspace with it)
-int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (NT / 64) * 8, 1024); }
+// bf16 mode: rows per wave of the grid-stride backward (A/B knob of tools/ln_probe.py; fewer rows per
+// wave = more blocks per CU in flight, more column-partial slabs for ln_part_reduce_kernel)
+static int g_ln_rows = 8;
+void tfk_ln_bwd_set_rows(int r) { g_ln_rows = r > 0 ? r : 8; }
+int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (NT / 64) * g_ln_rows, 4096); }
 static unsigned ln_bwd_blocks(int M, bool mxo) { return (unsigned)tfk_ln_bwd_blocks(M, mxo ? 1 : 0); }
 // part (optional): f32 workspace [blocks][2 or 3][W] for the column partials (no tail atomics)
 int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const float* mean, const float* rstd,

@@ -149,6 +149,7 @@ class Bottleneck:
             dx = self.conv_sc.backward(dysc, x, need_dx=need_dx, resid=dx, bnr=next_bnr)
         else:
             dx = self.conv1.backward(dy1, x, need_dx=need_dx, resid=dres, bnr=next_bnr)
+        streams.flush()  # this block's deferred weight gradients behind one side-stream fork
         return dx
 
 

@@ -124,7 +124,7 @@ class Conv2d:
 
     def backward(self, dy, x, need_dx: bool = True, resid=None, bnr=None, resid_stride: int = 1):
         g = self.geom(x.shape)
-        streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad, cin_used=self.cin_real), dy, x)
+        streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad, cin_used=self.cin_real), dy, x, deferrable=True)
         if self.b is not None:
             G.bias_grad(dy, self.b.grad)
             self.arena.grad_ready(self.w, self.b)
@@ -147,7 +147,7 @@ class Conv2d:
     def wgrad(self, dy, x):
         """Weight gradient only (side stream when enabled) + readiness notification."""
         g = self.geom(x.shape)
-        streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad, cin_used=self.cin_real), dy, x)
+        streams.run_wgrad(lambda: G.conv_wgrad(dy, x, g, self.w.grad, cin_used=self.cin_real), dy, x, deferrable=True)
         self.arena.grad_ready(self.w)
 
     def lattice_dgrad(self, dy, x):

@@ -276,6 +276,15 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
         return
     if RECORD is not None:
         RECORD.append(("wgrad", (N, K, M), ()))
+    if WGRAD_BLAS and wgrad_blas_ok(N, K, M):
+        # a plain library GEMM (no fused epilogue): hipBLASLt, bf16 operands, f32 accumulate and
+        # output straight into the arena gradient -- no split-K slabs, no reduce pass
+        v = gw.view(N, K)
+        if accumulate:
+            torch.ops.aten.addmm.dtype_out(v, dy2.t(), x2, torch.float32, beta=1, alpha=1, out=v)
+        else:
+            torch.ops.aten.mm.dtype_out(dy2.t(), x2, torch.float32, out=v)
+        return
     tuned = tuning.wgrad_config(N, K, M) if (N % 8 == 0 and K % 8 == 0 and split_target is None) else None
     tile = tuned[0] if tuned else pick_tile(N, K, splits_ok=True, big_ok=True, K=M, split_target=split_target,
                                             g4=N % 8 == 0 and K % 8 == 0)
@@ -286,6 +295,17 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
               split_stride=stride)
     _f32_out_splitk(run, N, K, M, tiles, gw.view(-1), accumulate, dy.device, split_target=split_target,
                     force_splits=tuned[1] if tuned else None, slot=_lib_mod.WGRAD_SLOT)
+
+
+# Weight gradients dW = dY^T X are plain GEMMs; where hipBLASLt's f32-output GEMM (aten mm.dtype_out)
+# measured faster than the g4 split-K path including its slab reduce (tools/wgrad_blas_ab.py), they
+# go to it. False: always the framework's kernels.
+WGRAD_BLAS = False
+
+
+def wgrad_blas_ok(N: int, K: int, M: int) -> bool:
+    """Shapes (gw N x K over M rows) on which the hipBLASLt weight gradient measured faster."""
+    return M <= 65536 and N * K >= 1 << 20
 
 
 def bias_grad(dy: torch.Tensor, gb: torch.Tensor, accumulate: bool = False) -> None:

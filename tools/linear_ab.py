@@ -25,6 +25,7 @@ FWD = {  # name: (N, K, extras)
     "qkv": (3072, 1024, ""),
     "kv": (2048, 1024, ""),
     "o": (1024, 1024, "resid"),
+    "logits": (33728, 1024, ""),
 }
 DGRAD = {  # name: (K_in = output cols of dx, N_out = reduction, extras)
     "ffn2": (4096, 1024, "dact_relu"),
@@ -32,6 +33,7 @@ DGRAD = {  # name: (K_in = output cols of dx, N_out = reduction, extras)
     "qkv": (1024, 3072, ""),
     "kv": (1024, 2048, ""),
     "o": (1024, 1024, ""),
+    "logits": (1024, 33728, ""),
 }
 
 
@@ -62,6 +64,7 @@ def main():
             G.pick_tile = orig
 
     jobs = []
+    blas = {}
     for name, (N, K, ex) in FWD.items():
         x, w = r(M, K), r(N, K) * 0.05
         aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if "aux" in ex else None
@@ -70,20 +73,26 @@ def main():
                   drop_seed=3)
         jobs.append((f"fwd_{name}", 2.0 * M * N * K, (lambda x=x, w=w, kw=kw: G.linear_fwd(x, w, **kw)),
                      orig(M, N, big_ok=True, K=K, g4=True)))
+        if not ex:
+            blas[f"fwd_{name}"] = lambda x=x, w=w: x @ w.t()
     for name, (Kin, Nout, ex) in DGRAD.items():
         dy, w = r(M, Nout), r(Nout, Kin) * 0.05
         src = r(M, Kin) if ex else None
         kw = dict(dact_src=src, dact="relu") if ex else {}
         jobs.append((f"dgrad_{name}", 2.0 * M * Nout * Kin, (lambda dy=dy, w=w, kw=kw: G.linear_dgrad(dy, w, **kw)),
                      orig(M, Kin, big_ok=True, K=Nout, g4=True)))
+        if not ex:
+            blas[f"dgrad_{name}"] = lambda dy=dy, w=w: dy @ w
     res = {j[0]: {v: [] for v in variants} for j in jobs}
     for _ in range(args.rounds):
         for name, fl, fn, _ in jobs:
             for v, tile in variants.items():
                 res[name][v].append(timed(fn, tile))
+            if name in blas:
+                res[name].setdefault("blas", []).append(timed(blas[name], None))
     for name, fl, fn, picked in jobs:
         out = {"op": name, "M": M, "picked": list(picked) if picked else None}
-        for v in variants:
+        for v in list(variants) + (["blas"] if name in blas else []):
             us = statistics.median(res[name][v])
             out[v + "_us"] = round(us, 1)
             out[v + "_tfs"] = round(fl / us / 1e6, 1)

@@ -23,6 +23,14 @@ inline void need_aligned(const torch::Tensor& t, int bytes, const char* n) {
 inline void need_numel(const torch::Tensor& t, long long n, const char* name) {
   TORCH_CHECK(t.numel() >= n, name, " too small: numel=", t.numel(), " < required ", n);
 }
+// uint8 aux / dact_src of a GEMM epilogue = relu bitmask [rows][ld/8] (gemm_params.h aux_bits,
+// the same bit layout as relu_bitmask below): contiguous, every 8-column chunk starting on a byte
+inline bool relu_mask(const torch::Tensor& t, long long ld, long long N, long long off, const char* what) {
+  if (t.scalar_type() != at::kByte) return false;
+  TORCH_CHECK(t.is_contiguous(), what, ": relu mask must be contiguous");
+  TORCH_CHECK(ld % 8 == 0 && N % 8 == 0 && off % 8 == 0, what, ": relu mask needs 8-column aligned rows");
+  return true;
+}
 template <typename T>
 T* opt_ptr(const c10::optional<torch::Tensor>& t) {
   return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;

@@ -215,13 +215,21 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   for (auto* t : {&aux, &dact_src}) {
     if (t->has_value() && (*t)->defined()) {
       TORCH_CHECK(epi == 0, "aux/dact need the bf16 epilogue");
-      need_bf16(**t, "aux/dact_src");
-      need_numel(**t, bC + (long long)(M - 1) * ldc + N, "aux/dact_src");
+      if (relu_mask(**t, ldc, N, batch > 1 ? sC : 0, "aux/dact_src")) {
+        need_numel(**t, (bC + (long long)(M - 1) * ldc + N + 7) / 8, "aux/dact_src relu mask");
+      } else {
+        need_bf16(**t, "aux/dact_src");
+        need_numel(**t, bC + (long long)(M - 1) * ldc + N, "aux/dact_src");
+      }
     }
   }
   p.aux = opt_ptr<void>(aux);
   p.dact_src = opt_ptr<const void>(dact_src);
   p.dact = dact;
+  p.aux_bits = p.aux && aux->scalar_type() == at::kByte;
+  p.dact_bits = p.dact_src && dact_src->scalar_type() == at::kByte;
+  TORCH_CHECK(!p.aux_bits || act == 1, "a relu-mask aux needs act relu");
+  TORCH_CHECK(!p.dact_bits || dact == 1, "a relu-mask dact_src needs dact relu");
   TORCH_CHECK(!p.dact_src || (dact >= 1 && dact <= 3), "dact must be 1 (relu), 2 (gelu) or 3 (tanh) with dact_src");
   TORCH_CHECK(act >= 0 && act <= 3, "act");
   TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "drop_p");
@@ -359,20 +367,28 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
   p.a_scale = As.data_ptr(); p.b_scale = Bs.data_ptr();
   if (bias.has_value() && bias->defined()) { need_f32(*bias, "bias"); need_numel(*bias, N, "bias"); }
   if (resid.has_value() && resid->defined()) { need_bf16(*resid, "resid"); need_numel(*resid, (long long)M * N, "resid"); }
-  if (aux.has_value() && aux->defined()) { need_bf16(*aux, "aux"); need_numel(*aux, (long long)M * N, "aux"); }
+  if (aux.has_value() && aux->defined()) {
+    if (relu_mask(*aux, N, N, 0, "aux")) need_numel(*aux, (long long)M * N / 8, "aux relu mask");
+    else { need_bf16(*aux, "aux"); need_numel(*aux, (long long)M * N, "aux"); }
+  }
   p.bias = opt_ptr<const float>(bias);
   p.resid = opt_ptr<const void>(resid);
   p.aux = opt_ptr<void>(aux);
+  p.aux_bits = p.aux && aux->scalar_type() == at::kByte;
+  TORCH_CHECK(!p.aux_bits || act == 1, "a relu-mask aux needs act relu");
   p.drop_p = (float)drop_p;
   p.drop_scale = drop_p > 0.0 ? 256.f / (float)(256 - drop_thr8_host((float)drop_p)) : 1.f;
   p.drop_seed = (unsigned long long)drop_seed;
   p.drop_seed_key = tfk_seed_key();
   if (dact_src.has_value() && dact_src->defined()) {
-    need_bf16(*dact_src, "dact_src"); need_numel(*dact_src, (long long)M * N, "dact_src");
+    if (relu_mask(*dact_src, N, N, 0, "dact_src")) need_numel(*dact_src, (long long)M * N / 8, "dact_src relu mask");
+    else { need_bf16(*dact_src, "dact_src"); need_numel(*dact_src, (long long)M * N, "dact_src"); }
     TORCH_CHECK(dact >= 1 && dact <= 3, "dact");
   }
   p.dact_src = opt_ptr<const void>(dact_src);
   p.dact = dact;
+  p.dact_bits = p.dact_src && dact_src->scalar_type() == at::kByte;
+  TORCH_CHECK(!p.dact_bits || dact == 1, "a relu-mask dact_src needs dact relu");
   p.beta = (float)beta;
   int ext = f32 ? 2 : ((p.aux || drop_p > 0.0 || p.dact_src) ? 1 : 0);
   if (mx_out.has_value()) {

@@ -94,6 +94,14 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// Relu keep-bits of an 8-column pre-activation chunk (bit e = v[e] > 0): the EXT epilogue's aux_bits.
+__device__ __forceinline__ unsigned char relu_bits8(bf16x8 v) {
+  unsigned b = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b |= (bf2f(v[e]) > 0.f ? 1u : 0u) << e;
+  return (unsigned char)b;
+}
+
 // Output row of GEMM row m under the out-map (identity without one).
 __device__ __forceinline__ long long out_row(const GemmParams& p, int m) {
   if (p.om_hp == 0) return m;
@@ -261,7 +269,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       auto group = [&](auto gsz, int g0) {
         constexpr int GS = decltype(gsz)::value;
         bf16x8 cv[GS], rr[GS], zv[GS], yv[GS], y2v[GS];
-        unsigned mk[GS];
+        unsigned mk[GS], zb[GS];
         long long off[GS];
         bool rok[GS];
         int mlog[GS], nlog[GS], lofs[GS];
@@ -281,7 +289,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           // smaller lattice tensor there, so resid + off[g] could run past its allocation
           if (p.resid) rr[g] = *(const bf16x8*)(rok[g] ? resid_b + bz * p.sC + mr * p.ldc + n : (const bf16*)p.C + off[g]);
           if constexpr (ext) {
-            if (p.dact_src) zv[g] = *(const bf16x8*)(dsrc_b + off[g]);
+            if (p.dact_src) {
+              if (p.dact_bits) zb[g] = ((const unsigned char*)p.dact_src)[off[g] >> 3];
+              else zv[g] = *(const bf16x8*)(dsrc_b + off[g]);
+            }
           }
           if constexpr (bnr) {
             yv[g] = *(const bf16x8*)(y_b + off[g]);
@@ -298,10 +309,18 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
             if (p.dact_src) {
+              if (p.dact_bits) {
 #pragma unroll
-              for (int e = 0; e < 8; ++e) f[e] *= act_grad(bf2f(zv[g][e]), p.dact);
+                for (int e = 0; e < 8; ++e) f[e] = (zb[g] >> e) & 1u ? f[e] : 0.f;
+              } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) f[e] *= act_grad(bf2f(zv[g][e]), p.dact);
+              }
             }
-            if (p.aux) *(bf16x8*)((bf16*)p.aux + off[g]) = v;
+            if (p.aux) {
+              if (p.aux_bits) ((unsigned char*)p.aux)[off[g] >> 3] = relu_bits8(v);
+              else *(bf16x8*)((bf16*)p.aux + off[g]) = v;
+            }
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] = act_apply(f[e], p.act);
             if (p.drop_p > 0.f) {
@@ -385,11 +404,20 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
           if (p.dact_src) {
-            bf16x8 zv = *(const bf16x8*)((const bf16*)p.dact_src + off);
+            if (p.dact_bits) {
+              const unsigned zb = ((const unsigned char*)p.dact_src)[off >> 3];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] *= act_grad(bf2f(zv[e]), p.dact);
+              for (int e = 0; e < 8; ++e) f[e] = (zb >> e) & 1u ? f[e] : 0.f;
+            } else {
+              bf16x8 zv = *(const bf16x8*)((const bf16*)p.dact_src + off);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) f[e] *= act_grad(bf2f(zv[e]), p.dact);
+            }
           }
-          if (p.aux) *(bf16x8*)((bf16*)p.aux + off) = v;
+          if (p.aux) {
+            if (p.aux_bits) ((unsigned char*)p.aux)[off >> 3] = relu_bits8(v);
+            else *(bf16x8*)((bf16*)p.aux + off) = v;
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] = act_apply(f[e], p.act);
           if (p.drop_p > 0.f) {
@@ -436,12 +464,19 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           *(bf16x8*)dst = v;
         }
       } else {
+        unsigned abits = 0;
         for (int e = 0; e < 8 && n + e < p.N; ++e) {
           const long long off = bz * p.sC + mo * p.ldc + n + e;
           float x = bf2f(v[e]);
           if constexpr (ext) {
-            if (p.dact_src) x *= act_grad(bf2f(((const bf16*)p.dact_src)[off]), p.dact);
-            if (p.aux) ((bf16*)p.aux)[off] = v[e];
+            if (p.dact_src) {
+              if (p.dact_bits) x = (((const unsigned char*)p.dact_src)[off >> 3] >> e) & 1u ? x : 0.f;
+              else x *= act_grad(bf2f(((const bf16*)p.dact_src)[off]), p.dact);
+            }
+            if (p.aux) {
+              if (p.aux_bits) abits |= (bf2f(v[e]) > 0.f ? 1u : 0u) << e;
+              else ((bf16*)p.aux)[off] = v[e];
+            }
             x = act_apply(x, p.act);
             if (p.drop_p > 0.f)
               x = drop_keep1(drop_seed32(eff_seed(p.drop_seed, p.drop_seed_key)), (unsigned long long)m * p.N + n + e, drop_thr8(p.drop_p)) ? x * p.drop_scale : 0.f;
@@ -449,6 +484,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           }
           if (rsrc) x += bf2f(rsrc[e]);
           dst[e] = f2bf(x);
+        }
+        if constexpr (ext) {
+          if (p.aux && p.aux_bits) ((unsigned char*)p.aux)[(bz * p.sC + mo * p.ldc + n) >> 3] = (unsigned char)abits;
         }
       }
     }

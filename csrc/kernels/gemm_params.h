@@ -46,6 +46,11 @@ struct GemmParams {
   void* aux;
   const void* dact_src;
   int dact;
+  // relu bitmasks instead of bf16 pre-activations: aux_bits -> aux is uint8 [rows][ldc/8], bit e of
+  // byte (m*ldc + n)/8 = (pre-activation of column n+e > 0); dact_bits -> dact_src is such a mask
+  // and the activation backward is relu' (1/16 of the bytes of a bf16 z, written and read)
+  int aux_bits;
+  int dact_bits;
   // inverted dropout after the activation, before the residual add; mask = hash(seed, m*N + n),
   // identical to misc.hip's dropout kernel on the contiguous [M][N] output (backward regenerates it)
   float drop_p, drop_scale;

@@ -151,7 +151,10 @@ class EncoderLayer:
     def _ffn(self, x, seed, training):
         cfg = self.cfg
         b, st = self.ffn_ln.forward(x, mx_out=self._mx(x, self.ff1, training))
-        z = torch.empty(b.shape[0], cfg.ffn, dtype=torch.bfloat16, device=x.device)
+        # relu: the FFN's activation backward only needs relu'(z) -> a 1-bit mask instead of bf16 z
+        # (1/16 of the bytes written here and read back by ff2's dgrad epilogue)
+        # (A/B same box: bf16 19.11 -> 18.70 ms/step, MX-fp8 18.04 -> 17.59)
+        z = torch.empty(b.shape[0], cfg.ffn // 8, dtype=torch.uint8, device=x.device)
         # fp8 training: ff1's epilogue writes MX(f) / MX(f^T) for ff2's forward and weight gradient --
         # f itself is never read (ff2's dgrad takes relu' from z), so its bf16 store is skipped
         mx = MX_PRODUCERS and self.ff1.fp8 and self.ff2.fp8 and training and b.shape[0] % 128 == 0

@@ -221,7 +221,8 @@ def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = 
         if bias is not None:
             y = y + bias.float()
         if aux is not None:
-            aux.view(-1, N).copy_(y)
+            from .gemm import store_aux_ref
+            store_aux_ref(aux, y, N)
         y = act_ref(y, act)
         if drop_p > 0:
             from .elementwise import dropout_keep, eff_seed, keep_scale
@@ -311,7 +312,7 @@ def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | Non
         from .gemm import act_grad_ref
         y = mx_dequantize(dq, ds) @ mx_dequantize(wq_, ws_).t()
         if dact_src is not None:
-            y = y * act_grad_ref(dact_src.float(), dact)
+            y = y * act_grad_ref(dact_src if dact_src.dtype == torch.uint8 else dact_src.float(), dact)
         if drop_p > 0:
             from .elementwise import dropout_keep, eff_seed, keep_scale
             y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) * keep_scale(drop_p)

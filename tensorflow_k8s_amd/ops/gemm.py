@@ -198,7 +198,7 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
         if bias is not None:
             y = y + bias.float()
         if aux is not None:
-            aux.view(-1, N).copy_(y)
+            store_aux_ref(aux, y, N)
         y = act_ref(y, act)
         if drop_p > 0:
             from .elementwise import dropout_keep, eff_seed, keep_scale
@@ -222,8 +222,32 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
     return y
 
 
+def relu_mask_pack(z: torch.Tensor) -> torch.Tensor:
+    """uint8 [rows, N/8] relu mask of pre-activations z [rows, N]: bit e of byte j = z[:, 8j+e] > 0
+    (the GEMM epilogue's aux_bits layout; CPU reference)."""
+    bits = (z.to(torch.bfloat16).float() > 0).reshape(z.shape[0], -1, 8).to(torch.int32)
+    return (bits << torch.arange(8, dtype=torch.int32)).sum(-1).to(torch.uint8)
+
+
+def relu_mask_unpack(m: torch.Tensor) -> torch.Tensor:
+    """f32 [rows, 8 * cols] 0/1 relu' from a uint8 relu mask [rows, cols] (CPU reference)."""
+    bits = (m.to(torch.int32).unsqueeze(-1) >> torch.arange(8, dtype=torch.int32)) & 1
+    return bits.reshape(m.shape[0], -1).float()
+
+
+def store_aux_ref(aux: torch.Tensor, y: torch.Tensor, N: int) -> None:
+    """CPU reference of the epilogue's aux store: the bf16 pre-activation, or its relu mask (uint8 aux)."""
+    if aux.dtype == torch.uint8:
+        aux.view(-1, N // 8).copy_(relu_mask_pack(y.reshape(-1, N)))
+    else:
+        aux.view(-1, N).copy_(y)
+
+
 def act_grad_ref(z: torch.Tensor, act: str | None) -> torch.Tensor:
-    """f32 derivative of the activation at pre-activation z (CPU reference)."""
+    """f32 derivative of the activation at pre-activation z (CPU reference); z may be the uint8 relu
+    mask (aux_bits) of a relu layer."""
+    if z.dtype == torch.uint8:
+        return relu_mask_unpack(z)
     z = z.float()
     if ACT[act] == 1:
         return (z > 0).float()
@@ -248,7 +272,7 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
     if not on_gpu(dy):
         dx = dy2.float() @ w.float()
         if dact_src is not None:
-            dx = dx * act_grad_ref(dact_src.reshape(-1, K), dact)
+            dx = dx * act_grad_ref(dact_src.reshape(dx.shape[0], -1), dact)
         if drop_p > 0:
             from .elementwise import dropout_keep, eff_seed, keep_scale
             dx = dx * dropout_keep(eff_seed(drop_seed), dx.numel(), drop_p).reshape(dx.shape) * keep_scale(drop_p)

@@ -659,3 +659,21 @@ def test_lib_gemm_routing_matches_native_engine(kind, monkeypatch):
            "wgrad": lambda: 2 * dy.float().t() @ x.float()}[kind]()
     assert rel(lib_out, ref) < 1e-2 and rel(native, ref) < 1e-2
     assert rel(lib_out, native) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 4096, 1024), (1000, 264, 128)])
+def test_relu_mask_aux_matches_bf16_aux(M, N, K):
+    """EXT epilogue with a uint8 relu-mask aux / dact_src (aux_bits, dact_bits) against the bf16
+    pre-activation path on the same operands: identical forward outputs, mask = (z > 0) bit for bit,
+    identical fused relu(+dropout) backward -- interior tiles and ragged edges."""
+    x, w, b = bf(M, K, seed=1).to(DEV), bf(N, K, scale=0.05, seed=2).to(DEV), torch.randn(N).to(DEV)
+    z = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    m = torch.empty(M, N // 8, device=DEV, dtype=torch.uint8)
+    y1 = G.linear_fwd(x, w, b, act="relu", aux=z, drop_p=0.1, drop_seed=7)
+    y2 = G.linear_fwd(x, w, b, act="relu", aux=m, drop_p=0.1, drop_seed=7)
+    assert torch.equal(y1, y2)
+    assert torch.equal(m.cpu(), G.relu_mask_pack(z.float().cpu()))
+    dy, w2 = bf(M, K, seed=3).to(DEV), bf(K, N, scale=0.05, seed=4).to(DEV)
+    d1 = G.linear_dgrad(dy, w2, dact_src=z, dact="relu", drop_p=0.1, drop_seed=7)
+    d2 = G.linear_dgrad(dy, w2, dact_src=m, dact="relu", drop_p=0.1, drop_seed=7)
+    assert torch.equal(d1, d2)

@@ -97,7 +97,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
           int batch, int64_t sA, int64_t sB, int64_t sC, int64_t split_stride, std::vector<int64_t> conv,
           std::vector<c10::optional<torch::Tensor>> bnr, int bn_relu, int bn_shards, c10::optional<torch::Tensor> aux,
           c10::optional<torch::Tensor> dact_src, int dact, double drop_p, int64_t drop_seed,
-          std::vector<int64_t> rowmap) {
+          std::vector<int64_t> rowmap, c10::optional<torch::Tensor> colsum) {
   need_bf16(A, "A");
   need_bf16(B, "B");
   TORCH_CHECK(epi == 0 || epi == 1, "epi");
@@ -228,6 +228,14 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
   p.dact = dact;
   p.aux_bits = p.aux && aux->scalar_type() == at::kByte;
   p.dact_bits = p.dact_src && dact_src->scalar_type() == at::kByte;
+  if (colsum.has_value() && colsum->defined()) {
+    need_f32(*colsum, "colsum");
+    need_numel(*colsum, N, "colsum");
+    TORCH_CHECK(epi == 0 && batch == 1 && !(stats.has_value() && stats->defined()) && !p.resid &&
+                    (p.dact_src || p.aux || drop_p > 0.0),
+                "colsum: bf16 EXT epilogue (aux / dact / dropout), batch 1, no BN statistics, no residual");
+  }
+  p.colsum = opt_ptr<float>(colsum);
   TORCH_CHECK(!p.aux_bits || act == 1, "a relu-mask aux needs act relu");
   TORCH_CHECK(!p.dact_bits || dact == 1, "a relu-mask dact_src needs dact relu");
   TORCH_CHECK(!p.dact_src || (dact >= 1 && dact <= 3), "dact must be 1 (relu), 2 (gelu) or 3 (tanh) with dact_src");
@@ -345,7 +353,7 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
                 c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, int act,
                 c10::optional<torch::Tensor> aux, double drop_p, int64_t drop_seed,
                 c10::optional<torch::Tensor> dact_src, int dact, double beta, int splits, int64_t split_stride,
-                c10::optional<std::vector<torch::Tensor>> mx_out, bool mx_skip_c) {
+                c10::optional<std::vector<torch::Tensor>> mx_out, bool mx_skip_c, c10::optional<torch::Tensor> colsum) {
   for (auto* t : {&A, &As, &B, &Bs}) need(*t, at::kByte, "mx operand");
   const bool f32 = C.scalar_type() == at::kFloat;
   if (!f32) need_bf16(C, "C");
@@ -390,6 +398,13 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
   p.dact_bits = p.dact_src && dact_src->scalar_type() == at::kByte;
   TORCH_CHECK(!p.dact_bits || dact == 1, "a relu-mask dact_src needs dact relu");
   p.beta = (float)beta;
+  if (colsum.has_value() && colsum->defined()) {
+    need_f32(*colsum, "colsum");
+    need_numel(*colsum, N, "colsum");
+    TORCH_CHECK(!f32 && !p.resid && (p.dact_src || p.aux || drop_p > 0.0),
+                "colsum: bf16 EXT epilogue (aux / dact / dropout), no residual");
+  }
+  p.colsum = opt_ptr<float>(colsum);
   int ext = f32 ? 2 : ((p.aux || drop_p > 0.0 || p.dact_src) ? 1 : 0);
   if (mx_out.has_value()) {
     // MX-fp8 copies of C from the epilogue: [qr [M][N], sr [M][N/32], qc [N][M], sc [N][M/32]]
@@ -839,7 +854,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_mxfp8", &gemm_mxfp8, py::arg("A"), py::arg("As"), py::arg("B"), py::arg("Bs"), py::arg("C"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("bias"), py::arg("resid"), py::arg("act"), py::arg("aux"), py::arg("drop_p"),
         py::arg("drop_seed"), py::arg("dact_src") = py::none(), py::arg("dact") = 0, py::arg("beta") = 0.0,
-        py::arg("splits") = 1, py::arg("split_stride") = 0, py::arg("mx_out") = py::none(), py::arg("mx_skip_c") = false);
+        py::arg("splits") = 1, py::arg("split_stride") = 0, py::arg("mx_out") = py::none(), py::arg("mx_skip_c") = false,
+        py::arg("colsum") = py::none());
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);

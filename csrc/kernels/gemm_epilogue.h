@@ -362,6 +362,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             *(bf16x8*)(Cs + lofs[g]) = v;  // the final value, for the MX pass
             if (!p.mx_skip_c) *(bf16x8*)((bf16*)p.C + off[g]) = v;
           } else {
+            if constexpr (ext) {
+              if (p.colsum) *(bf16x8*)(Cs + lofs[g]) = v;  // the final value, for the column sums
+            }
             *(bf16x8*)((bf16*)p.C + off[g]) = v;
           }
           if constexpr (bnr) {
@@ -461,6 +464,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           *(bf16x8*)(Cs + row * LDC_S + cc * 8) = v;
           if (!p.mx_skip_c) *(bf16x8*)dst = v;
         } else {
+          if constexpr (ext) {
+            if (p.colsum) *(bf16x8*)(Cs + row * LDC_S + cc * 8) = v;
+          }
           *(bf16x8*)dst = v;
         }
       } else {
@@ -484,6 +490,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           }
           if (rsrc) x += bf2f(rsrc[e]);
           dst[e] = f2bf(x);
+          if constexpr (ext) {
+            if (p.colsum) Cs[row * LDC_S + cc * 8 + e] = f2bf(x);
+          }
         }
         if constexpr (ext) {
           if (p.aux && p.aux_bits) ((unsigned char*)p.aux)[(bz * p.sC + mo * p.ldc + n) >> 3] = (unsigned char)abits;
@@ -491,6 +500,32 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       }
     }
     }  // ragged tile
+    if constexpr (ext) {
+      // p.colsum += column sums of the final tile (the LDS C tile holds every final value now):
+      // RG row groups per column -> partials in the reduction area behind the tile -> one global
+      // f32 atomic per column per block
+      if (p.colsum) {
+        constexpr int RG = NT >= BN ? NT / BN : 1;
+        float* part = (float*)(smem + BM * LDC_S * 2);  // [RG][BN] (<= [2][WM][BN])
+        static_assert(RG * BN <= 2 * WM * BN, "column-sum partials fit the reduction area");
+        const int rows = min(BM, p.M - m0), cols = min(BN, p.N - n0);
+        __syncthreads();
+        for (int t = tid; t < RG * BN; t += NT) {
+          const int rg = t / BN, col = t - rg * BN;
+          float a = 0.f;
+          if (col < cols)
+            for (int r = rg; r < rows; r += RG) a += bf2f(Cs[r * LDC_S + col]);
+          part[rg * BN + col] = a;
+        }
+        __syncthreads();
+        for (int col = tid; col < cols; col += NT) {
+          float a = 0.f;
+#pragma unroll
+          for (int rg = 0; rg < RG; ++rg) a += part[rg * BN + col];
+          atomicAdd(p.colsum + n0 + col, a);
+        }
+      }
+    }
     if constexpr (mx) {
       __syncthreads();  // every final chunk is in the LDS tile
       mx_tile_out<BM, BN, NT>(p, Cs, LDC_S, m0, n0);

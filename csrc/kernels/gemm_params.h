@@ -51,6 +51,9 @@ struct GemmParams {
   // and the activation backward is relu' (1/16 of the bytes of a bf16 z, written and read)
   int aux_bits;
   int dact_bits;
+  // EXT epilogue: += column sums of the bf16 output before any residual add ([N] f32; the bias
+  // gradient of the layer that consumes C, e.g. FFN1's from FFN2's dgrad -- no separate column pass)
+  float* colsum;
   // inverted dropout after the activation, before the residual add; mask = hash(seed, m*N + n),
   // identical to misc.hip's dropout kernel on the contiguous [M][N] output (backward regenerates it)
   float drop_p, drop_scale;

@@ -298,10 +298,12 @@ def mx_backward_ok(M: int, N: int, K: int) -> tuple[bool, bool]:
 
 def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None = None,
                     dact_src: torch.Tensor | None = None, dact: str | None = None, wt=None, dyq=None,
-                    drop_p: float = 0.0, drop_seed: int = 0, mx_out: bool = False) -> torch.Tensor:
+                    drop_p: float = 0.0, drop_seed: int = 0, mx_out: bool = False,
+                    colsum: torch.Tensor | None = None, mx_skip_c: bool = False) -> torch.Tensor:
     """dx[M,K] = dropout((MX(dy) @ MX(w^T)^T) [* act'(dact_src)]) (+ resid), bf16 -- the bf16
     linear_dgrad's epilogue order. wt: pre-quantized w^T (else the one the forward saved, else
-    quantized here); dyq: pre-quantized dy."""
+    quantized here); dyq: pre-quantized dy. colsum: as ops.gemm.linear_dgrad. mx_skip_c (with
+    mx_out): no bf16 dx -- every consumer takes the MX copies."""
     M, N = dy.shape
     K = w.shape[1]
     dq, ds = dyq if dyq is not None else mx_quantize(dy)
@@ -317,6 +319,8 @@ def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | Non
             from .elementwise import dropout_keep, eff_seed, keep_scale
             y = y * dropout_keep(eff_seed(drop_seed), y.numel(), drop_p).reshape(y.shape) * keep_scale(drop_p)
         y = y.to(torch.bfloat16)
+        if colsum is not None:
+            colsum.add_(y.float().sum(0))
         if resid is not None:
             y = (y.float() + resid.float()).to(torch.bfloat16)
         if mx_out and M % MX_BLOCK == 0 and K % MX_BLOCK == 0:
@@ -324,10 +328,17 @@ def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | Non
         return y
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
     mo = _mx_bufs(M, K, dx.device) if mx_out and M % MX_BLOCK == 0 and K % MX_BLOCK == 0 else None
+    fuse_cs = colsum is not None and resid is None and (dact_src is not None or drop_p > 0)
+    skip = bool(mo and mx_skip_c and (colsum is None or fuse_cs))
     lib().gemm_mxfp8(dq, ds, wq_, ws_, dx, M, K, N, None, resid, 0, None, drop_p, drop_seed,
-                     dact_src=dact_src, dact=ACT[dact] if dact_src is not None else 0, mx_out=list(mo) if mo else None)
+                     dact_src=dact_src, dact=ACT[dact] if dact_src is not None else 0, mx_out=list(mo) if mo else None,
+                     mx_skip_c=skip, colsum=colsum if fuse_cs else None)
     if mo:
         _register_out(dx, (mo[0], mo[1]), (mo[2], mo[3]))
+        if skip:
+            mark_no_c(dx)
+    if colsum is not None and not fuse_cs:
+        colsum.add_(dx.float().sum(0))
     return dx
 
 

@@ -161,12 +161,12 @@ def pick_splits(tiles: int, K: int, min_ktiles: int | None = None, target: int |
 
 def _gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile, *, alpha=1.0, beta=0.0, bias=None, resid=None,
           act=0, stats=None, shards=1, splits=1, batch=1, sA=0, sB=0, sC=0, split_stride=0, conv=NO_CONV, bnr=None,
-          aux=None, dact_src=None, dact=0, drop_p=0.0, drop_seed=0, rowmap=()):
+          aux=None, dact_src=None, dact=0, drop_p=0.0, drop_seed=0, rowmap=(), colsum=None):
     lib().gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile[0], tile[1], alpha, beta, bias, resid, act,
                stats, shards, splits, batch, sA, sB, sC, split_stride, conv,
                bnr.gemm_args() if bnr is not None else [],
                (int(bnr.relu) | (2 if bnr.premask else 0)) if bnr is not None else 0,
-               bnr.st.shards if bnr is not None else 1, aux, dact_src, dact, drop_p, drop_seed, list(rowmap))
+               bnr.st.shards if bnr is not None else 1, aux, dact_src, dact, drop_p, drop_seed, list(rowmap), colsum)
 
 
 def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, accumulate: bool, device,
@@ -262,10 +262,12 @@ def act_grad_ref(z: torch.Tensor, act: str | None) -> torch.Tensor:
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None = None,
                  dact_src: torch.Tensor | None = None, dact: str | None = None, drop_p: float = 0.0,
-                 drop_seed: int = 0) -> torch.Tensor:
+                 drop_seed: int = 0, colsum: torch.Tensor | None = None) -> torch.Tensor:
     """dx[M,K] = dropout((dy[M,N] @ w[N,K]) * act'(dact_src)) (+ resid). drop_p/drop_seed: the
     backward of a forward dropout on this layer's INPUT (mask = ops.elementwise.dropout_keep(eff_seed(drop_seed),
-    M*K, drop_p), e.g. the FFN's relu dropout) fused into the epilogue instead of a separate pass."""
+    M*K, drop_p), e.g. the FFN's relu dropout) fused into the epilogue instead of a separate pass.
+    colsum (f32 [K], with dact_src or dropout): += the column sums of dx before the residual add --
+    the bias gradient of the layer that consumes dx, from the epilogue instead of a column pass."""
     N, K = w.shape
     dy2 = dy.reshape(-1, N)
     M = dy2.shape[0]
@@ -277,17 +279,25 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
             from .elementwise import dropout_keep, eff_seed, keep_scale
             dx = dx * dropout_keep(eff_seed(drop_seed), dx.numel(), drop_p).reshape(dx.shape) * keep_scale(drop_p)
         dx = dx.to(torch.bfloat16)
+        if colsum is not None:
+            colsum.add_(dx.float().sum(0))
         if resid is not None:
             dx = (dx.float() + resid.reshape(-1, K).float()).to(torch.bfloat16)
         return dx
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
+    fuse_cs = colsum is not None and resid is None and (dact_src is not None or drop_p > 0)
     if resid is None and dact_src is None and drop_p == 0.0 and lib_gemm_ok("dgrad", M, K, N):
         torch.mm(dy2, w, out=dx)
+        if colsum is not None:
+            colsum.add_(dx.float().sum(0))
         return dx
     _gemm(dy2, w, dx, M, K, N, N, K, K, A_KIN, B_KOUT, EPI_BF16, pick_tile(M, K, big_ok=True, K=N, g4=K % 8 == 0),
           resid=resid.reshape(-1, K) if resid is not None else None,
           dact_src=dact_src.reshape(-1, K) if dact_src is not None else None,
-          dact=ACT[dact] if dact_src is not None else 0, drop_p=drop_p, drop_seed=drop_seed)
+          dact=ACT[dact] if dact_src is not None else 0, drop_p=drop_p, drop_seed=drop_seed,
+          colsum=colsum if fuse_cs else None)
+    if colsum is not None and not fuse_cs:
+        colsum.add_(dx.float().sum(0))  # plain epilogue: no fused column sums
     return dx
 
 

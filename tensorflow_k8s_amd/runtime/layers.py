@@ -72,6 +72,7 @@ def linear_dgrad(dy, w, fp8: bool, drop_p: float = 0.0, drop_seed: int = 0, dyq=
         if mx_backward_ok(dy.shape[0], dy.shape[1], w.shape[1])[0]:
             return linear_dgrad_mx(dy, w, dyq=dyq, drop_p=drop_p, drop_seed=drop_seed, **kw)
     kw.pop("mx_out", None)
+    kw.pop("mx_skip_c", None)
     return G.linear_dgrad(dy, w, drop_p=drop_p, drop_seed=drop_seed, **kw)
 
 
@@ -216,10 +217,13 @@ class Linear:
         return self.b.grad if self.b is not None and self.arena.prezeroed else None
 
     def backward(self, dy, x, need_dx: bool = True, resid=None, accumulate: bool = False, dact_src=None,
-                 dact=None, drop_p: float = 0.0, drop_seed: int = 0, mx_dx: bool = False, bias_done: bool = False):
+                 dact=None, drop_p: float = 0.0, drop_seed: int = 0, mx_dx: bool = False, bias_done: bool = False,
+                 dx_bias=None, mx_dx_only: bool = False):
         """dy: gradient of this layer's (pre-dropout, post-activation-backward) output. drop_p/drop_seed:
         a forward dropout on this layer's input, whose backward is fused into the dgrad epilogue.
-        mx_dx (fp8): the dgrad epilogue also emits MX(dx), MX(dx^T) for the producer's fp8 backward."""
+        mx_dx (fp8): the dgrad epilogue also emits MX(dx), MX(dx^T) for the producer's fp8 backward
+        (mx_dx_only: and no bf16 dx). dx_bias: the producer layer's bias gradient (its bias_sink()),
+        accumulated from dx's column sums in the dgrad epilogue."""
         dyq, dyt = fp8_dy(dy.reshape(-1, dy.shape[-1]), self.fin, self.fp8 and need_dx)
         linear_wgrad(dy, x, self.w.grad, self.fp8, accumulate=accumulate, split_target=self.split_target, dyt=dyt)
         if self.b is not None:
@@ -230,7 +234,9 @@ class Linear:
             self.arena.grad_ready(self.w)
         if not need_dx:
             return None
-        kw = {"mx_out": True} if mx_dx else {}
+        kw = {"mx_out": True, "mx_skip_c": mx_dx_only} if mx_dx else {}
+        if dx_bias is not None:
+            kw["colsum"] = dx_bias
         return linear_dgrad(dy, self.w.compute, self.fp8, resid=resid, dact_src=dact_src, dact=dact, drop_p=drop_p,
                             drop_seed=drop_seed, dyq=dyq, **kw)
 

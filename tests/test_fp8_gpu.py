@@ -363,3 +363,31 @@ def test_layernorm_bwd_mx_outputs(M, W, drop):
     torch.cuda.synchronize()
     assert torch.equal(q, q1) and torch.equal(s, s1) and torch.equal(qt, qt1) and torch.equal(st, st1)
     F8.clear_saved()
+
+
+def test_fp8_dgrad_column_sums_and_mx_only_output():
+    """MX-fp8 dgrad with the fused column sums and mx_skip_c: the sums equal those of the bf16 dx a
+    storing call produces, and the MX copies are the same bytes either way."""
+    from tensorflow_k8s_amd.ops import gemm as G
+    M, N, K = 1024, 512, 256
+    g = torch.Generator().manual_seed(11)
+    dy = (torch.randn(M, N, generator=g) * 0.5).to(torch.bfloat16).cuda()
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16).cuda()
+    mask = G.relu_mask_pack(torch.randn(M, K, generator=g)).cuda()
+    try:
+        cs1 = torch.zeros(K, device="cuda")
+        dx = F8.linear_dgrad_mx(dy, w, dact_src=mask, dact="relu", drop_p=0.1, drop_seed=2, mx_out=True, colsum=cs1)
+        q1 = [t.clone() for pair in F8.cached_dual(dx) for t in pair]
+        cs2 = torch.zeros(K, device="cuda")
+        dx2 = F8.linear_dgrad_mx(dy, w, dact_src=mask, dact="relu", drop_p=0.1, drop_seed=2, mx_out=True,
+                                 colsum=cs2, mx_skip_c=True)
+        q2 = [t.clone() for pair in F8.cached_dual(dx2) for t in pair]
+        torch.cuda.synchronize()
+        ref = dx.float().sum(0)
+        tol = 1e-3 * float(ref.abs().max()) + 1e-4
+        assert float((cs1 - ref).abs().max()) <= tol and float((cs2 - ref).abs().max()) <= tol
+        assert all(torch.equal(a, b) for a, b in zip(q1, q2))
+        with pytest.raises(RuntimeError):
+            F8._check_stored(dx2)  # no bf16 values behind an mx_skip_c output
+    finally:
+        F8.clear_saved()

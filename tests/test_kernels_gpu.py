@@ -677,3 +677,17 @@ def test_relu_mask_aux_matches_bf16_aux(M, N, K):
     d1 = G.linear_dgrad(dy, w2, dact_src=z, dact="relu", drop_p=0.1, drop_seed=7)
     d2 = G.linear_dgrad(dy, w2, dact_src=m, dact="relu", drop_p=0.1, drop_seed=7)
     assert torch.equal(d1, d2)
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 4096, 1024), (1000, 264, 128)])
+def test_dgrad_fused_column_sums(M, N, K):
+    """linear_dgrad(colsum=...) accumulates the column sums of the stored dx (the consumer layer's
+    bias gradient) in the EXT epilogue: matches dx.sum(0) of the same call, interior and ragged tiles."""
+    dy, w = bf(M, K, seed=3).to(DEV), bf(K, N, scale=0.05, seed=4).to(DEV)
+    x, w1 = bf(M, 64, seed=5).to(DEV), bf(N, 64, scale=0.1, seed=6).to(DEV)
+    m = torch.empty(M, N // 8, device=DEV, dtype=torch.uint8)
+    G.linear_fwd(x, w1, act="relu", aux=m)
+    cs = torch.full((N,), 0.5, device=DEV)
+    dx = G.linear_dgrad(dy, w, dact_src=m, dact="relu", drop_p=0.1, drop_seed=9, colsum=cs)
+    ref = dx.float().sum(0) + 0.5
+    assert float((cs - ref).abs().max()) <= 1e-3 * float(ref.abs().max()) + 1e-4

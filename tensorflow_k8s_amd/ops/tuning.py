@@ -18,7 +18,9 @@ from __future__ import annotations
 import json
 import os
 
-_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_wgrad.json")
+# TFK_WGRAD_TABLE: an alternative weight-gradient table (A/B of a fresh tools/wgrad_sweep.py --table)
+_PATH = os.environ.get("TFK_WGRAD_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                            "tuned_wgrad.json")
 # TFK_CONV_TABLE: an alternative conv tile table (A/B of a fresh tools/conv_sweep.py --table)
 _CONV_PATH = os.environ.get("TFK_CONV_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                 "tuned_conv.json")

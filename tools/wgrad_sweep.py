@@ -27,7 +27,7 @@ SHAPES = [(64, 64, 802816), (64, 256, 802816), (256, 64, 802816), (128, 256, 802
           (512, 256, 200704), (128, 512, 200704), (512, 128, 200704), (256, 512, 200704), (1024, 512, 50176),
           (256, 1024, 50176), (1024, 256, 50176), (512, 1024, 50176), (2048, 1024, 12544), (512, 2048, 12544),
           (2048, 512, 12544)]
-TILES = [(64, 64), (128, 64), (64, 128), (128, 128), (64, 256), (256, 64), (256, 256)]
+TILES = [(64, 64), (128, 64), (64, 128), (128, 128), (64, 256), (256, 64), (256, 128), (128, 256), (256, 256)]
 SPLITS = [1, 2, 4, 8, 16, 32, 64, 128, 256, 512]
 
 

@@ -24,11 +24,12 @@ from tensorflow_k8s_amd.ops import gemm as G  # noqa: E402
 from tensorflow_k8s_amd.ops import norm as BN  # noqa: E402
 from tensorflow_k8s_amd.ops import tuning  # noqa: E402
 
+# (256, 128) / (128, 256): the 8-wave 3-stage g4 tiles (gemm_g4.hip NST = 3)
 CANDS = {
-    "fwd_pw": [(128, 128), (256, 256), (128, 64), (64, 128), (256, 64), (64, 64)],
-    "fwd_gather": [(128, 128), (256, 256), (128, 64), (64, 128), (64, 64), (256, 64)],
-    "dgrad_pw": [(128, 128), (256, 256), (128, 64), (64, 128), (256, 64), (64, 64)],
-    "dgrad_fwd": [(128, 128), (256, 256), (128, 64), (64, 128), (64, 64), (256, 64)],
+    "fwd_pw": [(128, 128), (256, 256), (128, 64), (64, 128), (256, 64), (64, 64), (256, 128), (128, 256)],
+    "fwd_gather": [(128, 128), (256, 256), (128, 64), (64, 128), (64, 64), (256, 64), (256, 128), (128, 256)],
+    "dgrad_pw": [(128, 128), (256, 256), (128, 64), (64, 128), (256, 64), (64, 64), (256, 128), (128, 256)],
+    "dgrad_fwd": [(128, 128), (256, 256), (128, 64), (64, 128), (64, 64), (256, 64), (256, 128), (128, 256)],
 }
 
 

@@ -55,8 +55,14 @@ int main(int argc, char** argv) {
   const std::string scheme = srv.tls() ? "https://" : "http://";
   TFK_LOG(Info, "serving", Json(Json::object_t{{"url", Json(scheme + host + ":" + std::to_string(srv.port()))}}));
   if (!port_file.empty()) {
-    FILE* f = fopen(port_file.c_str(), "w");
-    if (f) { fprintf(f, "%d\n", srv.port()); fclose(f); }
+    // write-then-rename: a reader polling for the file never sees it created but still empty
+    const std::string tmp = port_file + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "w");
+    if (f) {
+      fprintf(f, "%d\n", srv.port());
+      fclose(f);
+      std::rename(tmp.c_str(), port_file.c_str());
+    }
   }
   printf("listening on %s%s:%d\n", scheme.c_str(), host.c_str(), srv.port());
   fflush(stdout);

@@ -44,8 +44,14 @@ int main(int argc, char** argv) {
   if (!srv.start(host, (int)port, &err)) { TFK_LOG(Error, "apiserver: " + err); return 1; }
   std::string url = "http://" + host + ":" + std::to_string(srv.port());
   if (!port_file.empty()) {
-    FILE* f = fopen(port_file.c_str(), "w");
-    if (f) { fprintf(f, "%d\n", srv.port()); fclose(f); }
+    // write-then-rename: a reader polling for the file never sees it created but still empty
+    const std::string tmp = port_file + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "w");
+    if (f) {
+      fprintf(f, "%d\n", srv.port());
+      fclose(f);
+      std::rename(tmp.c_str(), port_file.c_str());
+    }
   }
   printf("listening on %s\n", url.c_str());
   fflush(stdout);

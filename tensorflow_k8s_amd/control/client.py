@@ -180,11 +180,16 @@ class LocalCluster:
         e.setdefault("PYTHONPATH", ROOT)
         self.proc = subprocess.Popen(args, stdout=self.log, stderr=subprocess.STDOUT, env=e, start_new_session=True)
         dl = time.time() + 30
-        while time.time() < dl and not os.path.exists(self.port_file):
+        port = None
+        while time.time() < dl and port is None:
             if self.proc.poll() is not None:
                 raise RuntimeError(f"tfk-cluster exited: {open(self.log_path).read()[-2000:]}")
-            time.sleep(0.05)
-        port = int(open(self.port_file).read().strip())
+            try:  # the binary renames a complete file into place; tolerate older binaries' partial writes
+                port = int(open(self.port_file).read().strip())
+            except (OSError, ValueError):
+                time.sleep(0.05)
+        if port is None:
+            raise RuntimeError(f"tfk-cluster wrote no port within 30 s: {open(self.log_path).read()[-2000:]}")
         self.url = f"http://127.0.0.1:{port}"
         self.client = TfkClient(self.url)
         while not self.client.healthy():

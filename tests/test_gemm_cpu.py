@@ -31,3 +31,20 @@ def test_relu_mask_reference_matches_bf16_preactivation():
     dy = torch.randn(M, K, generator=g).to(torch.bfloat16)
     w2 = torch.randn(K, N, generator=g).to(torch.bfloat16)
     assert torch.equal(G.linear_dgrad(dy, w2, dact_src=z, dact="relu"), G.linear_dgrad(dy, w2, dact_src=m, dact="relu"))
+
+
+def test_dgrad_colsum_reference_is_bias_gradient_of_consumer():
+    """linear_dgrad(colsum=g) adds the column sums of the returned dx (before any residual) to g --
+    the bias gradient of the layer consuming dx (CPU reference path)."""
+    import torch
+    from tensorflow_k8s_amd.ops import gemm as G
+    g = torch.Generator().manual_seed(2)
+    M, N, K = 24, 16, 40
+    dy = torch.randn(M, N, generator=g).to(torch.bfloat16)
+    w = torch.randn(N, K, generator=g).to(torch.bfloat16)
+    z = torch.randn(M, K, generator=g)
+    m = G.relu_mask_pack(z)
+    cs = torch.full((K,), 2.0)
+    dx = G.linear_dgrad(dy, w, dact_src=m, dact="relu", colsum=cs)
+    assert torch.allclose(cs, dx.float().sum(0) + 2.0, atol=1e-5)
+    assert torch.equal(dx, G.linear_dgrad(dy, w, dact_src=m, dact="relu"))

@@ -39,6 +39,11 @@ def graph_hazards(model) -> list[str]:
     return out
 
 
+def ps_capture_ok(opt) -> bool:
+    """Optimizers whose per-bucket collective parameter-server update is verified under capture."""
+    return opt is None or type(opt).__name__ == "SGD"
+
+
 class StepRunner:
     def __init__(self, model, opt, strategy, batch, use_graph: bool = False, warmup_eager: int = 2,
                  agree=None, rank: int = 0):
@@ -47,6 +52,15 @@ class StepRunner:
         # a parameter-server strategy is capturable only on its collective (RCCL) transport
         self.use_graph = (use_graph and torch.cuda.is_available() and batch[0].is_cuda
                           and (not hasattr(strategy, "apply_gradients") or getattr(strategy, "capturable", False)))
+        self.fallback = ""  # why the step runs eager (refused or failed capture)
+        if self.use_graph and hasattr(strategy, "apply_gradients") and not ps_capture_ok(opt):
+            # KNOWN ISSUE (round 4): the captured collective-PS step with an Adam-family optimizer
+            # (per-bucket AdamW / LAMB regions) faults with an illegal address on replay (BERT-base and
+            # Transformer-big, one GPU, forced comm); the eager step runs correctly and the captured
+            # SGD step (ResNet) is verified (tests/test_bench_gpu.py). Run those eager until fixed.
+            self.use_graph = False
+            self.fallback = (f"collective parameter-server step with {type(opt).__name__}: capture disabled "
+                             "(known replay fault), running eager")
         if self.use_graph:
             bad = graph_hazards(model)
             if bad:
@@ -55,7 +69,6 @@ class StepRunner:
                 opt.enable_device_schedule()
         self.warmup_eager = warmup_eager
         self.agree, self.rank = agree, rank
-        self.fallback = ""  # why the step runs eager after a failed (agreed) capture
         self.graph = None
         self.n = 0
         self._loss = None

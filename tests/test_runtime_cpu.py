@@ -293,3 +293,17 @@ def test_step_region_advances_once_per_global_step(device_schedule):
         res.append((m.arena.master.clone(), opt.sync_step()))
     assert res[0][1] == res[1][1] == 6
     torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-6, atol=1e-7)
+
+
+def test_collective_ps_capture_guard_by_optimizer():
+    """Captured collective-PS steps are allowed only for the verified optimizer (SGD); Adam-family
+    per-bucket updates run eager (runtime.trainer.ps_capture_ok, known replay fault)."""
+    from tensorflow_k8s_amd.runtime.trainer import ps_capture_ok
+
+    class SGD: pass  # noqa: E701
+
+    class AdamW: pass  # noqa: E701
+
+    class LAMB: pass  # noqa: E701
+    assert ps_capture_ok(SGD()) and ps_capture_ok(None)
+    assert not ps_capture_ok(AdamW()) and not ps_capture_ok(LAMB())

@@ -165,7 +165,7 @@ def main():
         if wd is not None:
             wd.beat(phase="serve")
         if args.ps_transport == "gloo":
-            server.serve()
+            server.serve(beat=wd.beat if wd is not None else None)
         else:
             server.setup_collective(args.bucket_mb, world_comm, wire)
             server.serve_steps(0, args.warmup + args.steps, beat=wd.beat if wd is not None else None)

@@ -225,6 +225,7 @@ class RcclComm {
 
   // "" while healthy, else the asynchronous error RCCL recorded (peer lost, remote abort ...)
   std::string async_error() {
+    if (destroyed_.load()) return std::string();  // orderly teardown (destroy), not a failure
     if (!valid()) return "communicator aborted";
     ncclResult_t e = ncclSuccess;
     nccl_check(ncclCommGetAsyncError(comm_, &e), "ncclCommGetAsyncError");
@@ -240,7 +241,9 @@ class RcclComm {
   }
   // Orderly teardown (all ranks): finalize outstanding work, then free.
   void destroy() {
-    if (!comm_ || gone_.exchange(true)) return;
+    if (!comm_) return;
+    destroyed_.store(true);
+    if (gone_.exchange(true)) return;
     py::gil_scoped_release nogil;
     ncclCommFinalize(comm_);
     ncclCommDestroy(comm_);
@@ -253,6 +256,7 @@ class RcclComm {
   ncclComm_t comm_ = nullptr;
   int nranks_ = 0, rank_ = 0, device_ = 0;
   std::atomic<bool> gone_{false};
+  std::atomic<bool> destroyed_{false};
 };
 
 void group_start() { nccl_check(ncclGroupStart(), "ncclGroupStart"); }

@@ -438,8 +438,11 @@ class ParameterServer:
             a.slot(nm)[lo:hi].copy_(buf[(k + 1) * n:(k + 2) * n])
         self.opt.step_count = step
 
-    def serve(self) -> int:
-        """Serve until every worker has sent DONE. Returns the number of optimizer updates."""
+    def serve(self, beat=None) -> int:
+        """Serve until every worker has sent DONE. Returns the number of optimizer updates.
+        ``beat(step)`` is the watchdog heartbeat: called for every command received, so a healthy
+        server blocked in recv between worker steps is not mistaken for a hung one -- but a server
+        whose workers stop sending is (their gang restart is the recovery)."""
         a, lo, hi = self.arena, self.lo, self.hi
         n = hi - lo
         live = set(self.worker_ranks)
@@ -449,6 +452,8 @@ class ParameterServer:
         while live:
             src = dist.recv(hdr, None, group=self.group)  # any source
             cmd, step = int(hdr[0]), int(hdr[1])
+            if beat is not None:
+                beat(step)
             if cmd == DONE:
                 live.discard(src)
                 continue

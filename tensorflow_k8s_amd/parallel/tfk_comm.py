@@ -230,11 +230,13 @@ class RcclComm:
         return True
 
     def destroy(self):
+        # leave the live set FIRST: while ncclCommFinalize/Destroy runs (GIL released) the watchdog's
+        # async-error poll must not read the communicator's own teardown as an RCCL failure
+        with _LIVE_LOCK:
+            _LIVE.discard(self)
         if not self._aborted:
             self._aborted = True
             self._c.destroy()
-        with _LIVE_LOCK:
-            _LIVE.discard(self)
 
 
 class _RcclGroup:

@@ -118,6 +118,16 @@ def sync() -> None:
             main.wait_stream(s)
 
 
+def reset() -> None:
+    """Drop every queued (unissued) weight gradient and kept tensor: after a step capture that
+    raised mid-backward, the queue holds closures over the dropped graph's tensors, which must
+    never run in a later step (the caller synchronizes the device first)."""
+    global _flushes
+    _pending.clear()
+    _keep.clear()
+    _flushes = 0
+
+
 def join() -> None:
     """sync() + release the tensors the side-stream work read."""
     sync()

@@ -179,8 +179,10 @@ def run_ps(args, info, dev, world_comm, watchdog=None) -> int:
                                     comm=world_comm, wire_dtype=_wire(args),
                                     beat=watchdog.beat if watchdog is not None else None)
     else:
-        n = server.serve()
+        n = server.serve(beat=watchdog.beat if watchdog is not None else None)
     _log({"event": "done", "role": "ps", "index": info.task_index, "updates": n})
+    if watchdog is not None:
+        watchdog.exit_code = 0  # the job's part is done: a hung teardown is not a failure
     tfk_comm.shutdown()
     return EXIT_OK
 
@@ -307,6 +309,11 @@ def run_worker(args, info, dev, world_comm, watchdog=None) -> int:
         strat.shutdown()
     if world_comm is not None and not use_ps:
         world_comm.barrier()
+    if watchdog is not None:
+        # the result is out: the communicator teardown below must not be mistaken for an RCCL error
+        # (a destroyed communicator reports "aborted") or a hang turned into a retryable failure
+        watchdog.exit_code = 0
+        watchdog.stop()
     tfk_comm.shutdown()
     if info.is_chief:
         _log({"event": "done", "step": step, "loss": runner.last_loss()}, metrics_fh)

@@ -139,6 +139,8 @@ class StepRunner:
             self.graph, self.use_graph, self.fallback = None, False, err
             del g
             torch.cuda.synchronize()
+            from . import streams
+            streams.reset()  # weight gradients queued by the aborted capture must never run
             return False
         self.graph = g
         return True

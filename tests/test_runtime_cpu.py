@@ -306,3 +306,27 @@ def test_collective_ps_capture_guard_by_model():
     class Transformer:
         rng_state = None
     assert ps_capture_ok(ResNet()) and not ps_capture_ok(Transformer())
+
+
+def test_gloo_ps_task_survives_short_watchdog(tmp_path, native_ext):
+    """a gloo parameter-server task blocks in recv between worker pushes; with the
+    watchdog armed (here 2 s) it must beat on every command it receives, so a healthy job that runs
+    longer than the timeout (12 paced steps, ~4 s) ends 0 on every task -- not 143 on the ps."""
+    p = free_port()
+    out = _launch([("chief", 0), ("ps", 0)], {"chief": [f"c.svc:{p}"], "ps": ["p0.svc:1"]},
+                  BASE + ["--watchdog-timeout", "2", "--step-sleep", "0.35"], str(tmp_path))
+    assert all(v[0] == 0 for v in out.values()), {k: v[2][-1500:] for k, v in out.items()}
+    assert not any(e.get("kind") == "watchdog" for v in out.values() for e in v[1])
+    assert [e for e in out[("ps", 0)][1] if e["event"] == "done"][0]["updates"] == 12
+
+
+def test_streams_reset_drops_queued_weight_gradients():
+    """a capture that raises mid-backward leaves deferred weight-gradient closures
+    queued; StepRunner's fallback path calls streams.reset() so none of them runs in a later step."""
+    from tensorflow_k8s_amd.runtime import streams
+    ran = []
+    streams._pending.append((lambda: ran.append(1), (torch.zeros(1),)))
+    streams._keep.append(torch.zeros(1))
+    streams.reset()
+    streams.flush(force=True)
+    assert ran == [] and streams._pending == [] and streams._keep == []

@@ -108,8 +108,10 @@ struct Loader {
 
   // Issue this thread's DMA instructions of K-tile kt into image `img`. base = tile origin;
   // lim = rows left from the tile origin. Interior tiles with a full K-tile skip every edge test.
+  // en = false: every lane's offset is out of range -> the DMA writes zeros and touches no memory
+  // (lets a pipelined loop issue unconditionally, keeping its MFMA / DMA region one basic block)
   __device__ __forceinline__ void issue(const GemmParams& p, const char* base, long long step, int kt, int lim,
-                                        char* img, int w, int lane) const {
+                                        char* img, int w, int lane, bool en = true) const {
     const int krem = p.K - kt * BK;
     const bool inner = lim >= ROWS && krem >= BK;  // block-uniform
     if constexpr (MODE == CONV_WGRAD) {
@@ -122,7 +124,7 @@ struct Loader {
         const unsigned pp = fdiv(rem, p.fd_q_mul, p.fd_q_shift), qq = rem - pp * (unsigned)p.Q;
         const int h = (int)pp * p.sh + ch[i], wq = (int)qq * p.sw + cw[i];
         const bool ok = !(off[i] & OOB) && (int)pix < p.K && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
-        const unsigned vo = ok ? (unsigned)(((((long long)n * p.H + h) * p.W + wq) * p.Cin + off[i]) * 2) : OOB;
+        const unsigned vo = ok && en ? (unsigned)(((((long long)n * p.H + h) * p.W + wq) * p.Cin + off[i]) * 2) : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
       }
     } else if constexpr (MODE == CONV_FWD) {
@@ -139,7 +141,7 @@ struct Loader {
           const int h = ch[i] + rdh, wq = cw[i] + sdw;
           const bool ok = (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
           const int pix = (int)off[i] + tap;
-          const unsigned vo = ok ? (unsigned)(pix * p.Cin + c0 + k_of(i, w, lane)) * 2u : OOB;
+          const unsigned vo = ok && en ? (unsigned)(pix * p.Cin + c0 + k_of(i, w, lane)) * 2u : OOB;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
         }
       } else {
@@ -155,7 +157,7 @@ struct Loader {
           const bool ok = (int)k < p.K && (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H &&
                           (unsigned)wq < (unsigned)p.W;
           const int pix = (int)off[i] + (int)r * p.dh * p.W + (int)sx * p.dw;
-          const unsigned vo = ok ? (unsigned)(pix * p.Cin + (int)c) * 2u : OOB;
+          const unsigned vo = ok && en ? (unsigned)(pix * p.Cin + (int)c) * 2u : OOB;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
         }
       }
@@ -166,6 +168,7 @@ struct Loader {
       for (int i = 0; i < NI; ++i) {
         unsigned vo = off[i];
         if (!inner) vo = (row_of(i, w, lane) < lim && k_of(i, w, lane) < krem) ? vo : OOB;
+        if (!en) vo = OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
       }
     }

@@ -401,6 +401,8 @@ static void fast_div(unsigned d, unsigned* mul, int* shift) {
 extern "C" int tfk_halo_launch(const GemmParams& p, int epi, int batch, int splits, hipStream_t stream);
 extern "C" int tfk_g8_launch(const GemmParams& p, int amode, int bmode, int epi, int batch, int splits,
                              hipStream_t stream);
+extern "C" int tfk_g5_launch(const GemmParams& p, int amode, int bmode, int epi, int batch, int splits,
+                             hipStream_t stream);
 
 extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, int bmode, int epi, int batch,
                              int splits, hipStream_t stream) {
@@ -409,9 +411,11 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
     const int r = tfk_halo_launch(p_in, epi, batch, splits, stream);
     if (r != -1) return r;
   }
-  // dense 256x256: the 8-phase engine when enabled (gemm_g8.hip)
+  // 256x256: the mid-tile-barrier engine (gemm_g5.hip) or the 8-phase engine (gemm_g8.hip) when enabled
   if (bm == 256 && bn == 256) {
-    const int r = tfk_g8_launch(p_in, amode, bmode, epi, batch, splits, stream);
+    int r = tfk_g5_launch(p_in, amode, bmode, epi, batch, splits, stream);
+    if (r != -1) return r;
+    r = tfk_g8_launch(p_in, amode, bmode, epi, batch, splits, stream);
     if (r != -1) return r;
   }
   GemmParams p = p_in;

@@ -61,6 +61,8 @@ from . import tfk_comm
 
 PUSH, DONE, FETCH, LOAD, PULL = 1, 2, 3, 4, 5
 RUN_AHEAD = 2  # owner loop: at most this many global steps enqueued ahead of the device
+CAPTURE_OWNER = True  # GPU owners replay their per-step sequence from one hipGraph
+OWNER_WARMUP = 2  # eager owner steps before the capture (they size every lazily built table)
 
 
 def shard_bounds(numel: int, nshards: int, param_spans: list[tuple[int, int]] | None = None) -> list[tuple[int, int]]:
@@ -511,35 +513,70 @@ class ParameterServer:
         self._plan = CollectivePlan(a, self.shards, self.ps_ranks, self.worker_ranks, bucket_mb, self._comm, wire_dtype)
         self._plan.pull_master()
 
+    def _owner_step(self, mine) -> None:
+        """One global step of this owner's shard, all on streams (hipGraph-capturable): zero the
+        own gradient contribution, post the own buckets' reduces, per bucket wait -> unpack ->
+        fused optimizer on the bucket -> post its broadcast, then join every broadcast."""
+        a, plan, opt = self.arena, self._plan, self.opt
+        a.grad[self.lo:self.hi].zero_()  # the owner's own (zero) contribution to its reduces
+        if plan.wire is not None:
+            plan.wire[self.lo:self.hi].zero_()
+        reds = [plan.reduce(i, a.grad) for i in mine]
+        bcs = []
+        for k, (i, w) in enumerate(zip(mine, reds)):
+            w.wait()
+            plan.unpack(i)
+            lo, hi, _ = plan.buckets[i]
+            opt.region = (lo, hi)
+            opt.step_region(advance=k == 0)
+            bcs.append(plan.broadcast(i))
+        for w in bcs:
+            w.wait()
+        opt.region = (self.lo, self.hi)
+
+    def _capturable(self) -> bool:
+        return (self.arena.master.is_cuda and getattr(self._comm, "backend", "") == "rccl"
+                and CAPTURE_OWNER and hasattr(self.opt, "enable_device_schedule"))
+
     def serve_steps(self, start_step: int, end_step: int, checkpoint_every: int = 0, chief: int = 0,
                     final_checkpoint: bool = False, total_steps: int | None = None, beat=None) -> int:
         """Serve global steps start_step+1 .. end_step (after setup_collective). ``beat(step)`` is
-        the watchdog heartbeat; the host runs at most RUN_AHEAD steps ahead of the device."""
+        the watchdog heartbeat; the host runs at most RUN_AHEAD steps ahead of the device.
+
+        GPU owners (RCCL transport) capture the step once in a hipGraph after ``OWNER_WARMUP`` eager
+        steps and replay it: one host call per global step instead of ~4 per bucket (the learning
+        rate, step counter and bias corrections advance on the device, Optimizer.enable_device_schedule).
+        The collective sequence is the same captured or eager, so the workers' own graph-or-eager
+        decision needs no coordination with the owner; a failed owner capture runs eager
+        (``self.capture_fallback`` says why)."""
         a, plan, comm, opt = self.arena, self._plan, self._comm, self.opt
         total = end_step if total_steps is None else total_steps
         me = self.ps_ranks.index(comm.rank)
         mine = plan.buckets_of(me)
         ring = []
+        graph = None
+        use_graph = self._capturable()
+        if use_graph and opt._dev is None:
+            opt.step_count = start_step
+            opt.enable_device_schedule()
+        n_eager = 0
         for step in range(start_step + 1, end_step + 1):
             if len(ring) >= RUN_AHEAD:
                 ring.pop(0).synchronize()  # bounded run-ahead: step - RUN_AHEAD has completed
             if beat is not None:
                 beat(step)
-            a.grad[self.lo:self.hi].zero_()  # the owner's own (zero) contribution to its reduces
-            if plan.wire is not None:
-                plan.wire[self.lo:self.hi].zero_()
-            reds = [plan.reduce(i, a.grad) for i in mine]
-            bcs = []
-            for k, (i, w) in enumerate(zip(mine, reds)):
-                w.wait()
-                plan.unpack(i)
-                lo, hi, _ = plan.buckets[i]
-                opt.region = (lo, hi)
-                opt.step_region(advance=k == 0)
-                bcs.append(plan.broadcast(i))
-            for w in bcs:
-                w.wait()
-            opt.region = (self.lo, self.hi)
+            if graph is not None:
+                graph.replay()
+            elif use_graph and n_eager >= OWNER_WARMUP:
+                graph = self._capture_owner(mine)
+                if graph is None:
+                    use_graph = False
+                    self._owner_step(mine)
+                else:
+                    graph.replay()
+            else:
+                self._owner_step(mine)
+                n_eager += 1
             self.updates += 1
             if a.master.is_cuda:
                 ev = torch.cuda.Event()
@@ -551,4 +588,23 @@ class ParameterServer:
                 comm.send(self._state(), chief)
                 if a.master.is_cuda:
                     torch.cuda.current_stream().synchronize()
+        self.owner_graph = graph is not None
+        if opt._dev is not None:
+            opt.sync_step()
         return self.updates
+
+    capture_fallback = ""
+    owner_graph = False
+
+    def _capture_owner(self, mine):
+        """Capture one owner step (returns None and records why on failure)."""
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._owner_step(mine)
+        except Exception as e:  # noqa: BLE001 -- the owner then serves eagerly
+            self.capture_fallback = f"{type(e).__name__}: {e}"[:400]
+            torch.cuda.synchronize()
+            return None
+        return g

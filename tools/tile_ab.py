@@ -22,15 +22,23 @@ from tensorflow_k8s_amd.ops import gemm as G  # noqa: E402
 from tensorflow_k8s_amd.ops._lib import lib  # noqa: E402
 
 
+def _engine(t, on: bool):
+    """Switch the 256x256 engine a named tile stands for: "g8" (8-phase) or "g5" (mid-tile barrier)."""
+    if t == "g8":
+        lib().g8_set(1 if on else 0)
+    elif t == "g5":
+        lib().g5_set(8 if on else 0)
+
+
 def _g8(fn, t):
-    """Run fn on tile t; "g8" = the 256x256 tile with the 8-phase engine switched on."""
-    if t != "g8":
+    """Run fn on tile t; "g8" / "g5" = the 256x256 tile on that engine."""
+    if not isinstance(t, str):
         return fn(t)
-    lib().g8_set(1)
+    _engine(t, True)
     try:
         return fn((256, 256))
     finally:
-        lib().g8_set(0)
+        _engine(t, False)
 
 
 def tname(t):
@@ -52,7 +60,7 @@ CONV = {  # ResNet-50 bs256 3x3 convs (N, H, W, C, K): stride 1
     "r50_3x3_s4": (256, 14, 14, 256, 256),
     "r50_3x3_s5": (256, 7, 7, 512, 512),
 }
-TILES = [(256, 256), (128, 128), (256, 128), (128, 256), "g8"]  # "g8": 256x256 on the 8-phase engine
+TILES = [(256, 256), (128, 128), (256, 128), (128, 256), "g8", "g5"]  # "g8"/"g5": 256x256 on that engine
 
 
 def timeit(fn, iters):
@@ -71,7 +79,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="")
     ap.add_argument("--dirs", default="fwd,dgrad,wgrad,conv")
+    ap.add_argument("--tiles", default="", help="subset, e.g. 256x256,g8,g5")
     args = ap.parse_args()
+    if args.tiles:
+        TILES[:] = [t if t in ("g8", "g5") else tuple(int(v) for v in t.split("x")) for t in args.tiles.split(",")]
     dirs = set(args.dirs.split(","))
     dev = "cuda"
     for name, (M, N, K) in DENSE.items():
@@ -129,14 +140,14 @@ def main():
         outs = {}
         for _ in range(args.rounds):
             for t in TILES_C:
-                G.FORCE_TILE = (256, 256) if t == "g8" else t
-                lib().g8_set(1 if t == "g8" else 0)
+                G.FORCE_TILE = (256, 256) if isinstance(t, str) else t
+                _engine(t, True)
                 try:
                     res[t].append(fl / timeit(lambda: G.conv_fwd(x, w, g), args.iters) / 1e12)
                     outs[t] = G.conv_fwd(x, w, g)
                 finally:
                     G.FORCE_TILE = None
-                    lib().g8_set(0)
+                    _engine(t, False)
         ref = G._ref_conv(x, w, g)
         out = {"shape": name, "dir": "conv_fwd", "M": Nn * H * W, "N": Kc, "K": 9 * C}
         for t in TILES_C:

@@ -111,7 +111,7 @@ struct Loader {
   // en = false: every lane's offset is out of range -> the DMA writes zeros and touches no memory
   // (lets a pipelined loop issue unconditionally, keeping its MFMA / DMA region one basic block)
   __device__ __forceinline__ void issue(const GemmParams& p, const char* base, long long step, int kt, int lim,
-                                        char* img, int w, int lane, bool en = true) const {
+                                        char* img, int w, int lane, bool en = true, int only = -1) const {
     const int krem = p.K - kt * BK;
     const bool inner = lim >= ROWS && krem >= BK;  // block-uniform
     if constexpr (MODE == CONV_WGRAD) {
@@ -119,6 +119,7 @@ struct Loader {
       const unsigned PQ = (unsigned)(p.P * p.Q);
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
+        if (only >= 0 && i != only) continue;
         const unsigned pix = (unsigned)(kt * BK + k_of(i, w, lane));
         const unsigned n = fdiv(pix, p.fd_pq_mul, p.fd_pq_shift), rem = pix - n * PQ;
         const unsigned pp = fdiv(rem, p.fd_q_mul, p.fd_q_shift), qq = rem - pp * (unsigned)p.Q;
@@ -138,6 +139,7 @@ struct Loader {
         const int rdh = r * p.dh, sdw = s * p.dw, tap = rdh * p.W + sdw;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
+          if (only >= 0 && i != only) continue;
           const int h = ch[i] + rdh, wq = cw[i] + sdw;
           const bool ok = (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
           const int pix = (int)off[i] + tap;
@@ -150,6 +152,7 @@ struct Loader {
         // division (host: fd_pq = Cin, fd_q = S); k >= K (the ragged last K-tile) reads zeros
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
+          if (only >= 0 && i != only) continue;
           const unsigned k = (unsigned)(kt * BK + k_of(i, w, lane));
           const unsigned rs = fdiv(k, p.fd_pq_mul, p.fd_pq_shift), c = k - rs * (unsigned)p.Cin;
           const unsigned r = fdiv(rs, p.fd_q_mul, p.fd_q_shift), sx = rs - r * (unsigned)p.S;
@@ -166,6 +169,7 @@ struct Loader {
           __builtin_amdgcn_make_buffer_rsrc((void*)(base + kt * step), (short)0, NREC, 0x00020000);
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
+        if (only >= 0 && i != only) continue;
         unsigned vo = off[i];
         if (!inner) vo = (row_of(i, w, lane) < lim && k_of(i, w, lane) < krem) ? vo : OOB;
         if (!en) vo = OOB;

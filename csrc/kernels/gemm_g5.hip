@@ -57,7 +57,11 @@ __device__ __forceinline__ void interleave() {
   if (REM) __builtin_amdgcn_sched_group_barrier(0x008, REM, 0);
 }
 
-template <int AM, int BMD, int EPI, int WGM, int WGN>
+// SCHED 0: each phase's reads / DMA pieces are spread between its MFMAs by sched_group_barrier;
+// SCHED 1: the phase is written as fixed slots {MFMAs, one DMA piece, one fragment read} fenced by
+// sched_barrier, MFMAs first -- so right after the barrier the MFMA pipe restarts at once instead of
+// behind the DMA address setup the scheduler otherwise hoists there.
+template <int AM, int BMD, int EPI, int WGM, int WGN, int SCHED = 0>
 __global__ __launch_bounds__(WGM * WGN * 64, 1) void g5_kernel(GemmParams p) {
   constexpr int NW = WGM * WGN, NT = NW * 64;
   constexpr int TM = BM / WGM, TN = BN / WGN, FM = TM / 16, FN = TN / 16;
@@ -131,25 +135,68 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void g5_kernel(GemmParams p) {
   asm volatile("" ::: "memory");
   rd(stage(0), 0, r0a, r0b);
 
+  constexpr int NIA = Loader<BM, AM, NW>::NI;
+  // one fragment read (call) of slot q into (ra, rb): B fragments first, then A
+  auto rd1 = [&](const char* stg, int kk, int q, bf16x8 (&ra)[FM], bf16x8 (&rb)[FN]) {
+    if (q < FN) rb[q] = frag<BKO>(stg + A_BYTES, bc + q * 16, kk);
+    else if (q < FN + FM) ra[q - FN] = frag<AKO>(stg, ar + (q - FN) * 16, kk);
+  };
+  auto mm1 = [&](int q, const bf16x8 (&ra)[FM], const bf16x8 (&rb)[FN]) {
+    const int i = q / FN, j = q % FN;
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[j], ra[i], acc[i][j], 0, 0, 0);
+  };
+  constexpr int NM = FM * FN, NFR = FM + FN;
+
 #pragma unroll 1
   for (int kt = kt0; kt < kt1; ++kt) {
     const int s = (kt - kt0) & 1;
-    // phase A: MFMAs on k-half 0 || reads of k-half 1
-    rd(stage(s), 1, r1a, r1b);
-    mm(r0a, r0b);
-    interleave<FM * FN, NRD, 0>();
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (SCHED == 0) {
+      // phase A: MFMAs on k-half 0 || reads of k-half 1
+      rd(stage(s), 1, r1a, r1b);
+      mm(r0a, r0b);
+      interleave<FM * FN, NRD, 0>();
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      constexpr int PER = NM / NFR;
+#pragma unroll
+      for (int q = 0; q < NFR; ++q) {
+#pragma unroll
+        for (int t = 0; t < PER; ++t) mm1(q * PER + t, r0a, r0b);
+        rd1(stage(s), 1, q, r1a, r1b);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int t = NFR * PER; t < NM; ++t) mm1(t, r0a, r0b);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     // phase B: MFMAs on k-half 1 || DMA of tile kt+2 into the freed stage || reads of tile kt+1's
     // k-half 0 (past the last tile: zero-filling DMA, stale reads -- both unused)
-    issue(kt + 2, stage(s), kt + 2 < kt1);
-    rd(stage(s ^ 1), 0, r0a, r0b);
-    mm(r1a, r1b);
-    interleave<FM * FN, NRD, ND>();
-    __builtin_amdgcn_sched_barrier(0);
+    const bool en = kt + 2 < kt1;
+    if constexpr (SCHED == 0) {
+      issue(kt + 2, stage(s), en);
+      rd(stage(s ^ 1), 0, r0a, r0b);
+      mm(r1a, r1b);
+      interleave<FM * FN, NRD, ND>();
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      constexpr int SL = NFR > ND ? NFR : ND, PER = NM / SL;
+#pragma unroll
+      for (int q = 0; q < SL; ++q) {
+#pragma unroll
+        for (int t = 0; t < PER; ++t) mm1(q * PER + t, r1a, r1b);
+        if (q < NIA) la.issue(p, Ab, a_step, kt + 2, lim_a, stage(s), w, lane, en, q);
+        else if (q < ND) lb.issue(p, Bb, b_step, kt + 2, lim_b, stage(s) + A_BYTES, w, lane, en, q - NIA);
+        rd1(stage(s ^ 1), 0, q, r0a, r0b);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int t = SL * PER; t < NM; ++t) mm1(t, r1a, r1b);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if constexpr (NW == 4) {
       // 256 loop-carried accumulators: pin them to the AGPR half (hipcc 7.2 otherwise carries part
       // of them in VGPRs and shuffles with v_accvgpr moves every iteration)
@@ -171,7 +218,11 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void g5_kernel(GemmParams p) {
 template <int AM, int BMD, int EPI>
 int go(int mode, dim3 grid, hipStream_t stream, const GemmParams& p) {
   if (mode == 8) {
-    hipLaunchKernelGGL((g5_kernel<AM, BMD, EPI, 2, 4>), grid, dim3(512), 0, stream, p);
+    hipLaunchKernelGGL((g5_kernel<AM, BMD, EPI, 2, 4, 0>), grid, dim3(512), 0, stream, p);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
+  if (mode == 9) {
+    hipLaunchKernelGGL((g5_kernel<AM, BMD, EPI, 2, 4, 1>), grid, dim3(512), 0, stream, p);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   }
   return -1;
@@ -179,7 +230,7 @@ int go(int mode, dim3 grid, hipStream_t stream, const GemmParams& p) {
 
 }  // namespace g5
 
-// 0: off (default until measured), 8: the 8-wave kernel for every eligible 256x256 GEMM
+// 0: off (default until measured), 8 / 9: the 8-wave kernel (SCHED 0 / 1) for every eligible 256x256 GEMM
 static int g_g5 = -1;
 extern "C" void tfk_g5_set(int waves) { g_g5 = waves; }
 static int g5_mode() {
@@ -195,7 +246,7 @@ static int g5_mode() {
 extern "C" int tfk_g5_launch(const GemmParams& p_in, int amode, int bmode, int epi, int batch, int splits,
                              hipStream_t stream) {
   const int mode = g5_mode();
-  if (mode != 8) return -1;
+  if (mode != 8 && mode != 9) return -1;
   const bool dense = (amode == g4::KIN && (bmode == g4::KIN || bmode == g4::KOUT)) ||
                      (amode == g4::KOUT && bmode == g4::KOUT);
   const bool conv = amode == g4::CONV_FWD && bmode == g4::KIN && (p_in.Cin & 63) == 0;

@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--tfjob-worker", action="store_true", help=argparse.SUPPRESS)  # a pod of --via-operator
     # CPU rehearsal of the multi-rank code path (gloo, fp32 CPU executor; tests only -- not a measurement)
     ap.add_argument("--cpu-rehearsal", action="store_true", help=argparse.SUPPRESS)
+    # tests: report the L2 norm / sum of the master-weight change over the run (graph vs eager parity)
+    ap.add_argument("--report-update", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.via_operator:
         return run_via_operator(args)
@@ -190,6 +192,7 @@ def main():
         strat_name = "MultiWorkerMirroredStrategy (tfk_comm RCCL all-reduce)"
     strat.configure_optimizer(opt)
     strat.broadcast_parameters()
+    master0 = model.arena.master.clone() if args.report_update else None
     batch = synthetic_batch(model, args.batch, dev, seed=1000 + rank)
     # the whole step (fwd, bwd, RCCL bucket collectives, optimizer) replays from one hipGraph at every
     # world size; only a model with host-side per-step state (graph_hazards) runs eager
@@ -263,6 +266,10 @@ def main():
     loss = runner.last_loss()
     if runner.fallback:
         guards["capture_fallback"] = runner.fallback
+    if gpu and hasattr(model, "rng_state"):
+        # out-of-range events the bucketed embedding backward skipped (0: every step's counts valid)
+        from tensorflow_k8s_amd.ops._lib import lib
+        guards["emb_guard"] = int(lib().emb_guard_count())
     if wd is not None:
         guards["watchdog_s"] = wd.timeout_s
     comm_cfg["guards"] = guards
@@ -281,7 +288,7 @@ def main():
             "config": {"model": args.model, "global_batch": gb, "seq_len": seq, "per_gpu_batch": args.batch,
                        "parallelism": par, "strategy": strat_name,
                        "optimizer": opt_name, "hipgraph": runner.use_graph, "comm": comm_cfg},
-            "loss": loss}), flush=True)
+            "loss": loss, **_update_report(model, master0)}), flush=True)
     elif rank == worker_ranks[0]:
         is_r50 = args.model == "resnet50"
         base = _baseline(nworkers) if is_r50 else None
@@ -303,6 +310,13 @@ def main():
     tfk_comm.shutdown()
     if wd is not None:
         wd.stop()
+
+
+def _update_report(model, master0) -> dict:
+    if master0 is None:
+        return {}
+    d = (model.arena.master - master0).double()
+    return {"update_norm": float(d.norm()), "update_sum": float(d.sum())}
 
 
 def _rccl_version() -> str:

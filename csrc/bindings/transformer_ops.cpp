@@ -22,6 +22,7 @@ int tfk_embedding_fwd(const int*, const void*, int, const void*, int, const int*
                       float, hipStream_t);
 int tfk_embedding_bwd(const int*, const void*, int, float*, float*, int, const int*, float*, int, long long, int, float,
                       int*, hipStream_t);
+int tfk_emb_guard_count();
 int tfk_attn_fwd(const void*, const void*, const void*, void*, float*, const long long*, const long long*, const int*,
                  float, int, float, unsigned long long, hipStream_t);
 int tfk_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
@@ -227,6 +228,8 @@ void register_transformer_ops(pybind11::module& m) {
         py::arg("mx_out") = py::none());
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
+  // out-of-range events the bucketed embedding backward skipped since the last call (0 when healthy)
+  m.def("emb_guard_count", [] { return tfk_emb_guard_count(); });
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_set_waves", [](int w) { tfk_attn_set_waves(w); });

@@ -183,14 +183,22 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void g5_kernel(GemmParams p) {
       interleave<FM * FN, NRD, ND>();
       __builtin_amdgcn_sched_barrier(0);
     } else {
-      constexpr int SL = NFR > ND ? NFR : ND, PER = NM / SL;
+      // SCHED 1: slot q = {MFMAs, DMA piece q, read q}; SCHED 2: the DMA pieces go to the LAST ND
+      // slots and every slot orders its MFMAs first (sched_group_barrier), so the scalar descriptor
+      // setup of a piece never sits between the barrier and the first MFMA
+      constexpr int SL = NFR > ND ? NFR : ND, PER = NM / SL, D0 = SCHED == 2 ? SL - ND : 0;
 #pragma unroll
       for (int q = 0; q < SL; ++q) {
 #pragma unroll
         for (int t = 0; t < PER; ++t) mm1(q * PER + t, r1a, r1b);
-        if (q < NIA) la.issue(p, Ab, a_step, kt + 2, lim_a, stage(s), w, lane, en, q);
-        else if (q < ND) lb.issue(p, Bb, b_step, kt + 2, lim_b, stage(s) + A_BYTES, w, lane, en, q - NIA);
+        const int d = q - D0;
+        if (d >= 0 && d < NIA) la.issue(p, Ab, a_step, kt + 2, lim_a, stage(s), w, lane, en, d);
+        else if (d >= NIA && d < ND) lb.issue(p, Bb, b_step, kt + 2, lim_b, stage(s) + A_BYTES, w, lane, en, d - NIA);
         rd1(stage(s ^ 1), 0, q, r0a, r0b);
+        if constexpr (SCHED == 2) {
+          __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);  // the slot's MFMAs first
+          __builtin_amdgcn_sched_group_barrier(0x004, 32, 0);   // then its scalar setup
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -225,12 +233,16 @@ int go(int mode, dim3 grid, hipStream_t stream, const GemmParams& p) {
     hipLaunchKernelGGL((g5_kernel<AM, BMD, EPI, 2, 4, 1>), grid, dim3(512), 0, stream, p);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   }
+  if (mode == 10) {
+    hipLaunchKernelGGL((g5_kernel<AM, BMD, EPI, 2, 4, 2>), grid, dim3(512), 0, stream, p);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
   return -1;
 }
 
 }  // namespace g5
 
-// 0: off (default until measured), 8 / 9: the 8-wave kernel (SCHED 0 / 1) for every eligible 256x256 GEMM
+// 0: off (default until measured), 8 / 9 / 10: the 8-wave kernel (SCHED 0 / 1 / 2) for every eligible 256x256 GEMM
 static int g_g5 = -1;
 extern "C" void tfk_g5_set(int waves) { g_g5 = waves; }
 static int g5_mode() {
@@ -246,7 +258,7 @@ static int g5_mode() {
 extern "C" int tfk_g5_launch(const GemmParams& p_in, int amode, int bmode, int epi, int batch, int splits,
                              hipStream_t stream) {
   const int mode = g5_mode();
-  if (mode != 8 && mode != 9) return -1;
+  if (mode < 8 || mode > 10) return -1;
   const bool dense = (amode == g4::KIN && (bmode == g4::KIN || bmode == g4::KOUT)) ||
                      (amode == g4::KOUT && bmode == g4::KOUT);
   const bool conv = amode == g4::CONV_FWD && bmode == g4::KIN && (p_in.Cin & 63) == 0;

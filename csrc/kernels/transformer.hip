@@ -374,6 +374,12 @@ __global__ void embed_bwd_kernel(const int* __restrict__ ids, const bf16* __rest
 // scatter, int atomics only), then one block per touched row sums its tokens' dy rows in f32 and adds
 // the result to the row once. The scattered f32 atomics (8192 tokens x 1024 columns) ran at
 // ~37 G atomics/s: 223 us per call on Transformer-big's tied 33792 x 1024 table.
+// Out-of-range events of the bucketed backward (a corrupted count / cursor): the kernels skip the
+// access instead of faulting and count it here (tfk_emb_guard_count reads and clears it).
+__device__ int g_emb_guard = 0;
+__global__ void emb_zero_kernel(int* __restrict__ p, int n) {
+  for (int i = blockIdx.x * NT + threadIdx.x; i < n; i += gridDim.x * NT) p[i] = 0;
+}
 __global__ void emb_count_kernel(const int* __restrict__ ids, long long ntok, int V, int* __restrict__ cnt) {
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < ntok; i += (long long)gridDim.x * NT)
     atomicAdd(cnt + min(max(ids[i], 0), V - 1), 1);
@@ -402,19 +408,30 @@ __global__ __launch_bounds__(1024) void emb_scan_kernel(const int* __restrict__ 
 }
 __global__ void emb_bucket_kernel(const int* __restrict__ ids, long long ntok, int V, int* __restrict__ cursor,
                                   int* __restrict__ list) {
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < ntok; i += (long long)gridDim.x * NT)
-    list[atomicAdd(cursor + min(max(ids[i], 0), V - 1), 1)] = (int)i;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < ntok; i += (long long)gridDim.x * NT) {
+    const int pos = atomicAdd(cursor + min(max(ids[i], 0), V - 1), 1);
+    if ((unsigned long long)pos < (unsigned long long)ntok) list[pos] = (int)i;
+    else atomicAdd(&g_emb_guard, 1);
+  }
 }
 // one block per vocab row: dword[row] += scale * sum over the row's tokens of dy[token] (f32)
 __global__ void emb_reduce_kernel(const int* __restrict__ off, const int* __restrict__ cnt, const int* __restrict__ list,
-                                  const bf16* __restrict__ dy, float* __restrict__ dword, int W, float scale) {
+                                  const bf16* __restrict__ dy, float* __restrict__ dword, int W, float scale,
+                                  long long ntok) {
   const int row = blockIdx.x, n = cnt[row];
   if (n == 0) return;
-  const int* lst = list + off[row];
+  const int o = off[row];
+  if (n < 0 || o < 0 || (long long)o + n > ntok) {
+    if (threadIdx.x == 0) atomicAdd(&g_emb_guard, 1);
+    return;
+  }
+  const int* lst = list + o;
   for (int c = threadIdx.x * 8; c < W; c += NT * 8) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int k = 0; k < n; ++k) {
-      const bf16x8 g = *(const bf16x8*)(dy + (long long)lst[k] * W + c);
+      const int tok = lst[k];
+      if ((unsigned long long)tok >= (unsigned long long)ntok) continue;  // (never for consistent counts)
+      const bf16x8 g = *(const bf16x8*)(dy + (long long)tok * W + c);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += bf2f(g[e]);
     }
@@ -553,12 +570,16 @@ int tfk_embedding_bwd(const int* ids, const bf16* dy, int V, float* dword, float
   if (dtype && T > 4) return -3;
   if (scratch && W % 8 == 0 && (((uintptr_t)dword) & 15) == 0) {
     int *cnt = scratch, *off = scratch + V, *cursor = scratch + 2 * (long long)V, *list = scratch + 3 * (long long)V;
-    if (hipMemsetAsync(cnt, 0, (size_t)V * sizeof(int), s) != hipSuccess) return -1;
+    // counts zeroed by a KERNEL node, not hipMemsetAsync: a memset captured into a hipGraph whose
+    // step also forks onto the RCCL comm stream was not ordered before the counting kernel on
+    // replay (stale counts -> out-of-range bucket writes -> the round-4 illegal-address fault of the
+    // captured transformer steps with collectives; profiles/perf_log_r5.md)
+    hipLaunchKernelGGL(emb_zero_kernel, dim3((unsigned)min((V + NT - 1) / NT, 1024)), dim3(NT), 0, s, cnt, V);
     const unsigned g = (unsigned)grid_for(ntok, NT, 1024);
     hipLaunchKernelGGL(emb_count_kernel, dim3(g), dim3(NT), 0, s, ids, ntok, V, cnt);
     hipLaunchKernelGGL(emb_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, V, off, cursor);
     hipLaunchKernelGGL(emb_bucket_kernel, dim3(g), dim3(NT), 0, s, ids, ntok, V, cursor, list);
-    hipLaunchKernelGGL(emb_reduce_kernel, dim3((unsigned)V), dim3(NT), 0, s, off, cnt, list, dy, dword, W, scale);
+    hipLaunchKernelGGL(emb_reduce_kernel, dim3((unsigned)V), dim3(NT), 0, s, off, cnt, list, dy, dword, W, scale, ntok);
   } else {
     hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_for(ntok * (W / 8), NT, 8192)), dim3(NT), 0, s, ids, dy, V, dword,
                        ntok, W, scale);
@@ -571,4 +592,12 @@ int tfk_embedding_bwd(const int* ids, const bf16* dy, int V, float* dword, float
                        W);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+}
+// read and clear the bucketed-backward guard counter (host; synchronizes the device)
+extern "C" int tfk_emb_guard_count() {
+  int v = 0, z = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_emb_guard), sizeof(int)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_emb_guard), &z, sizeof(int)) != hipSuccess) return -1;
+  return v;
 }

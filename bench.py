@@ -141,11 +141,7 @@ def main():
     model = build_model(args.model, **({"fp8": True} if args.fp8 else {})).to(dev)
     if hasattr(model, "rng_stream"):
         model.rng_stream = rank  # each replica draws its own dropout masks
-    force_opt = os.environ.get("TFK_BENCH_OPT", "")  # diagnostics only: "adamw" / "sgd" for any model
-    if force_opt == "adamw":
-        opt = AdamW(model.arena, lr=1e-4, b2=0.98, eps=1e-9, weight_decay=0.0)
-        opt_name = "Adam (fused HIP, forced)"
-    elif is_cnn or force_opt == "sgd":
+    if is_cnn:
         opt = SGD(model.arena, lr=0.1 * args.batch * nworkers / 256, momentum=0.9, weight_decay=5e-5)
         opt_name = "SGD momentum 0.9 (fused HIP)"
     elif args.model.startswith("bert"):

@@ -286,8 +286,13 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
         return dx
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
     fuse_cs = colsum is not None and resid is None and (dact_src is not None or drop_p > 0)
-    if resid is None and dact_src is None and drop_p == 0.0 and lib_gemm_ok("dgrad", M, K, N):
+    plain = resid is None and dact_src is None and drop_p == 0.0
+    if plain and lib_gemm_ok("dgrad", M, K, N):
         torch.mm(dy2, w, out=dx)
+        if colsum is not None:
+            colsum.add_(dx.float().sum(0))
+        return dx
+    if plain and _dgrad_splitk(dy2, w, dx, M, K, N):
         if colsum is not None:
             colsum.add_(dx.float().sum(0))
         return dx
@@ -299,6 +304,29 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
     if colsum is not None and not fuse_cs:
         colsum.add_(dx.float().sum(0))  # plain epilogue: no fused column sums
     return dx
+
+
+# Plain input gradients whose output is too small to fill the chip with 256x256 tiles but whose
+# reduction is long (the tied-logits dgrad: dx[8192][1024] over the 33728-wide vocabulary = 128
+# tiles): split the reduction over the blocks, f32 slabs, one reduce pass writing the bf16 dx.
+DGRAD_SPLITK_MAX_TILES = 192
+DGRAD_SPLITK_MIN_RED = 4096
+
+
+def _dgrad_splitk(dy2, w, dx, M: int, K: int, N: int) -> bool:
+    tiles = ((M + 255) // 256) * ((K + 255) // 256)
+    if tiles >= DGRAD_SPLITK_MAX_TILES or N < DGRAD_SPLITK_MIN_RED or K % 8 or M % 8 or N % 8:
+        return False
+    nkt = (N + 63) // 64
+    splits = max(2, min(-(-256 // tiles), nkt // 16))
+    ns = int(lib().gemm_splits(N, splits))
+    if ns < 2:
+        return False
+    stride = ((M * K + 3) // 4) * 4
+    ws = workspace(dx.device, ns * stride, slot="splitk")
+    _gemm(dy2, w, ws, M, K, N, N, K, K, A_KIN, B_KOUT, EPI_F32, (256, 256), splits=splits, split_stride=stride)
+    lib().splitk_reduce(ws, ns, stride, M * K, None, dx.view(-1), False, 1.0)
+    return True
 
 
 def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate: bool = False,

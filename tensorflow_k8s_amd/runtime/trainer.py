@@ -39,15 +39,6 @@ def graph_hazards(model) -> list[str]:
     return out
 
 
-def ps_capture_ok(model) -> bool:
-    """Models whose collective parameter-server step is verified under capture: the CNNs. The
-    transformer models (device dropout-RNG state; BERT-base, Transformer-big) fault on replay with
-    SGD, AdamW and LAMB alike, one or many buckets (profiles/perf_log_r4.md). TFK_PS_CAPTURE=1 forces
-    capture, for diagnosing that fault."""
-    import os
-    return not hasattr(model, "rng_state") or os.environ.get("TFK_PS_CAPTURE") == "1"
-
-
 class StepRunner:
     def __init__(self, model, opt, strategy, batch, use_graph: bool = False, warmup_eager: int = 2,
                  agree=None, rank: int = 0):
@@ -57,14 +48,6 @@ class StepRunner:
         self.use_graph = (use_graph and torch.cuda.is_available() and batch[0].is_cuda
                           and (not hasattr(strategy, "apply_gradients") or getattr(strategy, "capturable", False)))
         self.fallback = ""  # why the step runs eager (refused or failed capture)
-        if self.use_graph and hasattr(strategy, "apply_gradients") and not ps_capture_ok(model):
-            # KNOWN ISSUE (round 4): the captured collective-PS step of the transformer models faults
-            # with an illegal address on replay (one GPU, forced comm; any optimizer, any bucket
-            # count); the eager step runs correctly and the captured ResNet step is verified
-            # (tests/test_bench_gpu.py). Run those eager until fixed.
-            self.use_graph = False
-            self.fallback = (f"collective parameter-server step of {type(model).__name__}: capture disabled "
-                             "(known replay fault), running eager")
         if self.use_graph:
             bad = graph_hazards(model)
             if bad:

@@ -83,3 +83,46 @@ def test_bench_collective_ps_colocated_one_gpu(tmp_path):
     assert c["parallelism"] == "ps1+worker1" and c["comm"]["transport"] == "rccl"
     assert c["comm"]["wire_mb_per_step"] > 0 and c["comm"]["buckets"] > 0
     assert c["hipgraph"] is True and d["loss"] is not None and d["loss"] == d["loss"]
+
+
+def _run_model(tmp_path, model, extra, batch=None):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--model", model, "--steps", "6", "--warmup", "3",
+           "--force-comm", "--report-update"] + (["--batch", str(batch)] if batch else []) + extra
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return _bench_line(r.stdout)
+
+
+def _captured_ok(d):
+    c = d["config"]
+    g = c["comm"]["guards"]
+    assert c["hipgraph"] is True and "capture_fallback" not in g, g
+    assert g["emb_guard"] == 0, g  # the bucketed embedding backward saw consistent counts every step
+
+
+def test_bench_collective_ps_bert_captured_matches_eager(tmp_path):
+    """BASELINE config 3's model on the collective (RCCL) parameter-server transport, colocated owner,
+    the whole worker step (reduce -> unpack -> step_region -> broadcast included) replayed from one
+    hipGraph -- the step that faulted on replay in round 4 (a hipMemsetAsync captured in the
+    embedding backward: perf_log_r5.md). Six steps captured vs eager: same loss, same master update."""
+    ps = ["--strategy", "ps", "--ps-transport", "rccl"]
+    graph = _run_model(tmp_path, "bert-base", ps)
+    eager = _run_model(tmp_path, "bert-base", ps + ["--graph", "0"])
+    _captured_ok(graph)
+    assert eager["config"]["hipgraph"] is False
+    assert abs(graph["loss"] - eager["loss"]) <= 1e-4 * abs(eager["loss"]), (graph["loss"], eager["loss"])
+    assert abs(graph["update_norm"] - eager["update_norm"]) <= 1e-3 * eager["update_norm"]
+    assert graph["update_norm"] > 0
+
+
+def test_bench_transformer_big_captured_with_collectives(tmp_path):
+    """Transformer-big with the RCCL collectives forced on at world size 1 (MWMS all-reduce buckets,
+    then the collective PS path): both steps replay from one hipGraph without the round-4 fault."""
+    mw = _run_model(tmp_path, "transformer-big", [])
+    _captured_ok(mw)
+    ps = _run_model(tmp_path, "transformer-big", ["--strategy", "ps", "--ps-transport", "rccl"])
+    _captured_ok(ps)
+    assert ps["config"]["comm"]["transport"] == "rccl" and ps["config"]["comm"]["buckets"] > 1
+    # the same model, data and optimizer: the PS update equals the MWMS one at world size 1
+    assert abs(ps["loss"] - mw["loss"]) <= 1e-3 * abs(mw["loss"]), (ps["loss"], mw["loss"])

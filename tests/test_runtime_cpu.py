@@ -295,19 +295,6 @@ def test_step_region_advances_once_per_global_step(device_schedule):
     torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-6, atol=1e-7)
 
 
-def test_collective_ps_capture_guard_by_model():
-    """Captured collective-PS steps are allowed only for the verified models (CNNs, no dropout-RNG
-    state); the transformer models run that step eager (runtime.trainer.ps_capture_ok, known fault)."""
-    from tensorflow_k8s_amd.runtime.trainer import ps_capture_ok
-
-    class ResNet:
-        pass
-
-    class Transformer:
-        rng_state = None
-    assert ps_capture_ok(ResNet()) and not ps_capture_ok(Transformer())
-
-
 def test_gloo_ps_task_survives_short_watchdog(tmp_path, native_ext):
     """a gloo parameter-server task blocks in recv between worker pushes; with the
     watchdog armed (here 2 s) it must beat on every command it receives, so a healthy job that runs

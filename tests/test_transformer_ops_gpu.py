@@ -147,6 +147,45 @@ def test_embedding():
         assert rel(out[DEV][k], out["cpu"][k]) < 1e-2, k
 
 
+def test_embedding_bwd_replayed_from_a_forked_graph():
+    """The bucketed word-row gradient (count -> scan -> scatter -> reduce) captured in a hipGraph whose
+    body also forks onto a second stream (as a data-parallel step forks onto the RCCL comm stream),
+    replayed 6 times: every replay equals the fp32 reference -- the per-call counts are zeroed by a
+    kernel node (a captured hipMemsetAsync was not reliably replayed: round-4 fault, perf_log_r5.md)
+    -- and the kernels' out-of-range guard never fires."""
+    from tensorflow_k8s_amd.ops._lib import lib
+    V, W, ntok = 4096, 256, 2048
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, V, (ntok,), dtype=torch.int32, generator=g)
+    dy = bf(ntok, W, seed=12)
+    ref = torch.zeros(V, W).index_add_(0, ids.long(), dy.float())
+    ids_d, dy_d = ids.to(DEV), dy.to(DEV)
+    dw = torch.zeros(V, W, device=DEV)
+    side = torch.cuda.Stream()
+    lib().emb_guard_count()
+
+    def body():
+        dw.zero_()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(1000)
+        T.embedding_bwd(ids_d, dy_d, dw)
+        torch.cuda.current_stream().wait_stream(side)
+
+    for _ in range(2):
+        body()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        body()
+    for _ in range(6):
+        dw.fill_(123.0)  # poison: only a complete replay restores the gradient
+        graph.replay()
+        torch.cuda.synchronize()
+        assert rel(dw, ref) < 1e-2
+    assert lib().emb_guard_count() == 0
+
+
 def test_linear_gelu_aux_and_dact():
     M, K, N = 256, 768, 3072
     x, w = bf(M, K, seed=12), bf(N, K, seed=13, scale=0.03)

@@ -47,10 +47,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     orig = G.pick_tile
-    variants = {"pick": None, "t256": (256, 256), "t128": (128, 128)}
+    G.LIB_GEMM = False  # the framework's own kernels in every variant; "blas" is the comparator
+    variants = {"pick": None, "t256": (256, 256), "t128": (128, 128), "g5s": "g5s"}
+    from tensorflow_k8s_amd.ops._lib import lib
 
     def timed(fn, tile):
-        G.pick_tile = orig if tile is None else (lambda *a, **k: tile)
+        G.pick_tile = orig if tile in (None, "g5s") else (lambda *a, **k: tile)
+        if tile == "g5s":
+            lib().g5_set(9)
         try:
             fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -62,6 +66,7 @@ def main():
             return e0.elapsed_time(e1) / args.iters * 1000.0
         finally:
             G.pick_tile = orig
+            lib().g5_set(0)
 
     jobs = []
     blas = {}

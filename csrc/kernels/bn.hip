@@ -10,6 +10,7 @@
 
 namespace {
 constexpr int NT = 256;
+constexpr int SHARD_UNROLL = 4;  // shards <= 16 (ops/norm.py SHARDS): loads per thread issued together
 
 // ---------------------------------------------------------------- forward
 // Sums NV per-channel vectors stored as [shards][NV][C] over the shards for channel c, zeroing the
@@ -24,10 +25,28 @@ __device__ __forceinline__ bool shard_sum(float* buf, int shards, int C, float (
 #pragma unroll
   for (int v = 0; v < NV; ++v) acc[v] = 0.f;
   if (c < C) {
-    for (int i = g; i < shards; i += 4) {
-      float* p = buf + (long long)i * NV * C;
+    if (shards <= 4 * SHARD_UNROLL) {
+      // every load of this thread's shards issued before any is used (clamped shard index, masked
+      // contribution): one memory latency instead of shards/4 chained ones -- the finalize kernels
+      // sit on the critical path between a conv and its BN apply
+      float x[SHARD_UNROLL][NV];
 #pragma unroll
-      for (int v = 0; v < NV; ++v) acc[v] += p[v * C + c];
+      for (int k = 0; k < SHARD_UNROLL; ++k) {
+        const int i = min(g + 4 * k, shards - 1);
+        const float* p = buf + (long long)i * NV * C;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) x[k][v] = p[v * C + c];
+      }
+#pragma unroll
+      for (int k = 0; k < SHARD_UNROLL; ++k)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] += g + 4 * k < shards ? x[k][v] : 0.f;
+    } else {
+      for (int i = g; i < shards; i += 4) {
+        float* p = buf + (long long)i * NV * C;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] += p[v * C + c];
+      }
     }
     for (int i = g; i < shards; i += 4) {
       float* p = buf + (long long)i * NV * C;

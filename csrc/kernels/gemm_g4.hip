@@ -484,7 +484,8 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
 // MX-fp8 GEMM on the g4 engine. p in BYTES (K, lda, ldb = bytes per row); needs K % 128 == 0,
 // lda/ldb % 16 == 0 and 16-B aligned operands. Returns -1 when not eligible (caller falls back).
 // Tile of the fp8 engine: 0 = by shape (256x256 16-wave blocks when they fill the chip, else
-// 128x128), 128 / 256 = forced (TFK_FP8_TILE or tfk_fp8_set_tile).
+// 256x128 8-wave blocks when those do, else 128x128), 128 / 256 / 384 (= 256x128) forced
+// (TFK_FP8_TILE or tfk_fp8_set_tile).
 static int g_fp8_tile = -1;
 extern "C" void tfk_fp8_set_tile(int t) { g_fp8_tile = t; }
 extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hipStream_t stream) {
@@ -510,27 +511,35 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
   p.kt_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
   const bool big = g_fp8_tile == 256 || (g_fp8_tile == 0 && p.M >= 256 && p.N >= 256 && t256 * splits >= 240);
-  const int T = big ? 256 : 128;
-  p.tiles_n = (p.N + T - 1) / T;
-  const int tiles = ((p.M + T - 1) / T) * p.tiles_n;
+  // 256x128 (8 waves of 64x64, one block per CU): the few-tile shapes 256x256 cannot fill -- an
+  // [8192][1024] dgrad is 128 tiles of 256x256 but exactly 256 of 256x128 (the 128x128 tile ran
+  // them at ~1 PF/s, a quarter of the MX rate)
+  const long long t_rect = (long long)((p.M + 255) / 256) * ((p.N + 127) / 128);
+  const bool rect = !big && (g_fp8_tile == 384 || (g_fp8_tile == 0 && p.M >= 256 && p.N >= 128 &&
+                                                    t_rect * splits >= 192));
+  const int TM = big || rect ? 256 : 128, TN = big ? 256 : 128;
+  p.tiles_n = (p.N + TN - 1) / TN;
+  const int tiles = ((p.M + TM - 1) / TM) * p.tiles_n;
   if (p.stats_shards < 1) p.stats_shards = 1;
   const dim3 grid(tiles, 1, splits);
-#define TFK_FP8_G4(BT)                                                                                          \
+#define TFK_FP8_G4(BTM, BTN)                                                                                    \
   {                                                                                                             \
-    const dim3 block(g4::nwaves<BT, BT>() * 64);                                                                \
+    const dim3 block(g4::nwaves<BTM, BTN>() * 64);                                                              \
     if (epi == EPI_F32)                                                                                         \
-      hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_F32>), grid, block, 0, stream, p, sld);                 \
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<BTM, BTN, EPI_F32>), grid, block, 0, stream, p, sld);               \
     else if (epi == EPI_BF16_EXT)                                                                               \
-      hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_BF16_EXT>), grid, block, 0, stream, p, sld);            \
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<BTM, BTN, EPI_BF16_EXT>), grid, block, 0, stream, p, sld);          \
     else if (epi == EPI_BF16_EXT_MX)                                                                            \
-      hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_BF16_EXT_MX>), grid, block, 0, stream, p, sld);         \
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<BTM, BTN, EPI_BF16_EXT_MX>), grid, block, 0, stream, p, sld);       \
     else                                                                                                        \
-      hipLaunchKernelGGL((g4::g4_fp8_kernel<BT, BT, EPI_BF16>), grid, block, 0, stream, p, sld);                \
+      hipLaunchKernelGGL((g4::g4_fp8_kernel<BTM, BTN, EPI_BF16>), grid, block, 0, stream, p, sld);              \
   }
   if (big) {
-    TFK_FP8_G4(256)
+    TFK_FP8_G4(256, 256)
+  } else if (rect) {
+    TFK_FP8_G4(256, 128)
   } else {
-    TFK_FP8_G4(128)
+    TFK_FP8_G4(128, 128)
   }
 #undef TFK_FP8_G4
   return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -213,10 +213,6 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
     x2 = x.reshape(-1, K)
     M = x2.shape[0]
     y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-    if (bias is None and act is None and resid is None and aux is None and drop_p == 0.0 and y.is_contiguous()
-            and lib_gemm_ok("fwd", M, N, K)):
-        torch.mm(x2, w.t(), out=y.view(M, N))
-        return y
     _gemm(x2, w, y, M, N, K, K, K, N, A_KIN, B_KIN, EPI_BF16, pick_tile(M, N, big_ok=True, K=K, g4=True), bias=bias, act=ACT[act],
           resid=resid.reshape(-1, N) if resid is not None else None, aux=aux, drop_p=drop_p, drop_seed=drop_seed)
     return y
@@ -287,11 +283,6 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
     fuse_cs = colsum is not None and resid is None and (dact_src is not None or drop_p > 0)
     plain = resid is None and dact_src is None and drop_p == 0.0
-    if plain and lib_gemm_ok("dgrad", M, K, N):
-        torch.mm(dy2, w, out=dx)
-        if colsum is not None:
-            colsum.add_(dx.float().sum(0))
-        return dx
     if plain and _dgrad_splitk(dy2, w, dx, M, K, N):
         if colsum is not None:
             colsum.add_(dx.float().sum(0))
@@ -345,15 +336,6 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
         return
     if RECORD is not None:
         RECORD.append(("wgrad", (N, K, M), ()))
-    if lib_gemm_ok("wgrad", N, K, M):
-        # a plain library GEMM (no fused epilogue): hipBLASLt, bf16 operands, f32 accumulate and
-        # output straight into the arena gradient -- no split-K slabs, no reduce pass
-        v = gw.view(N, K)
-        if accumulate:
-            torch.ops.aten.addmm.dtype_out(v, dy2.t(), x2, torch.float32, beta=1, alpha=1, out=v)
-        else:
-            torch.ops.aten.mm.dtype_out(dy2.t(), x2, torch.float32, out=v)
-        return
     tuned = tuning.wgrad_config(N, K, M) if (N % 8 == 0 and K % 8 == 0 and split_target is None) else None
     tile = tuned[0] if tuned else pick_tile(N, K, splits_ok=True, big_ok=True, K=M, split_target=split_target,
                                             g4=N % 8 == 0 and K % 8 == 0)
@@ -364,30 +346,6 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
               split_stride=stride)
     _f32_out_splitk(run, N, K, M, tiles, gw.view(-1), accumulate, dy.device, split_target=split_target,
                     force_splits=tuned[1] if tuned else None, slot=_lib_mod.WGRAD_SLOT)
-
-
-# Plain GEMMs -- no fused epilogue (bias / activation / residual / aux store / dropout / activation
-# backward / BN statistics) -- go to hipBLASLt (aten mm, mm.dtype_out for the f32 weight gradients)
-# on the shape classes where it measured faster than the framework's g4 engine in the production
-# entry points (tools/linear_ab.py, tools/wgrad_blas_ab.py; profiles/lib_gemm_ab_r4.md):
-#   fwd   M >= 4096, N >= 2048, K >= 1024   (Transformer-big q/kv/qkv projections, tied logits)
-#   dgrad M >= 4096, N, K >= 1024           (the same layers' input gradients)
-#   wgrad N*K >= 16M, M <= 65536             (the 33728 x 1024 tied-embedding gradient only; every
-#                                             smaller weight gradient is faster on g4 split-K)
-# Everything with an epilogue, every convolution and every MX-fp8 GEMM stays on the HIP kernels.
-# False: always the framework's kernels.
-LIB_GEMM = os.environ.get("TFK_LIB_GEMM", "1") != "0"
-
-
-def lib_gemm_ok(kind: str, M: int, N: int, K: int) -> bool:
-    """kind 'fwd'/'dgrad': C[M][N] = A[M][K] B over K; 'wgrad': gw[M=N_out][N=K_in] over K rows."""
-    if not LIB_GEMM:
-        return False
-    if kind == "wgrad":
-        return K <= 65536 and M * N >= 1 << 24
-    if kind == "fwd":
-        return M >= 4096 and N >= 2048 and K >= 1024
-    return M >= 4096 and N >= 1024 and K >= 1024
 
 
 def bias_grad(dy: torch.Tensor, gb: torch.Tensor, accumulate: bool = False) -> None:

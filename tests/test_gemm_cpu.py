@@ -1,15 +1,40 @@
 
 
-def test_lib_gemm_shape_classes(monkeypatch):
-    """Plain-GEMM routing to hipBLASLt covers only the measured shape classes (ops.gemm.LIB_GEMM)."""
+def test_no_vendor_gemm_in_the_op_layer():
+    """Every GEMM of the model path runs on the framework's HIP kernels: the op layer has no library
+    routing left (round 4 sent plain GEMMs of some shape classes to hipBLASLt through aten)."""
+    import inspect
     from tensorflow_k8s_amd.ops import gemm as G
-    assert G.lib_gemm_ok("fwd", 8192, 33728, 1024) and G.lib_gemm_ok("fwd", 8192, 3072, 1024)
-    assert not G.lib_gemm_ok("fwd", 8192, 1024, 1024) and not G.lib_gemm_ok("fwd", 256, 33728, 1024)
-    assert G.lib_gemm_ok("dgrad", 8192, 1024, 33728) and not G.lib_gemm_ok("dgrad", 2048, 1024, 3072)
-    assert G.lib_gemm_ok("wgrad", 33728, 1024, 8192)
-    assert not G.lib_gemm_ok("wgrad", 4096, 1024, 8192) and not G.lib_gemm_ok("wgrad", 256, 64, 802816)
-    monkeypatch.setattr(G, "LIB_GEMM", False)
-    assert not G.lib_gemm_ok("fwd", 8192, 33728, 1024)
+    src = inspect.getsource(G)
+    assert not hasattr(G, "lib_gemm_ok") and not hasattr(G, "LIB_GEMM")
+    for call in ("torch.mm(", "torch.matmul(", "aten.mm", "aten.addmm", "F.linear("):
+        assert call not in src, call
+
+
+def test_dgrad_splitk_policy():
+    """Plain input gradients with too few 256x256 output tiles and a long reduction (the tied-logits
+    dgrad) take the split-K path; wide outputs and short reductions do not."""
+    from tensorflow_k8s_amd.ops import gemm as G
+    calls = []
+
+    class FakeLib:
+        def gemm_splits(self, K, s):
+            return s
+
+        def splitk_reduce(self, *a):
+            calls.append("reduce")
+    import torch
+    orig_lib, orig_gemm, orig_ws = G.lib, G._gemm, G.workspace
+    G.lib, G._gemm = (lambda: FakeLib()), (lambda *a, **k: calls.append(("gemm", k.get("splits"))))
+    G.workspace = lambda dev, n, slot="": torch.empty(n)
+    try:
+        dx = torch.empty(8192, 1024, dtype=torch.bfloat16)
+        assert G._dgrad_splitk(None, None, dx, 8192, 1024, 33728)  # 128 tiles, 33728-long reduction
+        assert calls[0][0] == "gemm" and calls[0][1] >= 2 and calls[-1] == "reduce"
+        assert not G._dgrad_splitk(None, None, torch.empty(8192, 4096, dtype=torch.bfloat16), 8192, 4096, 1024)
+        assert not G._dgrad_splitk(None, None, dx, 8192, 1024, 1024)  # short reduction: one pass
+    finally:
+        G.lib, G._gemm, G.workspace = orig_lib, orig_gemm, orig_ws
 
 
 def test_relu_mask_reference_matches_bf16_preactivation():

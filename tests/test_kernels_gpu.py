@@ -631,34 +631,14 @@ def test_splitk_reduce_two_pass(S, n, acc):
         assert float((ob.double() - ref).abs().max()) < 0.02 * float(ref.abs().max()) + 1e-2
 
 
-@pytest.mark.parametrize("kind", ["fwd", "dgrad", "wgrad"])
-def test_lib_gemm_routing_matches_native_engine(kind, monkeypatch):
-    """Plain GEMMs of the logits class route to hipBLASLt (ops.gemm.lib_gemm_ok); the result must
-    match the g4 engine's (LIB_GEMM off) and the fp32 reference on the same operands."""
-    M, N, K = 4096, 16384, 1024  # rows, out features, in features: fwd/dgrad/wgrad all in the lib class
-    x, w, dy = bf(M, K, seed=1).to(DEV), bf(N, K, scale=0.05, seed=2).to(DEV), bf(M, N, seed=3).to(DEV)
-    if kind == "wgrad":
-        M, N, K = 2048, 8192, 2048  # gw 8192 x 2048 = 16M elements over 2048 rows
-        x, dy = bf(M, K, seed=1).to(DEV), bf(M, N, seed=3).to(DEV)
-
-    def run():
-        if kind == "fwd":
-            return G.linear_fwd(x, w)
-        if kind == "dgrad":
-            return G.linear_dgrad(dy, w)
-        gw = torch.zeros(N, K, device=DEV)
-        G.linear_wgrad(dy, x, gw)
-        G.linear_wgrad(dy, x, gw, accumulate=True)
-        return gw
-    assert G.lib_gemm_ok(kind, *((N, K, M) if kind == "wgrad" else (M, N if kind == "fwd" else K,
-                                                                         K if kind == "fwd" else N)))
-    lib_out = run()
-    monkeypatch.setattr(G, "LIB_GEMM", False)
-    native = run()
-    ref = {"fwd": lambda: x.float() @ w.float().t(), "dgrad": lambda: dy.float() @ w.float(),
-           "wgrad": lambda: 2 * dy.float().t() @ x.float()}[kind]()
-    assert rel(lib_out, ref) < 1e-2 and rel(native, ref) < 1e-2
-    assert rel(lib_out, native) < 1e-2
+@pytest.mark.parametrize("M,K,N", [(8192, 1024, 33728), (1024, 264, 8192)])
+def test_dgrad_splitk_matches_reference(M, K, N):
+    """Plain input gradients on the split-K path (few 256x256 output tiles, long reduction: the
+    tied-logits dgrad shape and a ragged one): f32 slabs + one bf16 reduce equal the fp32 reference."""
+    dy, w = bf(M, N, seed=3).to(DEV), bf(N, K, scale=0.05, seed=4).to(DEV)
+    dx = G.linear_dgrad(dy, w)
+    ref = dy.float() @ w.float()
+    assert rel(dx, ref) < 1e-2
 
 
 @pytest.mark.parametrize("M,N,K", [(8192, 4096, 1024), (1000, 264, 128)])

@@ -47,8 +47,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     orig = G.pick_tile
-    G.LIB_GEMM = False  # the framework's own kernels in every variant; "blas" is the comparator
-    variants = {"pick": None, "t256": (256, 256), "t128": (128, 128), "g5s": "g5s"}
+    variants = {"pick": None, "t256": (256, 256), "t128": (128, 128), "t256x128": (256, 128), "g5s": "g5s"}
     from tensorflow_k8s_amd.ops._lib import lib
 
     def timed(fn, tile):

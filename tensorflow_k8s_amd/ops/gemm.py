@@ -340,12 +340,52 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
     tile = tuned[0] if tuned else pick_tile(N, K, splits_ok=True, big_ok=True, K=M, split_target=split_target,
                                             g4=N % 8 == 0 and K % 8 == 0)
     tiles = ((N + tile[0] - 1) // tile[0]) * ((K + tile[1] - 1) // tile[1])
+    if tuned is None and split_target is None and tile == (256, 256) and _wgrad_tail_split(dy2, x2, gw, N, K, M,
+                                                                                           accumulate):
+        return
 
     def run(C, splits, stride, beta):
         _gemm(dy2, x2, C, N, K, M, N, K, K, A_KOUT, B_KOUT, EPI_F32, tile, beta=beta, splits=splits,
               split_stride=stride)
     _f32_out_splitk(run, N, K, M, tiles, gw.view(-1), accumulate, dy.device, split_target=split_target,
                     force_splits=tuned[1] if tuned else None, slot=_lib_mod.WGRAD_SLOT)
+
+
+# Weight gradients of a few whole rounds of 256x256 tiles plus a small tail (the tied-embedding
+# gradient 33728 x 1024 = 528 tiles = 2 rounds + 16 tiles: unsplit, the 16-tile tail costs a third
+# full-length round): the whole rounds run unsplit, the tail row-tiles split over the reduction
+# into f32 slabs reduced into their rows of gw.
+CHIP_BLOCKS = 256
+TAIL_MAX_FRAC = 0.25
+
+
+def _wgrad_tail_split(dy2, x2, gw, N: int, K: int, M: int, accumulate: bool) -> bool:
+    tn, tm = -(-K // 256), -(-N // 256)
+    tiles = tm * tn
+    rounds, rem = divmod(tiles, CHIP_BLOCKS)
+    if rounds < 1 or rem == 0 or rem > TAIL_MAX_FRAC * CHIP_BLOCKS or N % 8 or K % 8:
+        return False
+    rows_dp = (rounds * CHIP_BLOCKS) // tn  # whole row-tiles in the unsplit part
+    n0 = rows_dp * 256
+    if n0 >= N:
+        return False
+    nt = N - n0
+    tail_tiles = -(-nt // 256) * tn
+    nkt = (M + 63) // 64
+    splits = max(2, min(CHIP_BLOCKS // tail_tiles, nkt // 8))
+    ns = int(lib().gemm_splits(M, splits))
+    if ns < 2:
+        return False
+    g = gw.view(N, K)
+    # unsplit part: rows [0, n0)
+    _gemm(dy2, x2, g, n0, K, M, N, K, K, A_KOUT, B_KOUT, EPI_F32, (256, 256), beta=1.0 if accumulate else 0.0)
+    # tail rows [n0, N): A = dy columns n0.. (K-outer, lda = N), split over M into slabs
+    stride = ((nt * K + 3) // 4) * 4
+    ws = workspace(dy2.device, ns * stride, slot=_lib_mod.WGRAD_SLOT)
+    _gemm(dy2.view(-1)[n0:], x2, ws, nt, K, M, N, K, K, A_KOUT, B_KOUT, EPI_F32, (256, 256), splits=splits,
+          split_stride=stride)
+    lib().splitk_reduce(ws, ns, stride, nt * K, g[n0:].reshape(-1), None, accumulate, 1.0)
+    return True
 
 
 def bias_grad(dy: torch.Tensor, gb: torch.Tensor, accumulate: bool = False) -> None:

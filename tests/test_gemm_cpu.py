@@ -73,3 +73,31 @@ def test_dgrad_colsum_reference_is_bias_gradient_of_consumer():
     dx = G.linear_dgrad(dy, w, dact_src=m, dact="relu", colsum=cs)
     assert torch.allclose(cs, dx.float().sum(0) + 2.0, atol=1e-5)
     assert torch.equal(dx, G.linear_dgrad(dy, w, dact_src=m, dact="relu"))
+
+
+def test_wgrad_tail_split_policy():
+    """The tied-embedding weight gradient (528 tiles = 2 rounds + 16) splits only its 16-tile tail;
+    exact rounds, big tails and single-round gradients stay unsplit."""
+    import torch
+    from tensorflow_k8s_amd.ops import gemm as G
+    calls = []
+
+    class FakeLib:
+        def gemm_splits(self, K, s):
+            return s
+
+        def splitk_reduce(self, *a):
+            calls.append(("reduce", a[3]))
+    orig = G.lib, G._gemm, G.workspace
+    G.lib = lambda: FakeLib()
+    G._gemm = lambda A, B, C, M, N, K, *a, **k: calls.append(("gemm", M, k.get("splits", 1)))
+    G.workspace = lambda dev, n, slot="": torch.empty(n)
+    try:
+        gw = torch.empty(33728 * 1024)
+        assert G._wgrad_tail_split(torch.empty(8192, 33728), None, gw, 33728, 1024, 8192, False)
+        assert calls[0] == ("gemm", 32768, 1) and calls[1][1] == 960 and calls[1][2] >= 2
+        assert calls[2] == ("reduce", 960 * 1024)
+        assert not G._wgrad_tail_split(None, None, None, 4096, 4096, 8192, False)  # exactly 1 round
+        assert not G._wgrad_tail_split(None, None, None, 4096, 1024, 8192, False)  # under a round
+    finally:
+        G.lib, G._gemm, G.workspace = orig

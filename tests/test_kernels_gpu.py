@@ -631,6 +631,20 @@ def test_splitk_reduce_two_pass(S, n, acc):
         assert float((ob.double() - ref).abs().max()) < 0.02 * float(ref.abs().max()) + 1e-2
 
 
+@pytest.mark.parametrize("N,K,M", [(4352, 4096, 2048), (4300, 4096, 1024)])
+def test_wgrad_tail_split_matches_reference(N, K, M):
+    """Weight gradients of whole 256x256 rounds plus a small tail (272 tiles = 256 + 16): the tail
+    row-tiles run split-K into slabs (ops.gemm._wgrad_tail_split); overwrite and accumulate both
+    equal the fp32 reference, ragged tail included."""
+    dy, x = bf(M, N, seed=5).to(DEV), bf(M, K, seed=6).to(DEV)
+    gw = torch.full((N, K), float("nan"), device=DEV)
+    G.linear_wgrad(dy, x, gw)
+    ref = dy.float().t() @ x.float()
+    assert rel(gw, ref) < 1e-4
+    G.linear_wgrad(dy, x, gw, accumulate=True)
+    assert rel(gw, 2 * ref) < 1e-4
+
+
 @pytest.mark.parametrize("M,K,N", [(8192, 1024, 33728), (1024, 264, 8192)])
 def test_dgrad_splitk_matches_reference(M, K, N):
     """Plain input gradients on the split-K path (few 256x256 output tiles, long reduction: the

@@ -231,6 +231,9 @@ def main():
         runner.step()
         if gpu:
             evs[i + 1].record()
+            if wd is not None:
+                wd.beat_device(args.warmup + i, evs[i + 1], "train")  # device completion, not enqueue
+                continue
         beat(args.warmup + i)
     barrier()
     dt = time.perf_counter() - t0

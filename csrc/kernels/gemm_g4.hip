@@ -484,7 +484,7 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
 // MX-fp8 GEMM on the g4 engine. p in BYTES (K, lda, ldb = bytes per row); needs K % 128 == 0,
 // lda/ldb % 16 == 0 and 16-B aligned operands. Returns -1 when not eligible (caller falls back).
 // Tile of the fp8 engine: 0 = by shape (256x256 16-wave blocks when they fill the chip, else
-// 256x128 8-wave blocks when those do, else 128x128), 128 / 256 / 384 (= 256x128) forced
+// 128x128), 128 / 256 / 2561 (= 256x128, 8 waves) forced
 // (TFK_FP8_TILE or tfk_fp8_set_tile).
 static int g_fp8_tile = -1;
 extern "C" void tfk_fp8_set_tile(int t) { g_fp8_tile = t; }
@@ -511,12 +511,11 @@ extern "C" int tfk_g4_fp8_launch(const GemmParams& p_in, int epi, int splits, hi
   p.kt_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
   const bool big = g_fp8_tile == 256 || (g_fp8_tile == 0 && p.M >= 256 && p.N >= 256 && t256 * splits >= 240);
-  // 256x128 (8 waves of 64x64, one block per CU): the few-tile shapes 256x256 cannot fill -- an
-  // [8192][1024] dgrad is 128 tiles of 256x256 but exactly 256 of 256x128 (the 128x128 tile ran
-  // them at ~1 PF/s, a quarter of the MX rate)
-  const long long t_rect = (long long)((p.M + 255) / 256) * ((p.N + 127) / 128);
-  const bool rect = !big && (g_fp8_tile == 384 || (g_fp8_tile == 0 && p.M >= 256 && p.N >= 128 &&
-                                                    t_rect * splits >= 192));
+  // 256x128 (8 waves of 64x64, one block per CU), forced only (2561): on the few-tile Transformer-big
+  // shapes 256x256 cannot fill ([8192][1024] dgrads: 128 tiles of 256x256, 256 of 256x128) it
+  // measured slower than two 128x128 blocks per CU (43.9 vs 38.9 us per dgrad, 47.0 vs 41.1 per
+  // EXT forward; profiles/perf_log_r5.md), so the shape rule keeps 128x128 there
+  const bool rect = !big && g_fp8_tile == 2561;
   const int TM = big || rect ? 256 : 128, TN = big ? 256 : 128;
   p.tiles_n = (p.N + TN - 1) / TN;
   const int tiles = ((p.M + TM - 1) / TM) * p.tiles_n;

@@ -266,7 +266,14 @@ def run_worker(args, info, dev, world_comm, watchdog=None) -> int:
         step += 1
         n_last += 1
         if watchdog is not None:
-            watchdog.beat(step)
+            if dev.type == "cuda":
+                # follow the device: a replayed graph returns at once, so the heartbeat is the
+                # completion of an event recorded after the step (runtime/watchdog.py)
+                ev = torch.cuda.Event()
+                ev.record()
+                watchdog.beat_device(step, ev)
+            else:
+                watchdog.beat(step)
         if runner.fallback and not fell_back:
             fell_back = True
             _log({"event": "graph_fallback", "rank": info.rank, "step": step, "reason": runner.fallback[:500]})

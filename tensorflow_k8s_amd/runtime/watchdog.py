@@ -9,6 +9,13 @@ kernels exit instead of spinning on a dead peer) and exits with 143, the retryab
 operator bumps the restart generation, every rank re-rendezvouses and training resumes from the
 latest checkpoint (runtime/train.py, runtime/checkpoint.py).
 
+Device-side progress: a replayed hipGraph returns to the host at once, so a host heartbeat after
+``runner.step()`` only says the step was ENQUEUED. ``beat_device(step, event)`` (an event recorded
+after the step) makes the watchdog follow completion instead: while enqueued steps are pending,
+the clock runs from the last one the device finished, so a kernel or collective that hangs on the
+device fires the watchdog after ``timeout_s`` even though the host keeps enqueuing (until HIP's
+queue back-pressure blocks it) -- not only once the host itself stalls.
+
 Besides the heartbeat, every tick polls the registered health checks -- by default
 ``tfk_comm.async_errors()`` (ncclCommGetAsyncError of every live communicator): a peer that RCCL has
 already declared lost fires the watchdog at once instead of after the heartbeat timeout. The
@@ -43,6 +50,8 @@ class StepWatchdog:
         self.error = ""
         self.last_step = -1
         self._last = time.monotonic()
+        self._dev = []        # [(step, event)] enqueued steps whose completion is not yet seen
+        self.device_step = -1
         self._stop = threading.Event()
         self._fired = threading.Event()
         self._lock = threading.Lock()
@@ -57,11 +66,44 @@ class StepWatchdog:
 
     def beat(self, step: int | None = None, phase: str | None = None) -> None:
         with self._lock:
-            self._last = time.monotonic()
-            if step is not None:
-                self.last_step = step
+            if not self._dev:  # while device steps are pending, only their completion is progress
+                self._last = time.monotonic()
+                if step is not None:
+                    self.last_step = step
             if phase is not None:
                 self.phase = phase
+
+    MAX_PENDING = 256
+
+    def beat_device(self, step: int, event, phase: str | None = None) -> None:
+        """Step `step` was enqueued and `event` recorded after it (anything with .query())."""
+        with self._lock:
+            if not self._dev:
+                self._last = time.monotonic()  # the device clock starts at the first pending step
+            self._dev.append((step, event))
+            if len(self._dev) > self.MAX_PENDING:
+                del self._dev[1:len(self._dev) - self.MAX_PENDING + 1]  # keep the oldest
+            if phase is not None:
+                self.phase = phase
+
+    def _poll_device(self) -> None:
+        with self._lock:
+            pend = list(self._dev)
+        done = 0
+        for st, ev in pend:
+            try:
+                ok = ev.query()
+            except Exception:  # noqa: BLE001 -- a failed query is not progress
+                ok = False
+            if not ok:
+                break
+            done += 1
+        if done:
+            with self._lock:
+                st = self._dev[done - 1][0]
+                del self._dev[:done]
+                self.device_step = self.last_step = st
+                self._last = time.monotonic()
 
     def stop(self) -> None:
         self._stop.set()
@@ -82,6 +124,8 @@ class StepWatchdog:
     # ------------------------------------------------------------------ loop
     def _run(self) -> None:
         while not self._stop.wait(self.poll_s):
+            if self._dev:
+                self._poll_device()
             with self._lock:
                 idle = time.monotonic() - self._last
                 step = self.last_step

@@ -168,3 +168,36 @@ def test_bench_rehearsal_injected_probe_failure_runs_eager(tmp_path, native_ext)
     assert g["comm_self_test"]["ok"] is True and g["watchdog_s"] == 300.0
     assert "rank 1" in g["capture_probe"] and "injected" in g["capture_probe"]
     assert d["config"]["hipgraph"] is False
+
+
+def test_watchdog_follows_device_completion():
+    """beat_device: while enqueued steps are pending, only their completion counts as progress --
+    a device that stops completing fires the watchdog although the host keeps enqueuing (host
+    beats no longer mask it); completed steps keep it quiet."""
+    import time
+    from tensorflow_k8s_amd.runtime.watchdog import StepWatchdog
+
+    class Ev:
+        def __init__(self, done):
+            self.done = done
+
+        def query(self):
+            return self.done
+    fired = []
+    w = StepWatchdog(0.5, on_timeout=lambda step, idle: fired.append((step, idle)), poll_s=0.05).start()
+    try:
+        for i in range(8):  # a healthy device: every enqueued step completes
+            w.beat_device(i, Ev(True))
+            time.sleep(0.1)
+        assert not fired and w.device_step == 7
+        stuck = Ev(False)
+        w.beat_device(8, stuck)
+        for i in range(9, 20):  # the host keeps enqueuing (and beating) behind a hung step
+            w.beat_device(i, Ev(True))
+            w.beat(i)
+            time.sleep(0.1)
+            if fired:
+                break
+        assert fired and fired[0][0] == 7, fired  # last COMPLETED step
+    finally:
+        w.stop()

@@ -177,25 +177,6 @@ struct Loader {
       }
     }
   }
-
-  // Dense modes, issue split in two: the per-lane source offsets of K-tile kt (edge and `en`
-  // masking included) computed ahead -- e.g. among the MFMAs before a barrier -- and then the bare
-  // DMA of piece i, so the instructions right after the barrier are DMAs and MFMAs only.
-  __device__ __forceinline__ void offsets(const GemmParams& p, int kt, int lim, int w, int lane, bool en,
-                                          unsigned (&vo)[NI]) const {
-    static_assert(MODE == KIN || MODE == KOUT, "dense operands");
-    const int krem = p.K - kt * BK;
-    const bool inner = lim >= ROWS && krem >= BK;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      unsigned v = off[i];
-      if (!inner) v = (row_of(i, w, lane) < lim && k_of(i, w, lane) < krem) ? v : OOB;
-      vo[i] = en ? v : OOB;
-    }
-  }
-  __device__ __forceinline__ static void issue_piece(__amdgpu_buffer_rsrc_t rsrc, char* img, int w, int i, unsigned vo) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
-  }
 };
 
 }  // namespace g4

@@ -125,28 +125,18 @@ __device__ __forceinline__ long long resid_row(const GemmParams& p, long long mo
 // QUAD: the 8-phase engine's wave layout (gemm_g8.hip): wave (wm, wn) owns the four quadrant
 // sub-tiles rows {q*BM/2 + wm*64 + [0,64)} x cols {q'*BN/2 + wn*32 + [0,32)}; row fragment i covers
 // rows (i>>2)*BM/2 + wm*64 + (i&3)*16, column fragment j cols (j>>1)*BN/2 + wn*32 + (j&1)*16.
-// L32: 32x32x16 accumulators (gemm_g5.hip's g6 kernel), viewed as f32x4 units: unit (i, j) of lane
-// l holds C[m][n..n+3], m = i*32 + (l&31), n = (j>>2)*32 + (j&3)*8 + (l>>5)*4 -- registers 4g..4g+3
-// of the 32x32 fragment (j&3 = g) are 4 consecutive columns (cdna_hip_programming.md §3 C/D map).
-template <int BM, int BN, int NT, int WM, int EPI, int BNRG = 0, bool DRAIN = false, bool QUAD = false,
-          bool L32 = false>
-__device__ __forceinline__ void gemm_epilogue(
-    const GemmParams& p, f32x4 (&acc)[BM / WM / (L32 ? 32 : 16)][BN / (NT / 64 / WM) / (L32 ? 8 : 16)], char* smem,
-    int m0, int n0, int bz) {
+template <int BM, int BN, int NT, int WM, int EPI, int BNRG = 0, bool DRAIN = false, bool QUAD = false>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[BM / WM / 16][BN / (NT / 64 / WM) / 16],
+                                              char* smem, int m0, int n0, int bz) {
   constexpr int NW = NT / 64, WN = NW / WM;
   constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int FM = TM / (L32 ? 32 : 16), FN = TN / (L32 ? 8 : 16);
+  constexpr int FM = TM / 16, FN = TN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int ml = L32 ? lane & 31 : lane & 15, nl = L32 ? (lane >> 5) * 4 : (lane >> 4) * 4;
+  const int ml = lane & 15, nl = (lane >> 4) * 4;
   static_assert(!QUAD || (FM == 8 && FN == 4), "QUAD: 8 row x 4 column fragments per wave");
-  static_assert(!(QUAD && L32), "one accumulator layout");
-  auto frow = [&](int i) {
-    return QUAD ? (i >> 2) * (BM / 2) + wm * 64 + (i & 3) * 16 : L32 ? wm * TM + i * 32 : wm * TM + i * 16;
-  };
-  auto fcol = [&](int j) {
-    return QUAD ? (j >> 1) * (BN / 2) + wn * 32 + (j & 1) * 16 : L32 ? wn * TN + (j >> 2) * 32 + (j & 3) * 8 : wn * TN + j * 16;
-  };
+  auto frow = [&](int i) { return QUAD ? (i >> 2) * (BM / 2) + wm * 64 + (i & 3) * 16 : wm * TM + i * 16; };
+  auto fcol = [&](int j) { return QUAD ? (j >> 1) * (BN / 2) + wn * 32 + (j & 1) * 16 : wn * TN + j * 16; };
   constexpr bool ext = (EPI == EPI_BF16_EXT || EPI == EPI_BF16_EXT_MX), mx = (EPI == EPI_BF16_EXT_MX);
   if constexpr (EPI == EPI_F32) {
     // split_stride < 0: every split adds its partial straight into C with hardware f32 atomics
@@ -216,11 +206,7 @@ __device__ __forceinline__ void gemm_epilogue(
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float s = row16_sum(csum[j][r]), q = row16_sum(csq[j][r]);
-          if constexpr (L32) {  // a column's 32 rows sit on two 16-lane DPP rows
-            s += __shfl_xor(s, 16);
-            q += __shfl_xor(q, 16);
-          }
+          const float s = row16_sum(csum[j][r]), q = row16_sum(csq[j][r]);
           if (ml == 0) {
             const int nloc = fcol(j) + nl + r;
             red[wm * BN + nloc] = s;

@@ -220,193 +220,11 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void g5_kernel(GemmParams p) {
   gemm_epilogue<BM, BN, NT, WGM, EPI, (512 / WPS >= 256 ? 4 : 2)>(p, acc, smem, m0, n0, bz);
 }
 
-// ---------------------------------------------------------------------------------------------
-// g6: 4 waves (one per SIMD), each owning a 128x128 wave tile of v_mfma_f32_32x32x16_bf16
-// fragments (4 x 4 f32x16 accumulators = 256 AGPRs), dense operands (K-inner or K-outer).
-// The operands stream in k16 STEPS, not k-halves: one step is 4 A + 4 B fragments (32 VGPRs)
-// feeding 16 MFMAs (16 x 32 cycles), and the next step's 8 ds_read_b128 are spread between them,
-// so two register sets (64 VGPRs) keep the MFMA pipe fed -- the k-half double buffer of the 16x16
-// 4-wave form needs 128 and does not fit next to 256 accumulators under hipcc 7.2.
-// Per K-tile (4 steps, stage s): steps 0-2 MFMA || read the next step; s_waitcnt vmcnt(0)
-// lgkmcnt(0) + barrier (tile t+1 landed, stage s free); step 3 MFMA || LDS-DMA of tile t+2 into
-// stage s || read step 0 of tile t+1. LDS reads per MFMA-cycle: half the g4 256x256 tile's.
-// Fragment of 32 image rows from rb, k16 step ks: lane (r = l&31, h = l>>5) takes row rb + r,
-// k = 16 ks + 8h .. +7.
-//   K-inner image: 16-B chunk 2 ks + h of the row; conflict-free ds_read_b128 (the swizzle
-//     (row>>1)&7 is distinct inside each 16-lane group of consecutive rows).
-//   K-outer image (64-row blocks of [64 k][64 rows]): two ds_read_b64_tr_b16, k-rows
-//     16 ks + 8h + {0..3} and {4..7}; lane i of 16-lane group G = l>>4 supplies 4 columns
-//     (16 (G&1) + 4 (i&3) ..) of k-row i>>2 and receives column 16 (G&1) + i.
-template <bool KO>
-__device__ __forceinline__ bf16x8 frag32(const char* img, int rb, int ks) {
-  const int l = threadIdx.x & 63;
-  if constexpr (!KO) {
-    const int row = rb + (l & 31);
-    const int c = ks * 2 + (l >> 5);
-    return *(const bf16x8*)(img + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
-  } else {
-    const char* b = img + (rb >> 6) * 8192;
-    const int i = l & 15, q = i >> 2, pc = i & 3;
-    const int k0 = ks * 16 + 8 * (l >> 5) + q, k1 = k0 + 4;
-    const int ch = ((rb & 63) >> 3) + 2 * ((l >> 4) & 1) + (pc >> 1);
-    const int o0 = k0 * 128 + ((ch ^ g4::swz64(k0)) << 4) + (pc & 1) * 8;
-    const int o1 = k1 * 128 + ((ch ^ g4::swz64(k1)) << 4) + (pc & 1) * 8;
-    bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)(b + o0));
-    bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)(b + o1));
-    bf16x8 r;
-    r.lo = lo;
-    r.hi = hi;
-    return r;
-  }
-}
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-template <int AM, int BMD, int EPI>
-__global__ __launch_bounds__(256, 1) void g6_kernel(GemmParams p) {
-  constexpr int NW = 4, NT = 256, WGM = 2, WGN = 2, TM = 128, TN = 128, FM = 4, FN = 4;
-  constexpr bool AKO = (AM == KOUT), BKO = (BMD == KOUT);
-  constexpr int MAIN = 2 * STAGE, EPIB = epi_lds_bytes<BM, BN, WGM>();
-  __shared__ __attribute__((aligned(16))) char smem[MAIN > EPIB ? MAIN : EPIB];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w / WGN, wn = w % WGN;
-  const int bz = blockIdx.y;
-
-  const int tiles_m = (p.M + BM - 1) / BM;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GM = 4;
-  const int grp = tile / (GM * p.tiles_n), first_m = grp * GM;
-  const int gm = min(GM, tiles_m - first_m), inr = tile - grp * GM * p.tiles_n;
-  const int m0 = (first_m + inr % gm) * BM, n0 = (inr / gm) * BN;
-
-  const int nkt = (p.K + BK - 1) / BK;
-  const int kt0 = blockIdx.z * p.kt_per_split;
-  const int kt1 = min(nkt, kt0 + p.kt_per_split);
-
-  const char* Ab = (const char*)p.A + (long long)bz * p.sA * 2 + (AKO ? (long long)m0 * 2 : (long long)m0 * p.lda * 2);
-  const char* Bb = (const char*)p.B + (long long)bz * p.sB * 2 + (BKO ? (long long)n0 * 2 : (long long)n0 * p.ldb * 2);
-  const long long a_step = AKO ? (long long)BK * p.lda * 2 : BK * 2;
-  const long long b_step = BKO ? (long long)BK * p.ldb * 2 : BK * 2;
-  const int lim_a = p.M - m0, lim_b = p.N - n0;
-
-  using LA = Loader<BM, AM, NW>;
-  using LB = Loader<BN, BMD, NW>;
-  LA la;
-  LB lb;
-  la.init(p, lane, w, p.lda, m0, p.M);
-  lb.init(p, lane, w, p.ldb, n0, p.N);
-  constexpr int NIA = LA::NI, ND = NIA + LB::NI;
-  constexpr int NRD = FM * (AKO ? 2 : 1) + FN * (BKO ? 2 : 1);  // ds_read instructions per step
-
-  f32x16 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  auto stage = [&](int s) { return smem + s * STAGE; };
-  const int ar = wm * TM, bc = wn * TN;
-  bf16x8 ra0[FM], rb0[FN], ra1[FM], rb1[FN];
-  auto rd = [&](const char* stg, int ks, bf16x8 (&ra)[FM], bf16x8 (&rb)[FN]) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) rb[j] = frag32<BKO>(stg + A_BYTES, bc + j * 32, ks);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) ra[i] = frag32<AKO>(stg, ar + i * 32, ks);
-  };
-  auto mm = [&](const bf16x8 (&ra)[FM], const bf16x8 (&rb)[FN]) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rb[j], ra[i], acc[i][j], 0, 0, 0);
-  };
-
-  la.issue(p, Ab, a_step, kt0, lim_a, stage(0), w, lane);
-  lb.issue(p, Bb, b_step, kt0, lim_b, stage(0) + A_BYTES, w, lane);
-  la.issue(p, Ab, a_step, kt0 + 1, lim_a, stage(1), w, lane, kt0 + 1 < kt1);
-  lb.issue(p, Bb, b_step, kt0 + 1, lim_b, stage(1) + A_BYTES, w, lane, kt0 + 1 < kt1);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ND) : "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  rd(stage(0), 0, ra0, rb0);
-
-#pragma unroll 1
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int s = (kt - kt0) & 1;
-    const char* cur = stage(s);
-    rd(cur, 1, ra1, rb1);
-    mm(ra0, rb0);
-    interleave<FM * FN, NRD, 0>();
-    __builtin_amdgcn_sched_barrier(0);
-    rd(cur, 2, ra0, rb0);
-    mm(ra1, rb1);
-    interleave<FM * FN, NRD, 0>();
-    __builtin_amdgcn_sched_barrier(0);
-    // tile kt+2's DMA offsets among step 2's MFMAs (past the last tile: all out of range -> zeros)
-    const bool en = kt + 2 < kt1;
-    unsigned voa[NIA], vob[ND - NIA];
-    la.offsets(p, kt + 2, lim_a, w, lane, en, voa);
-    lb.offsets(p, kt + 2, lim_b, w, lane, en, vob);
-    rd(cur, 3, ra1, rb1);
-    mm(ra0, rb0);
-    interleave<FM * FN, NRD, 0>();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    // step 3 || DMA of tile kt+2 into the freed stage || step 0 of tile kt+1 (past the last tile:
-    // zero-filling DMA, stale reads -- both unused)
-    // fixed slots {MFMA, DMA piece q, fragment read q} fenced by sched_barrier: left to the
-    // scheduler, the 16 pieces' descriptor setup is hoisted between the barrier and the first MFMA
-    const char* nxt = stage(s ^ 1);
-    const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)(Ab + (kt + 2) * a_step), (short)0, g4::NREC, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)(Bb + (kt + 2) * b_step), (short)0, g4::NREC, 0x00020000);
-    static_assert(ND == FM * FN, "one DMA piece per MFMA slot");
-#pragma unroll
-    for (int q = 0; q < ND; ++q) {
-      acc[q / FN][q % FN] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rb1[q % FN], ra1[q / FN], acc[q / FN][q % FN], 0, 0, 0);
-      if (q < NIA) LA::issue_piece(rsa, stage(s), w, q, voa[q]);
-      else LB::issue_piece(rsb, stage(s) + A_BYTES, w, q - NIA, vob[q - NIA]);
-      if (q < FN) rb0[q] = frag32<BKO>(nxt + A_BYTES, bc + q * 32, 0);
-      else if (q < FN + FM) ra0[q - FN] = frag32<AKO>(nxt, ar + (q - FN) * 32, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) asm volatile("" : "+a"(acc[i][j]));
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  // f32x4 units of the L32 epilogue layout: registers 4g..4g+3 of fragment (i, j) -> unit (i, 4j+g)
-  f32x4 a4[FM][FN * 4];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        a4[i][4 * j + g] = f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-  gemm_epilogue<BM, BN, NT, WGM, EPI, 4, false, false, true>(p, a4, smem, m0, n0, bz);
-}
-
-// launch the 8-wave kernel (modes 8-10) or the 4-wave 32x32 kernel (mode 11, dense K-inner only;
-// the 4-wave 16x16 128x128-per-wave form runs out of architectural VGPRs for its two k-half
-// operand sets under hipcc 7.2 -- not instantiated)
+// launch the 8-wave kernel (the 4-wave 128x128-per-wave form runs out of architectural VGPRs for
+// its two operand register sets under hipcc 7.2 and shuffles accumulators through v_accvgpr moves
+// every K-tile -- not instantiated)
 template <int AM, int BMD, int EPI>
 int go(int mode, dim3 grid, hipStream_t stream, const GemmParams& p) {
-  // (the EXT epilogue does not fit next to the 32x32 accumulator view: 12 B/lane of scratch)
-  if constexpr ((AM == KIN || AM == KOUT) && (BMD == KIN || BMD == KOUT) && (EPI == EPI_BF16 || EPI == EPI_F32)) {
-    if (mode == 11) {
-      hipLaunchKernelGGL((g6_kernel<AM, BMD, EPI>), grid, dim3(256), 0, stream, p);
-      return hipGetLastError() == hipSuccess ? 0 : -2;
-    }
-  }
-  if (mode == 11) return -1;
   if (mode == 8) {
     hipLaunchKernelGGL((g5_kernel<AM, BMD, EPI, 2, 4, 0>), grid, dim3(512), 0, stream, p);
     return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -424,8 +242,7 @@ int go(int mode, dim3 grid, hipStream_t stream, const GemmParams& p) {
 
 }  // namespace g5
 
-// 0: off (default until measured), 8 / 9 / 10: the 8-wave kernel (SCHED 0 / 1 / 2) for every eligible
-// 256x256 GEMM; 11: the 4-wave 32x32 kernel (g6) for the dense K-inner ones
+// 0: off (default until measured), 8 / 9 / 10: the 8-wave kernel (SCHED 0 / 1 / 2) for every eligible 256x256 GEMM
 static int g_g5 = -1;
 extern "C" void tfk_g5_set(int waves) { g_g5 = waves; }
 static int g5_mode() {
@@ -441,7 +258,7 @@ static int g5_mode() {
 extern "C" int tfk_g5_launch(const GemmParams& p_in, int amode, int bmode, int epi, int batch, int splits,
                              hipStream_t stream) {
   const int mode = g5_mode();
-  if (mode < 8 || mode > 11) return -1;
+  if (mode < 8 || mode > 10) return -1;
   const bool dense = (amode == g4::KIN && (bmode == g4::KIN || bmode == g4::KOUT)) ||
                      (amode == g4::KOUT && bmode == g4::KOUT);
   const bool conv = amode == g4::CONV_FWD && bmode == g4::KIN && (p_in.Cin & 63) == 0;

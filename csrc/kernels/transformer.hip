@@ -144,10 +144,6 @@ __global__ __launch_bounds__(LNMX_NT) void ln_fwd_mx_kernel(const bf16* __restri
   tfk::mx_rows32_out<LNMX_NT>(&tile[0][0], LNMX_WMAX + 8, W, M, r0, qr, sr, qc, sc);
 }
 
-// rows per pipelined group of ln_bwd_kernel (LN_U rows of loads in flight per wave; one at W >
-// 1024, where two rows' registers push the accumulators into AGPR shuffles)
-template <int CPL>
-constexpr int ln_u() { return CPL >= 4 ? 1 : 2; }
 template <int CPL>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
@@ -176,10 +172,9 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
       gm[j][e] = c < nch ? gamma[c * 8 + e] : 0.f;
     }
   }
-  // rows software-pipelined in groups of LN_U: the next group's dy / x / dres (and mean / rstd) are
-  // loaded before this group's reductions and stores, so a wave keeps LN_U rows of loads in flight
-  // (one block of 4 waves per CU on Transformer-big's 8192 x 1024 rows: with one row in flight per
-  // wave, 24 KiB per CU, the kernel ran at 3 TB/s, latency-bound)
+  // rows software-pipelined: the next row's dy / x / dres (and mean / rstd) are loaded before this
+  // row's reductions and stores, so a wave keeps one row of loads in flight instead of paying two
+  // dependent memory latencies per row (measured 2.2 TB/s on Transformer-big's 8192 x 1024 rows)
   // MX mode (mq != null: emit MX-fp8 row + column blocks of the consumer gradient): a block owns 32
   // consecutive rows (8 per wave), stages their final values in an LDS tile behind `red` and
   // quantizes the tile after the row loop (the consumer's fp8 backward then skips its quantize pass)
@@ -188,29 +183,28 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
   int row = mxo ? blockIdx.x * 32 + wid * 8 : blockIdx.x * (NT / 64) + wid;
   const int rend = mxo ? row + 8 : M;
   bf16* mtile = (bf16*)(red + (NT / 64) * NS * W);  // [32][W + 8] (MX mode only)
-  constexpr int LN_U = ln_u<CPL>();
-  bf16x8 ndv[LN_U][CPL], nxv[LN_U][CPL], nrv[LN_U][CPL];
-  float nmu[LN_U], nrs[LN_U];
-  auto fetch = [&](int r0) {
+  bf16x8 ndv[CPL], nxv[CPL], nrv[CPL];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int r) {
+    nmu = mean[r];
+    nrs = rstd[r];
 #pragma unroll
-    for (int u = 0; u < LN_U; ++u) {
-      const int r = r0 + u * rstep;
-      if (r >= rend) break;
-      nmu[u] = mean[r];
-      nrs[u] = rstd[r];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        const int c = lane + 64 * j;
-        if (c < nch) {
-          ndv[u][j] = *(const bf16x8*)(dy + (long long)r * W + c * 8);
-          nxv[u][j] = *(const bf16x8*)(x + (long long)r * W + c * 8);
-          if (dres) nrv[u][j] = *(const bf16x8*)(dres + (long long)r * W + c * 8);
-        }
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        ndv[j] = *(const bf16x8*)(dy + (long long)r * W + c * 8);
+        nxv[j] = *(const bf16x8*)(x + (long long)r * W + c * 8);
+        if (dres) nrv[j] = *(const bf16x8*)(dres + (long long)r * W + c * 8);
       }
     }
   };
-  auto proc = [&](int row, const bf16x8 (&cdv)[CPL], const bf16x8 (&cxv)[CPL], const bf16x8 (&crv)[CPL], float mu,
-                  float rs) {
+  if (row < rend) fetch(row);
+  for (; row < rend; row += rstep) {
+    const float mu = nmu, rs = nrs;
+    bf16x8 cdv[CPL], cxv[CPL], crv[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) { cdv[j] = ndv[j]; cxv[j] = nxv[j]; crv[j] = nrv[j]; }
+    if (row + rstep < rend) fetch(row + rstep);
     float g[CPL][8], xh[CPL][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -272,22 +266,6 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
         }
       }
     }
-  };
-  if (row < rend) fetch(row);
-  for (; row < rend; row += LN_U * rstep) {
-    bf16x8 cdv[LN_U][CPL], cxv[LN_U][CPL], crv[LN_U][CPL];
-    float cmu[LN_U], crs[LN_U];
-#pragma unroll
-    for (int u = 0; u < LN_U; ++u) {
-      cmu[u] = nmu[u];
-      crs[u] = nrs[u];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) { cdv[u][j] = ndv[u][j]; cxv[u][j] = nxv[u][j]; crv[u][j] = nrv[u][j]; }
-    }
-    if (row + LN_U * rstep < rend) fetch(row + LN_U * rstep);
-#pragma unroll
-    for (int u = 0; u < LN_U; ++u)
-      if (row + u * rstep < rend) proc(row + u * rstep, cdv[u], cxv[u], crv[u], cmu[u], crs[u]);
   }
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {

@@ -16,6 +16,24 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #define LDS_AS __attribute__((address_space(3)))
 #define TFK_WAVE 64
 
+// LDS-DMA (buffer_load ... lds) of BYTES (16 or 4) per lane into LDS at `lds` + 16*lane (4*lane),
+// issued from inline asm: hipcc 7.2's waitcnt pass does not see it. Through the builtin it treats
+// every later ds_read_b64_tr_b16 as possibly reading the DMA's bytes and puts s_waitcnt vmcnt(0) in
+// front of it, so a transposed read of stage s waited for stage s^1's just-issued DMA (the K-outer
+// GEMMs and the weight-gradient kernels lost their DMA / MFMA overlap; plain ds_read_b128 is not
+// affected). Every caller waits for its DMAs itself (s_waitcnt vmcnt + barrier) before reading a
+// stage or reusing the LDS; M0 is written only here (no builtin LDS-DMA remains in the library, so
+// no compiler-tracked M0 value is clobbered).
+template <int BYTES>
+__device__ __forceinline__ void lds_dma(__amdgpu_buffer_rsrc_t rsrc, LDS_AS void* lds, unsigned voff) {
+  static_assert(BYTES == 16 || BYTES == 4, "dwordx4 or dword");
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)lds);
+  if constexpr (BYTES == 16)
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(rsrc) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(rsrc) : "memory");
+}
+
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
 

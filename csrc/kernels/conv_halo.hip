@@ -56,7 +56,7 @@ __device__ __forceinline__ void halo_issue(const GemmParams& p, char* img, int n
       const bool ok = pix < G::HPIX && (unsigned)h < (unsigned)p.H && (unsigned)x < (unsigned)W;
       const unsigned vo =
           ok ? (unsigned)(((((long long)n * p.H + h) * W + x) * p.Cin + ch * 64 + c * 8) * 2) : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + j * 1024), 16, vo, 0, 0, 0);
+      lds_dma<16>(rsrc, (LDS_AS void*)(img + j * 1024), vo);
     }
   }
 }

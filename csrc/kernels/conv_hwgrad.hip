@@ -129,7 +129,7 @@ __global__ __launch_bounds__(512, 1) void hwgrad_kernel(HWParams p) {
         const int n = n0 + b, hh = h0 * ST - 1 + hr, ww = col - 1;
         const bool ok = n < p.Nimg && col < G::HCR && (unsigned)hh < (unsigned)p.H && (unsigned)ww < (unsigned)p.W;
         const unsigned vo = ok ? (unsigned)(((((long long)n * p.H + hh) * p.W + ww) * p.C + ci0 + c * 8) * 2) : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (LDS_AS void*)(img + jd * 1024), 16, vo, 0, 0, 0);
+        lds_dma<16>(rx, (LDS_AS void*)(img + jd * 1024), vo);
       }
     }
     const long long pix0 = ((long long)n0 * p.P + h0) * Q;
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(512, 1) void hwgrad_kernel(HWParams p) {
         const int c = slot ^ (pswz(r) << 1);
         const bool ok = r < G::NPIX && pix0 + r < npx;
         const unsigned vo = ok ? (unsigned)(((pix0 + r) * p.K + co0 + c * 8) * 2) : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (LDS_AS void*)(img + G::XB + jd * 1024), 16, vo, 0, 0, 0);
+        lds_dma<16>(rd, (LDS_AS void*)(img + G::XB + jd * 1024), vo);
       }
     }
   };
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(512, 1) void stem_wgrad_kernel(SParams p) {
         const int hh = 2 * h0 - 3 + hr, ww = hc - 3;
         const bool ok = hr < G::HR && hc < G::HCR && (unsigned)hh < (unsigned)p.H && (unsigned)ww < (unsigned)p.W;
         const unsigned vo = ok ? (unsigned)((((long long)n * p.H + hh) * p.W + ww) * 16) : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (LDS_AS void*)(img + jd * 1024), 16, vo, 0, 0, 0);
+        lds_dma<16>(rx, (LDS_AS void*)(img + jd * 1024), vo);
       }
     }
     const long long pix0 = ((long long)n * p.P + h0) * Q;
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(512, 1) void stem_wgrad_kernel(SParams p) {
         const int r = 8 * jd + (lane >> 3);
         const int c = slot ^ (hwg::pswz(r) << 1);
         const unsigned vo = r < G::NPIX ? (unsigned)(((pix0 + r) * 64 + c * 8) * 2) : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (LDS_AS void*)(img + G::XB + jd * 1024), 16, vo, 0, 0, 0);
+        lds_dma<16>(rd, (LDS_AS void*)(img + G::XB + jd * 1024), vo);
       }
     }
   };

@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(GemmParams p, int band
         const int hh = 2 * h0 - 3 + hr, ww = hc - 3;
         const bool ok = hr < G::HR && hc < G::HCR && (unsigned)hh < (unsigned)p.H && (unsigned)ww < (unsigned)p.W;
         const unsigned vo = ok ? (unsigned)((((long long)n * p.H + hh) * p.W + ww) * 16) : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (LDS_AS void*)(smem + jd * 1024), 16, vo, 0, 0, 0);
+        lds_dma<16>(rx, (LDS_AS void*)(smem + jd * 1024), vo);
       }
     }
   }

@@ -126,7 +126,7 @@ struct Loader {
         const int h = (int)pp * p.sh + ch[i], wq = (int)qq * p.sw + cw[i];
         const bool ok = !(off[i] & OOB) && (int)pix < p.K && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
         const unsigned vo = ok && en ? (unsigned)(((((long long)n * p.H + h) * p.W + wq) * p.Cin + off[i]) * 2) : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
+        lds_dma<16>(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), vo);
       }
     } else if constexpr (MODE == CONV_FWD) {
       __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, NREC, 0x00020000);
@@ -144,7 +144,7 @@ struct Loader {
           const bool ok = (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
           const int pix = (int)off[i] + tap;
           const unsigned vo = ok && en ? (unsigned)(pix * p.Cin + c0 + k_of(i, w, lane)) * 2u : OOB;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
+          lds_dma<16>(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), vo);
         }
       } else {
         // Cin % 8 == 0, Cin < 64 (the stem's 3 channels padded to 8): a K-tile spans 64/Cin taps and
@@ -161,7 +161,7 @@ struct Loader {
                           (unsigned)wq < (unsigned)p.W;
           const int pix = (int)off[i] + (int)r * p.dh * p.W + (int)sx * p.dw;
           const unsigned vo = ok && en ? (unsigned)(pix * p.Cin + (int)c) * 2u : OOB;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
+          lds_dma<16>(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), vo);
         }
       }
     } else {
@@ -173,7 +173,7 @@ struct Loader {
         unsigned vo = off[i];
         if (!inner) vo = (row_of(i, w, lane) < lim && k_of(i, w, lane) < krem) ? vo : OOB;
         if (!en) vo = OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), 16, vo, 0, 0, 0);
+        lds_dma<16>(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), vo);
       }
     }
   }

@@ -260,7 +260,7 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), (occ_default<BM, BN>())) v
       (int)min((long long)(sc_is_a ? p.M : p.N) * sld, (long long)NREC), 0x00020000);
   auto issue_scales = [&](int kt, char* stg) {
     if (sc_issuer)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsc, (LDS_AS void*)(stg + sc_img), 4, sc_row * sld + kt * 4, 0, 0, 0);
+      lds_dma<4>(rsc, (LDS_AS void*)(stg + sc_img), sc_row * sld + kt * 4);
   };
   auto read_scales = [&](const char* stg, int (&sa)[FM], int (&sb)[FN]) {
 #pragma unroll

@@ -11,6 +11,26 @@ def test_no_vendor_gemm_in_the_op_layer():
         assert call not in src, call
 
 
+def test_lds_dma_only_through_the_asm_helper():
+    """Every LDS-DMA in the kernel library goes through common.h's lds_dma (inline asm): with the
+    builtin, hipcc puts s_waitcnt vmcnt(0) before each later ds_read_b64_tr_b16, so the K-outer GEMMs
+    and the weight-gradient kernels wait for the next stage's DMA mid-tile (profiles/perf_log_r5.md),
+    and a builtin next to the helper could be handed a stale compiler-tracked M0."""
+    import glob
+    import os
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "kernels")
+    srcs = glob.glob(os.path.join(root, "*.hip")) + glob.glob(os.path.join(root, "*.h"))
+    assert srcs
+    for path in srcs:
+        with open(path) as f:
+            text = f.read()
+        for builtin in ("__builtin_amdgcn_raw_ptr_buffer_load_lds", "__builtin_amdgcn_raw_buffer_load_lds",
+                        "__builtin_amdgcn_global_load_lds"):
+            assert builtin not in text, (os.path.basename(path), builtin)
+    with open(os.path.join(root, "common.h")) as f:
+        assert "offen lds" in f.read()
+
+
 def test_dgrad_splitk_policy():
     """Plain input gradients with too few 256x256 output tiles and a long reduction (the tied-logits
     dgrad) take the split-K path; wide outputs and short reductions do not."""

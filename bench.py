@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--force-comm", action="store_true",
                     help="1 GPU: still run the RCCL gradient all-reduce (world-size-1 tfk_comm communicator)")
     ap.add_argument("--fp8", type=int, default=0, help="transformer models: MX-fp8 linear GEMMs (fwd, dgrad, wgrad)")
+    ap.add_argument("--mx-wgrad", type=int, default=-1, help=argparse.SUPPRESS)  # A/B: fp8 weight gradients
     ap.add_argument("--via-operator", action="store_true",
                     help="measure through a TFJob: tfk-cluster gang-schedules one pod per GPU (TF_CONFIG rendezvous)")
     ap.add_argument("--tfjob-worker", action="store_true", help=argparse.SUPPRESS)  # a pod of --via-operator
@@ -138,6 +139,9 @@ def main():
 
     is_cnn = args.model.startswith("resnet")
     nworkers = len(worker_ranks)
+    if args.mx_wgrad >= 0:
+        from tensorflow_k8s_amd.ops import fp8 as _F8
+        _F8.MX_WGRAD = bool(args.mx_wgrad)
     model = build_model(args.model, **({"fp8": True} if args.fp8 else {})).to(dev)
     if hasattr(model, "rng_stream"):
         model.rng_stream = rank  # each replica draws its own dropout masks

@@ -220,172 +220,6 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void g5_kernel(GemmParams p) {
   gemm_epilogue<BM, BN, NT, WGM, EPI, (512 / WPS >= 256 ? 4 : 2)>(p, acc, smem, m0, n0, bz);
 }
 
-// ---------------------------------------------------------------------------------------------
-// g4p: the g4 256x256 tile (16 waves, 64x64 wave tiles, same loop) made PERSISTENT, with a direct
-// epilogue. Why: on a short-K GEMM of several rounds (Transformer-big FFN1, 16384x4096x1024: 1024
-// tiles = 4 rounds of 16 K-tiles) every round ends with all 256 CUs storing their 128 KiB tiles at
-// once through the LDS C tile and then waiting for the next tile's first DMA -- about 9 us per
-// round with the MFMA pipes idle (sq4096, 1 round, 1168 TF/s vs FFN1 952). Here one block per CU
-// walks tiles t = round * G + xcd_remap(block); after a tile's last K-tile the next tile's first
-// K-tile is DMA'd into stage 0 while this tile's accumulators go straight to global memory
-// (4 columns = 8 B per lane per fragment: alpha, bias, activation, residual), and the wait for that
-// DMA is counted past the stores, so the stores drain under the next tile's MFMAs.
-template <int BMD>
-__global__ __launch_bounds__(1024, 1) void g4p_kernel(GemmParams p, int ntiles) {
-  constexpr int NW = 16, WGN = 4, FM = 4, FN = 4, TM = 64, TN = 64;
-  constexpr bool BKO = (BMD == KOUT);
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w / WGN, wn = w % WGN;
-  const int bz = blockIdx.y;
-  const int G = gridDim.x;
-  const int tiles_m = (p.M + BM - 1) / BM;
-  constexpr int GM = 4;
-  auto origin = [&](int t, int& m0, int& n0) {
-    const int grp = t / (GM * p.tiles_n), first_m = grp * GM;
-    const int gm = min(GM, tiles_m - first_m), inr = t - grp * GM * p.tiles_n;
-    m0 = (first_m + inr % gm) * BM;
-    n0 = (inr / gm) * BN;
-  };
-  int t = xcd_remap(blockIdx.x, G);
-  if (t >= ntiles) return;  // block-uniform
-  const int nkt = (p.K + BK - 1) / BK;
-  const long long a_step = BK * 2, b_step = BKO ? (long long)BK * p.ldb * 2 : BK * 2;
-  const char* A0 = (const char*)p.A + (long long)bz * p.sA * 2;
-  const char* B0 = (const char*)p.B + (long long)bz * p.sB * 2;
-  auto a_base = [&](int m0) { return A0 + (long long)m0 * p.lda * 2; };
-  auto b_base = [&](int n0) { return B0 + (BKO ? (long long)n0 * 2 : (long long)n0 * p.ldb * 2); };
-  // dense operands: the per-lane offsets are relative to the tile origin (init's row0 unused)
-  Loader<BM, KIN, NW> la;
-  Loader<BN, BMD, NW> lb;
-  la.init(p, lane, w, p.lda, 0, p.M);
-  lb.init(p, lane, w, p.ldb, 0, p.N);
-  auto stage = [&](int s) { return smem + s * STAGE; };
-  const int ar = wm * TM, bc = wn * TN;
-
-  int m0, n0;
-  origin(t, m0, n0);
-  const char* Ab = a_base(m0);
-  const char* Bb = b_base(n0);
-  la.issue(p, Ab, a_step, 0, p.M - m0, stage(0), w, lane);
-  lb.issue(p, Bb, b_step, 0, p.N - n0, stage(0) + A_BYTES, w, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  f32x4 acc[FM][FN];
-  bf16x8 b0[FN], b1[FN];
-  bf16* C = (bf16*)p.C + bz * p.sC;
-  const bf16* R = p.resid ? (const bf16*)p.resid + bz * p.sC : nullptr;
-  const int ml = lane & 15, nl = (lane >> 4) * 4;
-#pragma unroll 1
-  for (;;) {
-    const int lim_a = p.M - m0, lim_b = p.N - n0;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < FN; ++j) b0[j] = frag<BKO>(stage(0) + A_BYTES, bc + j * 16, 0);
-#pragma unroll 1
-    for (int kt = 0; kt < nkt; ++kt) {
-      const int s = kt & 1;
-      const char* As = stage(s);
-      const char* Bs = As + A_BYTES;
-      const bool more = kt + 1 < nkt;
-      if (more) {
-        char* nx = stage(s ^ 1);
-        la.issue(p, Ab, a_step, kt + 1, lim_a, nx, w, lane);
-        lb.issue(p, Bb, b_step, kt + 1, lim_b, nx + A_BYTES, w, lane);
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) b1[j] = frag<BKO>(Bs, bc + j * 16, 1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const bf16x8 a = frag<false>(As, ar + i * 16, 0);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a, acc[i][j], 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const bf16x8 a = frag<false>(As, ar + i * 16, 1);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a, acc[i][j], 0, 0, 0);
-      }
-      if (more) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int j = 0; j < FN; ++j) b0[j] = frag<BKO>(stage(s ^ 1) + A_BYTES, bc + j * 16, 0);
-      }
-    }
-    // every wave is done reading the stages: the next tile's first K-tile goes to stage 0 now
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const int tn = t + G;
-    const bool has_next = tn < ntiles;  // block-uniform
-    int nm0 = 0, nn0 = 0;
-    if (has_next) {
-      origin(tn, nm0, nn0);
-      Ab = a_base(nm0);
-      Bb = b_base(nn0);
-      la.issue(p, Ab, a_step, 0, p.M - nm0, stage(0), w, lane);
-      lb.issue(p, Bb, b_step, 0, p.N - nn0, stage(0) + A_BYTES, w, lane);
-    }
-    // direct epilogue: unit (i, j) of lane l = C[m][n..n+3], m = i*16 + (l&15), n = j*16 + (l>>4)*4
-    const bool interior = m0 + BM <= p.M && n0 + BN <= p.N && (p.ldc & 3) == 0;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + bc + j * 16 + nl;
-      f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-      if (p.bias) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = n + r < p.N ? p.bias[n + r] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int m = m0 + ar + i * 16 + ml;
-        bf16x4 rv;
-        if (R) {
-          if (interior) {
-            rv = *(const bf16x4*)(R + (long long)m * p.ldc + n);
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) rv[r] = (m < p.M && n + r < p.N) ? R[(long long)m * p.ldc + n + r] : f2bf(0.f);
-          }
-        }
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = act_apply(acc[i][j][r] * p.alpha + bv[r], p.act);
-          if (R) v = bf2f(f2bf(v)) + bf2f(rv[r]);
-          o[r] = f2bf(v);
-        }
-        if (interior) {
-          *(bf16x4*)(C + (long long)m * p.ldc + n) = o;
-        } else if (m < p.M) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) C[(long long)m * p.ldc + n + r] = o[r];
-        }
-      }
-    }
-    if (!has_next) break;
-    // the next tile's stage 0 landed (its DMA is older than the stores, which keep draining);
-    // edge tiles issue a variable number of stores: wait for everything there
-    if (interior) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    t = tn;
-    m0 = nm0;
-    n0 = nn0;
-  }
-}
-
 // launch the 8-wave kernel (the 4-wave 128x128-per-wave form runs out of architectural VGPRs for
 // its two operand register sets under hipcc 7.2 and shuffles accumulators through v_accvgpr moves
 // every K-tile -- not instantiated)
@@ -408,8 +242,7 @@ int go(int mode, dim3 grid, hipStream_t stream, const GemmParams& p) {
 
 }  // namespace g5
 
-// 0: off (default until measured), 8 / 9 / 10: the 8-wave kernel (SCHED 0 / 1 / 2) for every eligible
-// 256x256 GEMM; 12: the persistent direct-epilogue g4 (g4p_kernel) for the plain bf16 ones
+// 0: off (default until measured), 8 / 9 / 10: the 8-wave kernel (SCHED 0 / 1 / 2) for every eligible 256x256 GEMM
 static int g_g5 = -1;
 extern "C" void tfk_g5_set(int waves) { g_g5 = waves; }
 static int g5_mode() {
@@ -425,26 +258,6 @@ static int g5_mode() {
 extern "C" int tfk_g5_launch(const GemmParams& p_in, int amode, int bmode, int epi, int batch, int splits,
                              hipStream_t stream) {
   const int mode = g5_mode();
-  if (mode == 12) {
-    // persistent direct-epilogue g4 (g4p_kernel): plain bf16 epilogues (alpha, bias, act, resid)
-    if (amode != g4::KIN || (bmode != g4::KIN && bmode != g4::KOUT) || epi != EPI_BF16 || splits != 1 ||
-        p_in.stats || p_in.beta != 0.f)
-      return -1;
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    }
-    GemmParams p = p_in;
-    p.tiles_n = (p.N + g5::BN - 1) / g5::BN;
-    const int tiles = ((p.M + g5::BM - 1) / g5::BM) * p.tiles_n;
-    const dim3 grid(tiles < cus ? tiles : cus, batch, 1);
-    // (the K-outer-B form spills 24 B/lane next to the direct epilogue: dgrads stay on g4)
-    if (bmode != g4::KIN) return -1;
-    hipLaunchKernelGGL((g5::g4p_kernel<g4::KIN>), grid, dim3(1024), 0, stream, p, tiles);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-  }
   if (mode < 8 || mode > 10) return -1;
   const bool dense = (amode == g4::KIN && (bmode == g4::KIN || bmode == g4::KOUT)) ||
                      (amode == g4::KOUT && bmode == g4::KOUT);

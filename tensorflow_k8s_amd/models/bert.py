@@ -25,6 +25,7 @@ from ..ops import elementwise as E
 from ..ops import gemm as G
 from ..ops import transformer as TR
 from ..ops.loss import softmax_xent
+from ..runtime import streams
 from ..runtime.arena import ParamArena, ParamSpec
 from ..runtime.layers import Embedding, FusedLinear, LayerNorm, Linear
 
@@ -256,15 +257,18 @@ class BertForPreTraining:
         dh = torch.zeros_like(h)
         TR.scatter_add_rows(dh, dhm, rows, S)  # rows = the MLM positions
         TR.scatter_add_rows(dh, dhc, None, S)  # the [CLS] rows
+        streams.flush()  # the heads' weight gradients behind one side-stream fork (under capture)
         # ---- encoder backward
         for layer in reversed(self.layers):
             dh = layer.backward(dh)
+            streams.flush()  # this layer's weight gradients, concurrent with the next layer's dgrads
         e, st, hd, s_emb = emb_saved
         de = self.ln_emb.backward(E.dropout(dh, hd, s_emb), e, st)
         self.pos.table.grad.zero_()
         self.typ.table.grad.zero_()
         TR.embedding_bwd(ids, de, self.word.table.grad, self.pos.table.grad, S, tt,
                          self.typ.table.grad[:self.cfg.type_vocab])  # real rows only (table padded to 64)
+        streams.join()  # side-stream weight gradients complete before anyone reads arena.grad
         self.arena.grad_ready(self.word.table, self.pos.table, self.typ.table)
         loss = mlm_loss.view(B, P).mean(1) + nsp_loss
         return loss, corr

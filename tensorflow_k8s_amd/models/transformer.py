@@ -24,6 +24,8 @@ from ..ops import elementwise as E
 from ..ops import gemm as G
 from ..ops import transformer as TR
 from ..ops.loss import softmax_xent
+from ..ops import fp8 as F8
+from ..runtime import streams
 from ..runtime.arena import ParamArena
 from ..runtime.layers import Embedding, FusedLinear, LayerNorm, Linear
 from .bert import _mix
@@ -159,7 +161,7 @@ class EncoderLayer:
         # f itself is never read (ff2's dgrad takes relu' from z), so its bf16 store is skipped
         mx = MX_PRODUCERS and self.ff1.fp8 and self.ff2.fp8 and training and b.shape[0] % 128 == 0
         f = self.ff1.forward(b, act="relu", aux=z, drop_p=cfg.relu_dropout if training else 0.0,
-                             drop_seed=_mix(seed, 5), mx_out=mx, mx_skip_c=mx)
+                             drop_seed=_mix(seed, 5), mx_out=mx, mx_skip_c=mx and F8.MX_WGRAD)
         x2 = self.ff2.forward(f, resid=x, drop_p=cfg.dropout if training else 0.0, drop_seed=_mix(seed, 6))
         return x2, (x, b, st, z, f)
 
@@ -365,13 +367,16 @@ class Transformer:
         for i in range(nd - 1, -1, -1):
             nxt = self.dec[i - 1].in_drop(tr, _mix(seed, 200 + i - 1)) if i > 0 else (p, _mix(seed, 0xE1))
             dy, dyd = self.dec[i].backward(dy, mem, dmem, din=dyd, out_drop=nxt)
+            streams.flush()  # this layer's weight gradients, concurrent with the next layer's dgrads
         scale = math.sqrt(cfg.hidden)
         TR.embedding_bwd(tgt_in, dyd, self.emb.table.grad, None, St, scale=scale)
         dx, dxd = self.enc_ln.backward(dmem, x, st_m, drop=self.enc[-1].in_drop(tr, _mix(seed, 100 + ne - 1)))
         for i in range(ne - 1, -1, -1):
             nxt = self.enc[i - 1].in_drop(tr, _mix(seed, 100 + i - 1)) if i > 0 else (p, _mix(seed, 0xE0))
             dx, dxd = self.enc[i].backward(dx, din=dxd, out_drop=nxt)
+            streams.flush()
         TR.embedding_bwd(src, dxd, self.emb.table.grad, None, Ss, scale=scale)
+        streams.join()  # side-stream weight gradients complete before anyone reads arena.grad
         self.arena.grad_ready(self.emb.table)
         return loss.view(B, St).mean(1), corr
 

@@ -290,10 +290,15 @@ def mx_quantize_t(x: torch.Tensor):
     return q, s
 
 
+# Weight gradients in MX-fp8 (True) or bf16 (False) in the fp8 models. A/B switch for tools and
+# bench.py --mx-wgrad; the default is the faster in-model measurement (profiles/perf_log_r5.md).
+MX_WGRAD = True
+
+
 def mx_backward_ok(M: int, N: int, K: int) -> tuple[bool, bool]:
     """(dgrad, wgrad) eligibility of a [M tokens, K in] x [N out, K in] linear layer: the
     reduction dims (N for dgrad, M for wgrad) must be multiples of 128 (one scaled-MFMA K-tile)."""
-    return N % 128 == 0 and K % 8 == 0, M % 128 == 0
+    return N % 128 == 0 and K % 8 == 0, MX_WGRAD and M % 128 == 0
 
 
 def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None = None,

@@ -64,6 +64,12 @@ def linear_wgrad(dy, x, gw, fp8: bool, accumulate: bool = False, split_target=No
     return G.linear_wgrad(dy, x, gw, accumulate=accumulate, split_target=split_target)
 
 
+def _mx_keep(dyt) -> tuple:
+    """The tensors of an MX operand (q, scales) a deferred weight gradient reads (kept alive by
+    runtime.streams until the join)."""
+    return tuple(t for t in (dyt or ()) if isinstance(t, torch.Tensor))
+
+
 def linear_dgrad(dy, w, fp8: bool, drop_p: float = 0.0, drop_seed: int = 0, dyq=None, **kw):
     """Input gradient: MX-fp8 when fp8 and the output width tiles (N % 128), else bf16; either way
     the input-dropout backward runs in the GEMM epilogue."""
@@ -225,10 +231,16 @@ class Linear:
         (mx_dx_only: and no bf16 dx). dx_bias: the producer layer's bias gradient (its bias_sink()),
         accumulated from dx's column sums in the dgrad epilogue."""
         dyq, dyt = fp8_dy(dy.reshape(-1, dy.shape[-1]), self.fin, self.fp8 and need_dx)
-        linear_wgrad(dy, x, self.w.grad, self.fp8, accumulate=accumulate, split_target=self.split_target, dyt=dyt)
-        if self.b is not None:
-            if not bias_done:
+
+        def wgrad():
+            linear_wgrad(dy, x, self.w.grad, self.fp8, accumulate=accumulate, split_target=self.split_target, dyt=dyt)
+            if self.b is not None and not bias_done:
                 G.bias_grad(dy, self.b.grad, accumulate=accumulate or self.arena.prezeroed)
+        # on a side stream under capture (runtime/streams.py), concurrent with the input-gradient chain;
+        # MX-fp8 ones are forked at once (their operands come from per-step caches), bf16 ones queue
+        # for the layer's flush()
+        streams.run_wgrad(wgrad, dy, x, *_mx_keep(dyt), deferrable=not self.fp8)
+        if self.b is not None:
             self.arena.grad_ready(self.w, self.b)
         else:
             self.arena.grad_ready(self.w)
@@ -285,9 +297,12 @@ class FusedLinear:
     def backward(self, dy, x, need_dx: bool = True, resid=None):
         w, gw, _, gb = self.views()
         dyq, dyt = fp8_dy(dy.reshape(-1, dy.shape[-1]), self.fin, self.fp8 and need_dx)
-        linear_wgrad(dy, x, gw, self.fp8, split_target=getattr(self, "split_target", None), dyt=dyt)
-        if gb is not None:
-            G.bias_grad(dy, gb, accumulate=self.arena.prezeroed)
+
+        def wgrad():
+            linear_wgrad(dy, x, gw, self.fp8, split_target=getattr(self, "split_target", None), dyt=dyt)
+            if gb is not None:
+                G.bias_grad(dy, gb, accumulate=self.arena.prezeroed)
+        streams.run_wgrad(wgrad, dy, x, *_mx_keep(dyt), deferrable=not self.fp8)
         self.arena.grad_ready(*[p.w for p in self.parts], *[p.b for p in self.parts if p.b is not None])
         if not need_dx:
             return None
@@ -325,7 +340,10 @@ class LayerNorm:
 
     def forward(self, x, mx_out: bool = False):
         """mx_out (fp8 training): y feeds only MX-fp8 GEMMs -- emit MX(y), MX(y^T), no bf16 y."""
-        y, mu, rs = TR.layernorm_fwd(x, self.gamma.master, self.beta.master, self.eps, mx_out=mx_out, skip_y=mx_out)
+        from ..ops import fp8 as F8
+        # the bf16 y stays when the consumer's weight gradient reads it in bf16 (F8.MX_WGRAD off)
+        y, mu, rs = TR.layernorm_fwd(x, self.gamma.master, self.beta.master, self.eps, mx_out=mx_out,
+                                     skip_y=mx_out and F8.MX_WGRAD)
         return y, (mu, rs)
 
     def backward(self, dy, x, stats, dres=None, drop=None, consumer=None):

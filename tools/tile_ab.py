@@ -32,8 +32,6 @@ def _engine(t, on: bool):
         lib().g5_set(9 if on else 0)
     elif t == "g5t":  # fixed slots, DMA pieces late, MFMAs first in each slot
         lib().g5_set(10 if on else 0)
-    elif t == "g4p":  # persistent g4 256x256 with the direct epilogue (plain bf16 forwards)
-        lib().g5_set(12 if on else 0)
 
 
 def _g8(fn, t):
@@ -88,7 +86,7 @@ def main():
     ap.add_argument("--tiles", default="", help="subset, e.g. 256x256,g8,g5")
     args = ap.parse_args()
     if args.tiles:
-        TILES[:] = [t if t in ("g8", "g5", "g5s", "g5t", "g4p") else tuple(int(v) for v in t.split("x")) for t in args.tiles.split(",")]
+        TILES[:] = [t if t in ("g8", "g5", "g5s", "g5t") else tuple(int(v) for v in t.split("x")) for t in args.tiles.split(",")]
     dirs = set(args.dirs.split(","))
     dev = "cuda"
     for name, (M, N, K) in DENSE.items():

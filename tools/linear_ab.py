@@ -47,13 +47,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     orig = G.pick_tile
-    variants = {"pick": None, "t256": (256, 256), "t128": (128, 128), "t256x128": (256, 128), "g5s": "g5s"}
-    from tensorflow_k8s_amd.ops._lib import lib
+    # "nosplit": the picker's tile with the few-tile dgrad split-K off (ops.gemm._dgrad_splitk)
+    variants = {"pick": None, "nosplit": "nosplit", "t256": (256, 256), "t128": (128, 128), "t256x128": (256, 128)}
 
     def timed(fn, tile):
-        G.pick_tile = orig if tile in (None, "g5s") else (lambda *a, **k: tile)
-        if tile == "g5s":
-            lib().g5_set(9)
+        G.pick_tile = orig if tile in (None, "nosplit") else (lambda *a, **k: tile)
+        split_max = G.DGRAD_SPLITK_MAX_TILES
+        if tile == "nosplit":
+            G.DGRAD_SPLITK_MAX_TILES = 0
         try:
             fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -65,7 +66,7 @@ def main():
             return e0.elapsed_time(e1) / args.iters * 1000.0
         finally:
             G.pick_tile = orig
-            lib().g5_set(0)
+            G.DGRAD_SPLITK_MAX_TILES = split_max
 
     jobs = []
     blas = {}

@@ -584,7 +584,9 @@ int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const f
   else return -3;
   if (part) {
     const int NS = dbias ? 3 : 2;
-    hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((NS * W + NT - 1) / NT, LN_PART_GROUPS), dim3(NT), 0, s, part,
+    // one group per <= 8 slabs (every load of a thread in flight at once), at least LN_PART_GROUPS
+    const int groups = std::min(256, std::max(LN_PART_GROUPS, ((int)grid.x + 7) / 8));
+    hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((NS * W + NT - 1) / NT, groups), dim3(NT), 0, s, part,
                        (int)grid.x, NS, W, dgamma, dbeta, dbias);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;

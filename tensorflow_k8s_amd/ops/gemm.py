@@ -300,8 +300,11 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | None =
 # Plain input gradients whose output is too small to fill the chip with 256x256 tiles but whose
 # reduction is long (the tied-logits dgrad: dx[8192][1024] over the 33728-wide vocabulary = 128
 # tiles): split the reduction over the blocks, f32 slabs, one reduce pass writing the bf16 dx.
+# Reductions of 4096 (Transformer-big FFN1's dgrad) run faster unsplit on 128x128 tiles since the
+# K-outer loop stopped waiting for the next stage's DMA (65.8 vs 77.8 us; tools/linear_ab.py,
+# profiles/linear_ab_r5.jsonl); the 33728-long logits reduction still gains (483 vs 576 us).
 DGRAD_SPLITK_MAX_TILES = 192
-DGRAD_SPLITK_MIN_RED = 4096
+DGRAD_SPLITK_MIN_RED = 8192
 
 
 def _dgrad_splitk(dy2, w, dx, M: int, K: int, N: int) -> bool:

@@ -53,6 +53,7 @@ def test_dgrad_splitk_policy():
         assert calls[0][0] == "gemm" and calls[0][1] >= 2 and calls[-1] == "reduce"
         assert not G._dgrad_splitk(None, None, torch.empty(8192, 4096, dtype=torch.bfloat16), 8192, 4096, 1024)
         assert not G._dgrad_splitk(None, None, dx, 8192, 1024, 1024)  # short reduction: one pass
+        assert not G._dgrad_splitk(None, None, dx, 8192, 1024, 4096)  # FFN1's dgrad: unsplit 128x128
     finally:
         G.lib, G._gemm, G.workspace = orig_lib, orig_gemm, orig_ws
 

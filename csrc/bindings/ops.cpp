@@ -36,7 +36,6 @@ void tfk_halo_set(int on);
 void tfk_fp8_set_tile(int t);
 void tfk_g8_set(int on);
 void tfk_g5_set(int waves);
-void tfk_g4_set_shortk_occ(int occ);
 int tfk_bn_finalize(float*, int, int, float, const float*, const float*, float, float, float*, float*, float*, float*,
                     float*, float*, hipStream_t);
 int tfk_bn_stats(const void*, long long, int, float*, int, hipStream_t);
@@ -897,7 +896,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("dropout", &dropout);
   m.def("set_rng_key", &set_rng_key);
   m.def("halo_set", &tfk_halo_set);
-  m.def("g4_set_shortk_occ", &tfk_g4_set_shortk_occ);  // A/B: BN-backward short-K dgrads at 3 or 4 blocks/CU
   m.def("g5_set", &tfk_g5_set);  // 256x256 GEMMs on the mid-tile-barrier engine: 4 / 8 waves, 0 off
   m.def("g8_set", &tfk_g8_set);  // 256x256 dense GEMMs on the 8-phase engine: 1 on, 0 off
   m.def("fp8_set_tile", &tfk_fp8_set_tile);  // fp8 g4 tile: 0 by shape, 128 / 256 forced, -1 -> TFK_FP8_TILE

@@ -20,6 +20,11 @@ enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1, EPI_BF16_BNR = 2, EPI_BF16_EXT = 3, EP
 // Both MX quantizations of the final [rows < BM][cols < BN] bf16 tile in LDS (row stride LDS_S):
 // row blocks of 32 columns -> mx_qr/mx_sr, column pairs of 32-row blocks (one 32-bit LDS word per
 // row holds both columns) -> mx_qc/mx_sc. Same bytes as fp8.hip's mx_quant_dual_kernel.
+// Column pass lane map: each 16-lane group is one 32-row group and 16 column pairs, a wave 4 row
+// groups -- so the 4 consecutive row groups of a column (4 x 32 B of qc = a full 128-B line, 4 scale
+// bytes of sc) go out from one store instruction, while each 32-lane half reads 2 row groups x 16
+// column pairs (2-way bank conflict). Lanes walking columns with one row group per wave wrote 32-B
+// pieces and single scale bytes 8 KiB apart: 31 us of a 93 us FFN1 forward (profiles/perf_log_r5.md).
 template <int BM, int BN, int NT>
 __device__ __forceinline__ void mx_tile_out(const GemmParams& p, const bf16* Cs, int lds_s, int m0, int n0) {
   const int tid = threadIdx.x;
@@ -48,10 +53,12 @@ __device__ __forceinline__ void mx_tile_out(const GemmParams& p, const bf16* Cs,
       sr[(m0 + row) * (N / 32) + n0 / 32 + blk] = (unsigned char)(ex + 127);
     }
   }
-  constexpr int NP = BN / 2, CBLK = NP * (BM / 32);
+  constexpr int NP = BN / 2, RGN = BM / 32, CBLK = NP * RGN;
+  static_assert(RGN % 4 == 0 && NP % 16 == 0 && NT % 64 == 0, "MX column pass: 4 row groups x 16 column pairs per wave");
 #pragma unroll
   for (int k0 = 0; k0 < CBLK; k0 += NT) {
-    const int k = k0 + tid, rg = k / NP, col = 2 * (k - rg * NP);
+    const int k = k0 + tid, q = k >> 6, l = k & 63;
+    const int rg = (q % (RGN / 4)) * 4 + (l >> 4), cp = (q / (RGN / 4)) * 16 + (l & 15), col = 2 * cp;
     if (k < CBLK && col < cols && rg * 32 < rows) {
       unsigned lo[16], hi[16];
 #pragma unroll
@@ -169,6 +176,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   } else {
     constexpr int LDC_S = BN + 8;  // padded bf16 row stride of the LDS C tile
     bf16* Cs = (bf16*)smem;
+    auto cso = [&](int row, int col) { return row * LDC_S + col; };  // element offset in the C tile
     float csum[FN][4], csq[FN][4];
 #pragma unroll
     for (int j = 0; j < FN; ++j)
@@ -194,7 +202,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           csq[j][r] += v * v;
           o[r] = f2bf(v);
         }
-        *(bf16x4*)(Cs + mloc * LDC_S + nloc) = o;
+        *(bf16x4*)(Cs + cso(mloc, nloc)) = o;
       }
     }
     // BN batch statistics (rows >= M were zero-filled -> contribute 0; no bias in conv use):
@@ -277,14 +285,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         for (int g = 0; g < GS; ++g) {
           const int idx = tid + (g0 + g) * NT;
           const int row = idx / CPR, cc = idx - row * CPR;
-          lofs[g] = row * LDC_S + cc * 8;
+          lofs[g] = cso(row, cc * 8);
           const int m = m0 + row, n = n0 + cc * 8;
           long long mo = m, mr = m;
           if constexpr (bnr) { mo = out_row(p, m); mr = resid_row(p, mo); }
           off[g] = bz * p.sC + mo * p.ldc + n;
           rok[g] = p.resid && mr >= 0;
           mlog[g] = m; nlog[g] = n;
-          cv[g] = *(const bf16x8*)(Cs + row * LDC_S + cc * 8);
+          cv[g] = *(const bf16x8*)(Cs + lofs[g]);
           // off the residual's sub-sampling lattice the (unused) load reads C itself: resid is the
           // smaller lattice tensor there, so resid + off[g] could run past its allocation
           if (p.resid) rr[g] = *(const bf16x8*)(rok[g] ? resid_b + bz * p.sC + mr * p.ldc + n : (const bf16*)p.C + off[g]);
@@ -397,7 +405,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       long long mo = m, mr = m;
       if constexpr (bnr) { mo = out_row(p, m); mr = resid_row(p, mo); }
       const bf16* rsrc = (p.resid && mr >= 0) ? (const bf16*)p.resid + bz * p.sC + mr * p.ldc + n : nullptr;
-      bf16x8 v = *(const bf16x8*)(Cs + row * LDC_S + cc * 8);
+      bf16x8 v = *(const bf16x8*)(Cs + cso(row, cc * 8));
       bf16* dst = C + mo * p.ldc + n;
       if (n + 7 < p.N && (p.ldc & 7) == 0) {
         const long long off = bz * p.sC + mo * p.ldc + n;
@@ -461,11 +469,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           }
         }
         if constexpr (mx) {
-          *(bf16x8*)(Cs + row * LDC_S + cc * 8) = v;
+          *(bf16x8*)(Cs + cso(row, cc * 8)) = v;
           if (!p.mx_skip_c) *(bf16x8*)dst = v;
         } else {
           if constexpr (ext) {
-            if (p.colsum) *(bf16x8*)(Cs + row * LDC_S + cc * 8) = v;
+            if (p.colsum) *(bf16x8*)(Cs + cso(row, cc * 8)) = v;
           }
           *(bf16x8*)dst = v;
         }
@@ -491,7 +499,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           if (rsrc) x += bf2f(rsrc[e]);
           dst[e] = f2bf(x);
           if constexpr (ext) {
-            if (p.colsum) Cs[row * LDC_S + cc * 8 + e] = f2bf(x);
+            if (p.colsum) Cs[cso(row, cc * 8 + e)] = f2bf(x);
           }
         }
         if constexpr (ext) {
@@ -514,7 +522,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           const int rg = t / BN, col = t - rg * BN;
           float a = 0.f;
           if (col < cols)
-            for (int r = rg; r < rows; r += RG) a += bf2f(Cs[r * LDC_S + col]);
+            for (int r = rg; r < rows; r += RG) a += bf2f(Cs[cso(r, col)]);
           part[rg * BN + col] = a;
         }
         __syncthreads();

@@ -200,7 +200,7 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
   __syncthreads();
   // BN-reduce chunks in flight per thread by VGPR budget: 512 / (waves per SIMD)
   constexpr int WPS = (NW * OCC) / 4 > 0 ? (NW * OCC) / 4 : 1;
-  gemm_epilogue<BM, BN, NTH, WGM, EPI, (512 / WPS >= 168 ? 4 : 2)>(p, acc, smem, m0, n0, bz);
+  gemm_epilogue<BM, BN, NTH, WGM, EPI, (512 / WPS >= 256 ? 4 : 2)>(p, acc, smem, m0, n0, bz);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -373,16 +373,6 @@ extern "C" int tfk_g4_ok(const GemmParams& p, int amode, int bmode) {
                        dim3(g4::nwaves<128, 128>() * 64), 0, stream, p);                            \
     return hipGetLastError() == hipSuccess ? 0 : -2;                                                \
   }
-// 3 blocks per CU instead of 4 for the BN-backward dgrads: a 168-VGPR budget holds 4 store-pass
-// chunks in flight per thread instead of 2 (A/B: tfk_g4_set_shortk_occ)
-static int g_shortk_occ = 4;
-extern "C" void tfk_g4_set_shortk_occ(int occ) { g_shortk_occ = occ == 3 ? 3 : 4; }
-#define TFK_G4_SHORTK3(AM_, BM2_, EPI_)                                                              \
-  if (g_shortk_occ == 3 && amode == AM_ && bmode == BM2_ && epi == EPI_) {                          \
-    hipLaunchKernelGGL((g4::g4_kernel<128, 128, AM_, BM2_, EPI_, 3>), dim3(tiles, batch, splits),    \
-                       dim3(g4::nwaves<128, 128>() * 64), 0, stream, p);                            \
-    return hipGetLastError() == hipSuccess ? 0 : -2;                                                \
-  }
 
 #ifndef G4_SHORTK_DEFAULT_KT
 #define G4_SHORTK_DEFAULT_KT 8  // measured ResNet-50 bs256: 2 -> 27.42, 4 -> 27.04, 8 -> 26.71, 16 -> 26.67 ms
@@ -442,7 +432,6 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
   // few K-tiles per block: the 4-blocks-per-CU single-stage instantiations (TFK_G4_SHORTK=0: off;
   // one K-tile measured ResNet-50 bs256: 30.40 -> 29.72 ms/step)
   if (p.kt_per_split <= shortk_max_kt() && bm == 128 && bn == 128 && !(amode == 2 && p.Cin < 64)) {
-    TFK_G4_SHORTK3(0, 1, EPI_BF16_BNR)
     TFK_G4_SHORTK(0, 0, EPI_BF16)
     TFK_G4_SHORTK(0, 1, EPI_BF16)
     TFK_G4_SHORTK(0, 1, EPI_BF16_BNR)

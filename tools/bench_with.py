@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """bench.py with native A/B switches applied first: --set NAME=INT calls lib().NAME(INT) (e.g.
-g4_set_shortk_occ=3, g5_set=9) before the model is built; everything else goes to bench.py.
+g5_set=9, g8_set=1, gemm_set_shortk=4) before the model is built; everything else goes to bench.py.
 A/B against plain `bench.py` in the same gpurun session.
 
-    python tools/bench_with.py --set g4_set_shortk_occ=3 --model resnet50 --steps 20 --warmup 5
+    python tools/bench_with.py --set g5_set=9 --model transformer-big --steps 20 --warmup 5
 """
 import argparse
 import os

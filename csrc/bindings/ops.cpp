@@ -99,9 +99,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
           int batch, int64_t sA, int64_t sB, int64_t sC, int64_t split_stride, std::vector<int64_t> conv,
           std::vector<c10::optional<torch::Tensor>> bnr, int bn_relu, int bn_shards, c10::optional<torch::Tensor> aux,
           c10::optional<torch::Tensor> dact_src, int dact, double drop_p, int64_t drop_seed,
-          std::vector<int64_t> rowmap, c10::optional<torch::Tensor> colsum,
-          std::vector<c10::optional<torch::Tensor>> fin, int fin_mode, double fin_count, double fin_eps,
-          double fin_momentum) {
+          std::vector<int64_t> rowmap, c10::optional<torch::Tensor> colsum) {
   need_bf16(A, "A");
   need_bf16(B, "B");
   TORCH_CHECK(epi == 0 || epi == 1, "epi");
@@ -290,40 +288,6 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int M, int N, int K
     }
     p.om_hp = r[0]; p.om_wp = r[1]; p.om_h = r[2]; p.om_w = r[3]; p.om_sh = r[4]; p.om_sw = r[5]; p.om_a = r[6];
     p.om_b = r[7]; p.rs_h = r[8]; p.rs_w = r[9]; p.rs_p = r[10]; p.rs_q = r[11]; p.rs_sh = r[12]; p.rs_sw = r[13];
-  }
-  // BN finalize by the last-arriving workgroup: [ticket, gamma, beta | gamma2, o0..o5] (GemmParams::fin_o)
-  if (!fin.empty()) {
-    TORCH_CHECK(fin.size() == 9, "fin needs 9 entries");
-    TORCH_CHECK(epi == 0 && batch == 1 && splits == 1 && fin_count > 0.0, "BN finalize: bf16 epilogue, batch 1, no split-K");
-    TORCH_CHECK((fin_mode == 1 && p.stats) || (fin_mode == 2 && p.bn_sums), "BN finalize mode 1 needs stats, 2 the BN reduce");
-    TORCH_CHECK(fin[0].has_value() && fin[0]->defined() && fin[0]->scalar_type() == at::kInt && fin[0]->is_cuda() &&
-                    fin[0]->numel() >= (tfk::FIN_GROUPS + 1) * tfk::FIN_LINE, "fin ticket: int32 device tensor of ",
-                (tfk::FIN_GROUPS + 1) * tfk::FIN_LINE, " (zeroed) counters");
-    TORCH_CHECK((fin_mode == 1 ? shards : bn_shards) <= tfk::FIN_MAX_SHARDS, "fin: at most ", tfk::FIN_MAX_SHARDS,
-                " shards");
-    const bool dual = fin_mode == 2 && p.bn_y2;
-    for (int i = 1; i < 9; ++i) {
-      // fwd: gamma beta | mean invstd scale shift [run_mean run_var]; bwd: gamma [gamma2] |
-      // dgamma dbeta coef [dgamma2 dbeta2 coef2] (exactly with a second BN)
-      const bool req = i <= 2 ? (i == 1 || fin_mode == 1 || dual) : i <= 5 ? true : (fin_mode == 1 ? i == 6 : dual);
-      const bool has = fin[i].has_value() && fin[i]->defined();
-      TORCH_CHECK(has || !req, "fin entry ", i, " missing");
-      if (!has) continue;
-      need_f32(*fin[i], "fin vec");
-      need_numel(*fin[i], (fin_mode == 2 && (i == 5 || i == 8)) ? 3LL * N : N, "fin vec");
-    }
-    TORCH_CHECK(fin_mode == 2 || (fin[7].has_value() && fin[7]->defined()) == (fin[8].has_value() && fin[8]->defined()),
-                "fin: running mean and variance together");
-    TORCH_CHECK(fin_mode == 1 || !dual || (p.bn_mean2 && p.bn_invstd2), "fin: dual BN needs mean2/invstd2");
-    TORCH_CHECK(fin_mode == 1 || (fin[8].has_value() && fin[8]->defined()) == dual, "fin: coef2 exactly with bn_y2");
-    p.fin_ticket = fin[0]->data_ptr<int>();
-    p.fin_mode = fin_mode;
-    p.fin_count = (float)fin_count;
-    p.fin_eps = (float)fin_eps;
-    p.fin_momentum = (float)fin_momentum;
-    p.fin_gamma = fin[1]->data_ptr<float>();
-    p.fin_beta = opt_ptr<const float>(fin[2]);
-    for (int i = 0; i < 6; ++i) p.fin_o[i] = opt_ptr<float>(fin[3 + i]);
   }
   check_rc(tfk_gemm_launch(p, bm, bn, amode, bmode, epi, batch, splits, cur_stream()), "gemm");
 }

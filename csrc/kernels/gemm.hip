@@ -445,23 +445,6 @@ static int engine() {
 }
 extern "C" void tfk_gemm_set_engine(int e) { g_pp = e; }
 
-extern "C" int tfk_bn_finalize(float*, int, int, float, const float*, const float*, float, float, float*, float*,
-                               float*, float*, float*, float*, hipStream_t);
-extern "C" int tfk_bn_bwd_finalize(float*, int, int, float, const float*, const float*, const float*, const float*,
-                                   const float*, const float*, float*, float*, float*, float*, float*, float*,
-                                   hipStream_t);
-
-// The BN finalize a GemmParams::fin_* descriptor asks for, as its own launch (engines that do not
-// run each tile in exactly one workgroup).
-static int fin_separately(const GemmParams& p, hipStream_t s) {
-  if (p.fin_mode == 1)
-    return tfk_bn_finalize(p.stats, p.stats_shards, p.N, p.fin_count, p.fin_gamma, p.fin_beta, p.fin_eps,
-                           p.fin_momentum, p.fin_o[4], p.fin_o[5], p.fin_o[0], p.fin_o[1], p.fin_o[2], p.fin_o[3], s);
-  return tfk_bn_bwd_finalize(p.bn_sums, p.bn_shards, p.N, p.fin_count, p.fin_gamma, p.bn_mean, p.bn_invstd,
-                             p.fin_beta, p.bn_mean2, p.bn_invstd2, p.fin_o[0], p.fin_o[1], p.fin_o[3], p.fin_o[4],
-                             p.fin_o[2], p.fin_o[5], s);
-}
-
 // Host launcher. Grid: x = tiles (M x N), y = batch, z = split-K. Returns 0 on success.
 // Register-staged engine: every instantiated (tile, operand modes, epilogue). -1 if absent.
 static int launch_reg(GemmParams p, int bm, int bn, int amode, int bmode, int epi, int batch, int splits,
@@ -518,14 +501,11 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
     }
   }
   // requested tile, else the 128x128 / 128x64 / 64x64 tiles every combination instantiates at
-  // least one of (the register engine's tile walk may split a tile: BN finalize as its own launch)
-  GemmParams q = p;
-  q.fin_ticket = nullptr;
-  int r = launch_reg(q, bm, bn, amode, bmode, epi, batch, splits, stream);
+  // least one of
+  int r = launch_reg(p, bm, bn, amode, bmode, epi, batch, splits, stream);
   const int fb[3][2] = {{128, 128}, {128, 64}, {64, 64}};
   for (int i = 0; i < 3 && r == -1; ++i)
-    if (!(bm == fb[i][0] && bn == fb[i][1])) r = launch_reg(q, fb[i][0], fb[i][1], amode, bmode, epi, batch, splits, stream);
-  if (r == 0 && p.fin_ticket) r = fin_separately(p, stream);
+    if (!(bm == fb[i][0] && bn == fb[i][1])) r = launch_reg(p, fb[i][0], fb[i][1], amode, bmode, epi, batch, splits, stream);
   return r;
 }
 

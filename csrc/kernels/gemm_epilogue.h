@@ -132,93 +132,6 @@ __device__ __forceinline__ long long resid_row(const GemmParams& p, long long mo
 // QUAD: the 8-phase engine's wave layout (gemm_g8.hip): wave (wm, wn) owns the four quadrant
 // sub-tiles rows {q*BM/2 + wm*64 + [0,64)} x cols {q'*BN/2 + wn*32 + [0,32)}; row fragment i covers
 // rows (i>>2)*BM/2 + wm*64 + (i&3)*16, column fragment j cols (j>>1)*BN/2 + wn*32 + (j&1)*16.
-// Last-arriver BatchNorm finalize (GemmParams::fin_*), at the very end of the epilogue. The
-// statistics were added by memory-side float atomics: once every wave's adds are performed
-// (s_waitcnt vmcnt(0)) and the workgroup has met, ONE lane takes an agent-scope ticket -- first in
-// its group's counter (workgroup id % FIN_GROUPS, each counter on its own 128-B line: one word
-// serialises ~88 adds/us, and a wave of finishing workgroups would queue on it), then the group's
-// last arriver in the top counter. The workgroup drawing the final top ticket reads every shard
-// with agent-scope (sc1) loads -- no L1/L2 copy can be stale -- all of a thread's shard loads in
-// flight at once (one memory round trip for C <= NT; the host fuses only such layers), writes the
-// per-channel outputs, and re-zeroes the shards (sc1 stores) and the counters it drew last.
-// Same arithmetic as bn.hip's bn_finalize_kernel / bn_bwd_finalize_kernel. flag: one LDS word of
-// the epilogue's tile space (a second __shared__ object would perturb the main loop's waits).
-template <int NT>
-__device__ __forceinline__ void bn_fin_tail(const GemmParams& p, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int nb = (int)(gridDim.x * gridDim.y * gridDim.z);
-    const int bid = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
-    const int grp = bid % FIN_GROUPS, gsz = (nb - grp + FIN_GROUPS - 1) / FIN_GROUPS, ng = min(nb, FIN_GROUPS);
-    int last = 0;
-    int* gc = p.fin_ticket + grp * FIN_LINE;
-    if (__hip_atomic_fetch_add(gc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsz - 1) {
-      __hip_atomic_store(gc, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int* top = p.fin_ticket + FIN_GROUPS * FIN_LINE;
-      last = __hip_atomic_fetch_add(top, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
-      if (last) __hip_atomic_store(top, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (*flag == 0) return;  // workgroup-uniform
-  const bool fwd = p.fin_mode == 1;
-  const int C = p.N, S = fwd ? p.stats_shards : p.bn_shards, NV = fwd ? 2 : 3;
-  float* buf = fwd ? p.stats : p.bn_sums;
-  const float cnt = p.fin_count;
-  for (int c = threadIdx.x; c < C; c += NT) {
-    float x[FIN_MAX_SHARDS][3];
-#pragma unroll
-    for (int k = 0; k < FIN_MAX_SHARDS; ++k) {  // every shard's loads issued before any is used
-      const float* sh = buf + (long long)min(k, S - 1) * NV * C + c;
-#pragma unroll
-      for (int w = 0; w < 3; ++w)
-        x[k][w] = __hip_atomic_load(sh + min(w, NV - 1) * C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    float v[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < FIN_MAX_SHARDS; ++k)
-#pragma unroll
-      for (int w = 0; w < 3; ++w) v[w] += k < S ? x[k][w] : 0.f;
-    for (int k = 0; k < S; ++k)
-      for (int w = 0; w < NV; ++w)
-        __hip_atomic_store(buf + ((long long)k * NV + w) * C + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (fwd) {
-      const double mean = (double)v[0] / cnt;
-      double var = (double)v[1] / cnt - mean * mean;
-      if (var < 0) var = 0;
-      const float inv = rsqrtf((float)var + p.fin_eps), g = p.fin_gamma[c], b = p.fin_beta[c];
-      p.fin_o[0][c] = (float)mean;
-      p.fin_o[1][c] = inv;
-      p.fin_o[2][c] = g * inv;
-      p.fin_o[3][c] = b - (float)mean * g * inv;
-      if (p.fin_o[4]) {
-        const float unb = cnt > 1.f ? (float)var * cnt / (cnt - 1.f) : (float)var, mo = p.fin_momentum;
-        p.fin_o[4][c] = (1.f - mo) * p.fin_o[4][c] + mo * (float)mean;
-        p.fin_o[5][c] = (1.f - mo) * p.fin_o[5][c] + mo * unb;
-      }
-    } else {
-      p.fin_o[0][c] = v[1];
-      p.fin_o[1][c] = v[0];
-      {
-        const float inv = p.bn_invstd[c], k1 = p.fin_gamma[c] * inv, k3 = v[1] / cnt;
-        p.fin_o[2][c] = k1;
-        p.fin_o[2][C + c] = -k1 * k3 * inv;
-        p.fin_o[2][2 * C + c] = k1 * (k3 * inv * p.bn_mean[c] - v[0] / cnt);
-      }
-      if (p.fin_o[5]) {
-        p.fin_o[3][c] = v[2];
-        p.fin_o[4][c] = v[0];
-        const float inv = p.bn_invstd2[c], k1 = p.fin_beta[c] * inv, k3 = v[2] / cnt;
-        p.fin_o[5][c] = k1;
-        p.fin_o[5][C + c] = -k1 * k3 * inv;
-        p.fin_o[5][2 * C + c] = k1 * (k3 * inv * p.bn_mean2[c] - v[0] / cnt);
-      }
-    }
-  }
-}
-
 template <int BM, int BN, int NT, int WM, int EPI, int BNRG = 0, bool DRAIN = false, bool QUAD = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[BM / WM / 16][BN / (NT / 64 / WM) / 16],
                                               char* smem, int m0, int n0, int bz) {
@@ -664,10 +577,6 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         atomicAdd(st + which * p.N + n, v);
       }
     }
-    // only the engines that run each tile in one workgroup (they instantiate with BNRG; the
-    // register engine and fp8.hip do not, and would spill with the tail compiled in)
-    if constexpr (BNRG != 0)
-      if (p.fin_ticket) bn_fin_tail<NT>(p, (int*)smem);
   }
 }
 

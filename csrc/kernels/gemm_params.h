@@ -2,9 +2,6 @@
 // device code and the host bindings so the layout can never drift.
 #pragma once
 namespace tfk {
-// BN-finalize tickets (GemmParams::fin_ticket): [FIN_GROUPS + 1][FIN_LINE] int32, group counters
-// then the top counter, each on its own 128-B line; statistics shards read per thread at once
-constexpr int FIN_GROUPS = 8, FIN_LINE = 32, FIN_MAX_SHARDS = 16;
 struct GemmParams {
   const void* A;
   const void* B;
@@ -85,17 +82,5 @@ struct GemmParams {
   void* mx_qc;
   void* mx_sc;
   int mx_skip_c;
-  // Last-arriver BatchNorm finalize (gemm_epilogue.h bn_fin_tail): the workgroup that draws the
-  // final ticket reduces the statistics shards this GEMM's epilogues just accumulated -- no separate
-  // finalize launch between the conv and its BN apply. fin_mode 1 (forward, stats): mean, invstd,
-  // scale, shift and the running statistics; 2 (backward, bn_sums): dgamma, dbeta, coef and, with
-  // a second BN (bn_y2), its dgamma2, dbeta2, coef2. Only set for engines that run each output tile
-  // in exactly one workgroup (g4 / halo); tfk_gemm_launch finalizes separately otherwise.
-  int* fin_ticket;       // arrival counter, 0 at rest (the last arriver re-zeroes it); null: none
-  int fin_mode;
-  float fin_count, fin_eps, fin_momentum;
-  const float* fin_gamma;
-  const float* fin_beta;  // forward: beta; backward: gamma2
-  float* fin_o[6];        // fwd: mean invstd scale shift run_mean run_var; bwd: dgamma dbeta coef dgamma2 dbeta2 coef2
 };
 }  // namespace tfk

@@ -8,8 +8,6 @@ fc1000) so checkpoints line up with TF-era tooling.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from ..ops import norm as BN
@@ -25,10 +23,6 @@ SIDE_SHORTCUT = True
 # BN-backward apply then reads no mask and an identity block's residual gradient is dz itself (no
 # second output pass).
 PREMASK = True
-# each BN's finalize (forward statistics, backward sums) runs in the last workgroup of the GEMM that
-# produced them (ops.norm.BNFinalize) instead of as its own launch between the GEMM and its consumer
-_FF = os.environ.get("TFK_BN_FUSE_FIN", "1")  # 1 both, 0 none, fwd / bwd (A/B)
-FUSE_FIN_FWD, FUSE_FIN_BWD = _FF in ("1", "fwd"), _FF in ("1", "bwd")
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
 
@@ -62,28 +56,28 @@ class Bottleneck:
             ssc = self.bn_sc.state(dev)
 
             def shortcut():
-                ysc = self.conv_sc.forward(x, ssc if training else None, bn=self._fin(self.bn_sc, training))
-                if training and not FUSE_FIN_FWD:
+                ysc = self.conv_sc.forward(x, ssc if training else None)
+                if training:
                     self.bn_sc.finalize(ysc.numel() // ysc.shape[-1])
                 sc.append(ysc)
             streams.run_wgrad(shortcut, x)
-        y1 = self.conv1.forward(x, s1 if training else None, bn=self._fin(self.bn1, training))
-        if training and not FUSE_FIN_FWD:
+        y1 = self.conv1.forward(x, s1 if training else None)
+        if training:
             self.bn1.finalize(y1.numel() // y1.shape[-1])
         a1 = BN.bn_apply(y1, s1, relu=True)
-        y2 = self.conv2.forward(a1, s2 if training else None, bn=self._fin(self.bn2, training))
-        if training and not FUSE_FIN_FWD:
+        y2 = self.conv2.forward(a1, s2 if training else None)
+        if training:
             self.bn2.finalize(y2.numel() // y2.shape[-1])
         a2 = BN.bn_apply(y2, s2, relu=True)
-        y3 = self.conv3.forward(a2, s3 if training else None, bn=self._fin(self.bn3, training))
-        if training and not FUSE_FIN_FWD:
+        y3 = self.conv3.forward(a2, s3 if training else None)
+        if training:
             self.bn3.finalize(y3.numel() // y3.shape[-1])
         ysc = None
         if self.proj:
             if not SIDE_SHORTCUT:
                 ssc = self.bn_sc.state(dev)
-                ysc = self.conv_sc.forward(x, ssc if training else None, bn=self._fin(self.bn_sc, training))
-                if training and not FUSE_FIN_FWD:
+                ysc = self.conv_sc.forward(x, ssc if training else None)
+                if training:
                     self.bn_sc.finalize(ysc.numel() // ysc.shape[-1])
                 sc.append(ysc)
             streams.sync()
@@ -98,18 +92,11 @@ class Bottleneck:
             self.saved = (x, y1, a1, y2, a2, y3, ysc, mk)
         return out
 
-    @staticmethod
-    def _fin(bn: BatchNorm, training: bool):
-        return bn if (training and FUSE_FIN_FWD) else None
-
     def tail_reduce(self) -> BN.BNReduce:
         """BN-backward reduction spec of this block's tail (relu(bn3(y3) + shortcut)); fused into
-        the epilogue of the NEXT block's final dgrad, which produces this block's dout (and, with
-        FUSE_FIN_BWD, finalizes it)."""
+        the epilogue of the NEXT block's final dgrad, which produces this block's dout."""
         x, y1, a1, y2, a2, y3, ysc, mk = self.saved
-        fin = self.bn3.fin_backward(y3.numel() // y3.shape[-1], self.bn_sc if self.proj else None) if FUSE_FIN_BWD else None
-        return BN.BNReduce(y3, self.bn3.st, a=mk, y2=ysc, st2=self.bn_sc.st if self.proj else None, premask=PREMASK,
-                           fin=fin)
+        return BN.BNReduce(y3, self.bn3.st, a=mk, y2=ysc, st2=self.bn_sc.st if self.proj else None, premask=PREMASK)
 
     def backward(self, dout, need_dx=True, dout_reduced=False, next_bnr: BN.BNReduce | None = None):
         """dout_reduced: the producer of dout already accumulated this block's tail BN sums.
@@ -122,13 +109,13 @@ class Bottleneck:
                                           self.bn3.beta.grad, cnt3, y2=ysc, st2=self.bn_sc.st,
                                           gamma2=self.bn_sc.gamma.master, dgamma2=self.bn_sc.gamma.grad,
                                           dbeta2=self.bn_sc.beta.grad, reduced=dout_reduced,
-                                          premasked=dout_reduced and PREMASK, finalized=dout_reduced and FUSE_FIN_BWD)
+                                          premasked=dout_reduced and PREMASK)
             dres = None
             self.arena.grad_ready(self.bn3.gamma, self.bn3.beta, self.bn_sc.gamma, self.bn_sc.beta)
         else:
             dy3, _, dres = BN.bn_backward(dout, mk, y3, self.bn3.st, self.bn3.gamma.master, self.bn3.gamma.grad,
                                           self.bn3.beta.grad, cnt3, want_dres=True, reduced=dout_reduced,
-                                          premasked=dout_reduced and PREMASK, finalized=dout_reduced and FUSE_FIN_BWD)
+                                          premasked=dout_reduced and PREMASK)
             self.arena.grad_ready(self.bn3.gamma, self.bn3.beta)
         lattice = self.proj and self.stride > 1 and need_dx and next_bnr is not None
         tl = []
@@ -137,18 +124,15 @@ class Bottleneck:
             # conv3 -> conv2 chain, joined before conv1's dgrad epilogue adds it
             streams.run_wgrad(lambda: tl.append(self.conv_sc.lattice_dgrad(dysc, x)), dysc, x)
         # bn2/bn1 have no residual input: relu mask recomputed from y, sums fused into the dgrad epilogue
-        cnt2, cnt1 = y2.numel() // y2.shape[-1], y1.numel() // y1.shape[-1]
-        fin2 = self.bn2.fin_backward(cnt2) if FUSE_FIN_BWD else None
-        da2 = self.conv3.backward(dy3, a2, bnr=BN.BNReduce(y2, self.bn2.st, premask=PREMASK, fin=fin2))
+        da2 = self.conv3.backward(dy3, a2, bnr=BN.BNReduce(y2, self.bn2.st, premask=PREMASK))
         dy2, _, _ = BN.bn_backward(da2, None, y2, self.bn2.st, self.bn2.gamma.master, self.bn2.gamma.grad,
-                                   self.bn2.beta.grad, cnt2, relu_from_y=True, reduced=True,
-                                   premasked=PREMASK, finalized=FUSE_FIN_BWD)
+                                   self.bn2.beta.grad, y2.numel() // y2.shape[-1], relu_from_y=True, reduced=True,
+                                   premasked=PREMASK)
         self.arena.grad_ready(self.bn2.gamma, self.bn2.beta)
-        fin1 = self.bn1.fin_backward(cnt1) if FUSE_FIN_BWD else None
-        da1 = self.conv2.backward(dy2, a1, bnr=BN.BNReduce(y1, self.bn1.st, premask=PREMASK, fin=fin1))
+        da1 = self.conv2.backward(dy2, a1, bnr=BN.BNReduce(y1, self.bn1.st, premask=PREMASK))
         dy1, _, _ = BN.bn_backward(da1, None, y1, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
-                                   self.bn1.beta.grad, cnt1, relu_from_y=True, reduced=True,
-                                   premasked=PREMASK, finalized=FUSE_FIN_BWD)
+                                   self.bn1.beta.grad, y1.numel() // y1.shape[-1], relu_from_y=True, reduced=True,
+                                   premasked=PREMASK)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
         if lattice:
             # strided projection: its dgrad only touches the stride lattice -> a dense GEMM over the
@@ -214,10 +198,9 @@ class ResNet:
     def _features(self, x):
         dev = x.device
         st = self.bn1.state(dev)
-        y0 = self.conv1.forward(x, st if self.training else None, bn=Bottleneck._fin(self.bn1, self.training))
+        y0 = self.conv1.forward(x, st if self.training else None)
         if self.training:
-            if not FUSE_FIN_FWD:
-                self.bn1.finalize(y0.numel() // y0.shape[-1])
+            self.bn1.finalize(y0.numel() // y0.shape[-1])
         else:
             self._eval_stats()
         a0 = BN.bn_apply(y0, st, relu=True)

@@ -161,15 +161,12 @@ def pick_splits(tiles: int, K: int, min_ktiles: int | None = None, target: int |
 
 def _gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile, *, alpha=1.0, beta=0.0, bias=None, resid=None,
           act=0, stats=None, shards=1, splits=1, batch=1, sA=0, sB=0, sC=0, split_stride=0, conv=NO_CONV, bnr=None,
-          aux=None, dact_src=None, dact=0, drop_p=0.0, drop_seed=0, rowmap=(), colsum=None, fin=None):
-    """fin: BNFinalize.gemm_args() -- the BN finalize run by the GEMM's last-arriving workgroup."""
-    fin_t, fin_mode, fin_cnt, fin_eps, fin_mom = fin if fin is not None else ([], 0, 0.0, 0.0, 0.0)
+          aux=None, dact_src=None, dact=0, drop_p=0.0, drop_seed=0, rowmap=(), colsum=None):
     lib().gemm(A, B, C, M, N, K, lda, ldb, ldc, amode, bmode, epi, tile[0], tile[1], alpha, beta, bias, resid, act,
                stats, shards, splits, batch, sA, sB, sC, split_stride, conv,
                bnr.gemm_args() if bnr is not None else [],
                (int(bnr.relu) | (2 if bnr.premask else 0)) if bnr is not None else 0,
-               bnr.st.shards if bnr is not None else 1, aux, dact_src, dact, drop_p, drop_seed, list(rowmap), colsum,
-               fin_t, fin_mode, fin_cnt, fin_eps, fin_mom)
+               bnr.st.shards if bnr is not None else 1, aux, dact_src, dact, drop_p, drop_seed, list(rowmap), colsum)
 
 
 def _f32_out_splitk(run, M: int, N: int, K: int, tiles: int, out: torch.Tensor, accumulate: bool, device,
@@ -459,15 +456,10 @@ def stem_fwd_ok(g: ConvGeom, cin_used: int | None) -> bool:
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor | None = None,
              shards: int = 1, bias: torch.Tensor | None = None, act: str | None = None,
-             cin_used: int | None = None, fin=None) -> torch.Tensor:
+             cin_used: int | None = None) -> torch.Tensor:
     """y[N,P,Q,K] = act(conv(x[N,H,W,C], w[K,R,S,C]) + bias); optionally accumulates BN batch
     statistics (sum, sumsq per output channel) of the f32 result into stats[shards][2][K].
-    cin_used: input channels that may be nonzero (the rest are zero padding).
-    fin (ops.norm.BNFinalize, forward, over ``stats``): that BN's finalize, by the GEMM's last
-    workgroup where the engine allows, else right after the conv."""
-    if fin is not None and stats is None:
-        raise ValueError("conv_fwd: fin finalizes the statistics of this conv (stats=...)")
-    M = g.N * g.P * g.Q
+    cin_used: input channels that may be nonzero (the rest are zero padding)."""
     if not on_gpu(x):
         y = _ref_conv(x, w, g)
         if bias is not None:
@@ -477,28 +469,22 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, g: ConvGeom, stats: torch.Tensor 
             yf = y.reshape(-1, g.K)
             stats.view(shards, 2, g.K)[0, 0] += yf.sum(0)
             stats.view(shards, 2, g.K)[0, 1] += (yf * yf).sum(0)
-        if fin is not None:
-            fin.run(M)
         return y.to(torch.bfloat16).contiguous()
+    M = g.N * g.P * g.Q
     y = torch.empty(g.N, g.P, g.Q, g.K, dtype=torch.bfloat16, device=x.device)
     if bias is None and act is None and stem_fwd_ok(g, cin_used):
         lib().stem_fwd(x, w, y, stats, shards)
-        if fin is not None:
-            fin.run(M)
         return y
-    fa = fin.gemm_args(M) if (fin is not None and fin.fusable()) else None
     tile = _conv_tile("fwd", g, lambda: pick_tile(M, g.K, big_ok=g.pointwise, K=g.R * g.S * g.C, mid_ok=g.pointwise,
                                                   g4=g.pointwise or g.C % 64 == 0 or (g.C % 8 == 0 and g.C < 64)),
                       (stats is not None, bias is not None, act is not None))
     if g.pointwise:
         _gemm(x, w, y, M, g.K, g.C, g.C, g.C, g.K, A_KIN, B_KIN, EPI_BF16, tile, stats=stats, shards=shards,
-              bias=bias, act=ACT[act], fin=fa)
+              bias=bias, act=ACT[act])
     else:
         Kd = g.R * g.S * g.C
         _gemm(x, w, y, M, g.K, Kd, 0, Kd, g.K, A_CONV_FWD, B_KIN, EPI_BF16, tile, stats=stats, shards=shards,
-              conv=g.vec(), bias=bias, act=ACT[act], fin=fa)
-    if fin is not None and fa is None:
-        fin.run(M)
+              conv=g.vec(), bias=bias, act=ACT[act])
     return y
 
 
@@ -614,18 +600,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, g: ConvGeom, resid: torch.Tens
             dz = bnr.reference_accumulate(dx)
             if bnr.premask:
                 dx = dz.to(torch.bfloat16).reshape(dx.shape).contiguous()
-            if bnr.fin is not None:
-                bnr.fin.run()
         return dx
-    fin = bnr.fin if bnr is not None else None
-    fa = fin.gemm_args() if (fin is not None and fin.fusable()) else None
-    dx = _conv_dgrad_gpu(dy, w, g, resid, wt, bnr, resid_stride, fa)
-    if fin is not None and fa is None:
-        fin.run()
-    return dx
-
-
-def _conv_dgrad_gpu(dy, w, g: ConvGeom, resid, wt, bnr, resid_stride: int, fa):
     M = g.N * g.H * g.W
     dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
     def _default_tile():
@@ -639,10 +614,10 @@ def _conv_dgrad_gpu(dy, w, g: ConvGeom, resid, wt, bnr, resid_stride: int, fa):
         s = resid_stride
         rmap = [0] * 8 + [g.H, g.W, -(-g.H // s), -(-g.W // s), s, s]
         _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid, bnr=bnr,
-              rowmap=rmap, fin=fa)
+              rowmap=rmap)
         return dx
     if g.pointwise:
-        _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid, bnr=bnr, fin=fa)
+        _gemm(dy, w, dx, M, g.C, g.K, g.K, g.C, g.C, A_KIN, B_KOUT, EPI_BF16, tile, resid=resid, bnr=bnr)
         return dx
     f = dgrad_as_fwd_geom(g) if (DGRAD_AS_FWD and G4_ENABLED and g.K % 64 == 0 and g.C % 8 == 0) else None
     if f is not None and g.C < DGRAD_AS_FWD_MIN_C and not halo_ok(f):
@@ -652,14 +627,13 @@ def _conv_dgrad_gpu(dy, w, g: ConvGeom, resid, wt, bnr, resid_stride: int, fa):
         Kd = g.R * g.S * g.K
         _gemm(dy, wf, dx, M, g.C, Kd, 0, Kd, g.C, A_CONV_FWD, B_KIN, EPI_BF16,
               _conv_tile("dgrad_fwd", g, lambda: pick_tile(M, g.C, K=Kd, mid_ok=False, g4=True), flags),
-              resid=resid, conv=f.vec(), bnr=bnr, fin=fa)
+              resid=resid, conv=f.vec(), bnr=bnr)
         return dx
     phases = _phases(g) if (bnr is not None and (g.sh > 1 or g.sw > 1)) else None
     if phases is not None:
         wt = wt if wt is not None else conv_weight_t(w, g)
         as_fwd = PHASES_AS_FWD and G4_ENABLED and g.K % 64 == 0
-        for pi, (a, b, Ha, Wb, r0, s0, Rp, Sp, php, pwp) in enumerate(phases):
-            pfa = fa if pi == len(phases) - 1 else None  # the sums are complete after the last phase
+        for a, b, Ha, Wb, r0, s0, Rp, Sp, php, pwp in phases:
             wp = wt[:, r0::g.sh, s0::g.sw, :]  # [C][Rp][Sp][K] sub-kernel (weights only)
             Mp, Kd = g.N * Ha * Wb, Rp * Sp * g.K
             rmap = [Ha, Wb, g.H, g.W, g.sh, g.sw, a, b] + [0] * 6
@@ -668,22 +642,21 @@ def _conv_dgrad_gpu(dy, w, g: ConvGeom, resid, wt, bnr, resid_stride: int, fa):
                 # on the LDS-DMA gather; GEMM rows walk the phase grid, the out-map scatters them
                 conv = [g.N, g.P, g.Q, g.K, Ha, Wb, g.C, Rp, Sp, 1, 1, Rp - 1 - php, Sp - 1 - pwp, 1, 1]
                 _gemm(dy, wp.flip(1, 2).contiguous(), dx, Mp, g.C, Kd, 0, Kd, g.C, A_CONV_FWD, B_KIN, EPI_BF16,
-                      pick_tile(Mp, g.C, K=Kd, mid_ok=False, g4=True), resid=resid, conv=conv, bnr=bnr, rowmap=rmap,
-                      fin=pfa)
+                      pick_tile(Mp, g.C, K=Kd, mid_ok=False, g4=True), resid=resid, conv=conv, bnr=bnr, rowmap=rmap)
             else:
                 conv = [g.N, Ha, Wb, g.C, g.P, g.Q, g.K, Rp, Sp, 1, 1, php, pwp, 1, 1]
                 _gemm(dy, wp.contiguous(), dx, Mp, g.C, Kd, 0, Kd, g.C, A_CONV_DGRAD, B_KIN, EPI_BF16,
-                      pick_tile(Mp, g.C, K=Kd, mid_ok=False), resid=resid, conv=conv, bnr=bnr, rowmap=rmap, fin=pfa)
+                      pick_tile(Mp, g.C, K=Kd, mid_ok=False), resid=resid, conv=conv, bnr=bnr, rowmap=rmap)
         return dx
     if g.R == 1 and g.S == 1:
         # strided 1x1: B(n=c, k=co) = W[co][c] is K-outer with ldb = C; gather handles the stride
         _gemm(dy, w, dx, M, g.C, g.K, 0, g.C, g.C, A_CONV_DGRAD, B_KOUT, EPI_BF16, tile, resid=resid,
-              conv=g.vec(), bnr=bnr, fin=fa)
+              conv=g.vec(), bnr=bnr)
     else:
         wt = wt if wt is not None else conv_weight_t(w, g)
         Kd = g.R * g.S * g.K
         _gemm(dy, wt, dx, M, g.C, Kd, 0, Kd, g.C, A_CONV_DGRAD, B_KIN, EPI_BF16, tile, resid=resid, conv=g.vec(),
-              bnr=bnr, fin=fa)
+              bnr=bnr)
     return dx
 
 

@@ -16,12 +16,6 @@ from ._lib import lib, on_gpu
 # (ResNet-50 bs256 step, same box): 8 -> 25.21, 12 -> 25.33, 16 -> 25.15-25.19, 32 -> 25.25-25.41,
 # 64 -> 25.70 ms -- the finalize kernels sit on the critical path and read every shard
 SHARDS = 16
-# BNFinalize in the producing GEMM (gemm_params.h FIN_*): ticket words, and the widest layer fused
-# -- the last workgroup reads every shard of C channels, one channel per thread: beyond its
-# 256 threads the reads take several memory round trips, slower than the separate 64-channel-per-
-# block finalize kernel (tested at up to 2048 channels in one tail: ResNet-50 step 21.85 -> 22.7 ms)
-FIN_TICKET_WORDS = 9 * 32
-FIN_MAX_C = 256
 
 
 class BNState:
@@ -37,8 +31,6 @@ class BNState:
         self.scale = torch.ones(C, dtype=torch.float32, device=device)
         self.shift = torch.zeros(C, dtype=torch.float32, device=device)
         self.coef = torch.zeros(3 * C, dtype=torch.float32, device=device)
-        # arrival counter of the producing GEMM's fused finalize (BNFinalize); 0 at rest
-        self.ticket = torch.zeros(FIN_TICKET_WORDS, dtype=torch.int32, device=device)
 
 
 def bn_finalize(st: BNState, count: float, gamma, beta, eps, momentum, run_mean, run_var) -> None:
@@ -58,54 +50,6 @@ def bn_finalize(st: BNState, count: float, gamma, beta, eps, momentum, run_mean,
         return
     lib().bn_finalize(st.stats, st.shards, C, float(count), gamma, beta, eps, momentum, run_mean, run_var, st.mean,
                       st.invstd, st.scale, st.shift)
-
-
-class BNFinalize:
-    """A BN finalize fused into the GEMM that produces its input (GemmParams::fin_*,
-    gemm_epilogue.h bn_fin_tail): the GEMM's last-arriving workgroup reduces the shards its
-    epilogues just accumulated, so no finalize launch sits between the GEMM and the consumer.
-
-    forward (mode 1): stats -> mean, invstd, scale, shift and the running statistics (bn_finalize);
-    backward (mode 2, beside a BNReduce): sums -> dgamma, dbeta, coef [+ the projection BN's]
-    (bn_bwd_finalize). Engines without a one-workgroup-per-tile grid, the stem kernel and the CPU
-    path run the same finalize as its own step (``run``)."""
-
-    def __init__(self, st: BNState, gamma, *, beta=None, eps: float = 0.0, momentum: float = 0.0, run_mean=None,
-                 run_var=None, dgamma=None, dbeta=None, st2: BNState | None = None, gamma2=None, dgamma2=None,
-                 dbeta2=None, count: float = 0.0):
-        self.mode = 1 if dgamma is None else 2
-        self.st, self.gamma, self.beta, self.eps, self.momentum = st, gamma, beta, eps, momentum
-        self.run_mean, self.run_var = run_mean, run_var
-        self.dgamma, self.dbeta, self.st2, self.gamma2, self.dgamma2, self.dbeta2 = dgamma, dbeta, st2, gamma2, dgamma2, dbeta2
-        self.count = float(count)
-
-    def fusable(self) -> bool:
-        """Whether the producing GEMM takes this finalize (else it runs as its own launch)."""
-        return self.st.C <= FIN_MAX_C and self.st.shards <= 16
-
-    def gemm_args(self, count: float | None = None):
-        """(tensors, mode, count, eps, momentum) of the gemm binding's fin arguments."""
-        st, cnt = self.st, float(count if count is not None else self.count)
-        if self.mode == 1:
-            t = [st.ticket, self.gamma, self.beta, st.mean, st.invstd, st.scale, st.shift, self.run_mean, self.run_var]
-        else:
-            st2 = self.st2
-            t = [st.ticket, self.gamma, self.gamma2 if st2 else None, self.dgamma, self.dbeta, st.coef,
-                 self.dgamma2 if st2 else None, self.dbeta2 if st2 else None, st2.coef if st2 else None]
-        return t, self.mode, cnt, float(self.eps), float(self.momentum)
-
-    def run(self, count: float | None = None) -> None:
-        """The same finalize as a separate step."""
-        cnt = float(count if count is not None else self.count)
-        if self.mode == 1:
-            bn_finalize(self.st, cnt, self.gamma, self.beta, self.eps, self.momentum, self.run_mean, self.run_var)
-            return
-        if not on_gpu(self.st.sums):
-            return  # the CPU bn_backward recomputes its sums from dA (reduced or not)
-        st, st2 = self.st, self.st2
-        lib().bn_bwd_finalize(st.sums, st.shards, st.C, cnt, self.gamma, st.mean, st.invstd, self.gamma2,
-                              st2.mean if st2 else None, st2.invstd if st2 else None, self.dgamma, self.dbeta,
-                              self.dgamma2, self.dbeta2, st.coef, st2.coef if st2 else None)
 
 
 def bn_stats(y: torch.Tensor, st: BNState) -> None:
@@ -174,10 +118,9 @@ class BNReduce:
     consumer: it then reads no mask, and an identity shortcut's gradient IS dz -- no second output)."""
 
     def __init__(self, y, st: BNState, a=None, relu: bool = True, y2=None, st2: BNState | None = None,
-                 premask: bool = False, fin: "BNFinalize | None" = None):
+                 premask: bool = False):
         self.y, self.st, self.a, self.relu, self.y2, self.st2 = y, st, a, relu, y2, st2
         self.premask = premask
-        self.fin = fin  # backward BNFinalize of these sums, by the producing GEMM (bn_backward(finalized=True))
 
     def gemm_args(self):
         st, st2 = self.st, self.st2
@@ -207,7 +150,7 @@ class BNReduce:
 
 def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=None, st2: BNState | None = None,
                 gamma2=None, dgamma2=None, dbeta2=None, want_dres: bool = False, relu_from_y: bool = False,
-                reduced: bool = False, premasked: bool = False, finalized: bool = False):
+                reduced: bool = False, premasked: bool = False):
     """Backward of a = relu?(bn(y) [+ bn2(y2) | + r]).
 
     a: post-activation output (bf16, or its packed relu bitmask) used for the relu mask (None -> no
@@ -215,11 +158,7 @@ def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=No
     is recomputed as y*scale+shift > 0, valid when there is no residual input). reduced: the
     per-channel sums were already accumulated into st.sums by the producer's GEMM epilogue
     (BNReduce). premasked: da already is dz (BNReduce(premask=True) producer): no mask is read
-    and dres is da itself. finalized: that producer also ran the finalize (BNReduce.fin): dgamma,
-    dbeta and st.coef are already written. Returns (dy, dy2, dres). Writes dgamma/dbeta (and the
-    second BN's)."""
-    if finalized and not reduced:
-        raise ValueError("bn_backward: finalized sums come from a fused-reduce producer (reduced=True)")
+    and dres is da itself. Returns (dy, dy2, dres). Writes dgamma/dbeta (and the second BN's)."""
     C = st.C
     if premasked:
         if not reduced:
@@ -252,10 +191,9 @@ def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=No
     if not reduced:
         L.bn_bwd_reduce(da, a, y, st.mean, st.invstd, y2, st2.mean if st2 else None, st2.invstd if st2 else None, M, C,
                         st.sums, st.shards, msc, msh)
-    if not finalized:
-        L.bn_bwd_finalize(st.sums, st.shards, C, float(count), gamma, st.mean, st.invstd, gamma2,
-                          st2.mean if st2 else None, st2.invstd if st2 else None, dgamma, dbeta, dgamma2, dbeta2,
-                          st.coef, st2.coef if st2 else None)
+    L.bn_bwd_finalize(st.sums, st.shards, C, float(count), gamma, st.mean, st.invstd, gamma2,
+                      st2.mean if st2 else None, st2.invstd if st2 else None, dgamma, dbeta, dgamma2, dbeta2, st.coef,
+                      st2.coef if st2 else None)
     dy = torch.empty_like(da)
     dy2 = torch.empty_like(da) if y2 is not None else None
     dres = torch.empty_like(da) if (want_dres and not premasked) else None

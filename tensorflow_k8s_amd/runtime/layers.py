@@ -124,13 +124,10 @@ class Conv2d:
         assert C == self.cin, f"conv expects {self.cin} input channels, got {C}"
         return G.ConvGeom(N, H, W, C, self.cout, self.k, self.k, self.stride, self.stride, self.pad, self.pad)
 
-    def forward(self, x, stats: BN.BNState | None = None, act: str | None = None, bn: "BatchNorm | None" = None):
-        """bn (training, with stats = bn's state): also finalize that BN's statistics -- by the conv
-        GEMM's last workgroup where the engine allows (ops.norm.BNFinalize)."""
+    def forward(self, x, stats: BN.BNState | None = None, act: str | None = None):
         g = self.geom(x.shape)
         return G.conv_fwd(x, self.w.compute, g, stats.stats if stats else None, stats.shards if stats else 1,
-                          bias=self.b.master if self.b is not None else None, act=act, cin_used=self.cin_real,
-                          fin=bn.fin_forward() if bn is not None else None)
+                          bias=self.b.master if self.b is not None else None, act=act, cin_used=self.cin_real)
 
     def backward(self, dy, x, need_dx: bool = True, resid=None, bnr=None, resid_stride: int = 1):
         g = self.geom(x.shape)
@@ -189,20 +186,6 @@ class BatchNorm:
     def finalize(self, count: int) -> None:
         BN.bn_finalize(self.st, float(count), self.gamma.master, self.beta.master, self.eps, self.momentum,
                        self.run_mean if self.training else None, self.run_var if self.training else None)
-
-    def fin_forward(self) -> BN.BNFinalize:
-        """This BN's forward finalize, for the conv producing its input (Conv2d.forward(bn=...))."""
-        return BN.BNFinalize(self.st, self.gamma.master, beta=self.beta.master, eps=self.eps, momentum=self.momentum,
-                             run_mean=self.run_mean if self.training else None,
-                             run_var=self.run_var if self.training else None)
-
-    def fin_backward(self, count: int, second: "BatchNorm | None" = None) -> BN.BNFinalize:
-        """This BN's backward finalize (dgamma, dbeta, coef; with ``second``, the projection BN sharing
-        the sums) for the GEMM producing the BN's input gradient (BNReduce(fin=...))."""
-        kw = {}
-        if second is not None:
-            kw = dict(st2=second.st, gamma2=second.gamma.master, dgamma2=second.gamma.grad, dbeta2=second.beta.grad)
-        return BN.BNFinalize(self.st, self.gamma.master, dgamma=self.gamma.grad, dbeta=self.beta.grad, count=count, **kw)
 
     def use_running_stats(self) -> None:
         """Inference: scale/shift from the moving statistics."""

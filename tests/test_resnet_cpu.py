@@ -109,24 +109,3 @@ def test_relu_bitmask_pack_roundtrip_and_backward():
         res.append((dy, dres, dg, db))
     for u, v in zip(*res):
         assert torch.equal(u, v)
-
-
-def test_fused_finalize_plumbing_matches_separate(monkeypatch):
-    """ResNet with each BN finalize handed to its producing conv / dgrad (FUSE_FIN_*, ops.norm.BNFinalize)
-    == the separate finalize calls: same outputs, running statistics and gradients (CPU path)."""
-    from tensorflow_k8s_amd.models import resnet as R
-    res = {}
-    for fuse in (False, True):
-        monkeypatch.setattr(R, "FUSE_FIN_FWD", fuse)
-        monkeypatch.setattr(R, "FUSE_FIN_BWD", fuse)
-        torch.manual_seed(0)
-        a = ParamArena()
-        b = Bottleneck(a, 2, 0, 64, 32, 2)
-        a.finalize("cpu")
-        x = torch.randn(2, 8, 8, 64).relu().to(torch.bfloat16)
-        out = b.forward(x)
-        dx = b.backward(torch.randn(out.shape, generator=torch.Generator().manual_seed(1)).to(torch.bfloat16))
-        res[fuse] = (out, dx, [bn.run_mean.clone() for bn in b.bns()], [p.grad.clone() for p in a.params])
-    assert torch.equal(res[False][0], res[True][0]) and torch.equal(res[False][1], res[True][1])
-    for u, v in zip(res[False][2] + res[False][3], res[True][2] + res[True][3]):
-        assert torch.equal(u, v)

@@ -10,15 +10,13 @@
 
 namespace {
 constexpr int NT = 256;
-// loads per thread issued together: shards <= 4*U take the all-in-flight path; the launchers pick
-// U = 4 for up to 16 shards and U = 16 for up to 64 (ops/norm.py shards_for: wide layers)
-constexpr int SHARD_UNROLL_MAX = 16;
+constexpr int SHARD_UNROLL = 4;  // shards <= 16 (ops/norm.py SHARDS): loads per thread issued together
 
 // ---------------------------------------------------------------- forward
 // Sums NV per-channel vectors stored as [shards][NV][C] over the shards for channel c, zeroing the
 // shards for the next accumulation. 256-thread blocks = 64 channels x 4 shard groups: each thread
 // issues shards/4 independent loads (latency-bound otherwise), then a 4-way LDS reduction.
-template <int NV, int SHARD_UNROLL>
+template <int NV>
 __device__ __forceinline__ bool shard_sum(float* buf, int shards, int C, float (&out)[NV]) {
   __shared__ float red[4][NV][64];
   const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -66,7 +64,6 @@ __device__ __forceinline__ bool shard_sum(float* buf, int shards, int C, float (
 }
 
 // stats: [shards][2][C] (sum, sumsq), zeroed again after reading so the next conv can accumulate.
-template <int U>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(float* stats, int shards, int C, float count,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                           float eps, float momentum, float* __restrict__ run_mean,
@@ -74,7 +71,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(float* stats, int shar
                                                           float* __restrict__ invstd_out, float* __restrict__ scale_out,
                                                           float* __restrict__ shift_out) {
   float sq[2];
-  if (!shard_sum<2, U>(stats, shards, C, sq)) return;
+  if (!shard_sum<2>(stats, shards, C, sq)) return;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const float s = sq[0], q = sq[1];
   double mean = (double)s / count;
@@ -259,7 +256,6 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ da, const bf16* __
 // Reduce shards; write dgamma/dbeta (+= if accumulate) and per-channel apply coefficients.
 // With k1 = gamma*invstd, dy = k1*(dz - mean(dz) - xhat*mean(dz*xhat)) is affine in (dz, y):
 // coef = [k1, A, B][C] with dy = k1*dz + A*y + B; coef2 the same for the second BN.
-template <int U>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(float* sums, int shards, int C, float count,
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, const float* __restrict__ gamma2,
@@ -267,7 +263,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(float* sums, int s
                                        float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dgamma2,
                                        float* __restrict__ dbeta2, float* __restrict__ coef, float* __restrict__ coef2) {
   float sv[3];
-  if (!shard_sum<3, U>(sums, shards, C, sv)) return;
+  if (!shard_sum<3>(sums, shards, C, sv)) return;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const float s0 = sv[0], s1 = sv[1], s2 = sv[2];
   dgamma[c] = s1;
@@ -375,8 +371,7 @@ int tfk_bn_finalize(float* stats, int shards, int C, float count, const float* g
                     float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* scale,
                     float* shift, hipStream_t s) {
   if (g_fin_skip & 1) return 0;
-  hipLaunchKernelGGL(shards <= 16 ? bn_finalize_kernel<4> : bn_finalize_kernel<SHARD_UNROLL_MAX>, dim3((C + 63) / 64),
-                     dim3(256), 0, s, stats, shards, C, count, gamma, beta, eps,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, stats, shards, C, count, gamma, beta, eps,
                      momentum, run_mean, run_var, mean, invstd, scale, shift);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -410,8 +405,7 @@ int tfk_bn_bwd_finalize(float* sums, int shards, int C, float count, const float
                         float* dgamma, float* dbeta, float* dgamma2, float* dbeta2, float* coef, float* coef2,
                         hipStream_t s) {
   if (g_fin_skip & 2) return 0;
-  hipLaunchKernelGGL(shards <= 16 ? bn_bwd_finalize_kernel<4> : bn_bwd_finalize_kernel<SHARD_UNROLL_MAX>,
-                     dim3((C + 63) / 64), dim3(256), 0, s, sums, shards, C, count, gamma, mean,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, sums, shards, C, count, gamma, mean,
                      invstd, gamma2, mean2, invstd2, dgamma, dbeta, dgamma2, dbeta2, coef, coef2);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -6,7 +6,6 @@ residual add of the same pass (dual form). Backward is reduce -> finalize -> app
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -17,25 +16,13 @@ from ._lib import lib, on_gpu
 # (ResNet-50 bs256 step, same box): 8 -> 25.21, 12 -> 25.33, 16 -> 25.15-25.19, 32 -> 25.25-25.41,
 # 64 -> 25.70 ms -- the finalize kernels sit on the critical path and read every shard
 SHARDS = 16
-# Layers of >= WIDE_C channels spread their atomics over WIDE_SHARDS copies: there every block
-# adds a full row of 256-2048 channels, and 16 shards serialise the memory-side adds
-# (tools/bn_stats_probe.py, 1x1 conv 802816 x 64 -> 256 forward: 135 us plain, 154 us with 16-shard
-# statistics, 134 us with 64; narrower layers: level or slower with 64). The finalize kernels
-# issue all of a thread's shard loads together up to 64 shards.
-WIDE_C = 256
-WIDE_SHARDS = int(os.environ.get("TFK_BN_WIDE_SHARDS", 64))
-
-
-def shards_for(C: int) -> int:
-    return WIDE_SHARDS if C >= WIDE_C else SHARDS
 
 
 class BNState:
     """Per-BN-layer device state: stats accumulators and the per-step saved statistics."""
 
-    def __init__(self, C: int, device, shards: int | None = None):
+    def __init__(self, C: int, device, shards: int = SHARDS):
         self.C = C
-        shards = shards_for(C) if shards is None else shards
         self.shards = shards if torch.device(device).type == "cuda" else 1
         self.stats = torch.zeros(self.shards * 2 * C, dtype=torch.float32, device=device)
         self.sums = torch.zeros(self.shards * 3 * C, dtype=torch.float32, device=device)

@@ -19,14 +19,7 @@ the reason) -- nobody is left waiting in a replayed collective its peer never is
 """
 from __future__ import annotations
 
-import os
-
 import torch
-
-# A/B: capture and replay the step on a high-priority stream (the side streams of runtime/streams.py
-# keep the default, lowest priority), so the dispatcher prefers the critical path's workgroups when
-# CUs free up. TFK_STEP_PRIO=<n>: torch stream priority (lower = higher priority); unset: default.
-STEP_PRIO = os.environ.get("TFK_STEP_PRIO")
 
 
 class GraphUnsafe(RuntimeError):
@@ -103,14 +96,7 @@ class StepRunner:
             if not self._capture():
                 self._loss, self._corr = self._step_body()  # agreed fallback: this step runs eager
                 return
-        if getattr(self, "_prio", None) is None:
-            self.graph.replay()
-            return
-        cur = torch.cuda.current_stream()
-        self._prio.wait_stream(cur)
-        with torch.cuda.stream(self._prio):
-            self.graph.replay()
-        cur.wait_stream(self._prio)
+        self.graph.replay()
 
     def _capture(self) -> bool:
         from .guard import Agreement, capture_fault
@@ -121,8 +107,7 @@ class StepRunner:
             capture_fault("step", self.rank)
             # thread-local capture: a watchdog thread polling RCCL / events while this thread
             # captures must not invalidate the capture (the default global mode would)
-            self._prio = torch.cuda.Stream(priority=int(STEP_PRIO)) if STEP_PRIO else None
-            with torch.cuda.graph(g, stream=self._prio, capture_error_mode="thread_local"):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._loss, self._corr = self._step_body()
         except Exception as e:  # noqa: BLE001 -- every failure votes no
             err = f"{type(e).__name__}: {e}"[:600]

@@ -90,6 +90,9 @@ def on_gpu(*ts) -> bool:
 _ws: dict = {}
 # split-K slab workspace slot of conv weight gradients; runtime/streams.py sets one per side stream
 WGRAD_SLOT = "splitk_wgrad"
+# True while runtime/streams.py issues weight gradients on a side stream (ops.gemm.conv_wgrad then
+# sizes its split-K grid for running beside the critical path: SIDE_WGRAD_FILL_DIV)
+ON_SIDE_STREAM = False
 
 
 def workspace(device: torch.device, numel: int, dtype=torch.float32, slot: str = "splitk") -> torch.Tensor:

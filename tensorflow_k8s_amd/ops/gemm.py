@@ -35,6 +35,12 @@ def act_ref(y: torch.Tensor, act) -> torch.Tensor:
 NO_CONV = [0] * 15
 TARGET_BLOCKS = int(os.environ.get("TFK_TARGET_BLOCKS", 1024))  # split-K fill target: ~4 blocks per CU on 256 CUs
 SPLIT_MIN_KTILES = int(os.environ.get("TFK_SPLIT_MIN_KTILES", 4))  # min 64-deep K tiles per split
+# Conv weight gradients issued on a side stream (runtime/streams.py) run concurrently with the
+# input-gradient chain: their split-K fill target and tuned split counts (swept in isolation) are
+# divided by SIDE_WGRAD_FILL_DIV so they hold fewer CU slots while the critical path's kernels wait
+# for them. ResNet-50 bs256 step, same box, alternating: 1 -> 21.94 / 22.01 / 21.92 / 22.09 / 22.00,
+# 2 -> 21.68 / 21.74 / 21.77 / 21.73 / 21.78, 3 -> 21.94 / 22.04 / 22.08, 4 -> 22.27 / 22.09 ms.
+SIDE_WGRAD_FILL_DIV = int(os.environ.get("TFK_SIDE_WGRAD_DIV", 2))
 # Split-K for f32 outputs (weight gradients): per-split workspace slabs + splitk_reduce (two
 # passes, bitwise deterministic). (f32 atomics from the epilogue were measured slower on MI355X,
 # ResNet-50 bs256 step 39.4 vs 32.1 ms: hundreds of splits hammering one small gradient from all
@@ -718,5 +724,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
             _gemm(dy, x, C, g.K, Nn, Kp, g.K, 0, Nn, A_KOUT, B_CONV_WGRAD, EPI_F32, tile, beta=beta, splits=sp,
                   split_stride=stride, conv=g.vec())
     # own slab workspace: conv weight gradients may run on the side stream (runtime/streams.py)
+    div = SIDE_WGRAD_FILL_DIV if _lib_mod.ON_SIDE_STREAM else 1
+    if div > 1 and splits is not None:
+        splits = max(1, splits // div)
     _f32_out_splitk(run, g.K, Nn, Kp, tiles, gw.view(-1), accumulate, dy.device, force_splits=splits,
-                    slot=_lib_mod.WGRAD_SLOT)
+                    slot=_lib_mod.WGRAD_SLOT, split_target=TARGET_BLOCKS // div)

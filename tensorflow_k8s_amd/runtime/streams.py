@@ -73,13 +73,13 @@ def _fork(items) -> None:
     k, side = _stream(dev)
     side.wait_stream(main)
     prev = _lib.WGRAD_SLOT
-    _lib.WGRAD_SLOT = f"splitk_wgrad{k}"
+    _lib.WGRAD_SLOT, _lib.ON_SIDE_STREAM = f"splitk_wgrad{k}", True
     try:
         with torch.cuda.stream(side):
             for fn, _ in items:
                 fn()
     finally:
-        _lib.WGRAD_SLOT = prev
+        _lib.WGRAD_SLOT, _lib.ON_SIDE_STREAM = prev, False
     for _, tensors in items:
         _keep.extend(tensors)
 

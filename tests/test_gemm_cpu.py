@@ -122,3 +122,24 @@ def test_wgrad_tail_split_policy():
         assert not G._wgrad_tail_split(None, None, None, 4096, 1024, 8192, False)  # under a round
     finally:
         G.lib, G._gemm, G.workspace = orig
+
+
+def test_side_stream_wgrad_fill(monkeypatch):
+    """Conv weight gradients issued on a side stream (runtime/streams.py sets ops._lib.ON_SIDE_STREAM)
+    use 1/SIDE_WGRAD_FILL_DIV of the tuned split count and of the split-K fill target."""
+    import torch
+    from tensorflow_k8s_amd.ops import _lib
+    from tensorflow_k8s_amd.ops import gemm as G
+    seen = []
+    monkeypatch.setattr(G, "on_gpu", lambda t: True)
+    monkeypatch.setattr(G, "stem_wgrad_slabs", lambda g, c: 0)
+    monkeypatch.setattr(G, "hwgrad_slabs", lambda g: 0)
+    monkeypatch.setattr(G.tuning, "wgrad_config", lambda *a: ((256, 256), 16))
+    monkeypatch.setattr(G, "_f32_out_splitk", lambda *a, **k: seen.append((k["force_splits"], k["split_target"])))
+    g = G.ConvGeom(8, 14, 14, 256, 256, 1, 1, 1, 1, 0, 0)
+    dy, x, gw = torch.empty(1), torch.empty(1), torch.empty(256 * 256)
+    G.conv_wgrad(dy, x, g, gw)
+    monkeypatch.setattr(_lib, "ON_SIDE_STREAM", True)
+    G.conv_wgrad(dy, x, g, gw)
+    d = G.SIDE_WGRAD_FILL_DIV
+    assert seen == [(16, G.TARGET_BLOCKS), (max(1, 16 // d), G.TARGET_BLOCKS // d)]

@@ -40,6 +40,7 @@ SPLIT_MIN_KTILES = int(os.environ.get("TFK_SPLIT_MIN_KTILES", 4))  # min 64-deep
 # divided by SIDE_WGRAD_FILL_DIV so they hold fewer CU slots while the critical path's kernels wait
 # for them. ResNet-50 bs256 step, same box, alternating: 1 -> 21.94 / 22.01 / 21.92 / 22.09 / 22.00,
 # 2 -> 21.68 / 21.74 / 21.77 / 21.73 / 21.78, 3 -> 21.94 / 22.04 / 22.08, 4 -> 22.27 / 22.09 ms.
+# Linear weight gradients likewise (Transformer-big 18.38 -> 18.18 ms/step, alternating).
 SIDE_WGRAD_FILL_DIV = int(os.environ.get("TFK_SIDE_WGRAD_DIV", 2))
 # Split-K for f32 outputs (weight gradients): per-split workspace slabs + splitk_reduce (two
 # passes, bitwise deterministic). (f32 atomics from the epilogue were measured slower on MI355X,
@@ -356,8 +357,15 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, accumulate
     def run(C, splits, stride, beta):
         _gemm(dy2, x2, C, N, K, M, N, K, K, A_KOUT, B_KOUT, EPI_F32, tile, beta=beta, splits=splits,
               split_stride=stride)
+    # beside the critical path (side stream): half the isolated-sweep fill, unless the model set
+    # its own in-model target (BERT's 512: 11.25 ms/step, halved to 256: 11.41)
+    div = SIDE_WGRAD_FILL_DIV if (_lib_mod.ON_SIDE_STREAM and split_target is None) else 1
+    fs = tuned[1] if tuned else None
+    if div > 1:
+        fs = max(1, fs // div) if fs is not None else None
+        split_target = TARGET_BLOCKS // div
     _f32_out_splitk(run, N, K, M, tiles, gw.view(-1), accumulate, dy.device, split_target=split_target,
-                    force_splits=tuned[1] if tuned else None, slot=_lib_mod.WGRAD_SLOT)
+                    force_splits=fs, slot=_lib_mod.WGRAD_SLOT)
 
 
 # Weight gradients of a few whole rounds of 256x256 tiles plus a small tail (the tied-embedding
@@ -679,6 +687,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
                splits: int | None = None, cin_used: int | None = None) -> None:
     """gw[K][R][S][C] (f32) (+)= sum over (n,p,q) dy[n,p,q,k] * x[n, p*sh-ph+r, q*sw-pw+s, c].
     cin_used: input channels that may be nonzero (the rest are zero padding, whose gradient is 0)."""
+    explicit = splits is not None
     Nn = g.R * g.S * g.C
     Kp = g.N * g.P * g.Q
     if not on_gpu(dy):
@@ -724,7 +733,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, g: ConvGeom, gw: torch.Tensor,
             _gemm(dy, x, C, g.K, Nn, Kp, g.K, 0, Nn, A_KOUT, B_CONV_WGRAD, EPI_F32, tile, beta=beta, splits=sp,
                   split_stride=stride, conv=g.vec())
     # own slab workspace: conv weight gradients may run on the side stream (runtime/streams.py)
-    div = SIDE_WGRAD_FILL_DIV if _lib_mod.ON_SIDE_STREAM else 1
+    div = SIDE_WGRAD_FILL_DIV if (_lib_mod.ON_SIDE_STREAM and not explicit) else 1
     if div > 1 and splits is not None:
         splits = max(1, splits // div)
     _f32_out_splitk(run, g.K, Nn, Kp, tiles, gw.view(-1), accumulate, dy.device, force_splits=splits,

@@ -143,3 +143,22 @@ def test_side_stream_wgrad_fill(monkeypatch):
     G.conv_wgrad(dy, x, g, gw)
     d = G.SIDE_WGRAD_FILL_DIV
     assert seen == [(16, G.TARGET_BLOCKS), (max(1, 16 // d), G.TARGET_BLOCKS // d)]
+
+
+def test_side_stream_linear_wgrad_fill(monkeypatch):
+    """Linear weight gradients on a side stream halve the isolated-sweep fill; a layer's own
+    split_target (set by the model from in-model measurements) is left alone."""
+    import torch
+    from tensorflow_k8s_amd.ops import _lib
+    from tensorflow_k8s_amd.ops import gemm as G
+    seen = []
+    monkeypatch.setattr(G, "on_gpu", lambda t: True)
+    monkeypatch.setattr(G.tuning, "wgrad_config", lambda *a: ((128, 128), 8))
+    monkeypatch.setattr(G, "_f32_out_splitk", lambda *a, **k: seen.append((k["force_splits"], k["split_target"])))
+    dy, x, gw = torch.empty(64, 1024), torch.empty(64, 1024), torch.empty(1024 * 1024)
+    monkeypatch.setattr(_lib, "ON_SIDE_STREAM", True)
+    G.linear_wgrad(dy, x, gw)
+    G.linear_wgrad(dy, x, gw, split_target=512)
+    d = G.SIDE_WGRAD_FILL_DIV
+    assert seen[0] == (max(1, 8 // d), G.TARGET_BLOCKS // d)
+    assert seen[1] == (None, 512)

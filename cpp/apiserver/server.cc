@@ -256,7 +256,8 @@ void ApiServer::do_watch(const HttpRequest& req, ResponseWriter& w, const std::s
   int64_t timeout_s = q("timeoutSeconds").empty() ? 1800 : std::stoll(q("timeoutSeconds"));
   ApiStatus st;
   auto watcher = store_->watch(plural, ns, rv, LabelSelector::parse(q("labelSelector")),
-                               FieldSelector::parse(q("fieldSelector")), &st);
+                               FieldSelector::parse(q("fieldSelector")), &st,
+                               plural == api::kPlural ? api_version : "");
   if (!watcher) {
     // Kubernetes sends 410 as an ERROR event inside a 200 stream; do the same.
     if (!w.start_stream(200)) return;
@@ -267,7 +268,6 @@ void ApiServer::do_watch(const HttpRequest& req, ResponseWriter& w, const std::s
     w.end_stream();
     return;
   }
-  watcher->requested_version = plural == api::kPlural ? api_version : "";
   if (!w.start_stream(200)) { watcher->close(); return; }
   int64_t deadline = mono_ms() + timeout_s * 1000;
   int64_t last_write = mono_ms();

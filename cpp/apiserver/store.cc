@@ -304,11 +304,11 @@ void Store::emit_locked(const std::string& plural, const std::string& type, cons
     if (!s || s->closed()) continue;
     live.push_back(w);
     if (s->plural() != plural) continue;
-    if (!s->requested_version.empty() && plural == "tfjobs") {
+    if (!s->requested_version().empty() && plural == "tfjobs") {
       WatchEvent cv = ev;
       auto it = converters_.find(plural);
-      if (it != converters_.end() && obj.at("apiVersion").str() != s->requested_version) {
-        try { cv.object = it->second(obj, s->requested_version); } catch (...) {}
+      if (it != converters_.end() && obj.at("apiVersion").str() != s->requested_version()) {
+        try { cv.object = it->second(obj, s->requested_version()); } catch (...) {}
       }
       s->deliver(cv);
     } else {
@@ -647,13 +647,14 @@ void Store::gc_dependents_locked(const std::string& owner_uid, const std::string
 }
 
 std::shared_ptr<Watcher> Store::watch(const std::string& plural, const std::string& ns, int64_t from_rv,
-                                      const LabelSelector& ls, const FieldSelector& fs, ApiStatus* st) {
+                                      const LabelSelector& ls, const FieldSelector& fs, ApiStatus* st,
+                                      const std::string& requested_version) {
   std::lock_guard<std::mutex> g(mu_);
   if (!resources_.count(plural)) {
     *st = ApiStatus::Err(404, "NotFound", "unknown resource " + plural);
     return nullptr;
   }
-  auto w = std::make_shared<Watcher>(plural, ns, ls, fs);
+  auto w = std::make_shared<Watcher>(plural, ns, ls, fs, requested_version);
   if (from_rv <= 0) {
     // no resourceVersion: start with synthetic ADDED events for the current state
     auto b = data_.find(plural);

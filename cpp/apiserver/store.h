@@ -81,23 +81,32 @@ struct WatchEvent {
 
 class Watcher {
  public:
-  Watcher(std::string plural, std::string ns, LabelSelector ls, FieldSelector fs)
-      : plural_(std::move(plural)), ns_(std::move(ns)), ls_(std::move(ls)), fs_(std::move(fs)) {}
+  // requested_version is fixed at construction: the watcher is published to the store's fan-out
+  // list (read by other request threads under the store lock) the moment Store::watch returns.
+  Watcher(std::string plural, std::string ns, LabelSelector ls, FieldSelector fs, std::string requested_version = "")
+      : plural_(std::move(plural)), ns_(std::move(ns)), requested_version_(std::move(requested_version)),
+        ls_(std::move(ls)), fs_(std::move(fs)) {}
   // Blocks up to timeout_ms; returns false on timeout or when closed with no events left.
   bool next(WatchEvent* ev, int64_t timeout_ms);
   void close();
-  bool closed() const { return closed_; }
+  bool closed() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return closed_;
+  }
   void deliver(const WatchEvent& ev);  // applies ns/selector filters
-  void max_queue_for_test(size_t n) { max_queue_ = n; }
+  void max_queue_for_test(size_t n) {
+    std::lock_guard<std::mutex> g(mu_);
+    max_queue_ = n;
+  }
   const std::string& plural() const { return plural_; }
-  std::string requested_version;       // convert objects to this version (TFJobs)
+  const std::string& requested_version() const { return requested_version_; }  // TFJob conversion target
 
  private:
   friend class Store;
-  std::string plural_, ns_;
+  const std::string plural_, ns_, requested_version_;
   LabelSelector ls_;
   FieldSelector fs_;
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::condition_variable cv_;
   std::deque<WatchEvent> q_;
   bool closed_ = false;
@@ -139,8 +148,10 @@ class Store {
   // propagation: Background (default) | Foreground | Orphan
   ApiStatus remove(const std::string& plural, const std::string& ns, const std::string& name,
                    const std::string& propagation, Json* out);
+  // requested_version: apiVersion the watcher's TFJob events are converted to ("" = stored version).
   std::shared_ptr<Watcher> watch(const std::string& plural, const std::string& ns, int64_t from_rv,
-                                 const LabelSelector& ls, const FieldSelector& fs, ApiStatus* st);
+                                 const LabelSelector& ls, const FieldSelector& fs, ApiStatus* st,
+                                 const std::string& requested_version = "");
   int64_t resource_version() const;
   size_t count(const std::string& plural) const;
   std::map<std::string, long long> counters() const;  // for /metrics

@@ -276,6 +276,17 @@ def main():
     if wd is not None:
         guards["watchdog_s"] = wd.timeout_s
     comm_cfg["guards"] = guards
+    bad = _numerics_failure(loss, guards.get("emb_guard", 0))
+    if bad:
+        # a corrupt run has no throughput: no metric line, non-zero exit
+        print(json.dumps({"error": bad, "rank": rank, "model": args.model, "ms_per_step": round(ms, 3)}),
+              file=sys.stderr, flush=True)
+        if wd is not None:
+            wd.exit_code = 0
+        tfk_comm.shutdown()
+        if wd is not None:
+            wd.stop()
+        return 3
     par = f"ps{len(ps_ranks)}+worker{nworkers}" if use_ps else f"dp{world}"
     if rank == worker_ranks[0] and not is_cnn:
         seq = model.cfg.seq_len if args.model.startswith("bert") else model.cfg.tgt_len
@@ -313,6 +324,16 @@ def main():
     tfk_comm.shutdown()
     if wd is not None:
         wd.stop()
+
+
+def _numerics_failure(loss, emb_guard: int) -> str | None:
+    """Why the measured run is invalid (non-finite final loss, skipped embedding rows), else None."""
+    import math
+    if loss is not None and not math.isfinite(float(loss)):
+        return f"non-finite loss {loss}"
+    if emb_guard:
+        return f"{emb_guard} out-of-range embedding events (emb_guard)"
+    return None
 
 
 def _update_report(model, master0) -> dict:

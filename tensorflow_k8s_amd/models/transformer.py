@@ -175,7 +175,9 @@ class EncoderLayer:
         # copies then serve ff1's dgrad and weight gradient and the bf16 dz is never stored
         sink1 = self.ff1.bias_sink()  # (same box: bf16 18.29 -> 18.21 ms/step, MX-fp8 17.47 -> 17.32)
         mx = MX_PRODUCERS and self.ff1.fp8
-        only = mx and sink1 is not None and (dy.numel() // dy.shape[-1]) % 128 == 0
+        # no bf16 dz only when both its consumers take MX copies: ff1's weight gradient reads bf16 dz
+        # unless it runs in MX-fp8 too (F8.MX_WGRAD)
+        only = mx and F8.MX_WGRAD and sink1 is not None and (dy.numel() // dy.shape[-1]) % 128 == 0
         dz = self.ff2.backward(dy, f, dact_src=z, dact="relu", drop_p=cfg.relu_dropout if training else 0.0,
                                drop_seed=_mix(seed, 5), mx_dx=mx,  # fp8: MX(dz) for ff1
                                bias_done=fused, dx_bias=sink1, mx_dx_only=only)

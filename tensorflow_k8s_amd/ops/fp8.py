@@ -232,6 +232,8 @@ def linear_fwd_mx(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = 
             y = (y.float() + resid.reshape(-1, N).float()).to(torch.bfloat16)
         if mx_out:
             _register_out(y, *mx_quantize_dual(y))
+            if mx_skip_c:
+                _poison_no_c(y)
         return y
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
     mo = _mx_bufs(M, N, y.device) if mx_out else None
@@ -269,6 +271,21 @@ def _check_stored(x: torch.Tensor) -> None:
     if _NO_C and (x.data_ptr(), _shape2(x)) in _NO_C:
         raise RuntimeError("fp8: a GEMM output produced with mx_skip_c (no bf16 values) reached a consumer "
                            "that reads bf16 -- produce it with mx_skip_c=False")
+
+
+def check_stored(*xs: torch.Tensor) -> None:
+    """Raise if any of xs is an MX-only output (its bf16 values were never stored)."""
+    for x in xs:
+        if x is not None:
+            _check_stored(x.reshape(-1, x.shape[-1]))
+
+
+def _poison_no_c(y: torch.Tensor) -> None:
+    """CPU emulation of mx_skip_c: the GPU epilogue never stores y's bf16 values, so the reference
+    path makes them NaN and marks y -- a bf16 consumer then raises (_check_stored) or, if it bypasses
+    the check, poisons the loss, exactly as the unwritten device memory would."""
+    y.fill_(float("nan"))
+    mark_no_c(y)
 
 
 def cached_dual(y: torch.Tensor):
@@ -311,6 +328,8 @@ def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | Non
     mx_out): no bf16 dx -- every consumer takes the MX copies."""
     M, N = dy.shape
     K = w.shape[1]
+    if dyq is None:
+        _check_stored(dy)
     dq, ds = dyq if dyq is not None else mx_quantize(dy)
     if wt is None:
         wt = take_t(w)
@@ -330,6 +349,9 @@ def linear_dgrad_mx(dy: torch.Tensor, w: torch.Tensor, resid: torch.Tensor | Non
             y = (y.float() + resid.float()).to(torch.bfloat16)
         if mx_out and M % MX_BLOCK == 0 and K % MX_BLOCK == 0:
             _register_out(y, *mx_quantize_dual(y))
+            fuse_cs = colsum is not None and resid is None and (dact_src is not None or drop_p > 0)
+            if mx_skip_c and (colsum is None or fuse_cs):
+                _poison_no_c(y)
         return y
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
     mo = _mx_bufs(M, K, dx.device) if mx_out and M % MX_BLOCK == 0 and K % MX_BLOCK == 0 else None

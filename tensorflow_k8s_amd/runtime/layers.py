@@ -48,10 +48,12 @@ def fp8_dy(dy, K: int, fp8: bool):
     from ..ops.fp8 import mx_backward_ok, mx_quantize_dual
     M, N = dy.shape
     dg, wg = mx_backward_ok(M, N, K)
+    from ..ops.fp8 import cached_dual
+    c = cached_dual(dy)  # the dgrad that produced dy already wrote its MX copies
     if dg and wg:
-        from ..ops.fp8 import cached_dual
-        c = cached_dual(dy)  # the dgrad that produced dy already wrote its MX copies
         return c if c is not None else mx_quantize_dual(dy)
+    if dg and c is not None:
+        return c[0], None
     return None, None
 
 
@@ -61,6 +63,8 @@ def linear_wgrad(dy, x, gw, fp8: bool, accumulate: bool = False, split_target=No
         from ..ops.fp8 import linear_wgrad_mx, mx_backward_ok
         if mx_backward_ok(dy.shape[0], dy.shape[1], x.shape[1])[1]:
             return linear_wgrad_mx(dy, x, gw, accumulate=accumulate, dyt=dyt)
+        from ..ops.fp8 import check_stored
+        check_stored(dy, x)  # the bf16 GEMM below reads bf16 values: none may be an MX-only output
     return G.linear_wgrad(dy, x, gw, accumulate=accumulate, split_target=split_target)
 
 
@@ -77,6 +81,8 @@ def linear_dgrad(dy, w, fp8: bool, drop_p: float = 0.0, drop_seed: int = 0, dyq=
         from ..ops.fp8 import linear_dgrad_mx, mx_backward_ok
         if mx_backward_ok(dy.shape[0], dy.shape[1], w.shape[1])[0]:
             return linear_dgrad_mx(dy, w, dyq=dyq, drop_p=drop_p, drop_seed=drop_seed, **kw)
+        from ..ops.fp8 import check_stored
+        check_stored(dy)
     kw.pop("mx_out", None)
     kw.pop("mx_skip_c", None)
     return G.linear_dgrad(dy, w, drop_p=drop_p, drop_seed=drop_seed, **kw)

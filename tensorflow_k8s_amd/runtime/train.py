@@ -15,7 +15,7 @@ the operator-injected TF_CONFIG). Per role:
 Exit codes follow the operator's restart policy (ExitCode): 0 success; 1 permanent user error;
 137 OOM (termination message "OOMKilled", permanent) ; 143 peer/rendezvous failure (retryable ->
 gang restart, resume from the latest checkpoint). Fault injection for the failure-recovery tests:
-TFK_FAULT_AT_STEP=<n> [TFK_FAULT_EXIT=<code>|137=SIGKILL] [TFK_FAULT_RANK=<r>]
+TFK_FAULT_AT_STEP=<n> [TFK_FAULT_EXIT=<code>|137=SIGKILL|nan=poison the weights] [TFK_FAULT_RANK=<r>]
 [TFK_FAULT_GENERATION=<g>|any, compared with the operator's TFK_RESTART_GENERATION, default 0].
 """
 from __future__ import annotations
@@ -139,7 +139,7 @@ def pick_device(args, info) -> torch.device:
     return torch.device("cuda", local)
 
 
-def maybe_fault(step: int, rank: int):
+def maybe_fault(step: int, rank: int, arena=None):
     at = os.environ.get("TFK_FAULT_AT_STEP")
     if not at or int(at) != step:
         return
@@ -147,6 +147,13 @@ def maybe_fault(step: int, rank: int):
         return
     gen = os.environ.get("TFK_FAULT_GENERATION", "0")
     if gen != "any" and gen != os.environ.get("TFK_RESTART_GENERATION", "0"):
+        return
+    if os.environ.get("TFK_FAULT_EXIT") == "nan":
+        # silent corruption instead of a crash: the next steps' loss is NaN (the numerics guard's case)
+        _log({"event": "fault_injected", "step": step, "rank": rank, "exit": "nan"})
+        if arena is not None:
+            arena.master.fill_(float("nan"))
+            arena.compute.fill_(float("nan"))
         return
     code = int(os.environ.get("TFK_FAULT_EXIT", "1"))
     _log({"event": "fault_injected", "step": step, "rank": rank, "exit": code})
@@ -277,29 +284,34 @@ def run_worker(args, info, dev, world_comm, watchdog=None) -> int:
         if runner.fallback and not fell_back:
             fell_back = True
             _log({"event": "graph_fallback", "rank": info.rank, "step": step, "reason": runner.fallback[:500]})
-        if step % max(1, args.log_every) == 0 or step == args.steps:
-            m = torch.tensor([runner.last_loss() or 0.0, runner.last_accuracy() or 0.0], dtype=torch.float32,
-                             device=dev if strat.name == "mwms" else "cpu")
+        # (same on every rank: the metrics reduction below is a collective)
+        ckpt_due = bool(ckpt is not None and args.checkpoint_every and step % args.checkpoint_every == 0
+                        and step < args.steps)
+        if step % max(1, args.log_every) == 0 or step == args.steps or ckpt_due:
+            # [loss, accuracy, embedding-guard events]: summed over the workers so every rank sees the
+            # same verdict and a corrupt step fails the job before anything is logged or checkpointed
+            m = torch.tensor([runner.last_loss() or 0.0, runner.last_accuracy() or 0.0, float(_emb_guard(dev))],
+                             dtype=torch.float32, device=dev if strat.name == "mwms" else "cpu")
             strat.all_reduce_metrics(m)
             if strat.name == "mwms":
                 m /= nworkers
             if dev.type == "cuda":
                 torch.cuda.synchronize()
+            _check_numerics(step, float(m[0]), float(m[2]))
             now = time.perf_counter()
             if info.is_chief:
                 _log({"event": "train", "step": step, "loss": round(float(m[0]), 6), "accuracy": round(float(m[1]), 6),
                       "examples_per_sec": round(gb * n_last / max(now - t_last, 1e-9), 2),
                       "lr": opt.lr(step - 1)}, metrics_fh)
             t_last, n_last = now, 0
-        if ckpt is not None and info.is_chief and args.checkpoint_every and step % args.checkpoint_every == 0 \
-                and step < args.steps:
+        if ckpt_due and info.is_chief:
             with tracer.span("checkpoint", cat="io", step=step):
                 if use_ps:
                     strat.fetch_state(opt)
                     opt.step_count = step  # the ps tasks ran the updates (a captured step keeps no host count)
                 path = ckpt.save(model.arena, opt, step)
             _log({"event": "checkpoint", "step": step, "path": path}, metrics_fh)
-        maybe_fault(step, info.rank)
+        maybe_fault(step, info.rank, model.arena)
         if args.step_sleep > 0:
             time.sleep(args.step_sleep)
     if args.trace_file:
@@ -325,6 +337,27 @@ def run_worker(args, info, dev, world_comm, watchdog=None) -> int:
     if info.is_chief:
         _log({"event": "done", "step": step, "loss": runner.last_loss()}, metrics_fh)
     return EXIT_OK
+
+
+class NumericsError(RuntimeError):
+    """A training step produced a non-finite loss or out-of-range embedding ids: permanent (a restart
+    from the last checkpoint would replay the same data and weights)."""
+
+
+def _emb_guard(dev) -> int:
+    """Out-of-range events the bucketed embedding backward skipped since the last read (GPU only)."""
+    if dev.type != "cuda":
+        return 0
+    from ..ops._lib import lib
+    return int(lib().emb_guard_count())
+
+
+def _check_numerics(step: int, loss: float, emb_guard: float) -> None:
+    import math
+    if not math.isfinite(loss):
+        raise NumericsError(f"NonFiniteLoss: loss {loss} at step {step}")
+    if emb_guard > 0:
+        raise NumericsError(f"EmbeddingGuard: {emb_guard:g} out-of-range embedding events by step {step}")
 
 
 def _guard_error():
@@ -380,6 +413,10 @@ def main(argv=None) -> int:
         # permanent (a restart would hit the same full disk); the previous checkpoint is intact
         _termination_message(f"CheckpointWriteFailed: {e}"[:2000])
         _log({"event": "error", "kind": "checkpoint", "message": str(e)[:500]})
+        return EXIT_USER
+    except NumericsError as e:
+        _termination_message(str(e))
+        _log({"event": "error", "kind": "numerics", "message": str(e)[:500]})
         return EXIT_USER
     except (cluster.RendezvousError, _guard_error()) as e:
         _termination_message(str(e))

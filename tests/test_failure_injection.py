@@ -55,3 +55,20 @@ def test_chief_replica_exits_143_on_port_in_use(tmp_path):
         assert ev[-1]["kind"] == "rendezvous"
     finally:
         s.close()
+
+
+def test_nonfinite_loss_fails_permanently(tmp_path):
+    """Silent numeric corruption (TFK_FAULT_EXIT=nan poisons the weights after step 2): the replica
+    stops at the next metrics point with exit 1 (permanent: a restart would replay the same state)
+    and a NonFiniteLoss termination reason, before the corrupt weights reach a checkpoint."""
+    env = dict(os.environ, TFK_TERMINATION_LOG=str(tmp_path / "term"), PYTHONPATH=ROOT, TFK_FAULT_AT_STEP="2",
+               TFK_FAULT_EXIT="nan")
+    env.pop("TF_CONFIG", None)
+    r = subprocess.run([sys.executable, "-m", "tensorflow_k8s_amd.runtime.train", "--model", "lenet", "--steps", "8",
+                        "--device", "cpu", "--log-every", "4", "--checkpoint-dir", str(tmp_path / "ckpt"),
+                        "--checkpoint-every", "4"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "NonFiniteLoss" in (tmp_path / "term").read_text()
+    ev = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert ev[-1]["kind"] == "numerics"
+    assert not [e for e in ev if e.get("event") == "checkpoint" and e.get("step", 0) >= 4]

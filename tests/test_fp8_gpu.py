@@ -162,6 +162,38 @@ def test_fp8_real_width_tracks_bf16_100_steps():
     assert abs(mf - mb) <= 0.025 * mb, (b[::10], f[::10])
 
 
+def test_fp8_bf16_weight_gradients_finite_and_track_mx_wgrad(monkeypatch):
+    """Transformer-big (6+6 layers, real widths, dropout on) in fp8 with bf16 weight gradients
+    (ops.fp8.MX_WGRAD False, bench.py --mx-wgrad 0): 20 AdamW steps stay finite and the mean loss is
+    within 2 % of the MX-fp8-weight-gradient run. Round 5 shipped this path with ff1's weight
+    gradient reading a never-stored bf16 dz (NaN loss)."""
+    from tensorflow_k8s_amd.models.transformer import Transformer, TransformerConfig
+    from tensorflow_k8s_amd.ops import fp8 as F8
+    from tensorflow_k8s_amd.runtime.optimizer import AdamW
+    curves = {}
+    for mxw in (True, False):
+        monkeypatch.setattr(F8, "MX_WGRAD", mxw)
+        c = TransformerConfig.big()
+        c.fp8 = True
+        m = Transformer(c).to("cuda", seed=11)
+        opt = AdamW(m.arena, lr=3e-4, b2=0.98, eps=1e-9, weight_decay=0.0)
+        batch = m.synthetic_batch(8, "cuda", seed=3)
+        ls = []
+        for _ in range(20):
+            loss, _ = m.forward_backward(*batch)
+            opt.step()
+            ls.append(float(loss.float().mean()))
+        assert torch.isfinite(m.arena.master).all()
+        curves[mxw] = ls
+        del m, opt, batch
+        torch.cuda.empty_cache()
+    a, b = curves[True], curves[False]
+    assert all(v == v and abs(v) != float("inf") for v in a + b), (a, b)
+    ma, mb = sum(a) / len(a), sum(b) / len(b)
+    print(f"fp8 loss, MX vs bf16 weight gradients, mean of 20 steps: {ma:.4f} vs {mb:.4f}")
+    assert abs(ma - mb) <= 0.02 * ma, (a, b)
+
+
 @pytest.mark.parametrize("tile", [128, 256, 2561])
 @pytest.mark.parametrize("M,N,K", [(512, 1024, 1024), (300, 200, 256), (1000, 520, 384)])
 def test_g4_fp8_engine_matches_register_engine(M, N, K, tile):

@@ -123,3 +123,18 @@ def test_dropout_rate_quantization_is_validated():
         TransformerConfig(dropout=0.9995)
     with pytest.raises(ValueError):
         BertConfig(attn_dropout=1e-3)
+
+
+def test_bench_refuses_corrupt_runs():
+    """bench.py prints no metric line (exit 3) for a non-finite final loss or skipped embedding rows."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b._numerics_failure(2.5, 0) is None
+    assert b._numerics_failure(None, 0) is None
+    assert "non-finite" in b._numerics_failure(float("nan"), 0)
+    assert "non-finite" in b._numerics_failure(float("inf"), 0)
+    assert "emb_guard" in b._numerics_failure(2.5, 3)

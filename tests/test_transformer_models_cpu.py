@@ -149,3 +149,41 @@ def test_layernorm_backward_bias_fusion_matches_column_sums(which, monkeypatch):
         monkeypatch.undo()
     assert torch.equal(res[True][0], res[False][0])
     torch.testing.assert_close(res[True][1], res[False][1], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mx_wgrad", [True, False])
+def test_transformer_fp8_mx_wgrad_switch_finite_and_tracks_bf16(mx_wgrad, monkeypatch):
+    """fp8 training with MX producers and either weight-gradient precision (ops.fp8.MX_WGRAD, bench.py
+    --mx-wgrad): every gradient is finite and tracks the bf16 model. The CPU reference poisons the bf16
+    values of MX-only outputs with NaN (ops.fp8._poison_no_c), so a bf16 consumer of one -- the
+    round-5 ff1 weight gradient reading the never-stored dz -- fails here instead of on the GPU."""
+    import tensorflow_k8s_amd.models.transformer as TM
+    from tensorflow_k8s_amd.ops import fp8 as F8
+    monkeypatch.setattr(F8, "MX_WGRAD", mx_wgrad)
+    res = {}
+    for fp8 in (False, True):
+        cfg = TM.TransformerConfig(vocab_size=500, hidden=128, enc_layers=1, dec_layers=1, heads=2, ffn=256,
+                                   src_len=64, tgt_len=64, max_len=128, dropout=0.1, attn_dropout=0.1,
+                                   relu_dropout=0.1, fp8=fp8)
+        m = TM.Transformer(cfg).to("cpu", seed=4)
+        loss, _ = m.forward_backward(*m.synthetic_batch(2, "cpu", seed=1))
+        res[fp8] = (float(loss.mean()), m.arena.grad.clone())
+    assert torch.isfinite(res[True][1]).all()
+    assert abs(res[True][0] - res[False][0]) / res[False][0] < 0.02
+    assert _cos(res[True][1], res[False][1]) > 0.98
+
+
+def test_mx_only_output_refuses_bf16_consumers():
+    """An MX-only GEMM output (mx_skip_c) raises when a bf16 consumer reaches it."""
+    from tensorflow_k8s_amd.ops import fp8 as F8
+    x = torch.randn(128, 128).bfloat16()
+    w = torch.randn(128, 128).bfloat16()
+    try:
+        y = F8.linear_fwd_mx(x, w, mx_out=True, mx_skip_c=True)
+        assert torch.isnan(y.float()).all()
+        with pytest.raises(RuntimeError, match="mx_skip_c"):
+            F8.check_stored(y)
+        with pytest.raises(RuntimeError, match="mx_skip_c"):
+            F8.linear_dgrad_mx(y, w)
+    finally:
+        F8.clear_saved()

@@ -384,7 +384,7 @@ def _wgrad_tail_split(dy2, x2, gw, N: int, K: int, M: int, accumulate: bool) -> 
         return False
     rows_dp = (rounds * CHIP_BLOCKS) // tn  # whole row-tiles in the unsplit part
     n0 = rows_dp * 256
-    if n0 >= N:
+    if n0 == 0 or n0 >= N:  # no whole row-tile in the unsplit part (inputs wider than 65536): no zero-row launch
         return False
     nt = N - n0
     tail_tiles = -(-nt // 256) * tn

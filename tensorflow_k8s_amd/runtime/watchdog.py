@@ -100,10 +100,15 @@ class StepWatchdog:
             done += 1
         if done:
             with self._lock:
-                st = self._dev[done - 1][0]
-                del self._dev[:done]
-                self.device_step = self.last_step = st
-                self._last = time.monotonic()
+                # retire by identity: beat_device may have trimmed the middle of the list since the
+                # snapshot, so a positional prefix could name newer, still-pending events
+                last = None
+                for ent in pend[:done]:
+                    if self._dev and self._dev[0] is ent:
+                        last = self._dev.pop(0)
+                if last is not None:
+                    self.device_step = self.last_step = last[0]
+                    self._last = time.monotonic()
 
     def stop(self) -> None:
         self._stop.set()

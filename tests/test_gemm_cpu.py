@@ -120,6 +120,9 @@ def test_wgrad_tail_split_policy():
         assert calls[2] == ("reduce", 960 * 1024)
         assert not G._wgrad_tail_split(None, None, None, 4096, 4096, 8192, False)  # exactly 1 round
         assert not G._wgrad_tail_split(None, None, None, 4096, 1024, 8192, False)  # under a round
+        n = len(calls)  # a row-tile wider than a round (K 76800 = 300 tiles, N 256): no 0-row launch
+        assert not G._wgrad_tail_split(None, None, None, 256, 76800, 8192, False)
+        assert len(calls) == n
     finally:
         G.lib, G._gemm, G.workspace = orig
 

@@ -201,3 +201,27 @@ def test_watchdog_follows_device_completion():
         assert fired and fired[0][0] == 7, fired  # last COMPLETED step
     finally:
         w.stop()
+
+
+def test_watchdog_poll_retires_by_identity_when_trimmed_concurrently():
+    """A beat_device that trims the pending list while _poll_device queries its snapshot must not
+    retire (or report as completed) a newer event that is still pending."""
+    from tensorflow_k8s_amd.runtime.watchdog import StepWatchdog
+    w = StepWatchdog(60.0)
+    w.MAX_PENDING = 3
+
+    class Ev:
+        def __init__(self, done, hook=None):
+            self.done, self.hook = done, hook
+
+        def query(self):
+            if self.hook:
+                self.hook()
+            return self.done
+    e2 = Ev(False)
+    w.beat_device(0, Ev(True))
+    w.beat_device(1, Ev(True, hook=lambda: w.beat_device(3, Ev(False))))  # trims entry 1 mid-poll
+    w.beat_device(2, e2)
+    w._poll_device()
+    assert w.device_step == 0
+    assert any(ev is e2 for _, ev in w._dev)

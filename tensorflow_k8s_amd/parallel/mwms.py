@@ -6,8 +6,10 @@ MI355X design: gradients live in ONE flat f32 arena buffer laid out in backward-
 so a bucket is a contiguous slice -> one ``all_reduce`` per bucket with no flatten copies. Buckets
 are launched the moment the backward pass has written their last gradient (executor readiness
 callbacks), so ring all-reduce over xGMI overlaps the remaining backward compute; RCCL runs on the
-communicator's high-priority comm stream (forked from the compute stream at launch) and the compute
-stream only waits on it right before the optimizer. Under hipGraph capture those forks/joins are
+communicator's high-priority comm stream (forked at launch from the compute stream AND the
+side streams that produced weight gradients, runtime/streams.py producers()) and the compute
+stream only waits on it right before the optimizer -- the input-gradient chain never stalls behind
+queued weight gradients at a bucket launch. Under hipGraph capture those forks/joins are
 graph edges: the captured step (forward, backward, bucket all-reduces, optimizer) is the step that
 runs at every world size.
 
@@ -17,7 +19,7 @@ runs at every world size.
 * The default wire is f32 (RCCL sums exactly what TF's f32 gradient aggregation sums).
   ``comm_dtype=torch.bfloat16`` (opt-in, like TF's CommunicationOptions) puts bf16 on the wire:
   the bucket is packed f32->bf16 by a HIP
-  cast kernel on the compute stream (the RCCL stream waits on it), all-reduced in bf16 (half the
+  cast kernel on the comm stream (after its producer waits), all-reduced in bf16 (half the
   xGMI bytes of f32: 51 MB instead of 102 MB per ResNet-50 step) and unpacked into the f32 arena
   right after the wait; the 1/world mean stays in the fused optimizer's grad_scale.
 * Bucket size default 32 MiB of f32 gradient: large enough to amortise RCCL launch/latency on the
@@ -128,14 +130,17 @@ class MultiWorkerMirroredStrategy:
     def _launch(self, b: Bucket):
         b.launched = True
         from ..runtime import streams
-        streams.sync()  # the bucket may hold weight gradients produced on the side stream
+        # the bucket may hold weight gradients produced on the side streams: the COMM stream waits
+        # for them (and for the compute stream); the compute stream's input-gradient chain does not
+        deps = streams.producers()
         view = self.arena.grad[b.start:b.end]
+        pre = None
         if self.wire is not None:
             from ..ops.optim import cast_f32_bf16
             w = self.wire[b.start:b.end]
-            cast_f32_bf16(view, w)
+            pre = (lambda v=view, w=w: cast_f32_bf16(v, w))  # packed on the comm stream
             view = w
-        b.work = self.comm.all_reduce(view, async_op=True)
+        b.work = self.comm.all_reduce(view, async_op=True, deps=deps, pre=pre)
 
     def finish_step(self):
         """Launch stragglers (in order), wait for every bucket (compute stream waits on the RCCL

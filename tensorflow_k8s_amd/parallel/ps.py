@@ -172,16 +172,16 @@ class ParameterServerStrategy:
         pl.pending[b] -= 1
         while self._next < len(pl.buckets) and pl.pending[self._next] <= 0:
             from ..runtime import streams
-            streams.sync()  # side-stream weight gradients of this bucket first
-            self._red.append(pl.reduce(self._next, self.arena.grad))
+            # side-stream weight gradients of this bucket: the reduce's comm stream waits on them
+            self._red.append(pl.reduce(self._next, self.arena.grad, deps=streams.producers()))
             self._next += 1
 
     def finish_step(self):
         if self.plan is not None:
             from ..runtime import streams
-            streams.sync()
+            deps = streams.producers()
             while self._next < len(self.plan.buckets):
-                self._red.append(self.plan.reduce(self._next, self.arena.grad))
+                self._red.append(self.plan.reduce(self._next, self.arena.grad, deps=deps))
                 self._next += 1
 
     def configure_optimizer(self, opt) -> None:
@@ -366,15 +366,18 @@ class CollectivePlan:
         return up + down
 
     # ---------------------------------------------------------------- per bucket
-    def reduce(self, i: int, grad: torch.Tensor):
-        """Worker: push bucket i's gradient to its owner (packed to the wire dtype first)."""
+    def reduce(self, i: int, grad: torch.Tensor, deps=()):
+        """Worker: push bucket i's gradient to its owner (packed to the wire dtype first, on the comm
+        stream). deps: the side streams that produced part of the bucket."""
         lo, hi, s = self.buckets[i]
         t = grad[lo:hi]
+        pre = None
         if self.wire is not None:
             from ..ops.optim import cast_f32_bf16
-            cast_f32_bf16(t, self.wire[lo:hi])
-            t = self.wire[lo:hi]
-        return self.red[s].reduce(t, self.root[s], async_op=True)
+            w = self.wire[lo:hi]
+            pre = (lambda t=t, w=w: cast_f32_bf16(t, w))
+            t = w
+        return self.red[s].reduce(t, self.root[s], async_op=True, deps=deps, pre=pre)
 
     def unpack(self, i: int) -> None:
         """Owner: the reduced bf16 bucket -> f32 gradient (after its reduce completed)."""

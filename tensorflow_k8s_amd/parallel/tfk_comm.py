@@ -157,16 +157,23 @@ class RcclComm:
         return c
 
     # ------------------------------------------------------------------ stream plumbing
-    def _fork(self):
+    def _fork(self, deps=()):
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        for d in deps:
+            self.stream.wait_stream(d)
 
     def _handle(self):
         ev = torch.cuda.Event()
         ev.record(self.stream)
         return _StreamHandle(ev)
 
-    def _run(self, fn, async_op: bool):
-        self._fork()
+    def _run(self, fn, async_op: bool, deps=(), pre=None):
+        """deps: further producer streams the collective waits on (besides the caller's stream);
+        pre: producer kernels (e.g. a wire-dtype pack) issued on the comm stream before it."""
+        self._fork(deps)
+        if pre is not None:
+            with torch.cuda.stream(self.stream):
+                pre()
         fn(self.stream.cuda_stream)
         h = self._handle()
         if async_op:
@@ -175,12 +182,13 @@ class RcclComm:
         return None
 
     # ------------------------------------------------------------------ collectives
-    def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False, out: torch.Tensor | None = None):
+    def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False, out: torch.Tensor | None = None,
+                   deps=(), pre=None):
         o = t if out is None else out
-        return self._run(lambda s: self._c.all_reduce(t, o, op, s), async_op)
+        return self._run(lambda s: self._c.all_reduce(t, o, op, s), async_op, deps, pre)
 
-    def reduce(self, t: torch.Tensor, root: int, op: str = "sum", async_op: bool = False):
-        return self._run(lambda s: self._c.reduce(t, t, root, op, s), async_op)
+    def reduce(self, t: torch.Tensor, root: int, op: str = "sum", async_op: bool = False, deps=(), pre=None):
+        return self._run(lambda s: self._c.reduce(t, t, root, op, s), async_op, deps, pre)
 
     def broadcast(self, t: torch.Tensor, root: int, async_op: bool = False):
         return self._run(lambda s: self._c.broadcast(t, root, s), async_op)
@@ -295,13 +303,17 @@ class TorchDistComm:
         g = self.dist.new_group([self._global[r] for r in sorted(ranks)])
         return TorchDistComm(g, self.store) if self.rank in ranks else None
 
-    def all_reduce(self, t, op="sum", async_op=False, out=None):
+    def all_reduce(self, t, op="sum", async_op=False, out=None, deps=(), pre=None):
+        if pre is not None:
+            pre()
         if out is not None and out.data_ptr() != t.data_ptr():
             out.copy_(t)
             t = out
         return self._w(self.dist.all_reduce(t, op=self._op(op), group=self.group, async_op=async_op), async_op)
 
-    def reduce(self, t, root, op="sum", async_op=False):
+    def reduce(self, t, root, op="sum", async_op=False, deps=(), pre=None):
+        if pre is not None:
+            pre()
         return self._w(self.dist.reduce(t, self._global[root], op=self._op(op), group=self.group, async_op=async_op),
                        async_op)
 

@@ -11,9 +11,11 @@ Ordering contract:
 * ``run_wgrad(fn, *tensors)`` forks after everything queued on the current stream and keeps
   ``tensors`` (what fn reads) alive until the next ``join()``. The caching allocator may otherwise
   hand their memory to later main-stream kernels while the side stream still reads it.
-* ``sync()``: the current stream waits for all side-stream work. Gradient-reduction hooks call it
-  before launching a bucket (MWMS all-reduce, PS reduce), because a bucket mixes gradients from
-  both streams.
+* ``producers()``: issue the queued weight gradients and return the side streams forked since the
+  last join. Gradient-bucket collectives (MWMS all-reduce, PS reduce) make THEIR comm stream wait
+  on these plus the current stream -- a bucket mixes gradients from both -- so the main stream's
+  input-gradient chain never waits for queued weight gradients at a bucket launch.
+* ``sync()``: the current stream waits for all side-stream work.
 * ``join()``: sync plus release the kept tensors. Models call it at the end of backward, before the
   optimizer reads ``arena.grad``.
 
@@ -60,6 +62,7 @@ DEFER = True
 FLUSH_EVERY = 1
 _pending: list = []
 _flushes = 0
+_used: dict[int, torch.cuda.Stream] = {}  # side streams forked since the last join (by id)
 
 
 def _concurrent(tensors) -> bool:
@@ -73,6 +76,7 @@ def _fork(items) -> None:
     main = torch.cuda.current_stream(dev)
     k, side = _stream(dev)
     side.wait_stream(main)
+    _used[id(side)] = side
     prev = _lib.WGRAD_SLOT
     _lib.WGRAD_SLOT, _lib.ON_SIDE_STREAM = f"splitk_wgrad{k}", True
     try:
@@ -110,6 +114,13 @@ def flush(force: bool = False) -> None:
         _fork(items)
 
 
+def producers() -> list:
+    """Issue the queued weight gradients; return the side streams (forked since the last join) that a
+    consumer of arena.grad on ANOTHER stream must wait on. The current stream is not joined."""
+    flush(force=True)
+    return list(_used.values())
+
+
 def sync() -> None:
     """The current stream waits for every weight gradient queued on the side stream."""
     flush(force=True)
@@ -126,6 +137,7 @@ def reset() -> None:
     global _flushes
     _pending.clear()
     _keep.clear()
+    _used.clear()
     _flushes = 0
 
 
@@ -133,3 +145,4 @@ def join() -> None:
     """sync() + release the tensors the side-stream work read."""
     sync()
     _keep.clear()
+    _used.clear()

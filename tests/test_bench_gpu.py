@@ -85,10 +85,10 @@ def test_bench_collective_ps_colocated_one_gpu(tmp_path):
     assert c["hipgraph"] is True and d["loss"] is not None and d["loss"] == d["loss"]
 
 
-def _run_model(tmp_path, model, extra, batch=None):
+def _run_model(tmp_path, model, extra, batch=None, force=True):
     env = dict(os.environ, PYTHONPATH=ROOT)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--model", model, "--steps", "6", "--warmup", "3",
-           "--force-comm", "--report-update"] + (["--batch", str(batch)] if batch else []) + extra
+           "--report-update"] + (["--force-comm"] if force else []) + (["--batch", str(batch)] if batch else []) + extra
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return _bench_line(r.stdout)
@@ -126,3 +126,20 @@ def test_bench_transformer_big_captured_with_collectives(tmp_path):
     assert ps["config"]["comm"]["transport"] == "rccl" and ps["config"]["comm"]["buckets"] > 1
     # the same model, data and optimizer: the PS update equals the MWMS one at world size 1
     assert abs(ps["loss"] - mw["loss"]) <= 1e-3 * abs(mw["loss"]), (ps["loss"], mw["loss"])
+
+
+@pytest.mark.parametrize("wire", ["f32", "bf16"])
+def test_forced_comm_captured_update_equals_no_comm(tmp_path, wire):
+    """World-size-1 MWMS with the RCCL bucket all-reduces forced on, captured: the bucket launches
+    make the comm stream (not the compute stream) wait on the side-stream weight gradients
+    (runtime/streams.py producers) and pack the bf16 wire there. The master update must equal the
+    no-comm captured step's: bit-for-bit on the f32 wire (a 1-rank sum is the identity), to bf16
+    rounding of the gradients on the bf16 wire. A bucket launched before one of its weight gradients
+    finished would reduce a stale slice and change the update."""
+    nc = _run_model(tmp_path, "resnet50", ["--comm-dtype", wire], batch=64, force=False)
+    fc = _run_model(tmp_path, "resnet50", ["--comm-dtype", wire], batch=64)
+    assert nc["config"]["hipgraph"] and fc["config"]["hipgraph"]
+    assert fc["config"]["comm"]["wire_mb_per_step"] > 0 and nc["config"]["comm"]["wire_mb_per_step"] == 0
+    tol = 1e-5 if wire == "f32" else 2e-2
+    assert abs(fc["update_norm"] - nc["update_norm"]) <= tol * nc["update_norm"], (fc["update_norm"], nc["update_norm"])
+    assert abs(fc["loss"] - nc["loss"]) <= tol * abs(nc["loss"]) + 1e-6, (fc["loss"], nc["loss"])

@@ -317,7 +317,7 @@ def main():
             "config": {"model": args.model, "global_batch": gb, "seq_len": None, "per_gpu_batch": args.batch,
                        "parallelism": par, "strategy": strat_name,
                        "optimizer": opt_name, "hipgraph": runner.use_graph, "comm": comm_cfg},
-            "loss": loss,
+            "loss": loss, **_update_report(model, master0),
         }), flush=True)
     if wd is not None:
         wd.exit_code = 0  # the result is out: a hung teardown must not turn the run into a failure

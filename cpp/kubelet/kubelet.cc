@@ -1,11 +1,14 @@
 #include "kubelet.h"
 
 #include "../api/types.h"
+#include "../controller/trainer.h"
 
 #include <dirent.h>
-#include <sched.h>
 #include <fcntl.h>
+#include <ftw.h>
+#include <sched.h>
 #include <signal.h>
+#include <sys/mount.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -111,6 +114,38 @@ static void mkdirs(const std::string& p) {
   }
 }
 
+static int rm_entry(const char* path, const struct stat*, int, struct FTW*) { return remove(path); }
+static void remove_tree(const std::string& p) { nftw(p.c_str(), rm_entry, 16, FTW_DEPTH | FTW_PHYS); }
+
+// One volumeMount resolved to its host directory.
+struct MountSpec {
+  std::string src, dst;
+  bool ro = false;
+};
+
+// Path substitution (no mount namespace): a token that IS a mount path or starts with "<mountPath>/"
+// -- at the start of the string or after '=', ':' or ',' (--flag=/mnt/x, PATH-like lists) -- is
+// rewritten onto the host directory. Longest mount path first.
+static std::string subst_paths(const std::string& s, const std::vector<MountSpec>& mounts) {
+  std::string out = s;
+  for (auto& m : mounts) {
+    if (m.dst.empty() || m.dst == m.src) continue;
+    size_t pos = 0;
+    while ((pos = out.find(m.dst, pos)) != std::string::npos) {
+      const bool start_ok = pos == 0 || out[pos - 1] == '=' || out[pos - 1] == ':' || out[pos - 1] == ',';
+      const size_t e = pos + m.dst.size();
+      const bool end_ok = e == out.size() || out[e] == '/' || out[e] == ':' || out[e] == ',';
+      if (start_ok && end_ok) {
+        out.replace(pos, m.dst.size(), m.src);
+        pos += m.src.size();
+      } else {
+        pos = e;
+      }
+    }
+  }
+  return out;
+}
+
 Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletOptions o) : client_(std::move(c)), opts_(std::move(o)) {
   if (opts_.gpus < 0) opts_.gpus = detect_gpus();
   if (opts_.cpu_milli <= 0) opts_.cpu_milli = (long long)sysconf(_SC_NPROCESSORS_ONLN) * 1000;
@@ -126,6 +161,58 @@ Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletOptions o) : client_(std::mov
   mkdirs(opts_.root_dir + "/logs");
   mkdirs(opts_.root_dir + "/term");
   pods_inf_.reset(new SharedInformer(client_, "pods", "", 10000, "", "spec.nodeName=" + opts_.node_name));
+  rec_ = std::make_shared<EventRecorder>(client_, "kubelet");
+}
+
+// Whether this kubelet may give containers a private mount namespace with bind mounts (needs
+// CAP_SYS_ADMIN): tried once in a throw-away child.
+bool Kubelet::mount_ns_supported() {
+  if (mount_ns_ >= 0) return mount_ns_ == 1;
+  std::string base = opts_.root_dir + "/nsprobe", src = base + "/src", dst = base + "/dst";
+  mkdirs(src);
+  mkdirs(dst);
+  pid_t pid = fork();
+  if (pid == 0) {
+    if (unshare(CLONE_NEWNS) != 0) _exit(1);
+    if (mount(nullptr, "/", nullptr, MS_REC | MS_PRIVATE, nullptr) != 0) _exit(2);
+    if (mount(src.c_str(), dst.c_str(), nullptr, MS_BIND, nullptr) != 0) _exit(3);
+    _exit(0);
+  }
+  int status = 1;
+  if (pid > 0) waitpid(pid, &status, 0);
+  mount_ns_ = (pid > 0 && WIFEXITED(status) && WEXITSTATUS(status) == 0) ? 1 : 0;
+  TFK_LOG(Info, "volume mounts", Json(Json::object_t{{"mode", Json(mount_ns_ ? "namespace" : "substitute")}}));
+  return mount_ns_ == 1;
+}
+
+std::map<std::string, std::string> Kubelet::pod_volumes(PodRun& pr, std::string* err) {
+  std::map<std::string, std::string> out;
+  for (auto& v : pr.pod.path("spec.volumes").items()) {
+    const std::string name = v.at("name").str();
+    if (v.at("hostPath").is_object()) {
+      const std::string path = v.path("hostPath.path").str(), type = v.path("hostPath.type").str();
+      struct stat sb;
+      const bool exists = stat(path.c_str(), &sb) == 0;
+      if (type == "DirectoryOrCreate" && !exists) {
+        mkdirs(path);
+      } else if (type == "Directory" && !(exists && S_ISDIR(sb.st_mode))) {
+        *err = "hostPath type check failed: " + path + " is not a directory";
+        return {};
+      }
+      out[name] = path;
+    } else if (v.at("persistentVolumeClaim").is_object()) {
+      // PVC-like: one directory per (namespace, claim) under the kubelet root, outliving pods
+      std::string d = opts_.root_dir + "/pvc/" + pr.ns + "/" + v.path("persistentVolumeClaim.claimName").str();
+      mkdirs(d);
+      out[name] = d;
+    } else {
+      // emptyDir (and kinds this node does not implement): a per-pod directory removed with the pod
+      std::string d = opts_.root_dir + "/pods/" + pr.uid + "/volumes/" + name;
+      mkdirs(d);
+      out[name] = d;
+    }
+  }
+  return out;
 }
 
 Kubelet::~Kubelet() {
@@ -184,6 +271,38 @@ void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
   for (auto& a : spec->at("command").items()) argv.push_back(a.str());
   for (auto& a : spec->at("args").items()) argv.push_back(a.str());
   if (argv.empty()) argv.push_back("/bin/true");
+  // volumes -> mounts of this container
+  std::string verr;
+  auto vols = pod_volumes(pr, &verr);
+  std::vector<MountSpec> mounts;
+  for (auto& vm : spec->at("volumeMounts").items()) {
+    auto it = vols.find(vm.at("name").str());
+    if (it == vols.end()) {
+      verr = "volumeMount " + vm.at("name").str() + " names no volume of the pod";
+      break;
+    }
+    MountSpec m;
+    m.src = it->second;
+    const std::string sub = vm.at("subPath").str();
+    if (!sub.empty()) {
+      m.src += "/" + sub;
+      mkdirs(m.src);
+    }
+    m.dst = vm.at("mountPath").str();
+    m.ro = vm.at("readOnly").as_bool(false);
+    while (m.dst.size() > 1 && m.dst.back() == '/') m.dst.pop_back();
+    if (!m.dst.empty() && m.dst != m.src) mounts.push_back(m);
+  }
+  if (!verr.empty()) {
+    c.state = "waiting";
+    c.waiting_reason = "CreateContainerConfigError";
+    c.next_start_ms = mono_ms() + opts_.restart_backoff_ms;
+    rec_->event(pr.pod, "Warning", "FailedMount", verr);
+    return;
+  }
+  std::sort(mounts.begin(), mounts.end(), [](const MountSpec& a, const MountSpec& b) { return a.dst.size() > b.dst.size(); });
+  const bool use_ns = !mounts.empty() && (opts_.volume_mode == "namespace" ||
+                                          (opts_.volume_mode == "auto" && mount_ns_supported()));
   std::map<std::string, std::string> env;
   for (char** e = environ; *e; ++e) {
     std::string kv = *e;
@@ -238,11 +357,52 @@ void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
   env["TFK_TERMINATION_LOG"] = c.term_path;
   if (opts_.local_dns) env["TFK_LOCAL_DNS"] = "1";
   std::string wd = spec->at("workingDir").str();
+  if (!mounts.empty() && !use_ns) {
+    // no mount namespace: the container sees its volumes at the host directories -- rewrite the
+    // paths it was given, and tell the runtime the map for paths it reads from elsewhere
+    std::string vmap;
+    for (auto& m : mounts) vmap += (vmap.empty() ? "" : ";") + m.dst + "=" + m.src;
+    for (auto& a : argv) a = subst_paths(a, mounts);
+    for (auto& kv : env) kv.second = subst_paths(kv.second, mounts);
+    wd = subst_paths(wd, mounts);
+    env["TFK_VOLUME_MAP"] = vmap;
+  }
+  for (auto& m : mounts)
+    if (use_ns) mkdirs(m.dst);  // the mount points (the namespace shares the host's tree)
+  std::vector<std::string> msrc, mdst;
+  std::vector<char> mro;
+  if (use_ns)
+    for (auto& m : mounts) { msrc.push_back(m.src); mdst.push_back(m.dst); mro.push_back(m.ro); }
+  static const char kMountFail[] = "tfk-kubelet: volume mount failed\n";
+  // resources.limits.memory (enforced by the sync loop's RSS poll)
+  c.mem_limit = 0;
+  c.mem_peak = 0;
+  const Json& ml = spec->path("resources.limits").at("memory");
+  if (ml.is_string() || ml.is_number()) {
+    long long b = ml.is_number() ? (long long)ml.as_double() : parse_bytes(ml.str());
+    if (b > 0) c.mem_limit = b;
+  }
+  // probes (their exec commands see the volumes at the host paths)
+  c.liveness.reset();
+  c.readiness.reset();
+  c.startup.reset();
+  c.liveness.spec = ProbeSpec::parse(spec->at("livenessProbe"), *spec);
+  c.readiness.spec = ProbeSpec::parse(spec->at("readinessProbe"), *spec);
+  c.startup.spec = ProbeSpec::parse(spec->at("startupProbe"), *spec);
+  for (ProbeState* ps : {&c.liveness, &c.readiness, &c.startup})
+    for (auto& a : ps->spec.command) a = subst_paths(a, mounts);
+  c.started = !c.startup.spec.enabled();
+  c.ready = false;
+  c.kill_reason.clear();
+  c.kill_deadline = 0;
   // Everything the child needs is built BEFORE fork(): the kubelet is multithreaded (informer,
   // HTTP and watch threads), so between fork and exec the child may only make async-signal-safe
   // calls -- a malloc there can deadlock on a lock another thread held at fork time.
   std::vector<std::string> envs;
   for (auto& kv : env) envs.push_back(kv.first + "=" + kv.second);
+  // exec probes run outside any mount namespace: their environment sees the volumes at host paths
+  c.env.clear();
+  for (auto& kv : env) c.env.push_back(kv.first + "=" + subst_paths(kv.second, mounts));
   std::vector<char*> ev, av;
   for (auto& s : envs) ev.push_back((char*)s.c_str());
   ev.push_back(nullptr);
@@ -273,6 +433,22 @@ void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
     signal(SIGINT, SIG_DFL);
     setsid();
     int fd = open(log_path, O_WRONLY | O_CREAT | O_APPEND, 0644);
+    if (!msrc.empty()) {
+      // private mount namespace: bind each volume at its mountPath (read-only when asked)
+      bool ok = unshare(CLONE_NEWNS) == 0 && mount(nullptr, "/", nullptr, MS_REC | MS_PRIVATE, nullptr) == 0;
+      for (size_t i = 0; ok && i < msrc.size(); ++i) {
+        ok = mount(msrc[i].c_str(), mdst[i].c_str(), nullptr, MS_BIND | MS_REC, nullptr) == 0;
+        if (ok && mro[i])
+          ok = mount(nullptr, mdst[i].c_str(), nullptr, MS_BIND | MS_REMOUNT | MS_RDONLY | MS_REC, nullptr) == 0;
+      }
+      if (!ok) {
+        if (fd >= 0) {
+          ssize_t wr = write(fd, kMountFail, sizeof(kMountFail) - 1);
+          (void)wr;
+        }
+        _exit(127);
+      }
+    }
     if (fd >= 0) { dup2(fd, 1); dup2(fd, 2); close(fd); }
     int nul = open("/dev/null", O_RDONLY);
     if (nul >= 0) { dup2(nul, 0); close(nul); }
@@ -304,11 +480,103 @@ void Kubelet::kill_pod(PodRun& pr, int sig) {
     if (c.pid > 0) kill(-c.pid, sig);
 }
 
+void Kubelet::kill_container(PodRun& pr, ContainerRun& c, const std::string& reason, const std::string& msg, bool now) {
+  if (c.pid <= 0 || !c.kill_reason.empty()) return;
+  c.kill_reason = reason;
+  rec_->event(pr.pod, "Warning", reason == "OOMKilled" ? "OOMKilling" : "Unhealthy", c.name + ": " + msg);
+  TFK_LOG(Warn, "killing container", Json(Json::object_t{{"pod", Json(pr.ns + "/" + pr.name)}, {"container", Json(c.name)},
+                                                       {"reason", Json(reason)}, {"message", Json(msg)}}));
+  std::ofstream(c.term_path + ".kubelet") << msg;
+  if (now) {
+    kill(-c.pid, SIGKILL);
+  } else {
+    const Json& g = pr.pod.path("spec.terminationGracePeriodSeconds");
+    kill(-c.pid, SIGTERM);
+    c.kill_deadline = mono_ms() + (g.is_number() ? (int64_t)(g.as_double() * 1000) : opts_.grace_ms);
+  }
+}
+
+// One probe: settle a finished execution (consecutive-success / failure counting), start the next
+// one when it is due. Returns whether a result was settled.
+bool Kubelet::step_probe(ProbeState& ps, ContainerRun& c) {
+  bool settled = false;
+  if (ps.inflight) {
+    const int st = ps.inflight->state.load(std::memory_order_acquire);
+    if (st == 0) return false;
+    if (st == 1) {
+      ps.fails = 0;
+      if (++ps.succ >= ps.spec.success_threshold) ps.ok = true;
+    } else {
+      ps.succ = 0;
+      ps.last_message = ps.inflight->message;
+      if (++ps.fails >= ps.spec.failure_threshold) ps.ok = false;
+    }
+    ps.inflight.reset();
+    settled = true;
+  }
+  const int64_t now = mono_ms();
+  if (ps.next_ms == 0) ps.next_ms = std::max(now, c.started_mono + ps.spec.initial_delay_ms);
+  if (!ps.inflight && now >= ps.next_ms) {
+    ps.inflight = launch_probe(ps.spec, c.env);
+    ps.next_ms = now + ps.spec.period_ms;
+  }
+  return settled;
+}
+
+void Kubelet::probe_container(PodRun& pr, ContainerRun& c) {
+  if (c.state != "running" || c.pid <= 0 || !c.kill_reason.empty()) return;
+  if (!c.started) {
+    step_probe(c.startup, c);
+    if (c.startup.ok) {
+      c.started = true;
+    } else if (c.startup.fails >= c.startup.spec.failure_threshold) {
+      kill_container(pr, c, "Unhealthy", "Startup probe failed: " + c.startup.last_message, false);
+      return;
+    }
+  }
+  if (!c.started) {
+    c.ready = false;
+    return;
+  }
+  if (c.liveness.spec.enabled()) {
+    step_probe(c.liveness, c);
+    if (c.liveness.fails >= c.liveness.spec.failure_threshold) {
+      kill_container(pr, c, "Unhealthy", "Liveness probe failed: " + c.liveness.last_message, false);
+      return;
+    }
+  }
+  if (c.readiness.spec.enabled()) {
+    step_probe(c.readiness, c);
+    c.ready = c.readiness.ok;
+  } else {
+    c.ready = true;
+  }
+}
+
+void Kubelet::check_memory(PodRun& pr) {
+  bool any = false;
+  for (auto& c : pr.containers) any |= c.mem_limit > 0 && c.pid > 0;
+  if (!any) return;
+  auto rss = session_rss_bytes();
+  for (auto& c : pr.containers) {
+    if (c.mem_limit <= 0 || c.pid <= 0 || !c.kill_reason.empty()) continue;
+    auto it = rss.find(c.pid);
+    const long long used = it == rss.end() ? 0 : it->second;
+    c.mem_peak = std::max(c.mem_peak, used);
+    if (used > c.mem_limit)
+      kill_container(pr, c, "OOMKilled", "memory limit exceeded: resident " + std::to_string(used >> 20) + " MiB > limit " +
+                                             std::to_string(c.mem_limit >> 20) + " MiB", true);
+  }
+}
+
 void Kubelet::reap() {
-  while (true) {
+  // only the containers' own pids: probe threads wait for their exec children themselves
+  std::vector<pid_t> pids;
+  for (auto& kv : pid_owner_) pids.push_back(kv.first);
+  for (pid_t want : pids) {
     int status = 0;
-    pid_t pid = waitpid(-1, &status, WNOHANG);
-    if (pid <= 0) break;
+    pid_t pid = waitpid(want, &status, WNOHANG);
+    if (pid <= 0) continue;
     auto it = pid_owner_.find(pid);
     if (it == pid_owner_.end()) continue;
     auto pit = pods_.find(it->second.first);
@@ -323,6 +591,18 @@ void Kubelet::reap() {
     std::ifstream tf(c.term_path);
     std::string msg((std::istreambuf_iterator<char>(tf)), std::istreambuf_iterator<char>());
     if (msg.find("OOMKilled") != std::string::npos) c.reason = "OOMKilled";
+    if (!c.kill_reason.empty()) {
+      // killed by this kubelet (memory limit, failed probe): its reason and message win
+      std::ifstream kf(c.term_path + ".kubelet");
+      std::string km((std::istreambuf_iterator<char>(kf)), std::istreambuf_iterator<char>());
+      if (c.kill_reason == "OOMKilled") c.reason = "OOMKilled";
+      if (!km.empty()) msg = km + (msg.empty() ? "" : "\n" + msg);
+      unlink((c.term_path + ".kubelet").c_str());
+      c.kill_reason.clear();
+      c.kill_deadline = 0;
+    }
+    c.ready = false;
+    for (ProbeState* ps : {&c.liveness, &c.readiness, &c.startup}) ps->inflight.reset();
     c.finished_at = rfc3339(now_ms());
     c.state = "terminated";
     Json term = Json::object();
@@ -349,13 +629,14 @@ void Kubelet::reap() {
 
 Json Kubelet::build_status(PodRun& pr) {
   Json st = Json::object();
-  bool all_done = true, any_failed = false, all_zero = true, any_running = false;
+  bool all_done = true, any_failed = false, all_zero = true, any_running = false, all_ready = !pr.containers.empty();
   Json css = Json::array();
   for (auto& c : pr.containers) {
     Json cs = Json::object();
     cs["name"] = c.name;
     cs["restartCount"] = c.restarts;
-    cs["ready"] = c.state == "running";
+    cs["ready"] = c.state == "running" && c.ready;
+    cs["started"] = c.state == "running" && c.started;
     cs["image"] = "";
     if (c.state == "running") {
       cs["state"]["running"]["startedAt"] = c.started_at;
@@ -368,6 +649,7 @@ Json Kubelet::build_status(PodRun& pr) {
     if (c.last_terminated.is_object() && !(c.state == "terminated" && c.done))
       cs["lastState"]["terminated"] = c.last_terminated;
     css.push_back(cs);
+    all_ready = all_ready && c.state == "running" && c.ready;
     if (!c.done) all_done = false;
     if (c.done && c.exit_code != 0) { any_failed = true; all_zero = false; }
   }
@@ -385,8 +667,11 @@ Json Kubelet::build_status(PodRun& pr) {
   st["containerStatuses"] = css;
   Json rc = Json::object();
   rc["type"] = "Ready";
-  rc["status"] = any_running ? "True" : "False";
-  st["conditions"] = Json(Json::array_t{rc});
+  rc["status"] = all_ready ? "True" : "False";
+  Json cr = Json::object();
+  cr["type"] = "ContainersReady";
+  cr["status"] = all_ready ? "True" : "False";
+  st["conditions"] = Json(Json::array_t{rc, cr});
   return st;
 }
 
@@ -409,6 +694,8 @@ void Kubelet::update_status(PodRun& pr) {
 
 void Kubelet::sync_once() {
   reap();
+  const bool poll_mem = mono_ms() - last_mem_poll_ >= opts_.memory_poll_ms;
+  if (poll_mem) last_mem_poll_ = mono_ms();
   std::set<std::string> live;
   for (auto& p : pods_inf_->indexer().list()) {
     if (p.path("spec.nodeName").str() != opts_.node_name) continue;
@@ -477,6 +764,16 @@ void Kubelet::sync_once() {
         c.next_start_ms = 0;
         start_container(pr, c);
       }
+    if (!pr.killing) {
+      for (auto& c : pr.containers) {
+        probe_container(pr, c);
+        if (c.pid > 0 && c.kill_deadline > 0 && mono_ms() > c.kill_deadline) {
+          kill(-c.pid, SIGKILL);  // a probe-killed container that ignored SIGTERM
+          c.kill_deadline = 0;
+        }
+      }
+      if (poll_mem) check_memory(pr);
+    }
     update_status(pr);
   }
   // pods removed from the API (or rebound elsewhere): stop their containers
@@ -490,8 +787,12 @@ void Kubelet::sync_once() {
     bool alive = false;
     for (auto& c : pr.containers) alive |= c.pid > 0;
     if (pr.killing && alive && mono_ms() > pr.kill_deadline) kill_pod(pr, SIGKILL);
-    if (pr.killing && !alive && !live.count(it->first)) it = pods_.erase(it);
-    else ++it;
+    if (pr.killing && !alive && !live.count(it->first)) {
+      remove_tree(opts_.root_dir + "/pods/" + it->first);  // the pod's emptyDir volumes
+      it = pods_.erase(it);
+    } else {
+      ++it;
+    }
   }
   if (mono_ms() - last_heartbeat_ > opts_.heartbeat_ms) {
     register_node(true);

@@ -5,6 +5,14 @@
 // OOMKilled via the termination-message file, restartCount, lastState), keeps per-container log
 // files (tfk.io/log-path), heartbeats its Node object, and injects faults on request
 // (annotation tfk.io/fault-kill-after-ms / tfk.io/fault-signal / tfk.io/fault-generation).
+// Health checking (k8s-operator.md:1): liveness / readiness / startup probes (probe.h) -- a failed
+// liveness or startup probe kills the container (restart per policy), readiness drives
+// containerStatuses[].ready and the pod's Ready condition. Memory: resources.limits.memory is
+// enforced by polling the container session's resident set; a breach is SIGKILLed with reason
+// OOMKilled (permanent, k8s-operator.md:5). Storage (:2): hostPath, emptyDir (lives as long as the
+// pod) and persistentVolumeClaim (a per-namespace directory under the kubelet root) volumes at
+// their volumeMounts' mountPath -- bind mounts in a private mount namespace when the kubelet may
+// create one, else path substitution in args/env/workingDir plus TFK_VOLUME_MAP for the runtime.
 #pragma once
 #include <sys/types.h>
 
@@ -14,6 +22,7 @@
 #include <vector>
 
 #include "../cache/informer.h"
+#include "probe.h"
 
 namespace tfk {
 
@@ -32,6 +41,8 @@ struct KubeletOptions {
   std::string gpu_numa;   // e.g. "0,0,0,0,1,1,1,1"
   std::string numa_cpus;  // e.g. "0-47,96-143;48-95,144-191" (';' separates NUMA nodes)
   bool pin_cpus = true;   // sched_setaffinity of containers to their GPUs' NUMA CPUs
+  std::string volume_mode = "auto";  // auto | namespace | substitute (see header comment)
+  int64_t memory_poll_ms = 200;      // resources.limits.memory enforcement period
 };
 
 struct Topology {
@@ -55,6 +66,16 @@ struct ContainerRun {
   Json last_terminated;
   std::string log_path, term_path;
   bool done = false;  // terminal, no more restarts
+  // health checking
+  ProbeState liveness, readiness, startup;
+  bool started = false;  // startupProbe passed (or none)
+  bool ready = false;
+  std::vector<std::string> env;  // the container's environment (exec probes run in it)
+  // kill requested by the kubelet itself: reason reported at exit (OOMKilled) / SIGKILL deadline
+  std::string kill_reason;
+  int64_t kill_deadline = 0;
+  long long mem_limit = 0;  // bytes, 0 = unlimited
+  long long mem_peak = 0;
 };
 
 struct PodRun {
@@ -87,13 +108,22 @@ class Kubelet {
   void kill_pod(PodRun& pr, int sig);
   void update_status(PodRun& pr);
   Json build_status(PodRun& pr);
+  void probe_container(PodRun& pr, ContainerRun& c);
+  bool step_probe(ProbeState& ps, ContainerRun& c);  // true when the result changed this call
+  void kill_container(PodRun& pr, ContainerRun& c, const std::string& reason, const std::string& msg, bool now);
+  void check_memory(PodRun& pr);
+  // volume name -> host directory for this pod ("" + *err on a bad volume)
+  std::map<std::string, std::string> pod_volumes(PodRun& pr, std::string* err);
+  bool mount_ns_supported();
   std::shared_ptr<Client> client_;
   KubeletOptions opts_;
   std::unique_ptr<SharedInformer> pods_inf_;
   std::map<std::string, PodRun> pods_;  // uid -> run
   std::map<pid_t, std::pair<std::string, size_t>> pid_owner_;
-  int64_t last_heartbeat_ = 0;
+  int64_t last_heartbeat_ = 0, last_mem_poll_ = 0;
   Topology topo_;
+  std::shared_ptr<class EventRecorder> rec_;
+  int mount_ns_ = -1;  // -1 unknown, 0 no, 1 yes
 };
 
 }  // namespace tfk

@@ -23,6 +23,7 @@ int main(int argc, char** argv) {
   fs.add_int("gpus", &gpus, "node amd.com/gpu capacity (-1 = detect)");
   fs.add_string("gpu-numa", &ko.gpu_numa, "NUMA node per GPU, e.g. 0,0,0,0,1,1,1,1 (default: sysfs)");
   fs.add_string("numa-cpus", &ko.numa_cpus, "CPU list per NUMA node, ';'-separated (default: sysfs)");
+  fs.add_string("volume-mode", &ko.volume_mode, "volume mounts: auto | namespace (bind mounts) | substitute (path rewrite)");
   fs.add_string("root-dir", &ko.root_dir, "kubelet state/log dir");
   fs.add_int("restart-backoff-ms", &backoff, "kubelet restart backoff");
   fs.add_int("threadiness", &so.threadiness, "operator workers");

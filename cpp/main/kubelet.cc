@@ -16,6 +16,7 @@ int main(int argc, char** argv) {
   fs.add_int("gpus", &gpus, "amd.com/gpu capacity (-1 = detect)");
   fs.add_string("gpu-numa", &ko.gpu_numa, "NUMA node per GPU, e.g. 0,0,0,0,1,1,1,1 (default: sysfs)");
   fs.add_string("numa-cpus", &ko.numa_cpus, "CPU list per NUMA node, ';'-separated (default: sysfs)");
+  fs.add_string("volume-mode", &ko.volume_mode, "volume mounts: auto | namespace (bind mounts) | substitute (path rewrite)");
   fs.add_string("root-dir", &ko.root_dir, "state/log directory");
   fs.add_int("restart-backoff-ms", &backoff, "base container restart backoff");
   fs.add_int("grace-ms", &grace, "termination grace period");
@@ -23,6 +24,7 @@ int main(int argc, char** argv) {
   fs.add_string("log-level", &level, "log level");
   std::string err;
   if (!fs.parse(argc, argv, &err)) { fprintf(stderr, "%s\n", err.c_str()); return 2; }
+  if (fs.help_requested()) { printf("%s", fs.usage().c_str()); return 0; }
   InitLogging("tfk-kubelet", json, level);
   ko.gpus = (int)gpus;
   ko.restart_backoff_ms = backoff;

@@ -24,6 +24,7 @@
 #include "../apiserver/store.h"
 #include "../cache/informer.h"
 #include "../client/client.h"
+#include "../kubelet/probe.h"
 #include "../common/json.h"
 #include "../common/util.h"
 #include "../controller/trainer.h"
@@ -806,6 +807,62 @@ TEST(tf_bundle_roundtrip) {
   CHECK(!r2.read("dense/kernel", &bytes, &err));
   std::string cmd = "rm -rf " + dir;
   CHECK(system(cmd.c_str()) == 0);
+}
+
+TEST(kubelet_quantities_and_probe_specs) {
+  CHECK_EQ(parse_bytes("128Mi"), 128LL << 20);
+  CHECK_EQ(parse_bytes("2Gi"), 2LL << 30);
+  CHECK_EQ(parse_bytes("1G"), 1000000000LL);
+  CHECK_EQ(parse_bytes("1500k"), 1500000LL);
+  CHECK_EQ(parse_bytes("4096"), 4096LL);
+  CHECK_EQ(parse_bytes("12Qi"), -1LL);
+  CHECK_EQ(parse_bytes(""), -1LL);
+  Json ctr = Json::parse(R"({"name":"tensorflow","ports":[{"name":"http","containerPort":8080}]})");
+  ProbeSpec h = ProbeSpec::parse(Json::parse(R"({"httpGet":{"port":"http","path":"healthz"},"periodSeconds":2})"), ctr);
+  CHECK_EQ(h.kind, std::string("http"));
+  CHECK_EQ(h.port, 8080);
+  CHECK_EQ(h.path, std::string("/healthz"));
+  CHECK_EQ(h.period_ms, (int64_t)2000);
+  CHECK_EQ(h.timeout_ms, (int64_t)1000);  // Kubernetes defaults
+  CHECK_EQ(h.failure_threshold, 3);
+  CHECK(!ProbeSpec::parse(Json(), ctr).enabled());
+}
+
+TEST(kubelet_probe_handlers) {
+  auto wait = [](std::shared_ptr<ProbeSlot> s) {
+    for (int i = 0; i < 400 && s->state.load() == 0; ++i) usleep(10000);
+    return s->state.load();
+  };
+  std::vector<std::string> env = {"PATH=/usr/bin:/bin"};
+  ProbeSpec ok;
+  ok.kind = "exec";
+  ok.command = {"true"};
+  CHECK_EQ(wait(launch_probe(ok, env)), 1);
+  ProbeSpec bad = ok;
+  bad.command = {"sh", "-c", "exit 3"};
+  auto sb = launch_probe(bad, env);
+  CHECK_EQ(wait(sb), 2);
+  CHECK(sb->message.find("exited with 3") != std::string::npos);
+  ProbeSpec slow = ok;
+  slow.command = {"sleep", "5"};
+  slow.timeout_ms = 100;
+  auto ss = launch_probe(slow, env);
+  CHECK_EQ(wait(ss), 2);
+  CHECK(ss->message.find("timed out") != std::string::npos);
+  // tcp: a listening socket passes, a closed port fails
+  int fd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  CHECK(bind(fd, (sockaddr*)&a, sizeof a) == 0 && listen(fd, 4) == 0);
+  socklen_t l = sizeof a;
+  getsockname(fd, (sockaddr*)&a, &l);
+  ProbeSpec t;
+  t.kind = "tcp";
+  t.port = ntohs(a.sin_port);
+  CHECK_EQ(wait(launch_probe(t, env)), 1);
+  close(fd);
+  CHECK_EQ(wait(launch_probe(t, env)), 2);
 }
 
 int main(int argc, char** argv) { return tfk_test::run_all(argc, argv); }

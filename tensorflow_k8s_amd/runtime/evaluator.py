@@ -47,7 +47,9 @@ def run_evaluator(args) -> int:
     mgr = CheckpointManager(args.checkpoint_dir, args.keep)
     seen = set()
     deadline = time.time() + args.eval_timeout
+    from . import health
     while True:
+        health.beat()
         latest = mgr.latest()
         if latest is not None and latest not in seen:
             seen.add(latest)

@@ -92,7 +92,25 @@ def parse_args(argv=None):
     # evaluator
     ap.add_argument("--eval-batches", type=int, default=4)
     ap.add_argument("--eval-timeout", type=float, default=600.0)
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    for k in ("checkpoint_dir", "metrics_file", "trace_file"):
+        setattr(args, k, volume_path(getattr(args, k)))
+    return args
+
+
+def volume_path(p: str) -> str:
+    """A path under a volumeMount's mountPath -> the host directory behind it, when the kubelet ran
+    this container without a mount namespace (TFK_VOLUME_MAP="<mountPath>=<hostDir>;..."; the kubelet
+    already rewrote the paths in args/env, this covers ones from config files or code)."""
+    vm = os.environ.get("TFK_VOLUME_MAP", "")
+    if not p or not vm:
+        return p
+    best = None
+    for ent in vm.split(";"):
+        dst, _, src = ent.partition("=")
+        if dst and (p == dst or p.startswith(dst.rstrip("/") + "/")) and (best is None or len(dst) > len(best[0])):
+            best = (dst, src)
+    return best[1] + p[len(best[0]):] if best else p
 
 
 def model_kwargs(args) -> dict:
@@ -163,6 +181,17 @@ def maybe_fault(step: int, rank: int, arena=None):
     os._exit(code)
 
 
+def _beats(watchdog):
+    """Heartbeat callback of a serving loop: the liveness file (runtime/health.py) + the watchdog."""
+    from . import health
+
+    def beat(*a, **k):
+        health.beat()
+        if watchdog is not None:
+            watchdog.beat(*a, **k)
+    return beat
+
+
 def run_ps(args, info, dev, world_comm, watchdog=None) -> int:
     from ..models import build_model
     from ..parallel import tfk_comm
@@ -184,9 +213,9 @@ def run_ps(args, info, dev, world_comm, watchdog=None) -> int:
         n = server.serve_collective(start, args.steps, args.checkpoint_every if args.checkpoint_dir else 0,
                                     chief=0, final_checkpoint=bool(args.checkpoint_dir), bucket_mb=args.bucket_mb,
                                     comm=world_comm, wire_dtype=_wire(args),
-                                    beat=watchdog.beat if watchdog is not None else None)
+                                    beat=_beats(watchdog))
     else:
-        n = server.serve(beat=watchdog.beat if watchdog is not None else None)
+        n = server.serve(beat=_beats(watchdog))
     _log({"event": "done", "role": "ps", "index": info.task_index, "updates": n})
     if watchdog is not None:
         watchdog.exit_code = 0  # the job's part is done: a hung teardown is not a failure
@@ -266,7 +295,9 @@ def run_worker(args, info, dev, world_comm, watchdog=None) -> int:
     t_last, n_last = time.perf_counter(), 0
     fell_back = False
     step = start
+    from . import health
     while step < args.steps:
+        health.beat()
         with tracer.span("step", cat="train", step=step):
             runner.set_batch(*batches[step % len(batches)])
             runner.step()
@@ -367,6 +398,8 @@ def _guard_error():
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    from . import health
+    health.beat(force=True)  # alive; later beats: setup phases and every step
     from ..parallel import cluster
     from .checkpoint import CheckpointWriteError
     info = cluster.resolve()
@@ -398,6 +431,7 @@ def main(argv=None) -> int:
             _log({"event": "comm_self_test", "rank": info.rank, **comm_self_test(world_comm)})
             if watchdog is not None:
                 watchdog.beat(phase="setup")
+            health.beat()
         try:
             if info.is_ps:
                 return run_ps(args, info, dev, world_comm, watchdog)

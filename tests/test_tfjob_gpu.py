@@ -86,23 +86,29 @@ def test_config4_resnet152_chief_evaluator_fault_restart(gpu_cluster, tmp_path):
     """BASELINE config 4 on the MI355X: ResNet-152 Chief (GPU) + Evaluator (same GPU, outside the
     training world). The chief SIGKILLs itself at step 9 (exit 137, retryable) -> gang restart ->
     resume from the newest complete checkpoint -> Succeeded; the evaluator follows the checkpoint
-    directory and reports an eval for the final checkpoint, which was written after the restart."""
+    directory and reports an eval for the final checkpoint, which was written after the restart.
+    Both replicas mount the checkpoint volume (persistentVolumeClaim) at /tfk-ckpt."""
     c = gpu_cluster.client
-    ck = str(tmp_path / "ck152")
+    # the checkpoints live on a declared volume (a PVC-like directory of the kubelet) mounted into
+    # the chief and the evaluator at /tfk-ckpt (SURVEY §5.4 storage)
+    ck = "/tfk-ckpt/r152"
+    vol = [{"name": "ckpt", "persistentVolumeClaim": {"claimName": "r152-ckpt"}}]
+    mnt = [{"name": "ckpt", "mountPath": "/tfk-ckpt"}]
     common = ["--model", "resnet152", "--image-size", "64", "--num-classes", "100", "--device", "cuda",
               "--checkpoint-dir", ck]
     chief = {"name": "tensorflow", "image": "tfk/runtime", "command": TRAIN,
              "args": common + ["--batch", "16", "--steps", "12", "--checkpoint-every", "4", "--log-every", "2"],
              "env": [{"name": "TFK_FAULT_AT_STEP", "value": "9"}, {"name": "TFK_FAULT_EXIT", "value": "137"}],
-             "resources": {"limits": {"amd.com/gpu": 1}}}
+             "resources": {"limits": {"amd.com/gpu": 1}}, "volumeMounts": mnt}
     evaluator = {"name": "tensorflow", "image": "tfk/runtime", "command": TRAIN,
-                 "args": common + ["--batch", "8", "--eval-batches", "2", "--eval-timeout", "300"]}
+                 "args": common + ["--batch", "8", "--eval-batches", "2", "--eval-timeout", "300"], "volumeMounts": mnt}
     job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": "r152", "namespace": "default"},
            "spec": {"runPolicy": {"backoffLimit": 2, "cleanPodPolicy": "None"},
                     "tfReplicaSpecs": {
-                        "Chief": {"replicas": 1, "restartPolicy": "ExitCode", "template": {"spec": {"containers": [chief]}}},
+                        "Chief": {"replicas": 1, "restartPolicy": "ExitCode",
+                                  "template": {"spec": {"containers": [chief], "volumes": vol}}},
                         "Evaluator": {"replicas": 1, "restartPolicy": "OnFailure",
-                                      "template": {"spec": {"containers": [evaluator]}}}}}}
+                                      "template": {"spec": {"containers": [evaluator], "volumes": vol}}}}}}
     c.create(job)
     j = c.wait_tfjob("r152", timeout=360)
     st = j["status"]
@@ -129,3 +135,5 @@ def test_config4_resnet152_chief_evaluator_fault_restart(gpu_cluster, tmp_path):
     assert any(e["step"] == 12 for e in evals), (evals, c.logs("r152-evaluator-0")[-2000:])
     last = [e for e in evals if e["step"] == 12][-1]
     assert last["loss"] == last["loss"] and 0.0 <= last["accuracy"] <= 1.0 and last["examples"] == 16
+    host = os.path.join(str(tmp_path), "cluster", "kubelet", "pvc", "default", "r152-ckpt", "r152")
+    assert "model.ckpt-12" in open(os.path.join(host, "checkpoint")).read()

@@ -23,7 +23,7 @@ def test_unit_tests(control_plane_bin):
 
 @pytest.mark.parametrize("san", ["thread", "address"])
 def test_unit_tests_sanitized(san):
-    r = subprocess.run(["make", "-C", os.path.join(ROOT, "cpp"), f"-j{min(8, os.cpu_count() or 2)}", f"SAN={san}"],
+    r = subprocess.run(["make", "-C", os.path.join(ROOT, "cpp"), f"-j{max(2, min(8, os.cpu_count() or 2) // 2)}", f"SAN={san}"],
                        capture_output=True, text=True, timeout=1800)
     assert r.returncode == 0, r.stderr[-3000:]
     env = {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1", "ASAN_OPTIONS": "detect_leaks=1"}

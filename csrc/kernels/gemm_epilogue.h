@@ -17,6 +17,24 @@ namespace tfk {
 // the LDS C tile after the store pass (the MX-fp8 engine's producer GEMMs: no separate quantize pass).
 enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1, EPI_BF16_BNR = 2, EPI_BF16_EXT = 3, EPI_BF16_EXT_MX = 4 };
 
+// LDS C-tile swizzle. The accumulator pass stores 8-B pieces (ds_write_b64: 4 groups of 16
+// contiguous lanes = 16 rows x one 4-column piece; bank = dword mod 32). With the padded row stride
+// (BN + 8 elements = 4 mod 32 dwords for BN = 64/128/256) rows r and r+8 of a group hit the same two
+// banks: every accumulator store was a 2-way conflict (the 57-66 % LDS-conflict share of the
+// short-K GEMMs, profiles/pmc_resnet50_r5.txt). Swapping the two 8-B halves of each 16-B chunk in
+// rows with bit 3 set puts rows 8..15 on the banks rows 0..7 leave free, while 16-B chunks stay
+// 16-B aligned for the store pass's ds_read_b128 (which swaps the halves back in registers).
+__device__ __forceinline__ int cswz(int row) { return ((row >> 3) & 1) << 2; }  // element XOR of column
+__device__ __forceinline__ u32x4 cswap(u32x4 v, int row) {
+  return (row & 8) ? u32x4{v[2], v[3], v[0], v[1]} : v;
+}
+__device__ __forceinline__ bf16x8 crd8(const bf16* p, int row) {  // logical 8-column chunk at its 16-B slot
+  return __builtin_bit_cast(bf16x8, cswap(*(const u32x4*)p, row));
+}
+__device__ __forceinline__ void cwr8(bf16* p, bf16x8 v, int row) {
+  *(u32x4*)p = cswap(__builtin_bit_cast(u32x4, v), row);
+}
+
 // Both MX quantizations of the final [rows < BM][cols < BN] bf16 tile in LDS (row stride LDS_S):
 // row blocks of 32 columns -> mx_qr/mx_sr, column pairs of 32-row blocks (one 32-bit LDS word per
 // row holds both columns) -> mx_qc/mx_sc. Same bytes as fp8.hip's mx_quant_dual_kernel.
@@ -42,7 +60,7 @@ __device__ __forceinline__ void mx_tile_out(const GemmParams& p, const bf16* Cs,
       unsigned pp[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const u32x4 h = *(const u32x4*)(Cs + row * lds_s + blk * 32 + q * 8);
+        const u32x4 h = cswap(*(const u32x4*)(Cs + row * lds_s + blk * 32 + q * 8), row);
         pp[4 * q] = h[0]; pp[4 * q + 1] = h[1]; pp[4 * q + 2] = h[2]; pp[4 * q + 3] = h[3];
       }
       unsigned w[8];
@@ -63,8 +81,9 @@ __device__ __forceinline__ void mx_tile_out(const GemmParams& p, const bf16* Cs,
       unsigned lo[16], hi[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const unsigned a = *(const unsigned*)(Cs + (rg * 32 + 2 * r) * lds_s + col);
-        const unsigned b = *(const unsigned*)(Cs + (rg * 32 + 2 * r + 1) * lds_s + col);
+        const int ra = rg * 32 + 2 * r, rb = ra + 1;
+        const unsigned a = *(const unsigned*)(Cs + ra * lds_s + (col ^ cswz(ra)));
+        const unsigned b = *(const unsigned*)(Cs + rb * lds_s + (col ^ cswz(rb)));
         lo[r] = __builtin_amdgcn_perm(b, a, 0x05040100u);
         hi[r] = __builtin_amdgcn_perm(b, a, 0x07060302u);
       }
@@ -176,7 +195,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
   } else {
     constexpr int LDC_S = BN + 8;  // padded bf16 row stride of the LDS C tile
     bf16* Cs = (bf16*)smem;
-    auto cso = [&](int row, int col) { return row * LDC_S + col; };  // element offset in the C tile
+    // element offset of logical (row, col) in the swizzled C tile; cbase: a 16-B chunk's slot (col % 8 == 0)
+    auto cso = [&](int row, int col) { return row * LDC_S + (col ^ cswz(row)); };
+    auto cbase = [&](int row, int col8) { return row * LDC_S + col8; };
     float csum[FN][4], csq[FN][4];
 #pragma unroll
     for (int j = 0; j < FN; ++j)
@@ -280,19 +301,20 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         unsigned mk[GS], zb[GS];
         long long off[GS];
         bool rok[GS];
-        int mlog[GS], nlog[GS], lofs[GS];
+        int mlog[GS], nlog[GS], lofs[GS], lrow[GS];
 #pragma unroll
         for (int g = 0; g < GS; ++g) {
           const int idx = tid + (g0 + g) * NT;
           const int row = idx / CPR, cc = idx - row * CPR;
-          lofs[g] = cso(row, cc * 8);
+          lofs[g] = cbase(row, cc * 8);
+          lrow[g] = row;
           const int m = m0 + row, n = n0 + cc * 8;
           long long mo = m, mr = m;
           if constexpr (bnr) { mo = out_row(p, m); mr = resid_row(p, mo); }
           off[g] = bz * p.sC + mo * p.ldc + n;
           rok[g] = p.resid && mr >= 0;
           mlog[g] = m; nlog[g] = n;
-          cv[g] = *(const bf16x8*)(Cs + lofs[g]);
+          cv[g] = crd8(Cs + lofs[g], row);
           // off the residual's sub-sampling lattice the (unused) load reads C itself: resid is the
           // smaller lattice tensor there, so resid + off[g] could run past its allocation
           if (p.resid) rr[g] = *(const bf16x8*)(rok[g] ? resid_b + bz * p.sC + mr * p.ldc + n : (const bf16*)p.C + off[g]);
@@ -367,11 +389,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             }
           }
           if constexpr (mx) {
-            *(bf16x8*)(Cs + lofs[g]) = v;  // the final value, for the MX pass
+            cwr8(Cs + lofs[g], v, lrow[g]);  // the final value, for the MX pass
             if (!p.mx_skip_c) *(bf16x8*)((bf16*)p.C + off[g]) = v;
           } else {
             if constexpr (ext) {
-              if (p.colsum) *(bf16x8*)(Cs + lofs[g]) = v;  // the final value, for the column sums
+              if (p.colsum) cwr8(Cs + lofs[g], v, lrow[g]);  // the final value, for the column sums
             }
             *(bf16x8*)((bf16*)p.C + off[g]) = v;
           }
@@ -405,7 +427,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
       long long mo = m, mr = m;
       if constexpr (bnr) { mo = out_row(p, m); mr = resid_row(p, mo); }
       const bf16* rsrc = (p.resid && mr >= 0) ? (const bf16*)p.resid + bz * p.sC + mr * p.ldc + n : nullptr;
-      bf16x8 v = *(const bf16x8*)(Cs + cso(row, cc * 8));
+      bf16x8 v = crd8(Cs + cbase(row, cc * 8), row);
       bf16* dst = C + mo * p.ldc + n;
       if (n + 7 < p.N && (p.ldc & 7) == 0) {
         const long long off = bz * p.sC + mo * p.ldc + n;
@@ -469,11 +491,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
           }
         }
         if constexpr (mx) {
-          *(bf16x8*)(Cs + cso(row, cc * 8)) = v;
+          cwr8(Cs + cbase(row, cc * 8), v, row);
           if (!p.mx_skip_c) *(bf16x8*)dst = v;
         } else {
           if constexpr (ext) {
-            if (p.colsum) *(bf16x8*)(Cs + cso(row, cc * 8)) = v;
+            if (p.colsum) cwr8(Cs + cbase(row, cc * 8), v, row);
           }
           *(bf16x8*)dst = v;
         }

@@ -9,6 +9,7 @@
 
 #include "bind_util.h"
 #include "../kernels/gemm_params.h"
+#include "../kernels/bn_fin.h"
 
 // common.h drop_thr8 (8-bit dropout threshold round(256 p)), host copy in the same float arithmetic
 static inline int drop_thr8_host(float p) {
@@ -48,7 +49,15 @@ int tfk_bn_bwd_finalize(float*, int, int, float, const float*, const float*, con
                         const float*, float*, float*, float*, float*, float*, float*, hipStream_t);
 int tfk_bn_bwd_apply(const void*, const void*, const void*, const float*, void*, const void*, const float*, void*, void*,
                      long long, int, const float*, const float*, const uint8_t*, hipStream_t);
-int tfk_maxpool_fwd(const void*, void*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+int tfk_bn_fin_ok(int, int);
+int tfk_bn_apply_fin(const void*, const tfk::BnFin*, const void*, const tfk::BnFin*, int, void*, long long, int, uint8_t*,
+                     hipStream_t);
+int tfk_bn_bwd_apply_fin(const void*, const void*, const float*, int, const tfk::BnBwdFin*, const void*,
+                         const tfk::BnBwdFin*, void*, void*, void*, long long, int, const float*, const float*,
+                         const uint8_t*, hipStream_t);
+int tfk_bn_zero(float*, long long, hipStream_t);
+int tfk_maxpool_fwd(const void*, void*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int, int,
+                    const float*, const float*, hipStream_t);
 int tfk_maxpool_bwd(const void*, const uint8_t*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                     const void*, const float*, const float*, const float*, const float*, const uint8_t*, float*, int,
                     hipStream_t);
@@ -467,6 +476,108 @@ void bn_apply(torch::Tensor y, torch::Tensor scale, torch::Tensor shift, c10::op
            "bn_apply");
 }
 
+// Finalize-in-apply BN (bn.hip). f = [stats, gamma, beta, run_mean, run_var, mean, invstd, scale, shift]
+// (stats undefined: apply with the given scale/shift, nothing finalized).
+static tfk::BnFin bn_fin_of(const std::vector<c10::optional<torch::Tensor>>& f, double eps, double momentum, int shards,
+                            int C) {
+  TORCH_CHECK(f.size() == 9, "bn fin: [stats, gamma, beta, run_mean, run_var, mean, invstd, scale, shift]");
+  tfk::BnFin b{};
+  const bool fin = f[0].has_value() && f[0]->defined();
+  if (fin) {
+    need_f32(*f[0], "stats");
+    need_numel(*f[0], (long long)shards * 2 * C, "stats");
+    for (int i : {1, 2, 5, 6})
+      TORCH_CHECK(f[i].has_value() && f[i]->defined(), "bn fin: gamma/beta/mean/invstd required");
+  }
+  for (int i = 1; i < 9; ++i)
+    if (f[i].has_value() && f[i]->defined()) { need_f32(*f[i], "bn vec"); need_numel(*f[i], C, "bn vec"); }
+  TORCH_CHECK(f[7].has_value() && f[7]->defined() && f[8].has_value() && f[8]->defined(), "bn fin: scale/shift required");
+  b.stats = fin ? f[0]->data_ptr<float>() : nullptr;
+  b.gamma = opt_ptr<const float>(f[1]);
+  b.beta = opt_ptr<const float>(f[2]);
+  b.run_mean = opt_ptr<float>(f[3]);
+  b.run_var = opt_ptr<float>(f[4]);
+  b.mean = opt_ptr<float>(f[5]);
+  b.invstd = opt_ptr<float>(f[6]);
+  b.scale = f[7]->data_ptr<float>();
+  b.shift = f[8]->data_ptr<float>();
+  b.eps = (float)eps;
+  b.momentum = (float)momentum;
+  b.shards = shards;
+  return b;
+}
+
+bool bn_fin_ok(int C, int shards) { return tfk_bn_fin_ok(C, shards) != 0; }
+
+void bn_apply_fin(torch::Tensor y, std::vector<c10::optional<torch::Tensor>> f, double eps, double momentum, int shards,
+                  c10::optional<torch::Tensor> r, std::vector<c10::optional<torch::Tensor>> f2, double eps2,
+                  double momentum2, int shards2, bool relu, torch::Tensor out, int64_t M, int C,
+                  c10::optional<torch::Tensor> mask) {
+  need_bf16(y, "y"); need_bf16(out, "out"); need_numel(y, M * C, "y"); need_numel(out, M * C, "out");
+  need_aligned(y, 16, "y"); need_aligned(out, 16, "out");
+  TORCH_CHECK(C % 64 == 0, "bn_apply_fin: C % 64");
+  uint8_t* mk = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(relu && mask->scalar_type() == torch::kUInt8, "bn_apply_fin: mask is the relu bitmask (uint8)");
+    need_numel(*mask, M * C / 8, "mask");
+    mk = mask->data_ptr<uint8_t>();
+  }
+  const tfk::BnFin a = bn_fin_of(f, eps, momentum, shards, C);
+  tfk::BnFin b{};
+  const bool dual = !f2.empty();
+  if (dual) b = bn_fin_of(f2, eps2, momentum2, shards2, C);
+  if (r.has_value() && r->defined()) { need_bf16(*r, "r"); need_numel(*r, M * C, "r"); need_aligned(*r, 16, "r"); }
+  TORCH_CHECK(!dual || (r.has_value() && r->defined()), "bn_apply_fin: a second BN needs r");
+  check_rc(tfk_bn_apply_fin(y.data_ptr(), &a, opt_ptr<const void>(r), dual ? &b : nullptr, relu ? 1 : 0, out.data_ptr(),
+                            M, C, mk, cur_stream()),
+           "bn_apply_fin");
+}
+
+// g = [gamma, mean, invstd, dgamma, dbeta] per BN; g2 empty without a second BN.
+static tfk::BnBwdFin bn_bwd_fin_of(const std::vector<torch::Tensor>& g, int C) {
+  TORCH_CHECK(g.size() == 5, "bn bwd fin: [gamma, mean, invstd, dgamma, dbeta]");
+  for (auto& t : g) { need_f32(t, "bn vec"); need_numel(t, C, "bn vec"); }
+  return tfk::BnBwdFin{g[0].data_ptr<float>(), g[1].data_ptr<float>(), g[2].data_ptr<float>(), g[3].data_ptr<float>(),
+                       g[4].data_ptr<float>()};
+}
+
+void bn_bwd_apply_fin(torch::Tensor da, c10::optional<torch::Tensor> amask_t, torch::Tensor y, torch::Tensor sums,
+                      int shards, std::vector<torch::Tensor> g, c10::optional<torch::Tensor> y2,
+                      std::vector<torch::Tensor> g2, torch::Tensor dy, c10::optional<torch::Tensor> dy2,
+                      c10::optional<torch::Tensor> dres, int64_t M, int C, c10::optional<torch::Tensor> mscale,
+                      c10::optional<torch::Tensor> mshift) {
+  need_bf16(da, "da"); need_bf16(y, "y"); need_bf16(dy, "dy");
+  for (auto* t : {&da, &y, &dy}) { need_numel(*t, M * C, "bn bwd tensor"); need_aligned(*t, 16, "bn bwd tensor"); }
+  TORCH_CHECK(C % 64 == 0, "bn_bwd_apply_fin: C % 64");
+  need_f32(sums, "sums"); need_numel(sums, (long long)shards * 3 * C, "sums");
+  const uint8_t* amask = nullptr;
+  if (amask_t.has_value() && amask_t->defined()) {
+    TORCH_CHECK(amask_t->scalar_type() == torch::kUInt8, "bn_bwd_apply_fin: the relu mask is the packed bitmask");
+    need_numel(*amask_t, M * C / 8, "mask");
+    amask = amask_t->data_ptr<uint8_t>();
+  }
+  const tfk::BnBwdFin a = bn_bwd_fin_of(g, C);
+  tfk::BnBwdFin b{};
+  const bool two = y2.has_value() && y2->defined();
+  if (two) {
+    b = bn_bwd_fin_of(g2, C);
+    TORCH_CHECK(dy2.has_value() && dy2->defined(), "bn_bwd_apply_fin: y2 needs dy2");
+    need_numel(*y2, M * C, "y2"); need_numel(*dy2, M * C, "dy2");
+  }
+  if (dres.has_value() && dres->defined()) need_numel(*dres, M * C, "dres");
+  if (mscale.has_value() && mscale->defined()) { need_numel(*mscale, C, "mscale"); need_numel(*mshift, C, "mshift"); }
+  check_rc(tfk_bn_bwd_apply_fin(da.data_ptr(), y.data_ptr(), sums.data_ptr<float>(), shards, &a, opt_ptr<const void>(y2),
+                                two ? &b : nullptr, dy.data_ptr(), opt_ptr<void>(dy2), opt_ptr<void>(dres), M, C,
+                                opt_ptr<const float>(mscale), opt_ptr<const float>(mshift), amask, cur_stream()),
+           "bn_bwd_apply_fin");
+}
+
+void bn_zero(torch::Tensor t) {
+  need_f32(t, "bn accumulators");
+  TORCH_CHECK(t.is_contiguous(), "bn_zero: contiguous");
+  check_rc(tfk_bn_zero(t.data_ptr<float>(), t.numel(), cur_stream()), "bn_zero");
+}
+
 void bn_bwd_reduce(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tensor y, torch::Tensor mean,
                    torch::Tensor invstd, c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> mean2,
                    c10::optional<torch::Tensor> invstd2, int64_t M, int C, torch::Tensor sums, int shards,
@@ -529,8 +640,12 @@ void bn_bwd_apply(torch::Tensor da, c10::optional<torch::Tensor> a, torch::Tenso
 }
 
 // geom = [N, H, W, C, P, Q, KH, KW, sh, sw, ph, pw]
-void maxpool_fwd(torch::Tensor x, torch::Tensor y, torch::Tensor idx, std::vector<int64_t> g) {
+// bn (optional [scale, shift]): pool relu(x*scale + shift) -- the producer BN applied on the fly
+void maxpool_fwd(torch::Tensor x, torch::Tensor y, torch::Tensor idx, std::vector<int64_t> g,
+                 std::vector<torch::Tensor> bn) {
   TORCH_CHECK(g.size() == 12, "geom");
+  TORCH_CHECK(bn.empty() || bn.size() == 2, "maxpool_fwd: bn = [scale, shift]");
+  for (auto& t : bn) { need_f32(t, "bn vec"); need_numel(t, g[3], "bn vec"); }
   need_bf16(x, "x"); need_bf16(y, "y"); need(idx, at::kByte, "idx");
   TORCH_CHECK(g[3] % 8 == 0, "C%8");
   need_numel(x, g[0] * g[1] * g[2] * g[3], "x");
@@ -538,7 +653,8 @@ void maxpool_fwd(torch::Tensor x, torch::Tensor y, torch::Tensor idx, std::vecto
   need_numel(idx, g[0] * g[4] * g[5] * g[3], "idx");
   TORCH_CHECK(g[6] * g[7] <= 255, "window too large");
   check_rc(tfk_maxpool_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), g[0], g[1], g[2], g[3], g[4], g[5], g[6],
-                           g[7], g[8], g[9], g[10], g[11], cur_stream()),
+                           g[7], g[8], g[9], g[10], g[11], bn.empty() ? nullptr : bn[0].data_ptr<float>(),
+                           bn.empty() ? nullptr : bn[1].data_ptr<float>(), cur_stream()),
            "maxpool_fwd");
 }
 // bnr (optional, the gemm's 10-entry BN-reduce spec without y2): also accumulate the BN-backward
@@ -864,6 +980,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_finalize", &bn_bwd_finalize);
   m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("bn_fin_ok", &bn_fin_ok);
+  m.def("bn_apply_fin", &bn_apply_fin);
+  m.def("bn_bwd_apply_fin", &bn_bwd_apply_fin);
+  m.def("bn_zero", &bn_zero);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

@@ -7,8 +7,13 @@
 // Backward: reduce (sum dz, sum dz*xhat[, sum dz*xhat2]) -> finalize (dgamma/dbeta + apply
 // coefficients) -> apply (dy[, dy2 | dres]), where dz = da * 1[a > 0].
 #include "common.h"
+#include "bn_fin.h"
+
+#include <algorithm>
 
 namespace {
+using tfk::BnFin;
+using tfk::BnBwdFin;
 constexpr int NT = 256;
 constexpr int SHARD_UNROLL = 4;  // shards <= 16 (ops/norm.py SHARDS): loads per thread issued together
 
@@ -353,6 +358,253 @@ __global__ void bn_bwd_apply_kernel(const bf16* __restrict__ da, const bf16* __r
   }
 }
 
+// ---------------------------------------------------------------- finalize folded into apply
+// The separate finalize launches sat on the critical path between each conv and its BN pass
+// (ResNet-50 bs256: skipping all 102 of them measured 0.71 ms/step, profiles/perf_log_r5.md). Here
+// every apply block finalizes the 64-channel slice it streams: it reduces the slice's shard
+// partials (L2-resident: the producing GEMM's atomics just wrote them) into LDS, derives its
+// coefficients, and row group 0 of the slice writes the saved statistics / running stats /
+// parameter gradients. The shards are NOT zeroed here (every block of the slice reads them): the
+// owning model zeroes all pooled BN accumulators once per step (tfk_bn_zero, ops/norm.py BNPool).
+// Grid: x = C/64 channel slices, y = row groups; block = 8 chunk lanes x 32 rows.
+constexpr int FIN_SHARDS = 16;  // pooled states (ops/norm.py SHARDS)
+
+
+// Sum [shards][NV][C] over the shards for channels c0..c0+63 into tot[NV][64] (LDS). All threads.
+template <int NV>
+__device__ __forceinline__ void slice_sum(const float* __restrict__ buf, int shards, int C, int c0,
+                                          float (*part)[NV][64], float (*tot)[64]) {
+  const int t = threadIdx.x;
+  for (int q = t; q < FIN_SHARDS * NV * 8; q += NT) {
+    const int i = q / (NV * 8), rem = q - i * NV * 8, v = rem >> 3, ch = rem & 7;
+    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (i < shards) load8(buf + ((long long)i * NV + v) * C + c0 + ch * 8, x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[i][v][ch * 8 + e] = x[e];
+  }
+  __syncthreads();
+  if (t < NV * 64) {
+    const int v = t >> 6, c = t & 63;
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < FIN_SHARDS; ++i) a += part[i][v][c];
+    tot[v][c] = a;
+  }
+  __syncthreads();
+}
+
+// Forward finalize of channel slice c0 into sc/sh (LDS); row group 0 publishes the statistics.
+__device__ __forceinline__ void fin_fwd(const BnFin& f, int C, int c0, float count, float (*part)[2][64],
+                                        float (*tot)[64], float* sc, float* sh) {
+  if (f.stats == nullptr) {
+    if (threadIdx.x < 64) {
+      sc[threadIdx.x] = f.scale[c0 + threadIdx.x];
+      sh[threadIdx.x] = f.shift[c0 + threadIdx.x];
+    }
+    return;
+  }
+  slice_sum<2>(f.stats, f.shards, C, c0, part, tot);
+  if (threadIdx.x < 64) {
+    const int c = c0 + threadIdx.x;
+    const double mean = (double)tot[0][threadIdx.x] / count;
+    double var = (double)tot[1][threadIdx.x] / count - mean * mean;
+    if (var < 0) var = 0;
+    const float inv = rsqrtf((float)var + f.eps);
+    const float g = f.gamma[c], b = f.beta[c];
+    const float scale = g * inv, shift = b - (float)mean * g * inv;
+    sc[threadIdx.x] = scale;
+    sh[threadIdx.x] = shift;
+    if (blockIdx.y == 0) {
+      f.mean[c] = (float)mean;
+      f.invstd[c] = inv;
+      f.scale[c] = scale;
+      f.shift[c] = shift;
+      if (f.run_mean) {
+        const float unb = count > 1.f ? (float)var * count / (count - 1.f) : (float)var;
+        f.run_mean[c] = (1.f - f.momentum) * f.run_mean[c] + f.momentum * (float)mean;
+        f.run_var[c] = (1.f - f.momentum) * f.run_var[c] + f.momentum * unb;
+      }
+    }
+  }
+}
+
+constexpr int FIN_ROWS = 4;  // rows per thread per iteration (loads issued together)
+
+__global__ __launch_bounds__(256) void bn_apply_fin_kernel(const bf16* __restrict__ y, BnFin f, const bf16* __restrict__ r,
+                                                           BnFin f2, int dual, int relu, bf16* __restrict__ out,
+                                                           long long M, int C, unsigned char* __restrict__ mask,
+                                                           long long rows_per_block) {
+  __shared__ float part[FIN_SHARDS][2][64];
+  __shared__ float tot[2][64];
+  __shared__ float sc[2][64], sh[2][64];
+  const int c0 = blockIdx.x * 64;
+  const float count = (float)M;
+  fin_fwd(f, C, c0, count, part, tot, sc[0], sh[0]);
+  if (dual) {
+    __syncthreads();
+    fin_fwd(f2, C, c0, count, part, tot, sc[1], sh[1]);
+  }
+  __syncthreads();
+  const int ch = threadIdx.x & 7, rsub = threadIdx.x >> 3;
+  float s[8], b[8], rs[8], rb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s[e] = sc[0][ch * 8 + e]; b[e] = sh[0][ch * 8 + e];
+    rs[e] = dual ? sc[1][ch * 8 + e] : 0.f; rb[e] = dual ? sh[1][ch * 8 + e] : 0.f;
+  }
+  const long long r0 = (long long)blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  const int cc = c0 + ch * 8;
+  for (long long base = r0 + rsub; base < r1; base += 32 * FIN_ROWS) {
+    bf16x8 v[FIN_ROWS], rv[FIN_ROWS];
+#pragma unroll
+    for (int k = 0; k < FIN_ROWS; ++k) {
+      const long long row = base + 32 * k;
+      if (row < r1) {
+        v[k] = *(const bf16x8*)(y + row * C + cc);
+        if (r) rv[k] = *(const bf16x8*)(r + row * C + cc);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < FIN_ROWS; ++k) {
+      const long long row = base + 32 * k;
+      if (row >= r1) break;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = bf2f(v[k][e]) * s[e] + b[e];
+      if (r) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += dual ? bf2f(rv[k][e]) * rs[e] + rb[e] : bf2f(rv[k][e]);
+      }
+      bf16x8 w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w[e] = f2bf(relu ? fmaxf(o[e], 0.f) : o[e]);
+      const long long i = row * C + cc;
+      *(bf16x8*)(out + i) = w;
+      if (mask) {
+        unsigned bits = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bits |= (bf2f(w[e]) > 0.f ? 1u : 0u) << e;
+        mask[i >> 3] = (unsigned char)bits;
+      }
+    }
+  }
+}
+
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(const bf16* __restrict__ da, const bf16* __restrict__ y,
+                                                               const float* __restrict__ sums, int shards, BnBwdFin f,
+                                                               const bf16* __restrict__ y2, BnBwdFin f2,
+                                                               bf16* __restrict__ dy, bf16* __restrict__ dy2,
+                                                               bf16* __restrict__ dres, long long M, int C,
+                                                               const float* __restrict__ mscale,
+                                                               const float* __restrict__ mshift,
+                                                               const unsigned char* __restrict__ amask,
+                                                               long long rows_per_block) {
+  __shared__ float part[FIN_SHARDS][3][64];
+  __shared__ float tot[3][64];
+  __shared__ float cf[6][64];  // k1, A, B (, k1b, A2, B2)
+  const int c0 = blockIdx.x * 64;
+  const float count = (float)M;
+  slice_sum<3>(sums, shards, C, c0, part, tot);
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x, c = c0 + l;
+    const float s0 = tot[0][l], s1 = tot[1][l], s2 = tot[2][l];
+    {
+      const float inv = f.invstd[c], k1 = f.gamma[c] * inv, k3 = s1 / count;
+      cf[0][l] = k1;
+      cf[1][l] = -k1 * k3 * inv;
+      cf[2][l] = k1 * (k3 * inv * f.mean[c] - s0 / count);
+    }
+    if (y2) {
+      const float inv = f2.invstd[c], k1 = f2.gamma[c] * inv, k3 = s2 / count;
+      cf[3][l] = k1;
+      cf[4][l] = -k1 * k3 * inv;
+      cf[5][l] = k1 * (k3 * inv * f2.mean[c] - s0 / count);
+    }
+    if (blockIdx.y == 0) {
+      f.dgamma[c] = s1;
+      f.dbeta[c] = s0;
+      if (y2) { f2.dgamma[c] = s2; f2.dbeta[c] = s0; }
+    }
+  }
+  __syncthreads();
+  const int ch = threadIdx.x & 7, rsub = threadIdx.x >> 3;
+  const int cc = c0 + ch * 8;
+  float k1[8], A[8], B[8], k1b[8], A2[8], B2[8], ms[8], mh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    k1[e] = cf[0][ch * 8 + e]; A[e] = cf[1][ch * 8 + e]; B[e] = cf[2][ch * 8 + e];
+    k1b[e] = y2 ? cf[3][ch * 8 + e] : 0.f; A2[e] = y2 ? cf[4][ch * 8 + e] : 0.f; B2[e] = y2 ? cf[5][ch * 8 + e] : 0.f;
+  }
+  if (mscale) { load8(mscale + cc, ms); load8(mshift + cc, mh); }
+  const long long r0 = (long long)blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  for (long long base = r0 + rsub; base < r1; base += 32 * FIN_ROWS) {
+    bf16x8 g[FIN_ROWS], yv[FIN_ROWS], y2v[FIN_ROWS];
+    unsigned mb[FIN_ROWS];
+#pragma unroll
+    for (int k = 0; k < FIN_ROWS; ++k) {
+      const long long row = base + 32 * k;
+      if (row < r1) {
+        const long long i = row * C + cc;
+        g[k] = *(const bf16x8*)(da + i);
+        yv[k] = *(const bf16x8*)(y + i);
+        if (y2) y2v[k] = *(const bf16x8*)(y2 + i);
+        mb[k] = amask ? amask[i >> 3] : 0xffu;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < FIN_ROWS; ++k) {
+      const long long row = base + 32 * k;
+      if (row >= r1) break;
+      const long long i = row * C + cc;
+      float dz[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dz[e] = bf2f(g[k][e]);
+        if (amask) {
+          if (!((mb[k] >> e) & 1u)) dz[e] = 0.f;
+        } else if (mscale) {
+          if (!(bf2f(yv[k][e]) * ms[e] + mh[e] > 0.f)) dz[e] = 0.f;
+        }
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(k1[e] * dz[e] + A[e] * bf2f(yv[k][e]) + B[e]);
+      *(bf16x8*)(dy + i) = o;
+      if (y2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(k1b[e] * dz[e] + A2[e] * bf2f(y2v[k][e]) + B2[e]);
+        *(bf16x8*)(dy2 + i) = o;
+      }
+      if (dres) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(dz[e]);
+        *(bf16x8*)(dres + i) = o;
+      }
+    }
+  }
+}
+
+__global__ void bn_zero_kernel(float* __restrict__ p, long long n) {
+  const long long i = ((long long)blockIdx.x * NT + threadIdx.x) * 4;
+  if (i + 3 < n) *(f32x4*)(p + i) = f32x4{0.f, 0.f, 0.f, 0.f};
+  else
+    for (long long k = i; k < n; ++k) p[k] = 0.f;
+}
+
+// Grid of the slice kernels: C/64 x row groups, ~FIN_BLOCKS blocks, >= 256 rows (8 row iterations of
+// 32) per block so the finalize prologue amortizes.
+constexpr int FIN_BLOCKS = 4096;
+static dim3 fin_grid(long long M, int C, long long* rows_per_block) {
+  const int slices = C / 64;
+  long long groups = std::max(1LL, std::min<long long>((M + 255) / 256, FIN_BLOCKS / slices));
+  long long rpb = (M + groups - 1) / groups;
+  rpb = (rpb + 31) / 32 * 32;
+  groups = (M + rpb - 1) / rpb;
+  *rows_per_block = rpb;
+  return dim3(slices, (unsigned)groups);
+}
+
 int grid_for(long long work, int per_block, int cap = 4096) {
   long long g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -392,6 +644,37 @@ int tfk_bn_apply(const bf16* y, const float* scale, const float* shift, const bf
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+// Eligibility of the finalize-in-apply kernels: 64-channel slices, <= FIN_SHARDS shards.
+int tfk_bn_fin_ok(int C, int shards) { return (C % 64 == 0 && shards >= 1 && shards <= FIN_SHARDS) ? 1 : 0; }
+
+int tfk_bn_apply_fin(const bf16* y, const BnFin* f, const bf16* r, const BnFin* f2, int relu, bf16* out, long long M, int C,
+                     unsigned char* mask, hipStream_t s) {
+  if (!tfk_bn_fin_ok(C, f->stats ? f->shards : 1) || (f2 && f2->stats && f2->shards > FIN_SHARDS)) return -2;
+  long long rpb;
+  const dim3 grid = fin_grid(M, C, &rpb);
+  BnFin none{};
+  hipLaunchKernelGGL(bn_apply_fin_kernel, grid, dim3(NT), 0, s, y, *f, r, f2 ? *f2 : none, f2 ? 1 : 0, relu, out, M, C,
+                     mask, rpb);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int tfk_bn_bwd_apply_fin(const bf16* da, const bf16* y, const float* sums, int shards, const BnBwdFin* f, const bf16* y2,
+                         const BnBwdFin* f2, bf16* dy, bf16* dy2, bf16* dres, long long M, int C, const float* mscale,
+                         const float* mshift, const unsigned char* amask, hipStream_t s) {
+  if (!tfk_bn_fin_ok(C, shards) || (y2 && !f2)) return -2;
+  long long rpb;
+  const dim3 grid = fin_grid(M, C, &rpb);
+  BnBwdFin none{};
+  hipLaunchKernelGGL(bn_bwd_apply_fin_kernel, grid, dim3(NT), 0, s, da, y, sums, shards, *f, y2, f2 ? *f2 : none, dy, dy2,
+                     dres, M, C, mscale, mshift, amask, rpb);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int tfk_bn_zero(float* p, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(bn_zero_kernel, dim3((unsigned)((n + NT * 4 - 1) / (NT * 4))), dim3(NT), 0, s, p, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int tfk_bn_bwd_reduce(const bf16* da, const bf16* a, const bf16* y, const float* mean, const float* invstd, const bf16* y2,
                       const float* mean2, const float* invstd2, long long M, int C, float* sums, int shards,
                       const float* mscale, const float* mshift, const unsigned char* amask, hipStream_t s) {

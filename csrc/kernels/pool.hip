@@ -5,8 +5,12 @@
 namespace {
 constexpr int NT = 256;
 
+// bsc/bsh (optional): the pooled input is relu(x*bsc + bsh) of the producer's BatchNorm, applied
+// here element by element (rounded to bf16 as the standalone BN pass stores it) -- the ResNet stem's
+// BN output is read only by this pool, so it is never written (2 x 411 MB per bs-256 step).
 __global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, uint8_t* __restrict__ idx, int N, int H,
-                                   int W, int C, int P, int Q, int KH, int KW, int sh, int sw, int ph, int pw) {
+                                   int W, int C, int P, int Q, int KH, int KW, int sh, int sw, int ph, int pw,
+                                   const float* __restrict__ bsc, const float* __restrict__ bsh) {
   const int cpr = C >> 3;
   const long long total = (long long)N * P * Q * cpr;
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
@@ -16,10 +20,14 @@ __global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict_
     long long t = pix / Q;
     int p = (int)(t % P);
     int n = (int)(t / P);
-    float best[8];
+    float best[8], sc[8], sf[8];
     uint8_t bi[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY; bi[e] = 0;
+      sc[e] = bsc ? bsc[cc * 8 + e] : 1.f;
+      sf[e] = bsc ? bsh[cc * 8 + e] : 0.f;
+    }
     for (int r = 0; r < KH; ++r) {
       int h = p * sh - ph + r;
       if ((unsigned)h >= (unsigned)H) continue;
@@ -30,6 +38,7 @@ __global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict_
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float f = bf2f(v[e]);
+          if (bsc) f = bf2f(f2bf(fmaxf(f * sc[e] + sf[e], 0.f)));
           if (f > best[e]) { best[e] = f; bi[e] = (uint8_t)(r * KW + s); }
         }
       }
@@ -182,10 +191,10 @@ int grid_for(long long work, int cap = 8192) {
 
 extern "C" {
 int tfk_maxpool_fwd(const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int KH, int KW, int sh,
-                    int sw, int ph, int pw, hipStream_t s) {
+                    int sw, int ph, int pw, const float* bsc, const float* bsh, hipStream_t s) {
   long long total = (long long)N * P * Q * (C / 8);
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, x, y, idx, N, H, W, C, P, Q, KH, KW, sh, sw,
-                     ph, pw);
+                     ph, pw, bsc, bsh);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int tfk_maxpool_bwd(const bf16* dy, const uint8_t* idx, bf16* dx, int N, int H, int W, int C, int P, int Q, int KH, int KW,

@@ -23,6 +23,8 @@ SIDE_SHORTCUT = True
 # BN-backward apply then reads no mask and an identity block's residual gradient is dz itself (no
 # second output pass).
 PREMASK = True
+# the stem BN + relu applied inside the max-pool forward (ops.pool.maxpool_fwd bn=): no stem activation
+POOL_BN = True
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
 
@@ -58,27 +60,27 @@ class Bottleneck:
             def shortcut():
                 ysc = self.conv_sc.forward(x, ssc if training else None)
                 if training:
-                    self.bn_sc.finalize(ysc.numel() // ysc.shape[-1])
+                    self.bn_sc.finalize(ysc.numel() // ysc.shape[-1], defer=True)
                 sc.append(ysc)
             streams.run_wgrad(shortcut, x)
         y1 = self.conv1.forward(x, s1 if training else None)
         if training:
-            self.bn1.finalize(y1.numel() // y1.shape[-1])
+            self.bn1.finalize(y1.numel() // y1.shape[-1], defer=True)
         a1 = BN.bn_apply(y1, s1, relu=True)
         y2 = self.conv2.forward(a1, s2 if training else None)
         if training:
-            self.bn2.finalize(y2.numel() // y2.shape[-1])
+            self.bn2.finalize(y2.numel() // y2.shape[-1], defer=True)
         a2 = BN.bn_apply(y2, s2, relu=True)
         y3 = self.conv3.forward(a2, s3 if training else None)
         if training:
-            self.bn3.finalize(y3.numel() // y3.shape[-1])
+            self.bn3.finalize(y3.numel() // y3.shape[-1], defer=True)
         ysc = None
         if self.proj:
             if not SIDE_SHORTCUT:
                 ssc = self.bn_sc.state(dev)
                 ysc = self.conv_sc.forward(x, ssc if training else None)
                 if training:
-                    self.bn_sc.finalize(ysc.numel() // ysc.shape[-1])
+                    self.bn_sc.finalize(ysc.numel() // ysc.shape[-1], defer=True)
                 sc.append(ysc)
             streams.sync()
             ysc = sc[0]
@@ -180,6 +182,12 @@ class ResNet:
     # ------------------------------------------------------------------ setup
     def to(self, device, seed: int = 1234) -> "ResNet":
         self.arena.finalize(device, seed)
+        # every BN layer's accumulators in one buffer, zeroed once per training step: the BN passes
+        # then finalize their statistics themselves (ops/norm.py BNPool, FUSED_FIN)
+        bns = self.batchnorms()
+        self._bn_pool = BN.BNPool([bn.C for bn in bns], device)
+        for bn, st in zip(bns, self._bn_pool.states):
+            bn.st = st
         return self
 
     def batchnorms(self):
@@ -197,14 +205,22 @@ class ResNet:
     # ------------------------------------------------------------------ compute
     def _features(self, x):
         dev = x.device
+        if self.training and getattr(self, "_bn_pool", None) is not None:
+            self._bn_pool.zero()  # this step's BN statistics and backward sums accumulate from zero
         st = self.bn1.state(dev)
         y0 = self.conv1.forward(x, st if self.training else None)
         if self.training:
-            self.bn1.finalize(y0.numel() // y0.shape[-1])
+            self.bn1.finalize(y0.numel() // y0.shape[-1], defer=not POOL_BN)
         else:
             self._eval_stats()
-        a0 = BN.bn_apply(y0, st, relu=True)
-        p0, idx = PL.maxpool_fwd(a0, 3, 2, 1)
+        if POOL_BN:
+            # the stem BN's apply runs inside the max pool: its output is read by nothing else
+            p0, idx = PL.maxpool_fwd(y0, 3, 2, 1, bn=(st.scale, st.shift))
+            a0 = y0.shape
+        else:
+            a0 = BN.bn_apply(y0, st, relu=True)
+            p0, idx = PL.maxpool_fwd(a0, 3, 2, 1)
+            a0 = a0.shape
         h = p0
         for b in self.blocks:
             h = b.forward(h, self.training)
@@ -241,7 +257,7 @@ class ResNet:
         for i in range(nb - 1, -1, -1):
             nxt = self.blocks[i - 1].tail_reduce() if i > 0 else None
             dh = self.blocks[i].backward(dh, dout_reduced=i < nb - 1, next_bnr=nxt)
-        da0 = PL.maxpool_bwd(dh, idx, a0.shape, 3, 2, 1)
+        da0 = PL.maxpool_bwd(dh, idx, a0, 3, 2, 1)  # a0: the stem activation's shape
         dy0, _, _ = BN.bn_backward(da0, None, y0, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
                                    self.bn1.beta.grad, y0.numel() // y0.shape[-1], relu_from_y=True)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)

@@ -7,6 +7,8 @@ residual add of the same pass (dual form). Backward is reduce -> finalize -> app
 from __future__ import annotations
 
 
+import os
+
 import torch
 
 from ._lib import lib, on_gpu
@@ -16,16 +18,25 @@ from ._lib import lib, on_gpu
 # (ResNet-50 bs256 step, same box): 8 -> 25.21, 12 -> 25.33, 16 -> 25.15-25.19, 32 -> 25.25-25.41,
 # 64 -> 25.70 ms -- the finalize kernels sit on the critical path and read every shard
 SHARDS = 16
+# Finalize folded into the apply passes (bn.hip bn_apply_fin / bn_bwd_apply_fin) for pooled states:
+# no separate finalize launch between a conv and its BN pass (A/B switch).
+FUSED_FIN = os.environ.get("TFK_BN_FUSED_FIN", "1") != "0"
 
 
 class BNState:
-    """Per-BN-layer device state: stats accumulators and the per-step saved statistics."""
+    """Per-BN-layer device state: stats accumulators and the per-step saved statistics.
+    acc: optional flat f32 view [shards*5*C] to hold stats + sums (a BNPool's slice)."""
 
-    def __init__(self, C: int, device, shards: int = SHARDS):
+    def __init__(self, C: int, device, shards: int = SHARDS, acc: torch.Tensor | None = None):
         self.C = C
         self.shards = shards if torch.device(device).type == "cuda" else 1
-        self.stats = torch.zeros(self.shards * 2 * C, dtype=torch.float32, device=device)
-        self.sums = torch.zeros(self.shards * 3 * C, dtype=torch.float32, device=device)
+        n2, n3 = self.shards * 2 * C, self.shards * 3 * C
+        if acc is None:
+            acc = torch.zeros(n2 + n3, dtype=torch.float32, device=device)
+        self.stats = acc[:n2]
+        self.sums = acc[n2:n2 + n3]
+        self.pooled = False  # a BNPool zeroes the accumulators once per step (the fused kernels need it)
+        self.fin = None      # deferred forward finalize (gamma, beta, eps, momentum, run_mean, run_var)
         self.mean = torch.zeros(C, dtype=torch.float32, device=device)
         self.invstd = torch.ones(C, dtype=torch.float32, device=device)
         self.scale = torch.ones(C, dtype=torch.float32, device=device)
@@ -33,8 +44,41 @@ class BNState:
         self.coef = torch.zeros(3 * C, dtype=torch.float32, device=device)
 
 
-def bn_finalize(st: BNState, count: float, gamma, beta, eps, momentum, run_mean, run_var) -> None:
+class BNPool:
+    """The accumulators (stats + backward sums) of a model's BN layers in ONE flat buffer, zeroed by
+    one kernel at the start of each training step -- the finalize-in-apply kernels read the shards
+    from every block of a layer's apply pass, so they cannot zero them themselves."""
+
+    def __init__(self, Cs: list[int], device, shards: int = SHARDS):
+        self.device = torch.device(device)
+        shards = shards if self.device.type == "cuda" else 1
+        sizes = [shards * 5 * C for C in Cs]
+        self.buf = torch.zeros(sum(sizes), dtype=torch.float32, device=device)
+        self.states, o = [], 0
+        for C, n in zip(Cs, sizes):
+            st = BNState(C, device, shards, acc=self.buf[o:o + n])
+            st.pooled = True
+            self.states.append(st)
+            o += n
+
+    def zero(self) -> None:
+        if on_gpu(self.buf):
+            lib().bn_zero(self.buf)
+        else:
+            self.buf.zero_()
+
+
+def _fused(st: BNState) -> bool:
+    return FUSED_FIN and st.pooled and on_gpu(st.stats) and bool(lib().bn_fin_ok(st.C, st.shards))
+
+
+def bn_finalize(st: BNState, count: float, gamma, beta, eps, momentum, run_mean, run_var, defer: bool = False) -> None:
+    """defer (pooled GPU states): leave the finalize to the next bn_apply on st, which folds it into
+    its pass (bn_apply_fin); count is then that pass's row count."""
     C = st.C
+    if defer and _fused(st):
+        st.fin = (gamma, beta, eps, momentum, run_mean, run_var)
+        return
     if not on_gpu(st.stats):
         s = st.stats.view(st.shards, 2, C).sum(0)
         mean = s[0] / count
@@ -105,6 +149,20 @@ def bn_apply(y, st: BNState, relu: bool, r=None, rst: BNState | None = None, out
         return (o, pack_relu_mask(o)) if mask else o
     out = out if out is not None else torch.empty_like(y)
     mk = torch.empty(y.numel() // 8, dtype=torch.uint8, device=y.device) if mask else None
+    if st.fin is not None or (rst is not None and rst.fin is not None):
+        # the deferred finalize(s) of st (and the shortcut BN rst) run inside this pass
+        def spec(b: BNState):
+            if b.fin is None:
+                return [None] * 7 + [b.scale, b.shift], 0.0, 0.0, b.shards
+            gamma, beta, eps, momentum, rm, rv = b.fin
+            return [b.stats, gamma, beta, rm, rv, b.mean, b.invstd, b.scale, b.shift], eps, momentum, b.shards
+        f, e, m, sh = spec(st)
+        f2, e2, m2, sh2 = spec(rst) if rst is not None else ([], 0.0, 0.0, 0)
+        lib().bn_apply_fin(y, f, e, m, sh, r, f2, e2, m2, sh2, relu, out, y.numel() // C, C, mk)
+        st.fin = None
+        if rst is not None:
+            rst.fin = None
+        return (out, mk) if mask else out
     lib().bn_apply(y, st.scale, st.shift, r, rst.scale if rst is not None else None,
                    rst.shift if rst is not None else None, relu, out, y.numel() // C, C, mk)
     return (out, mk) if mask else out
@@ -191,6 +249,17 @@ def bn_backward(da, a, y, st: BNState, gamma, dgamma, dbeta, count: float, y2=No
     if not reduced:
         L.bn_bwd_reduce(da, a, y, st.mean, st.invstd, y2, st2.mean if st2 else None, st2.invstd if st2 else None, M, C,
                         st.sums, st.shards, msc, msh)
+    if _fused(st) and (a is None or a.dtype == torch.uint8):
+        # finalize folded into the apply pass (sums zeroed by the state's BNPool at step start)
+        dy = torch.empty_like(da)
+        dy2 = torch.empty_like(da) if y2 is not None else None
+        dres = torch.empty_like(da) if (want_dres and not premasked) else None
+        g2 = [gamma2, st2.mean, st2.invstd, dgamma2, dbeta2] if y2 is not None else []
+        L.bn_bwd_apply_fin(da, a, y, st.sums, st.shards, [gamma, st.mean, st.invstd, dgamma, dbeta], y2, g2, dy, dy2,
+                           dres, M, C, msc, msh)
+        if want_dres and premasked:
+            dres = da
+        return dy, dy2, dres
     L.bn_bwd_finalize(st.sums, st.shards, C, float(count), gamma, st.mean, st.invstd, gamma2,
                       st2.mean if st2 else None, st2.invstd if st2 else None, dgamma, dbeta, dgamma2, dbeta2, st.coef,
                       st2.coef if st2 else None)

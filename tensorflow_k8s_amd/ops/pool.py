@@ -11,16 +11,20 @@ def _out(n, k, s, p):
     return (n + 2 * p - k) // s + 1
 
 
-def maxpool_fwd(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1):
+def maxpool_fwd(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1, bn=None):
+    """bn = (scale, shift): pool relu(x*scale + shift) (bf16-rounded) -- the producer BatchNorm's
+    apply fused into the pool, so its output is never materialized."""
     N, H, W, C = x.shape
     P, Q = _out(H, k, s, p), _out(W, k, s, p)
     if not on_gpu(x):
+        if bn is not None:
+            x = torch.relu(x.float() * bn[0] + bn[1]).to(torch.bfloat16)
         xn = x.float().permute(0, 3, 1, 2)
         y, idx = F.max_pool2d(xn, k, s, p, return_indices=True)
         return y.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous(), (idx, xn.shape)
     y = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=x.device)
     idx = torch.empty(N, P, Q, C, dtype=torch.uint8, device=x.device)
-    lib().maxpool_fwd(x, y, idx, [N, H, W, C, P, Q, k, k, s, s, p, p])
+    lib().maxpool_fwd(x, y, idx, [N, H, W, C, P, Q, k, k, s, s, p, p], list(bn) if bn is not None else [])
     return y, idx
 
 

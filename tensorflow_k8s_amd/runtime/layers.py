@@ -189,9 +189,10 @@ class BatchNorm:
             self.st = BN.BNState(self.C, device)
         return self.st
 
-    def finalize(self, count: int) -> None:
+    def finalize(self, count: int, defer: bool = False) -> None:
+        """defer: fold the finalize into the next bn_apply on this layer's state (pooled GPU states)."""
         BN.bn_finalize(self.st, float(count), self.gamma.master, self.beta.master, self.eps, self.momentum,
-                       self.run_mean if self.training else None, self.run_var if self.training else None)
+                       self.run_mean if self.training else None, self.run_var if self.training else None, defer=defer)
 
     def use_running_stats(self) -> None:
         """Inference: scale/shift from the moving statistics."""

@@ -182,6 +182,55 @@ def test_bn_fused_forward_backward(proj, C):
         assert rel(out[DEV][k], v) < 1e-2, k
 
 
+@pytest.mark.parametrize("C", [64, 256, 192])
+@pytest.mark.parametrize("proj", [False, True])
+def test_bn_finalize_in_apply_matches_separate(proj, C, monkeypatch):
+    """The finalize-in-apply BN passes (bn.hip bn_apply_fin / bn_bwd_apply_fin, pooled states,
+    ops/norm.py FUSED_FIN) equal the separate finalize + apply kernels: activations, relu bitmask,
+    saved mean/invstd/scale/shift, running statistics, input gradients (incl. the projection-shortcut
+    BN and the identity residual) and dgamma/dbeta -- for the tensor-mask and relu-from-y backwards.
+    Ragged row counts (M not a multiple of a block's rows) included."""
+    N, H, W = 3, 11, 13
+    M = N * H * W
+    y, r = bf(N, H, W, C, seed=31).to(DEV), bf(N, H, W, C, seed=32).to(DEV)
+    da = bf(N, H, W, C, seed=33).to(DEV)
+    gamma, beta = (torch.rand(C) + 0.5).to(DEV), (torch.randn(C) * 0.1).to(DEV)
+    gamma2, beta2 = (torch.rand(C) + 0.5).to(DEV), (torch.randn(C) * 0.1).to(DEV)
+    res = {}
+    for fused in (False, True):
+        monkeypatch.setattr(BN, "FUSED_FIN", fused)
+        pool = BN.BNPool([C, C], DEV)
+        st, st2 = pool.states
+        pool.zero()
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        BN.bn_stats(y, st)
+        BN.bn_finalize(st, M, gamma, beta, 1e-5, 0.1, rm, rv, defer=True)
+        if proj:
+            BN.bn_stats(r, st2)
+            BN.bn_finalize(st2, M, gamma2, beta2, 1e-5, 0.1, None, None, defer=True)
+        assert (st.fin is not None) == fused
+        a, mk = BN.bn_apply(y, st, True, r=r, rst=st2 if proj else None, mask=True)
+        dg, db, dg2, db2 = (torch.zeros(C, device=DEV) for _ in range(4))
+        dy, dy2, dres = BN.bn_backward(da, mk, y, st, gamma, dg, db, M, y2=r if proj else None,
+                                       st2=st2 if proj else None, gamma2=gamma2 if proj else None, dgamma2=dg2,
+                                       dbeta2=db2, want_dres=not proj)
+        pool.zero()
+        dg3, db3 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        dy3, _, _ = BN.bn_backward(da, None, y, st, gamma, dg3, db3, M, relu_from_y=True)
+        torch.cuda.synchronize()
+        res[fused] = dict(a=a, mk=mk, mean=st.mean.clone(), invstd=st.invstd.clone(), scale=st.scale.clone(),
+                          shift=st.shift.clone(), rm=rm, rv=rv, dy=dy, dy2=dy2, dres=dres, dg=dg, db=db, dg2=dg2,
+                          db2=db2, dy3=dy3, dg3=dg3, db3=db3)
+    for k, v in res[False].items():
+        if v is None:
+            assert res[True][k] is None, k
+            continue
+        if v.dtype == torch.uint8:
+            assert (res[True][k] != v).float().mean() < 1e-3, k  # a bf16 tie may round the other way
+        else:
+            assert rel(res[True][k], v) < 1e-3, k
+
+
 @pytest.mark.parametrize("proj", [False, True])
 def test_bn_relu_bitmask(proj):
     """bn_apply(mask=True) writes the packed relu mask of its output (bit e of byte i = a[8i+e] > 0),
@@ -258,6 +307,24 @@ def test_pools():
     assert rel(PL.avgpool_fwd(x.to(DEV)), PL.avgpool_fwd(x)) < 1e-2
     g = bf(2, 64, seed=13)
     assert rel(PL.avgpool_bwd(g.to(DEV), x.shape), PL.avgpool_bwd(g, x.shape)) < 1e-2
+
+
+@pytest.mark.parametrize("C", [64, 24])
+def test_maxpool_fused_bn_relu_equals_separate(C):
+    """maxpool_fwd(y, bn=(scale, shift)) -- the stem BN + relu applied inside the pool -- equals the
+    pool over the materialized bn_apply output bit for bit (values and argmax bytes), and the CPU
+    reference of the fused form."""
+    y = bf(3, 23, 19, C, seed=41).to(DEV)
+    scale = (torch.rand(C) * 2 - 0.5).to(DEV)  # some negative: the BN may flip the order
+    shift = (torch.randn(C) * 0.3).to(DEV)
+    st = BN.BNState(C, DEV)
+    st.scale.copy_(scale); st.shift.copy_(shift)
+    a = BN.bn_apply(y, st, relu=True)
+    p_ref, i_ref = PL.maxpool_fwd(a, 3, 2, 1)
+    p, i = PL.maxpool_fwd(y, 3, 2, 1, bn=(scale, shift))
+    assert torch.equal(p, p_ref) and torch.equal(i, i_ref)
+    p_cpu, _ = PL.maxpool_fwd(y.cpu(), 3, 2, 1, bn=(scale.cpu(), shift.cpu()))
+    assert rel(p, p_cpu) < 1e-2  # the CPU reference rounds x*scale+shift without an FMA
 
 
 @pytest.mark.parametrize("B,V,smooth", [(64, 1000, 0.1), (33, 30522, 0.0), (16, 37, 0.1)])

@@ -64,3 +64,27 @@ def test_side_stream_wgrad_matches_single_stream(mode, monkeypatch):
         runs.append((r.last_loss(), m.arena.master.clone()))
     assert abs(runs[0][0] - runs[1][0]) < 1e-2
     assert float((runs[0][1] - runs[1][1]).norm() / runs[0][1].norm()) < 1e-2
+
+
+def test_bn_finalize_in_apply_resnet_step_matches(monkeypatch):
+    """A captured ResNet-50 training step with the BN finalizes folded into the BN passes (pooled
+    accumulators zeroed once per step, ops/norm.py FUSED_FIN) follows the separate-finalize step:
+    loss, master weights and the BN running statistics after 4 SGD steps."""
+    from tensorflow_k8s_amd.ops import norm as BN
+    torch.manual_seed(0)
+    ms = [ResNet(50, num_classes=10).to("cuda") for _ in range(2)]
+    ms[1].arena.master.copy_(ms[0].arena.master)
+    ms[1].arena.refresh_compute()
+    x, y = synthetic_imagenet(16, "cuda", image_size=96, num_classes=10)
+    runs = []
+    for m, fused in zip(ms, (False, True)):
+        monkeypatch.setattr(BN, "FUSED_FIN", fused)
+        opt = SGD(m.arena, lr=0.01)
+        r = StepRunner(m, opt, None, (x, y), use_graph=True)
+        for _ in range(4):
+            r.step()
+        torch.cuda.synchronize()
+        runs.append((r.last_loss(), m.arena.master.clone(), torch.cat([b.tensor.reshape(-1) for b in m.arena.buffers])))
+    assert abs(runs[0][0] - runs[1][0]) < 1e-3 * abs(runs[0][0]), (runs[0][0], runs[1][0])
+    assert float((runs[0][1] - runs[1][1]).norm() / runs[0][1].norm()) < 1e-3
+    assert float((runs[0][2] - runs[1][2]).norm() / runs[0][2].norm()) < 1e-3

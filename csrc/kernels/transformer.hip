@@ -144,8 +144,8 @@ __global__ __launch_bounds__(LNMX_NT) void ln_fwd_mx_kernel(const bf16* __restri
   tfk::mx_rows32_out<LNMX_NT>(&tile[0][0], LNMX_WMAX + 8, W, M, r0, qr, sr, qc, sc);
 }
 
-template <int CPL, int NTB = NT>
-__global__ __launch_bounds__(NTB) void ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+template <int CPL>
+__global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, const bf16* __restrict__ dres,
                                                     bf16* __restrict__ dx, float* __restrict__ dgamma,
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(NTB) void ln_bwd_kernel(const bf16* __restrict__ dy
                                                     unsigned char* __restrict__ mst, float* __restrict__ part) {
   // dbias (optional): += column sums of the gradient this kernel hands its consumer (dxd, else dx)
   // -- that Linear's bias gradient, reduced with dgamma/dbeta instead of a separate column-sum pass
-  extern __shared__ float red[];  // [min(NTB,256)/64][2 or 3][W]: waves w and w+4 share slot w & 3
+  extern __shared__ float red[];  // [NT/64][2 or 3][W]
   const int NS = dbias ? 3 : 2;
   const unsigned long long drop_seed = eff_seed(drop_salt, drop_key);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -179,10 +179,10 @@ __global__ __launch_bounds__(NTB) void ln_bwd_kernel(const bf16* __restrict__ dy
   // consecutive rows (8 per wave), stages their final values in an LDS tile behind `red` and
   // quantizes the tile after the row loop (the consumer's fp8 backward then skips its quantize pass)
   const bool mxo = mq != nullptr;
-  const int rstep = mxo ? 1 : gridDim.x * (NTB / 64);
-  int row = mxo ? blockIdx.x * 32 + wid * 8 : blockIdx.x * (NTB / 64) + wid;
+  const int rstep = mxo ? 1 : gridDim.x * (NT / 64);
+  int row = mxo ? blockIdx.x * 32 + wid * 8 : blockIdx.x * (NT / 64) + wid;
   const int rend = mxo ? row + 8 : M;
-  bf16* mtile = (bf16*)(red + (NT / 64) * NS * W);  // [32][W + 8] (MX mode only; NTB == NT)
+  bf16* mtile = (bf16*)(red + (NT / 64) * NS * W);  // [32][W + 8] (MX mode only)
   bf16x8 ndv[CPL], nxv[CPL], nrv[CPL];
   float nmu = 0.f, nrs = 0.f;
   auto fetch = [&](int r) {
@@ -267,40 +267,26 @@ __global__ __launch_bounds__(NTB) void ln_bwd_kernel(const bf16* __restrict__ dy
       }
     }
   }
-  // per-wave column partials -> LDS slots of 4 waves (8-wave blocks: the upper half adds into the
-  // lower half's slots after a barrier, so the LDS stays [4][NS][W])
-  constexpr int SLOTS = NTB / 64 < 4 ? NTB / 64 : 4;
 #pragma unroll
-  for (int half = 0; half < NTB / 64 / SLOTS; ++half) {
-    if (wid / SLOTS == half) {
-      const int ws = wid % SLOTS;
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nch)
 #pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        const int c = lane + 64 * j;
-        if (c < nch)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float* r0 = &red[(ws * NS + 0) * W + c * 8 + e];
-            float* r1 = &red[(ws * NS + 1) * W + c * 8 + e];
-            *r0 = half ? *r0 + dg[j][e] : dg[j][e];
-            *r1 = half ? *r1 + db[j][e] : db[j][e];
-            if (dbias) {
-              float* r2 = &red[(ws * NS + 2) * W + c * 8 + e];
-              *r2 = half ? *r2 + bs[j][e] : bs[j][e];
-            }
-          }
+      for (int e = 0; e < 8; ++e) {
+        red[(wid * NS + 0) * W + c * 8 + e] = dg[j][e];
+        red[(wid * NS + 1) * W + c * 8 + e] = db[j][e];
+        if (dbias) red[(wid * NS + 2) * W + c * 8 + e] = bs[j][e];
       }
-    }
-    __syncthreads();
   }
+  __syncthreads();
   // block partials: plain stores into this block's slab row (part), reduced by ln_part_reduce_kernel
   // -- every block adding atomically into the same 2-3 x W floats serialised on those few lines at
   // the kernel's tail (256 adders per address on Transformer-big's 8192 rows)
   float* prow = part ? part + (long long)blockIdx.x * NS * W : nullptr;
-  for (int col = threadIdx.x; col < W; col += NTB) {
+  for (int col = threadIdx.x; col < W; col += NT) {
     float a = 0.f, b2 = 0.f, b3 = 0.f;
 #pragma unroll
-    for (int w = 0; w < SLOTS; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
       a += red[(w * NS) * W + col];
       b2 += red[(w * NS + 1) * W + col];
       if (dbias) b3 += red[(w * NS + 2) * W + col];
@@ -570,18 +556,8 @@ int tfk_layernorm_fwd_mx(const bf16* x, const float* gamma, const float* beta, b
 // bf16 mode: rows per wave of the grid-stride backward (A/B knob of tools/ln_probe.py; fewer rows per
 // wave = more blocks per CU in flight, more column-partial slabs for ln_part_reduce_kernel)
 static int g_ln_rows = 8;
-// bf16 mode: threads per block (256 or 512; A/B knob of tools/ln_probe.py, TFK_LN_BWD_NT)
-static int g_ln_nt = -1;
-static int ln_nt() {
-  if (g_ln_nt < 0) {
-    const char* e = getenv("TFK_LN_BWD_NT");
-    g_ln_nt = (e && atoi(e) == 512) ? 512 : 256;
-  }
-  return g_ln_nt;
-}
 void tfk_ln_bwd_set_rows(int r) { g_ln_rows = r > 0 ? r : 8; }
-void tfk_ln_bwd_set_nt(int nt) { g_ln_nt = nt == 512 ? 512 : (nt < 0 ? -1 : 256); }
-int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (ln_nt() / 64) * g_ln_rows, 4096); }
+int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (NT / 64) * g_ln_rows, 4096); }
 static unsigned ln_bwd_blocks(int M, bool mxo) { return (unsigned)tfk_ln_bwd_blocks(M, mxo ? 1 : 0); }
 // part (optional): f32 workspace [blocks][2 or 3][W] for the column partials (no tail atomics)
 int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const float* mean, const float* rstd,
@@ -593,14 +569,7 @@ int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const f
   if (mxo && (M % 32 || W % 32 || W > 1024)) return -3;
   dim3 grid(ln_bwd_blocks(M, mxo));
   const size_t sh = (size_t)(NT / 64) * (dbias ? 3 : 2) * W * sizeof(float) + (mxo ? (size_t)32 * (W + 8) * 2 : 0);
-  if (!mxo && ln_nt() == 512 && cpl <= 2) {  // (W <= 1024: the CPL = 4 kernel spills at 512 threads)
-#define TFK_LN_BWD512(C_)                                                                                        \
-  hipLaunchKernelGGL((ln_bwd_kernel<C_, 512>), grid, dim3(512), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma,  \
-                     dbeta, M, W, dxd, drop_p, drop_seed, tfk_seed_key(), dbias, nullptr, nullptr, nullptr, nullptr, part)
-    if (cpl <= 1) TFK_LN_BWD512(1);
-    else TFK_LN_BWD512(2);
-#undef TFK_LN_BWD512
-  } else if (cpl <= 1)
+  if (cpl <= 1)
     hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
                        dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
                        (unsigned char*)mqt, (unsigned char*)mst, part);

@@ -8,6 +8,8 @@ fc1000) so checkpoints line up with TF-era tooling.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops import norm as BN
@@ -24,7 +26,8 @@ SIDE_SHORTCUT = True
 # second output pass).
 PREMASK = True
 # the stem BN + relu applied inside the max-pool forward (ops.pool.maxpool_fwd bn=): no stem activation
-POOL_BN = True
+# (A/B: TFK_POOL_BN=0)
+POOL_BN = os.environ.get("TFK_POOL_BN", "1") != "0"
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
 

@@ -19,8 +19,10 @@ from ._lib import lib, on_gpu
 # 64 -> 25.70 ms -- the finalize kernels sit on the critical path and read every shard
 SHARDS = 16
 # Finalize folded into the apply passes (bn.hip bn_apply_fin / bn_bwd_apply_fin) for pooled states:
-# no separate finalize launch between a conv and its BN pass (A/B switch).
-FUSED_FIN = os.environ.get("TFK_BN_FUSED_FIN", "1") != "0"
+# no separate finalize launch between a conv and its BN pass. Opt-in (TFK_BN_FUSED_FIN=1): measured
+# SLOWER in the captured ResNet-50 step (21.57 / 21.60 vs 21.31 / 21.36 ms, profiles/perf_log_r6.md) --
+# the per-block finalize prologue and the 64-channel slice layout cost more than the launches saved.
+FUSED_FIN = os.environ.get("TFK_BN_FUSED_FIN", "0") == "1"
 
 
 class BNState:
@@ -62,6 +64,10 @@ class BNPool:
             o += n
 
     def zero(self) -> None:
+        """Zero every accumulator (only the fused kernels need it: the separate finalize kernels
+        zero the shards they read)."""
+        if not FUSED_FIN:
+            return
         if on_gpu(self.buf):
             lib().bn_zero(self.buf)
         else:

@@ -113,8 +113,8 @@ def test_relu_bitmask_pack_roundtrip_and_backward():
 
 def test_bn_pool_states_and_deferred_finalize_cpu():
     """ResNet.to() puts every BN layer's accumulators in one BNPool buffer (zeroed once per training
-    step); on the CPU a deferred finalize runs at once (the fused kernels are GPU-only), so the
-    executor's numbers are unchanged."""
+    step when the fused finalize kernels are on); on the CPU a deferred finalize runs at once (the
+    fused kernels are GPU-only), so the executor's numbers are unchanged."""
     import torch
     from tensorflow_k8s_amd.models.resnet import ResNet, synthetic_imagenet
     from tensorflow_k8s_amd.ops import norm as BN
@@ -123,10 +123,10 @@ def test_bn_pool_states_and_deferred_finalize_cpu():
     bns = m.batchnorms()
     assert len(pool.states) == len(bns) and all(bn.st is st for bn, st in zip(bns, pool.states))
     assert all(st.pooled and st.stats.data_ptr() >= pool.buf.data_ptr() for st in pool.states)
-    pool.buf.fill_(7.0)
     x, y = synthetic_imagenet(2, "cpu", image_size=64, num_classes=10)
     loss, _ = m.forward_backward(x, y)
     assert torch.isfinite(loss).all()
+    assert all(float(st.stats.abs().sum()) == 0.0 for st in pool.states)  # every finalize re-zeroed its shards
     st = BN.BNState(8, "cpu")
     BN.bn_finalize(st, 4.0, torch.ones(8), torch.zeros(8), 1e-5, 0.1, None, None, defer=True)
     assert st.fin is None  # not pooled / not on the GPU: finalized immediately

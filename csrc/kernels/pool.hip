@@ -147,6 +147,102 @@ __global__ void maxpool_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* _
   }
 }
 
+// 3x3 / stride 2 / pad 1 (the ResNet stem pool): an input row h is covered by output row h/2
+// (even h) or rows (h-1)/2 and (h+1)/2 (odd h), likewise columns -- at most 4 windows, whose dy and
+// argmax loads are ALL issued before any is used (the generic kernel's loop over the window range
+// has one dependent load pair in flight per thread: latency-bound, 42 % of the HBM floor). BNR as
+// in maxpool_bwd_kernel; the pixel's y is loaded with the windows.
+template <bool BNR>
+__global__ __launch_bounds__(NT) void maxpool_bwd_k3s2_kernel(
+    const bf16* __restrict__ dy, const uint8_t* __restrict__ idx, bf16* __restrict__ dx, int N, int H, int W, int C,
+    int P, int Q, const bf16* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ mscale, const float* __restrict__ mshift, const unsigned char* __restrict__ amask,
+    float* __restrict__ sums, int shards) {
+  const int cpr = C >> 3;
+  const long long total = (long long)N * H * W * cpr;
+  float s0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mu[8], is[8], ms[8], mh[8];
+  const int c0 = (threadIdx.x % cpr) * 8;
+  if constexpr (BNR) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e];
+      ms[e] = mscale ? mscale[c0 + e] : 1.f; mh[e] = mshift ? mshift[c0 + e] : 0.f;
+    }
+  }
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int cc = (int)(i % cpr);
+    const long long pix = i / cpr;
+    const int w = (int)(pix % W);
+    const long long t = pix / W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    // candidate windows: rows pa = (h+1)/2 (always valid when < P), pb = (h-1)/2 (odd h only)
+    const int pa = (h + 1) >> 1, pb = (h - 1) >> 1, qa = (w + 1) >> 1, qb = (w - 1) >> 1;
+    const bool va = pa < P, vb = (h & 1) && pb >= 0, wa = qa < Q, wb = (w & 1) && qb >= 0;
+    const int pr[2] = {va ? pa : 0, vb ? pb : 0}, qr[2] = {wa ? qa : 0, wb ? qb : 0};
+    const bool vr[2] = {va, vb}, vc[2] = {wa, wb};
+    bf16x8 g[4];
+    uint2 id[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long long o = (((long long)n * P + pr[k >> 1]) * Q + qr[k & 1]) * C + cc * 8;
+      g[k] = *(const bf16x8*)(dy + o);
+      id[k] = *(const uint2*)(idx + o);
+    }
+    bf16x8 yv;
+    if constexpr (BNR) yv = *(const bf16x8*)(y + i * 8);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!(vr[k >> 1] && vc[k & 1])) continue;
+      const int r = h - (pr[k >> 1] * 2 - 1), sc = w - (qr[k & 1] * 2 - 1);
+      const uint8_t want = (uint8_t)(r * 3 + sc);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t word = e < 4 ? id[k].x : id[k].y;
+        if (((word >> (8 * (e & 3))) & 0xff) == want) acc[e] += bf2f(g[k][e]);
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
+    *(bf16x8*)(dx + i * 8) = o;
+    if constexpr (BNR) {
+      const unsigned mb = amask ? amask[i] : 0xffu;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float yf = bf2f(yv[e]);
+        float dz = bf2f(o[e]);
+        if (!((mb >> e) & 1u)) dz = 0.f;
+        if (!amask && mscale && !(yf * ms[e] + mh[e] > 0.f)) dz = 0.f;
+        s0[e] += dz;
+        s1[e] += dz * (yf - mu[e]) * is[e];
+      }
+    }
+  }
+  if constexpr (BNR) {
+    __shared__ float red[2][NT * 8];
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[0][t * 8 + e] = s0[e]; red[1][t * 8 + e] = s1[e]; }
+    __syncthreads();
+    if (t < cpr) {
+      float* st = sums + (long long)(blockIdx.x % shards) * 3 * C;
+      for (int pass = 0; pass < 2; ++pass) {
+        float a8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a8[e] = 0.f;
+        for (int rr = t; rr < NT; rr += cpr)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a8[e] += red[pass][rr * 8 + e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) atomicAdd(st + pass * C + c0 + e, a8[e]);
+      }
+    }
+  }
+}
+
 // x [N][HW][C] -> y [N][C] (bf16), mean over HW. One block per (n, 8*NT channel slab).
 __global__ void avgpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int HW, int C) {
   const int n = blockIdx.y;
@@ -202,6 +298,18 @@ int tfk_maxpool_bwd(const bf16* dy, const uint8_t* idx, bf16* dx, int N, int H, 
                     const float* mscale, const float* mshift, const unsigned char* amask, float* sums, int shards,
                     hipStream_t s) {
   long long total = (long long)N * H * W * (C / 8);
+  if (KH == 3 && KW == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 && NT % (C / 8) == 0 &&
+      P == (H - 1) / 2 + 1 && Q == (W - 1) / 2 + 1) {
+    if (sums) {
+      if (shards < 1) return -1;
+      hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel<true>, dim3(grid_for(total)), dim3(NT), 0, s, dy, idx, dx, N, H, W, C, P,
+                         Q, y, mean, invstd, mscale, mshift, amask, sums, shards);
+    } else {
+      hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel<false>, dim3(grid_for(total)), dim3(NT), 0, s, dy, idx, dx, N, H, W, C,
+                         P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   if (sums) {
     if (NT % (C / 8) != 0 || shards < 1) return -1;
     hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(grid_for(total)), dim3(NT), 0, s, dy, idx, dx, N, H, W, C, P, Q, KH,

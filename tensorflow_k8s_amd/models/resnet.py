@@ -28,6 +28,8 @@ PREMASK = True
 # the stem BN + relu applied inside the max-pool forward (ops.pool.maxpool_fwd bn=): no stem activation
 # (A/B: TFK_POOL_BN=0)
 POOL_BN = os.environ.get("TFK_POOL_BN", "1") != "0"
+# the stem BN's backward reduction fused into the max-pool backward (A/B: TFK_POOL_BNR=0)
+POOL_BNR = os.environ.get("TFK_POOL_BNR", "1") != "0"
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 IN_CH_PAD = 8  # RGB padded to 8 channels -> 16-B NHWC pixels for the implicit-GEMM gather
 
@@ -260,9 +262,13 @@ class ResNet:
         for i in range(nb - 1, -1, -1):
             nxt = self.blocks[i - 1].tail_reduce() if i > 0 else None
             dh = self.blocks[i].backward(dh, dout_reduced=i < nb - 1, next_bnr=nxt)
-        da0 = PL.maxpool_bwd(dh, idx, a0, 3, 2, 1)  # a0: the stem activation's shape
+        # a0: the stem activation's shape; the stem BN's backward sums accumulate inside the pool's
+        # backward (relu mask from y0), so no separate reduction pass re-reads dx and y0
+        bnr = BN.BNReduce(y0, self.bn1.st) if POOL_BNR else None
+        da0 = PL.maxpool_bwd(dh, idx, a0, 3, 2, 1, bnr=bnr)
         dy0, _, _ = BN.bn_backward(da0, None, y0, self.bn1.st, self.bn1.gamma.master, self.bn1.gamma.grad,
-                                   self.bn1.beta.grad, y0.numel() // y0.shape[-1], relu_from_y=True)
+                                   self.bn1.beta.grad, y0.numel() // y0.shape[-1], relu_from_y=True,
+                                   reduced=bnr is not None)
         self.arena.grad_ready(self.bn1.gamma, self.bn1.beta)
         self.conv1.backward(dy0, x0, need_dx=False)
         streams.join()  # side-stream weight gradients complete before anyone reads arena.grad

@@ -276,6 +276,7 @@ void Kubelet::start_container(PodRun& pr, ContainerRun& c) {
   auto vols = pod_volumes(pr, &verr);
   std::vector<MountSpec> mounts;
   for (auto& vm : spec->at("volumeMounts").items()) {
+    if (!verr.empty()) break;  // a volume of the pod failed its checks
     auto it = vols.find(vm.at("name").str());
     if (it == vols.end()) {
       verr = "volumeMount " + vm.at("name").str() + " names no volume of the pod";

@@ -178,3 +178,27 @@ def _volume_job(cluster, tmp_path):
     evals = _wait(lambda: [e for e in _events(c.logs("vol-evaluator-0")) if e.get("event") == "eval"
                            and e["step"] == 16], 60, "evaluator eval of the final checkpoint")
     assert evals[-1]["loss"] == evals[-1]["loss"]
+
+
+def test_bad_volume_blocks_container_with_failed_mount(cluster, tmp_path):
+    """A hostPath volume of type Directory that does not exist: the container is never started
+    (waiting, CreateContainerConfigError) and the kubelet records a FailedMount event; a readOnly
+    mount of an existing directory is bind-mounted / substituted like any other."""
+    c = cluster.client
+    missing = str(tmp_path / "nope")
+    ctr = _container(["python3", "-c", "pass"], volumeMounts=[{"name": "v", "mountPath": "/tfk-missing"}])
+    c.create(_job("badvol", {"Chief": _rs(1, ctr, volumes=[{"name": "v", "hostPath": {"path": missing,
+                                                                                       "type": "Directory"}}])}))
+
+    def waiting():
+        try:
+            p = c.get("pods", "badvol-chief-0")
+        except Exception:  # noqa: BLE001 -- not created yet
+            return None
+        cs = p.get("status", {}).get("containerStatuses") or []
+        w = cs[0]["state"].get("waiting", {}) if cs else {}
+        return w if w.get("reason") == "CreateContainerConfigError" else None
+    _wait(waiting, 60, "CreateContainerConfigError")
+    ev = _wait(lambda: _cluster_events(c, "FailedMount"), 30, "FailedMount event")
+    assert missing in ev[0]["message"], ev
+    assert not os.path.exists(missing)

@@ -21,6 +21,8 @@ import torch
 from ..ops._lib import lib
 
 SLOT_SUFFIX = {"Momentum": "Momentum", "Adam": "Adam", "Adam_1": "Adam_1"}
+# fault injection (tests): seconds every asynchronous checkpoint write stalls before writing
+FAULT_WRITE_DELAY_S = float(os.environ.get("TFK_FAULT_CKPT_DELAY_S", "0"))
 
 
 class CheckpointWriteError(RuntimeError):
@@ -74,6 +76,9 @@ class CheckpointManager:
 
         def work():
             try:
+                if FAULT_WRITE_DELAY_S > 0:
+                    import time
+                    time.sleep(FAULT_WRITE_DELAY_S)  # fault injection: a slow disk
                 names = sorted(tensors)
                 lib().ckpt_write(os.path.join(self.dir, name), names, [torch.from_numpy(tensors[n]) for n in names])
                 existing = self.all_checkpoints()

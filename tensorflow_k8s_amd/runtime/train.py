@@ -255,6 +255,7 @@ def run_worker(args, info, dev, world_comm, watchdog=None) -> int:
     wrank = info.worker_ranks.index(info.rank) if info.rank in info.worker_ranks else 0
 
     ckpt = CheckpointManager(args.checkpoint_dir, args.keep) if args.checkpoint_dir else None
+    _ACTIVE["ckpt"] = ckpt
     start = 0
     if ckpt is not None:
         s = ckpt.restore(model.arena, opt)
@@ -396,8 +397,29 @@ def _guard_error():
     return CommSelfTestError
 
 
+# the replica's in-flight state a graceful stop must not lose (SIGTERM handler below)
+_ACTIVE: dict = {}
+TERM_FLUSH_S = float(os.environ.get("TFK_TERM_FLUSH_S", "10"))
+
+
+def _on_sigterm(signum, frame):
+    """Graceful stop (gang restart, resize, job deletion: the kubelet's SIGTERM before its SIGKILL
+    deadline): let an asynchronous checkpoint write that is in flight finish -- the newest
+    checkpoint is what the next generation resumes from -- then exit 143 (retryable)."""
+    mgr = _ACTIVE.get("ckpt")
+    t = getattr(mgr, "_thread", None)
+    flushed = False
+    if t is not None and t.is_alive():
+        t.join(timeout=TERM_FLUSH_S)
+        flushed = not t.is_alive()
+    _log({"event": "terminated", "signal": int(signum), "checkpoint_flushed": flushed})
+    sys.stdout.flush()
+    os._exit(EXIT_RETRY)
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
+    signal.signal(signal.SIGTERM, _on_sigterm)
     from . import health
     health.beat(force=True)  # alive; later beats: setup phases and every step
     from ..parallel import cluster

@@ -72,3 +72,38 @@ def test_nonfinite_loss_fails_permanently(tmp_path):
     ev = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert ev[-1]["kind"] == "numerics"
     assert not [e for e in ev if e.get("event") == "checkpoint" and e.get("step", 0) >= 4]
+
+
+def test_sigterm_flushes_inflight_checkpoint(tmp_path):
+    """A graceful stop (the kubelet's SIGTERM on gang restart / resize) while an asynchronous
+    checkpoint write is in flight: the replica lets the write finish, then exits 143 -- the next
+    generation resumes from that checkpoint instead of an older one (or none)."""
+    import signal
+    import time
+    env = dict(os.environ, PYTHONPATH=ROOT, TFK_FAULT_CKPT_DELAY_S="2")
+    env.pop("TF_CONFIG", None)
+    ck = tmp_path / "ck"
+    p = subprocess.Popen([sys.executable, "-u", "-m", "tensorflow_k8s_amd.runtime.train", "--model", "lenet",
+                          "--steps", "1000", "--device", "cpu", "--checkpoint-dir", str(ck), "--checkpoint-every", "3",
+                          "--step-sleep", "0.05"], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    lines = []
+    try:
+        dl = time.time() + 120
+        while time.time() < dl:
+            line = p.stdout.readline()
+            if not line:
+                break
+            lines.append(line)
+            if '"event": "checkpoint"' in line:
+                p.send_signal(signal.SIGTERM)  # the write stalls 2 s: it is in flight now
+                break
+        out, _ = p.communicate(timeout=60)
+        lines.append(out)
+    finally:
+        if p.poll() is None:
+            p.kill()
+    assert p.returncode == 143, "".join(lines)[-2000:]
+    ev = [json.loads(l) for l in "".join(lines).splitlines() if l.startswith("{")]
+    term = [e for e in ev if e.get("event") == "terminated"]
+    assert term and term[-1]["checkpoint_flushed"] is True, ev[-3:]
+    assert (ck / "model.ckpt-3.index").exists() and "model.ckpt-3" in (ck / "checkpoint").read_text()

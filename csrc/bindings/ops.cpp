@@ -35,7 +35,6 @@ void tfk_set_seed_key(const unsigned long long* k);
 int tfk_rng_advance(unsigned long long* st, unsigned long long stream, hipStream_t s);
 void tfk_halo_set(int on);
 void tfk_bn_fin_skip(int v);
-int tfk_bn_set_unroll(int u);
 void tfk_fp8_set_tile(int t);
 void tfk_g8_set(int on);
 void tfk_g5_set(int waves);
@@ -1019,7 +1018,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_rng_key", &set_rng_key);
   m.def("halo_set", &tfk_halo_set);
   m.def("bn_fin_skip", &tfk_bn_fin_skip);
-  m.def("bn_set_unroll", [](int u) { TORCH_CHECK(tfk_bn_set_unroll(u) == 0, "bn_set_unroll: 1, 2 or 4"); });
   m.def("g5_set", &tfk_g5_set);  // 256x256 GEMMs on the mid-tile-barrier engine: 4 / 8 waves, 0 off
   m.def("g8_set", &tfk_g8_set);  // 256x256 dense GEMMs on the 8-phase engine: 1 on, 0 off
   m.def("fp8_set_tile", &tfk_fp8_set_tile);  // fp8 g4 tile: 0 by shape, 128 / 256 forced, -1 -> TFK_FP8_TILE

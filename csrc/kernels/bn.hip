@@ -136,7 +136,7 @@ __device__ __forceinline__ void load8(const float* __restrict__ p, float (&v)[8]
 // Streaming passes: with FIXED a thread owns one 8-channel chunk (tid % cpr) and walks rows, so
 // per-channel coefficients are loaded once into registers; needs NT % cpr == 0 (C | 2048). Other
 // C use the flat layout and reload the chunk's coefficients per element group.
-template <bool FIXED, int U = 1>
+template <bool FIXED>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const bf16* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
                                 const bf16* __restrict__ r, const float* __restrict__ rscale, const float* __restrict__ rshift,
                                 int relu, bf16* __restrict__ out, long long M, int C, unsigned char* __restrict__ mask) {
@@ -159,48 +159,36 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const bf16* __restrict__ y
     load8(scale + c0, s); load8(shift + c0, b);
     if (rscale) { load8(rscale + c0, rs); load8(rshift + c0, rb); }
   }
-  // U > 1: the loads of U grid-stride iterations are issued before any is used (more bytes in
-  // flight per wave; the loop otherwise waits for each 16-B load before issuing the next)
-  for (; i < end; i += U * step) {
+  for (; i < end; i += step) {
     if (!FIXED) {
       c0 = (int)((i >> 3) % cpr) * 8;
       load8(scale + c0, s); load8(shift + c0, b);
       if (rscale) { load8(rscale + c0, rs); load8(rshift + c0, rb); }
     }
-    bf16x8 v[U], rv[U];
+    bf16x8 v = *(const bf16x8*)(y + i);
+    float o[8];
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const long long j = (k == 0 || i + k * step < end) ? i + k * step : i;  // past the end: reload i
-      v[k] = *(const bf16x8*)(y + j);
-      if (r) rv[k] = *(const bf16x8*)(r + j);
+    for (int e = 0; e < 8; ++e) o[e] = bf2f(v[e]) * s[e] + b[e];
+    if (r) {
+      bf16x8 rv = *(const bf16x8*)(r + i);
+      if (rscale) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += bf2f(rv[e]) * rs[e] + rb[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += bf2f(rv[e]);
+      }
     }
+    bf16x8 w;
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const long long j = i + k * step;
-      if (k > 0 && j >= end) continue;
-      float o[8];
+    for (int e = 0; e < 8; ++e) w[e] = f2bf(relu ? fmaxf(o[e], 0.f) : o[e]);
+    *(bf16x8*)(out + i) = w;
+    if (mask) {
+      // bit e of byte i/8 = (out[i+e] > 0): the backward's relu mask at 1/16 of out's bytes
+      unsigned bits = 0;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = bf2f(v[k][e]) * s[e] + b[e];
-      if (r) {
-        if (rscale) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] += bf2f(rv[k][e]) * rs[e] + rb[e];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] += bf2f(rv[k][e]);
-        }
-      }
-      bf16x8 w;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) w[e] = f2bf(relu ? fmaxf(o[e], 0.f) : o[e]);
-      *(bf16x8*)(out + j) = w;
-      if (mask) {
-        // bit e of byte j/8 = (out[j+e] > 0): the backward's relu mask at 1/16 of out's bytes
-        unsigned bits = 0;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bits |= (bf2f(w[e]) > 0.f ? 1u : 0u) << e;
-        mask[j >> 3] = (unsigned char)bits;
-      }
+      for (int e = 0; e < 8; ++e) bits |= (bf2f(w[e]) > 0.f ? 1u : 0u) << e;
+      mask[i >> 3] = (unsigned char)bits;
     }
   }
 }
@@ -303,7 +291,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(float* sums, int s
 
 // dy = k1*dz + A*y + B; optional dy2 (projection-shortcut BN) or dres = dz (identity shortcut).
 // Relu mask: a > 0 if a is given, else y*mscale + mshift > 0 if mscale is given, else none.
-template <bool FIXED, int U = 1>
+template <bool FIXED>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16* __restrict__ da, const bf16* __restrict__ a, const bf16* __restrict__ y,
                                     const float* __restrict__ coef, bf16* __restrict__ dy, const bf16* __restrict__ y2,
                                     const float* __restrict__ coef2, bf16* __restrict__ dy2, bf16* __restrict__ dres,
@@ -330,53 +318,42 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16* __restrict
     if (!a && mscale) { load8(mscale + c0, ms); load8(mshift + c0, mh); }
   };
   if (FIXED) load_coefs();
-  for (; i < end; i += U * step) {
+  for (; i < end; i += step) {
     if (!FIXED) {
       c0 = (int)((i >> 3) % cpr) * 8;
       load_coefs();
     }
-    // U > 1: every load of U grid-stride iterations is issued before any is used (as bn_apply)
-    bf16x8 g[U], yv[U], av[U], y2v[U];
-    unsigned mb[U];
+    bf16x8 g = *(const bf16x8*)(da + i);
+    bf16x8 yv = *(const bf16x8*)(y + i);
+    bf16x8 av;
+    if (a) av = *(const bf16x8*)(a + i);
+    const unsigned mb = amask ? amask[i >> 3] : 0xffu;
+    float dz[8];
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const long long j = (k == 0 || i + k * step < end) ? i + k * step : i;  // past the end: reload i
-      g[k] = *(const bf16x8*)(da + j);
-      yv[k] = *(const bf16x8*)(y + j);
-      if (a) av[k] = *(const bf16x8*)(a + j);
-      mb[k] = amask ? amask[j >> 3] : 0xffu;
-      if (y2) y2v[k] = *(const bf16x8*)(y2 + j);
+    for (int e = 0; e < 8; ++e) {
+      dz[e] = bf2f(g[e]);
+      if (amask) {
+        if (!((mb >> e) & 1u)) dz[e] = 0.f;
+      } else if (a) {
+        if (!(bf2f(av[e]) > 0.f)) dz[e] = 0.f;
+      } else if (mscale) {
+        if (!(bf2f(yv[e]) * ms[e] + mh[e] > 0.f)) dz[e] = 0.f;
+      }
     }
+    bf16x8 o;
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const long long j = i + k * step;
-      if (k > 0 && j >= end) continue;
-      float dz[8];
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(k1[e] * dz[e] + A[e] * bf2f(yv[e]) + B[e]);
+    *(bf16x8*)(dy + i) = o;
+    if (y2) {
+      bf16x8 y2v = *(const bf16x8*)(y2 + i);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        dz[e] = bf2f(g[k][e]);
-        if (amask) {
-          if (!((mb[k] >> e) & 1u)) dz[e] = 0.f;
-        } else if (a) {
-          if (!(bf2f(av[k][e]) > 0.f)) dz[e] = 0.f;
-        } else if (mscale) {
-          if (!(bf2f(yv[k][e]) * ms[e] + mh[e] > 0.f)) dz[e] = 0.f;
-        }
-      }
-      bf16x8 o;
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(k1b[e] * dz[e] + A2[e] * bf2f(y2v[e]) + B2[e]);
+      *(bf16x8*)(dy2 + i) = o;
+    }
+    if (dres) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(k1[e] * dz[e] + A[e] * bf2f(yv[k][e]) + B[e]);
-      *(bf16x8*)(dy + j) = o;
-      if (y2) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(k1b[e] * dz[e] + A2[e] * bf2f(y2v[k][e]) + B2[e]);
-        *(bf16x8*)(dy2 + j) = o;
-      }
-      if (dres) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(dz[e]);
-        *(bf16x8*)(dres + j) = o;
-      }
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(dz[e]);
+      *(bf16x8*)(dres + i) = o;
     }
   }
 }
@@ -638,17 +615,10 @@ int grid_for(long long work, int per_block, int cap = 4096) {
 // launches, 2 the backward ones, 3 both -- the step time then bounds what fusing them into the
 // producing GEMM can save. Numerics are wrong while it is set.
 int g_fin_skip = 0;
-// Loads in flight per thread in the FIXED-layout apply passes (1, 2 or 4; tfk_bn_set_unroll, A/B knob).
-int g_bn_unroll = 1;
 }  // namespace
 
 extern "C" {
 void tfk_bn_fin_skip(int v) { g_fin_skip = v; }
-int tfk_bn_set_unroll(int u) {
-  if (u != 1 && u != 2 && u != 4) return -1;
-  g_bn_unroll = u;
-  return 0;
-}
 int tfk_bn_finalize(float* stats, int shards, int C, float count, const float* gamma, const float* beta, float eps,
                     float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* scale,
                     float* shift, hipStream_t s) {
@@ -666,13 +636,8 @@ int tfk_bn_apply(const bf16* y, const float* scale, const float* shift, const bf
                  const float* rshift, int relu, bf16* out, long long M, int C, unsigned char* mask, hipStream_t s) {
   const int cpr = C / 8;
   if (NT % cpr == 0) {
-    const dim3 g(grid_for(M, (NT / cpr) * 4, 8192));
-    if (g_bn_unroll == 4)
-      hipLaunchKernelGGL((bn_apply_kernel<true, 4>), g, dim3(NT), 0, s, y, scale, shift, r, rscale, rshift, relu, out, M, C, mask);
-    else if (g_bn_unroll == 2)
-      hipLaunchKernelGGL((bn_apply_kernel<true, 2>), g, dim3(NT), 0, s, y, scale, shift, r, rscale, rshift, relu, out, M, C, mask);
-    else
-      hipLaunchKernelGGL((bn_apply_kernel<true, 1>), g, dim3(NT), 0, s, y, scale, shift, r, rscale, rshift, relu, out, M, C, mask);
+    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(grid_for(M, (NT / cpr) * 4, 8192)), dim3(NT), 0, s, y, scale, shift, r,
+                       rscale, rshift, relu, out, M, C, mask);
   } else {
     hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(grid_for(M * cpr, NT * 4, 8192)), dim3(NT), 0, s, y, scale, shift,
                        r, rscale, rshift, relu, out, M, C, mask);
@@ -732,16 +697,8 @@ int tfk_bn_bwd_apply(const bf16* da, const bf16* a, const bf16* y, const float* 
                      const float* mshift, const unsigned char* amask, hipStream_t s) {
   const int cpr = C / 8;
   if (NT % cpr == 0) {
-    const dim3 g(grid_for(M, (NT / cpr) * 4, 8192));
-    if (g_bn_unroll == 4)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 4>), g, dim3(NT), 0, s, da, a, y, coef, dy, y2, coef2, dy2, dres, M, C,
-                         mscale, mshift, amask);
-    else if (g_bn_unroll == 2)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 2>), g, dim3(NT), 0, s, da, a, y, coef, dy, y2, coef2, dy2, dres, M, C,
-                         mscale, mshift, amask);
-    else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 1>), g, dim3(NT), 0, s, da, a, y, coef, dy, y2, coef2, dy2, dres, M, C,
-                         mscale, mshift, amask);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid_for(M, (NT / cpr) * 4, 8192)), dim3(NT), 0, s, da, a, y, coef,
+                       dy, y2, coef2, dy2, dres, M, C, mscale, mshift, amask);
   } else {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid_for(M * cpr, NT * 4, 8192)), dim3(NT), 0, s, da, a, y,
                        coef, dy, y2, coef2, dy2, dres, M, C, mscale, mshift, amask);

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""BatchNorm streaming passes at ResNet-50 bs256 shapes: device-event time per call and effective
-HBM bandwidth of bn_apply (+relu +packed mask) and bn_bwd_apply (bitmask relu) for each setting of
-the loads-in-flight knob (lib().bn_set_unroll), interleaved rounds in one process, plus a bit-equality
-check of every setting against unroll 1.   python tools/bn_probe.py [--iters 20] [--rounds 3]"""
+"""BatchNorm streaming passes at ResNet-50 bs256 shapes, each kernel alone on the GPU: device-event
+time per call and effective HBM bandwidth of bn_apply (+relu +packed mask) and bn_bwd_apply (bitmask
+relu), median of interleaved rounds. (Round 6 measured 5.0-6.8 TB/s, at the ~6.3 TB/s copy ceiling;
+issuing 2 or 4 grid-stride iterations' loads up front measured slower: profiles/perf_log_r6.md.)
+    python tools/bn_probe.py [--iters 20] [--rounds 3]"""
 import argparse
 import json
 import os
@@ -17,7 +18,6 @@ from tensorflow_k8s_amd.ops._lib import lib  # noqa: E402
 
 # (rows = N*H*W, C): the stage shapes of ResNet-50 at batch 256
 SHAPES = [(256 * 56 * 56, 64), (256 * 56 * 56, 256), (256 * 28 * 28, 512), (256 * 14 * 14, 1024), (256 * 7 * 7, 2048)]
-UNROLLS = (1, 2, 4)
 
 
 def _time(fn, iters):
@@ -47,30 +47,16 @@ def main():
         dy = torch.empty_like(y)
         fwd = lambda: lib().bn_apply(y, scale, shift, None, None, None, True, a, M, C, mask)  # noqa: E731
         bwd = lambda: lib().bn_bwd_apply(da, mask, y, coef, dy, None, None, None, None, M, C, None, None)  # noqa: E731
-        ref = {}
-        for u in UNROLLS:
-            lib().bn_set_unroll(u)
-            fwd(); bwd()
-            torch.cuda.synchronize()
-            got = (a.clone(), mask.clone(), dy.clone())
-            if u == 1:
-                ref = got
-            else:
-                for g, r in zip(got, ref):
-                    assert torch.equal(g, r), f"unroll {u} differs from unroll 1 at {(M, C)}"
         res = {}
         for _ in range(args.rounds):
-            for u in UNROLLS:
-                lib().bn_set_unroll(u)
-                res.setdefault(("fwd", u), []).append(_time(fwd, args.iters))
-                res.setdefault(("bwd", u), []).append(_time(bwd, args.iters))
-        lib().bn_set_unroll(1)
+            res.setdefault("fwd", []).append(_time(fwd, args.iters))
+            res.setdefault("bwd", []).append(_time(bwd, args.iters))
         nb = M * C * 2
         bytes_ = {"fwd": 2 * nb + nb // 16, "bwd": 3 * nb + nb // 16}
         row = {}
-        for (k, u), v in res.items():
+        for k, v in res.items():
             us = statistics.median(v)
-            row[f"{k}_u{u}"] = {"us": round(us, 2), "TB/s": round(bytes_[k] / us / 1e6, 2)}
+            row[k] = {"us": round(us, 2), "TB/s": round(bytes_[k] / us / 1e6, 2)}
         out[f"{M}x{C}"] = row
         print(json.dumps({f"{M}x{C}": row}), flush=True)
         del y, da, a, mask, dy

@@ -49,6 +49,22 @@ def main():
     print(f"per step: span {span / 1e6 / a.last:.3f} ms, busy {busy / 1e6 / a.last:.3f} ms, "
           f"idle {idle / 1e6 / a.last:.3f} ms ({100 * idle / span:.1f}%), kernel sum {ksum / 1e6 / a.last:.3f} ms "
           f"(overlap x{ksum / max(busy, 1):.2f}), {len(gaps) / a.last:.0f} gaps/step")
+    # per hardware queue: dispatches and busy time (a captured step's parallel branches -- the
+    # weight-gradient side streams, the comm stream -- land on their own queues)
+    per_q = collections.defaultdict(list)
+    for s_, e_, _, q in win:
+        per_q[q].append((s_, e_))
+    print("per queue (per step): dispatches, busy ms")
+    for q, iv in sorted(per_q.items(), key=lambda kv: -len(kv[1])):
+        qb, qe = 0, None
+        for s_, e_ in sorted(iv):
+            if qe is None or s_ > qe:
+                qb += e_ - s_
+                qe = e_
+            elif e_ > qe:
+                qb += e_ - qe
+                qe = e_
+        print(f"  queue {q}: {len(iv) / a.last:6.0f}  {qb / 1e6 / a.last:8.3f}")
     by_pair = collections.Counter()
     for g, p, n in gaps:
         by_pair[(p[:60], n[:60])] += g

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """LayerNorm backward at Transformer-big's shape (8192 x 1024, bf16 mode with the consumer dropout
-fused, as the model runs it): device-event time per call for rows-per-wave settings of the grid,
-interleaved rounds in one process.   python tools/ln_probe.py [--iters 50] [--rounds 5]"""
+fused, as the model runs it): device-event time per call for (rows per wave, rows of loads in flight
+per wave) settings, interleaved rounds in one process, outputs checked against the default.   python tools/ln_probe.py [--iters 50] [--rounds 5]"""
 import argparse
 import json
 import os
@@ -27,23 +27,30 @@ def main():
     gamma, beta = torch.rand(W, device="cuda") + 0.5, torch.zeros(W, device="cuda")
     _, mean, rstd = T.layernorm_fwd(x, gamma, beta)
     dg, db = torch.zeros(W, device="cuda"), torch.zeros(W, device="cuda")
-    res = {}
+    dres = torch.randn(M, W, device="cuda").to(torch.bfloat16)  # the residual branch's gradient
+    res, ref, err = {}, None, {}
+    cfgs = ((8, 1), (8, 2), (4, 2), (4, 1))
     for _ in range(args.rounds):
-        for rows in (8, 4, 2, 1):
+        for rows, pf in cfgs:
             lib().ln_bwd_set_rows(rows)
-            fn = lambda: T.layernorm_bwd(dy, x, gamma, mean, rstd, dg, db, drop=(0.1, 5))  # noqa: E731
-            fn()
+            lib().ln_bwd_set_prefetch(pf)
+            fn = lambda: T.layernorm_bwd(dy, x, gamma, mean, rstd, dg, db, dres=dres, drop=(0.1, 5))  # noqa: E731
+            out = fn()
+            dxo = out[0] if isinstance(out, (tuple, list)) else out
+            if ref is None:
+                ref = dxo.float().clone()
+            err[f"rows{rows}_pf{pf}"] = (dxo.float() - ref).abs().max().item()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(args.iters):
                 fn()
             e1.record()
             torch.cuda.synchronize()
-            res.setdefault(rows, []).append(e0.elapsed_time(e1) / args.iters * 1000.0)
+            res.setdefault(f"rows{rows}_pf{pf}", []).append(e0.elapsed_time(e1) / args.iters * 1000.0)
     lib().ln_bwd_set_rows(8)
-    print(json.dumps({"shape": [M, W], "us_per_call_by_rows_per_wave": {r: round(statistics.median(v), 2)
-                                                                          for r, v in res.items()}}))
-
+    lib().ln_bwd_set_prefetch(1)
+    print(json.dumps({"shape": [M, W], "us_per_call": {k: round(statistics.median(v), 2) for k, v in res.items()},
+                      "max_abs_dx_diff_vs_rows8_pf1": err}))
 
 if __name__ == "__main__":
     main()

@@ -10,4 +10,6 @@ cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 300 rocprofv3 --kernel-trace -d $D -o rn -- python3 $R/bench.py --steps 10 --warmup 3 "$@" > $O/bench.log 2>&1 || exit 3
 DB=$(find $D -name "*.db" | head -1)
 python3 $R/tools/rocpd_summary.py $DB --steps 13 > $O/kernels.txt 2>&1
-python3 $R/tools/rocpd_timeline.py $DB --steps 13 --last 3 --top 30 > $O/timeline.txt 2>&1
+# step windows aligned on the model's first kernel
+case "$*" in *bert*|*transformer*) FIRST=embed_fwd ;; *) FIRST=stem_fwd ;; esac
+python3 $R/tools/rocpd_timeline.py $DB --steps 13 --last 3 --top 30 --first $FIRST > $O/timeline.txt 2>&1

@@ -91,8 +91,25 @@ def main():
     print("largest all-idle time by (previous kernel -> next kernel), per step:")
     for (p, n), g in by_pair.most_common(a.top):
         print(f"  {g / 1e3 / nsteps:8.1f} us   {p}  ->  {n}")
+    # the largest single idle gaps, located by step and offset from the step's first dispatch (a
+    # gap that moves from step to step points at the host: graph-node submission falling behind)
+    if a.first:
+        step_t0 = [rows[i][0] for i in starts[-a.last - 1:]]
+        singles = []
+        cur, prev = None, None
+        for s, e, name, q in win:
+            if cur is not None and s > cur:
+                k = max(i for i, t in enumerate(step_t0) if t <= s)
+                singles.append((s - cur, k, (cur - step_t0[k]) / 1e3, prev, name))
+            if cur is None or e > cur:
+                cur, prev = e, name
+        print("largest single idle gaps: us, step, offset into the step (us), previous -> next")
+        for g, k, off, p, n in sorted(singles, reverse=True)[:10]:
+            print(f"  {g / 1e3:8.1f}  {k}  {off:9.1f}   {p[:50]}  ->  {n[:50]}")
     # main queue = the one with the most dispatches; its gaps = time the chain waits (on an event of
-    # another queue, or a launch). Attribute each gap to what the other queues ran inside it.
+    # another queue, or a launch). Attribute each gap to what the other queues ran inside it. (A
+    # replayed hipGraph may move a stream's chain between hardware queues after a fork / join: read
+    # this section only when the other queues' kernels are side-stream kernels.)
     mq = max(per_q, key=lambda q: len(per_q[q]))
     mk = sorted(per_q[mq])
     others = sorted((s, e, n) for q, iv in per_q.items() if q != mq for s, e, n in iv)

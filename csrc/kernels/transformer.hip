@@ -144,7 +144,7 @@ __global__ __launch_bounds__(LNMX_NT) void ln_fwd_mx_kernel(const bf16* __restri
   tfk::mx_rows32_out<LNMX_NT>(&tile[0][0], LNMX_WMAX + 8, W, M, r0, qr, sr, qc, sc);
 }
 
-template <int CPL, int PF = 1>
+template <int CPL>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, const bf16* __restrict__ dres,
@@ -183,39 +183,28 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
   int row = mxo ? blockIdx.x * 32 + wid * 8 : blockIdx.x * (NT / 64) + wid;
   const int rend = mxo ? row + 8 : M;
   bf16* mtile = (bf16*)(red + (NT / 64) * NS * W);  // [32][W + 8] (MX mode only)
-  // PF rows of loads in flight per wave: slot q of the ring holds row + (q + 1) * rstep's operands
-  // (PF = 2: the row loop is bound by one memory latency per row at PF = 1 -- 5 row tensors on
-  // Transformer-big's residual + dropout form are 84 MB per call)
-  bf16x8 ndv[PF][CPL], nxv[PF][CPL], nrv[PF][CPL];
-  float nmu[PF], nrs[PF];
-  auto fetch = [&](int q, int r) {
-    nmu[q] = mean[r];
-    nrs[q] = rstd[r];
+  bf16x8 ndv[CPL], nxv[CPL], nrv[CPL];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int r) {
+    nmu = mean[r];
+    nrs = rstd[r];
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
       const int c = lane + 64 * j;
       if (c < nch) {
-        ndv[q][j] = *(const bf16x8*)(dy + (long long)r * W + c * 8);
-        nxv[q][j] = *(const bf16x8*)(x + (long long)r * W + c * 8);
-        if (dres) nrv[q][j] = *(const bf16x8*)(dres + (long long)r * W + c * 8);
+        ndv[j] = *(const bf16x8*)(dy + (long long)r * W + c * 8);
+        nxv[j] = *(const bf16x8*)(x + (long long)r * W + c * 8);
+        if (dres) nrv[j] = *(const bf16x8*)(dres + (long long)r * W + c * 8);
       }
     }
   };
-#pragma unroll
-  for (int q = 0; q < PF; ++q)
-    if (row + q * rstep < rend) fetch(q, row + q * rstep);
+  if (row < rend) fetch(row);
   for (; row < rend; row += rstep) {
-    const float mu = nmu[0], rs = nrs[0];
+    const float mu = nmu, rs = nrs;
     bf16x8 cdv[CPL], cxv[CPL], crv[CPL];
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) { cdv[j] = ndv[0][j]; cxv[j] = nxv[0][j]; crv[j] = nrv[0][j]; }
-#pragma unroll
-    for (int q = 0; q + 1 < PF; ++q) {  // shift the ring (register renames after unrolling)
-      nmu[q] = nmu[q + 1]; nrs[q] = nrs[q + 1];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) { ndv[q][j] = ndv[q + 1][j]; nxv[q][j] = nxv[q + 1][j]; nrv[q][j] = nrv[q + 1][j]; }
-    }
-    if (row + PF * rstep < rend) fetch(PF - 1, row + PF * rstep);
+    for (int j = 0; j < CPL; ++j) { cdv[j] = ndv[j]; cxv[j] = nxv[j]; crv[j] = nrv[j]; }
+    if (row + rstep < rend) fetch(row + rstep);
     float g[CPL][8], xh[CPL][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -568,13 +557,6 @@ int tfk_layernorm_fwd_mx(const bf16* x, const float* gamma, const float* beta, b
 // wave = more blocks per CU in flight, more column-partial slabs for ln_part_reduce_kernel)
 static int g_ln_rows = 8;
 void tfk_ln_bwd_set_rows(int r) { g_ln_rows = r > 0 ? r : 8; }
-// rows of loads in flight per wave in the bf16-mode row loop (1 or 2; A/B knob)
-static int g_ln_pf = 1;
-int tfk_ln_bwd_set_prefetch(int pf) {
-  if (pf != 1 && pf != 2) return -1;
-  g_ln_pf = pf;
-  return 0;
-}
 int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (NT / 64) * g_ln_rows, 4096); }
 static unsigned ln_bwd_blocks(int M, bool mxo) { return (unsigned)tfk_ln_bwd_blocks(M, mxo ? 1 : 0); }
 // part (optional): f32 workspace [blocks][2 or 3][W] for the column partials (no tail atomics)
@@ -589,10 +571,6 @@ int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const f
   const size_t sh = (size_t)(NT / 64) * (dbias ? 3 : 2) * W * sizeof(float) + (mxo ? (size_t)32 * (W + 8) * 2 : 0);
   if (cpl <= 1)
     hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
-                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
-                       (unsigned char*)mqt, (unsigned char*)mst, part);
-  else if (cpl <= 2 && g_ln_pf == 2 && !mxo)
-    hipLaunchKernelGGL((ln_bwd_kernel<2, 2>), grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
                        dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
                        (unsigned char*)mqt, (unsigned char*)mst, part);
   else if (cpl <= 2)

@@ -36,7 +36,7 @@ MODE = os.environ.get("TFK_CONCURRENT_WGRAD", "auto")
 # reduce then overlaps the next weight gradient's GEMM. Measured (ResNet-50 bs256, same box):
 # 1 -> 25.64 ms, 2 -> 25.41 ms, 3 -> 25.76 ms; re-measured with the halved side-stream wgrad fill
 # (round 5, alternating): 1 -> 21.85 / 21.95, 2 -> 21.64 / 21.73 / 21.71, 3 -> 22.20 / 22.16 / 22.18
-NSIDE = 2
+NSIDE = int(os.environ.get("TFK_NSIDE", "2"))
 _side: dict[tuple[int, int], torch.cuda.Stream] = {}
 _keep: list[torch.Tensor] = []
 _rr = 0

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""LayerNorm backward at Transformer-big's shape (8192 x 1024, bf16 mode with the consumer dropout
-fused, as the model runs it): device-event time per call for (rows per wave, rows of loads in flight
-per wave) settings, interleaved rounds in one process, outputs checked against the default.   python tools/ln_probe.py [--iters 50] [--rounds 5]"""
+"""LayerNorm backward (default: Transformer-big's 8192 x 1024 with the residual-branch gradient and
+the consumer dropout fused, as the model runs it; --shape / --no-dres / --dbias for other call
+forms, e.g. BERT-base: --shape 8192 768 --dbias): device-event time per call for rows-per-wave
+settings, interleaved rounds in one process, outputs checked against the default.
+    python tools/ln_probe.py [--iters 50] [--rounds 5] [--shape M W] [--no-dres] [--dbias]"""
 import argparse
 import json
 import os
@@ -20,20 +22,24 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--shape", type=int, nargs=2, default=(8192, 1024), metavar=("M", "W"))
+    ap.add_argument("--no-dres", action="store_true", help="no residual-branch gradient")
+    ap.add_argument("--dbias", action="store_true", help="also reduce the consumer's bias gradient")
     args = ap.parse_args()
-    M, W = 8192, 1024
+    M, W = args.shape
     x = torch.randn(M, W, device="cuda").to(torch.bfloat16)
     dy = torch.randn(M, W, device="cuda").to(torch.bfloat16)
     gamma, beta = torch.rand(W, device="cuda") + 0.5, torch.zeros(W, device="cuda")
     _, mean, rstd = T.layernorm_fwd(x, gamma, beta)
     dg, db = torch.zeros(W, device="cuda"), torch.zeros(W, device="cuda")
-    dres = torch.randn(M, W, device="cuda").to(torch.bfloat16)  # the residual branch's gradient
+    dres = None if args.no_dres else torch.randn(M, W, device="cuda").to(torch.bfloat16)  # residual branch
+    dbias = torch.zeros(W, device="cuda") if args.dbias else None
     res, ref, err = {}, None, {}
     cfgs = ((8, 1), (4, 1))  # (rows per wave, rows of loads in flight: 2 measured slower, removed)
     for _ in range(args.rounds):
         for rows, pf in cfgs:
             lib().ln_bwd_set_rows(rows)
-            fn = lambda: T.layernorm_bwd(dy, x, gamma, mean, rstd, dg, db, dres=dres, drop=(0.1, 5))  # noqa: E731
+            fn = lambda: T.layernorm_bwd(dy, x, gamma, mean, rstd, dg, db, dres=dres, drop=(0.1, 5), dbias=dbias)  # noqa: E731
             out = fn()
             dxo = out[0] if isinstance(out, (tuple, list)) else out
             if ref is None:
@@ -47,7 +53,7 @@ def main():
             torch.cuda.synchronize()
             res.setdefault(f"rows{rows}_pf{pf}", []).append(e0.elapsed_time(e1) / args.iters * 1000.0)
     lib().ln_bwd_set_rows(8)
-    print(json.dumps({"shape": [M, W], "us_per_call": {k: round(statistics.median(v), 2) for k, v in res.items()},
+    print(json.dumps({"shape": [M, W], "dres": dres is not None, "dbias": dbias is not None, "us_per_call": {k: round(statistics.median(v), 2) for k, v in res.items()},
                       "max_abs_dx_diff_vs_rows8_pf1": err}))
 
 if __name__ == "__main__":

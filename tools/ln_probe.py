@@ -2,7 +2,8 @@
 """LayerNorm backward (default: Transformer-big's 8192 x 1024 with the residual-branch gradient and
 the consumer dropout fused, as the model runs it; --shape / --no-dres / --dbias for other call
 forms, e.g. BERT-base: --shape 8192 768 --dbias): device-event time per call for rows-per-wave
-settings, interleaved rounds in one process, outputs checked against the default.
+settings (calls replayed from a captured graph), interleaved rounds in one process, outputs checked
+against the default.
     python tools/ln_probe.py [--iters 50] [--rounds 5] [--shape M W] [--no-dres] [--dbias]"""
 import argparse
 import json
@@ -47,10 +48,17 @@ def main():
             if ref is None:
                 ref = dxo.float().clone()
             err[f"rows{rows}_g{pf}"] = (dxo.float() - ref).abs().max().item()
+            # the calls replay from one captured graph: host launch overhead (allocation, binding,
+            # two launches per call) would otherwise set a ~20-25 us floor of its own
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(args.iters):
+                    fn()
+            g.replay()
+            torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(args.iters):
-                fn()
+            g.replay()
             e1.record()
             torch.cuda.synchronize()
             res.setdefault(f"rows{rows}_g{pf}", []).append(e0.elapsed_time(e1) / args.iters * 1000.0)

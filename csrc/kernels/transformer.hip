@@ -144,7 +144,7 @@ __global__ __launch_bounds__(LNMX_NT) void ln_fwd_mx_kernel(const bf16* __restri
   tfk::mx_rows32_out<LNMX_NT>(&tile[0][0], LNMX_WMAX + 8, W, M, r0, qr, sr, qc, sc);
 }
 
-template <int CPL, int G = 0>
+template <int CPL>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, const bf16* __restrict__ dres,
@@ -172,9 +172,9 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
       gm[j][e] = c < nch ? gamma[c * 8 + e] : 0.f;
     }
   }
-  // Row loop, G == 0: software-pipelined by one row (the next row's dy / x / dres and mean / rstd
-  // are loaded before this row's reductions and stores; measured 2.2 TB/s on Transformer-big's
-  // 8192 x 1024 rows without it). G > 0: groups of G rows whose loads are all issued up front.
+  // rows software-pipelined: the next row's dy / x / dres (and mean / rstd) are loaded before this
+  // row's reductions and stores, so a wave keeps one row of loads in flight instead of paying two
+  // dependent memory latencies per row (measured 2.2 TB/s on Transformer-big's 8192 x 1024 rows)
   // MX mode (mq != null: emit MX-fp8 row + column blocks of the consumer gradient): a block owns 32
   // consecutive rows (8 per wave), stages their final values in an LDS tile behind `red` and
   // quantizes the tile after the row loop (the consumer's fp8 backward then skips its quantize pass)
@@ -183,9 +183,28 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
   int row = mxo ? blockIdx.x * 32 + wid * 8 : blockIdx.x * (NT / 64) + wid;
   const int rend = mxo ? row + 8 : M;
   bf16* mtile = (bf16*)(red + (NT / 64) * NS * W);  // [32][W + 8] (MX mode only)
-  // one row's reductions and stores from its loaded dy / x / dres chunks
-  auto do_row = [&](int row, float mu, float rs, const bf16x8 (&cdv)[CPL], const bf16x8 (&cxv)[CPL],
-                    const bf16x8 (&crv)[CPL]) {
+  bf16x8 ndv[CPL], nxv[CPL], nrv[CPL];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int r) {
+    nmu = mean[r];
+    nrs = rstd[r];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        ndv[j] = *(const bf16x8*)(dy + (long long)r * W + c * 8);
+        nxv[j] = *(const bf16x8*)(x + (long long)r * W + c * 8);
+        if (dres) nrv[j] = *(const bf16x8*)(dres + (long long)r * W + c * 8);
+      }
+    }
+  };
+  if (row < rend) fetch(row);
+  for (; row < rend; row += rstep) {
+    const float mu = nmu, rs = nrs;
+    bf16x8 cdv[CPL], cxv[CPL], crv[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) { cdv[j] = ndv[j]; cxv[j] = nxv[j]; crv[j] = nrv[j]; }
+    if (row + rstep < rend) fetch(row + rstep);
     float g[CPL][8], xh[CPL][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -246,58 +265,6 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
           if (mxo) *(bf16x8*)(mtile + (row - blockIdx.x * 32) * (W + 8) + c * 8) = o;
         }
       }
-    }
-  };
-  if constexpr (G == 0) {
-    bf16x8 ndv[CPL], nxv[CPL], nrv[CPL];
-    float nmu = 0.f, nrs = 0.f;
-    auto fetch = [&](int r) {
-      nmu = mean[r];
-      nrs = rstd[r];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        const int c = lane + 64 * j;
-        if (c < nch) {
-          ndv[j] = *(const bf16x8*)(dy + (long long)r * W + c * 8);
-          nxv[j] = *(const bf16x8*)(x + (long long)r * W + c * 8);
-          if (dres) nrv[j] = *(const bf16x8*)(dres + (long long)r * W + c * 8);
-        }
-      }
-    };
-    if (row < rend) fetch(row);
-    for (; row < rend; row += rstep) {
-      const float mu = nmu, rs = nrs;
-      bf16x8 cdv[CPL], cxv[CPL], crv[CPL];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) { cdv[j] = ndv[j]; cxv[j] = nxv[j]; crv[j] = nrv[j]; }
-      if (row + rstep < rend) fetch(row + rstep);
-      do_row(row, mu, rs, cdv, cxv, crv);
-    }
-  } else {
-    // G rows per group, every load of the group issued before its first row is used and no
-    // register copies of in-flight loads (the G == 0 ring's copies made hipcc wait for the
-    // prefetched row at every iteration: one full memory latency per row). Loads are
-    // unconditional: rows past the end and lanes past the row reload valid addresses.
-    const int cl = lane < nch ? lane : 0;
-    for (; row < rend; row += G * rstep) {
-      bf16x8 gdv[G][CPL], gxv[G][CPL], grv[G][CPL];
-      float gmu[G], grs[G];
-#pragma unroll
-      for (int q = 0; q < G; ++q) {
-        const int r = row + q * rstep < rend ? row + q * rstep : row;
-        gmu[q] = mean[r];
-        grs[q] = rstd[r];
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-          const int c = lane + 64 * j < nch ? lane + 64 * j : cl;
-          gdv[q][j] = *(const bf16x8*)(dy + (long long)r * W + c * 8);
-          gxv[q][j] = *(const bf16x8*)(x + (long long)r * W + c * 8);
-          if (dres) grv[q][j] = *(const bf16x8*)(dres + (long long)r * W + c * 8);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < G; ++q)
-        if (q == 0 || row + q * rstep < rend) do_row(row + q * rstep, gmu[q], grs[q], gdv[q], gxv[q], grv[q]);
     }
   }
 #pragma unroll
@@ -590,14 +557,6 @@ int tfk_layernorm_fwd_mx(const bf16* x, const float* gamma, const float* beta, b
 // wave = more blocks per CU in flight, more column-partial slabs for ln_part_reduce_kernel)
 static int g_ln_rows = 8;
 void tfk_ln_bwd_set_rows(int r) { g_ln_rows = r > 0 ? r : 8; }
-// row-loop form of the W <= 1024 kernels: 0 = one-row software pipeline, 2 / 4 / 8 = rows per
-// group with every load of a group issued up front (A/B knob: tools/ln_probe.py)
-static int g_ln_group = 0;
-int tfk_ln_bwd_set_group(int g) {
-  if (g != 0 && g != 2 && g != 4 && g != 8) return -1;
-  g_ln_group = g;
-  return 0;
-}
 int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (NT / 64) * g_ln_rows, 4096); }
 static unsigned ln_bwd_blocks(int M, bool mxo) { return (unsigned)tfk_ln_bwd_blocks(M, mxo ? 1 : 0); }
 // part (optional): f32 workspace [blocks][2 or 3][W] for the column partials (no tail atomics)
@@ -610,25 +569,19 @@ int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const f
   if (mxo && (M % 32 || W % 32 || W > 1024)) return -3;
   dim3 grid(ln_bwd_blocks(M, mxo));
   const size_t sh = (size_t)(NT / 64) * (dbias ? 3 : 2) * W * sizeof(float) + (mxo ? (size_t)32 * (W + 8) * 2 : 0);
-#define TFK_LN_BWD(CPL_, G_)                                                                                        \
-  hipLaunchKernelGGL((ln_bwd_kernel<CPL_, G_>), grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, \
-                     M, W, dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,         \
-                     (unsigned char*)mqt, (unsigned char*)mst, part)
-  if (cpl <= 1) {
-    if (g_ln_group == 8) TFK_LN_BWD(1, 8);
-    else if (g_ln_group == 4) TFK_LN_BWD(1, 4);
-    else if (g_ln_group == 2) TFK_LN_BWD(1, 2);
-    else TFK_LN_BWD(1, 0);
-  } else if (cpl <= 2) {
-    if (g_ln_group == 8) TFK_LN_BWD(2, 8);
-    else if (g_ln_group == 4) TFK_LN_BWD(2, 4);
-    else if (g_ln_group == 2) TFK_LN_BWD(2, 2);
-    else TFK_LN_BWD(2, 0);
-  }
+  if (cpl <= 1)
+    hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
+                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
+                       (unsigned char*)mqt, (unsigned char*)mst, part);
+  else if (cpl <= 2)
+    hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
+                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
+                       (unsigned char*)mqt, (unsigned char*)mst, part);
   else if (cpl <= 4)
-    TFK_LN_BWD(4, 0);
+    hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
+                       dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
+                       (unsigned char*)mqt, (unsigned char*)mst, part);
   else return -3;
-#undef TFK_LN_BWD
   if (part) {
     const int NS = dbias ? 3 : 2;
     // one group per <= 8 slabs (every load of a thread in flight at once), at least LN_PART_GROUPS

@@ -36,12 +36,12 @@ def main():
     dres = None if args.no_dres else torch.randn(M, W, device="cuda").to(torch.bfloat16)  # residual branch
     dbias = torch.zeros(W, device="cuda") if args.dbias else None
     res, ref, err = {}, None, {}
-    # (rows per wave, row-loop group: 0 = one-row pipeline, G = G rows' loads issued up front)
-    cfgs = ((8, 0), (8, 2), (8, 4), (8, 8), (4, 4))
+    # (rows per wave, unused): issuing 2-8 rows' loads up front and a two-row prefetch ring both
+    # measured slower (profiles/perf_log_r6.md)
+    cfgs = ((8, 0), (4, 0))
     for _ in range(args.rounds):
         for rows, pf in cfgs:
             lib().ln_bwd_set_rows(rows)
-            lib().ln_bwd_set_group(pf)
             fn = lambda: T.layernorm_bwd(dy, x, gamma, mean, rstd, dg, db, dres=dres, drop=(0.1, 5), dbias=dbias)  # noqa: E731
             out = fn()
             dxo = out[0] if isinstance(out, (tuple, list)) else out
@@ -63,7 +63,6 @@ def main():
             torch.cuda.synchronize()
             res.setdefault(f"rows{rows}_g{pf}", []).append(e0.elapsed_time(e1) / args.iters * 1000.0)
     lib().ln_bwd_set_rows(8)
-    lib().ln_bwd_set_group(0)
     print(json.dumps({"shape": [M, W], "dres": dres is not None, "dbias": dbias is not None, "us_per_call": {k: round(statistics.median(v), 2) for k, v in res.items()},
                       "max_abs_dx_diff_vs_rows8_g0": err}))
 

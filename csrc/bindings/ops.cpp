@@ -23,7 +23,6 @@ int tfk_gemm_splits(int K, int splits);
 void tfk_gemm_set_persist(int on);
 void tfk_gemm_set_engine(int e);
 void tfk_g4_set_shortk(int on);
-int tfk_g4_set_bnr_group(int g);
 extern "C" void tfk_fp8_set_engine(int e);
 int tfk_mx_quant(const void*, void*, void*, long long, hipStream_t);
 int tfk_mx_quant_t(const void*, void*, void*, int, int, hipStream_t);
@@ -964,7 +963,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_persist", &gemm_set_persist);
   m.def("gemm_set_engine", &gemm_set_engine);
   m.def("gemm_set_shortk", &gemm_set_shortk);
-  m.def("g4_set_bnr_group", [](int g) { TORCH_CHECK(tfk_g4_set_bnr_group(g) == 0, "g4_set_bnr_group: 0, 4 or 8"); });
   m.def("fp8_set_engine", &fp8_set_engine);
   m.def("mx_quant", &mx_quant);
   m.def("mx_quant_t", &mx_quant_t);

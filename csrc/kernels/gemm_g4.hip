@@ -54,8 +54,7 @@ constexpr int nwaves() { return (BM / 64) * (BN / 64); }
 template <int BM, int BN>
 constexpr int occ_default() { return (BM * BN <= 128 * 128) ? 2 : 1; }
 
-// BG > 0: BN-reduce epilogue chunks in flight per thread (default: by the VGPR budget)
-template <int BM, int BN, int AM, int BMD, int EPI, int OCC = occ_default<BM, BN>(), int NST = 2, int BG = 0>
+template <int BM, int BN, int AM, int BMD, int EPI, int OCC = occ_default<BM, BN>(), int NST = 2>
 __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmParams p) {
   constexpr int NW = nwaves<BM, BN>(), NTH = NW * 64, WGM = BM / 64, WGN = BN / 64;
   constexpr int LBM = BMD == 2 ? CONV_WGRAD : BMD;  // B_CONV_WGRAD (= 2 in the B-mode numbering)
@@ -201,7 +200,7 @@ __global__ __launch_bounds__((nwaves<BM, BN>() * 64), OCC) void g4_kernel(GemmPa
   __syncthreads();
   // BN-reduce chunks in flight per thread by VGPR budget: 512 / (waves per SIMD)
   constexpr int WPS = (NW * OCC) / 4 > 0 ? (NW * OCC) / 4 : 1;
-  gemm_epilogue<BM, BN, NTH, WGM, EPI, (BG > 0 ? BG : 512 / WPS >= 256 ? 4 : 2)>(p, acc, smem, m0, n0, bz);
+  gemm_epilogue<BM, BN, NTH, WGM, EPI, (512 / WPS >= 256 ? 4 : 2)>(p, acc, smem, m0, n0, bz);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -390,24 +389,6 @@ static int shortk_max_kt() {
 }
 // < 0: back to the environment / built-in default
 extern "C" void tfk_g4_set_shortk(int max_kt) { g_shortk = max_kt < 0 ? -1 : max_kt; }
-// BN-reduce 128x128 GEMMs (the BN-backward dgrads): 0 = the single-stage 4-blocks-per-CU variant for
-// few K-tiles (2 BN-input chunks in flight per thread, its 128-VGPR budget), 4 / 8 = the 2-stage
-// 2-blocks-per-CU kernel with that many chunks' loads issued before the first is used (A/B knob:
-// TFK_G4_BNR_G or tfk_g4_set_bnr_group)
-static int g_bnr_g = -1;
-static int bnr_group() {
-  if (g_bnr_g < 0) {
-    const char* e = getenv("TFK_G4_BNR_G");
-    const int g = e ? atoi(e) : 0;
-    g_bnr_g = (g == 4 || g == 8) ? g : 0;
-  }
-  return g_bnr_g;
-}
-extern "C" int tfk_g4_set_bnr_group(int g) {
-  if (g != 0 && g != 4 && g != 8) return -1;
-  g_bnr_g = g;
-  return 0;
-}
 
 static void fast_div(unsigned d, unsigned* mul, int* shift) {
   int s = 0;
@@ -450,19 +431,6 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
   }
   // few K-tiles per block: the 4-blocks-per-CU single-stage instantiations (TFK_G4_SHORTK=0: off;
   // one K-tile measured ResNet-50 bs256: 30.40 -> 29.72 ms/step)
-  if (bnr_group() && epi == EPI_BF16_BNR && bm == 128 && bn == 128 && !(amode == 2 && p.Cin < 64)) {
-#define TFK_G4_BNRG(AM_, BM2_, G_)                                                                                  \
-  if (amode == AM_ && bmode == BM2_ && g_bnr_g == G_) {                                                           \
-    hipLaunchKernelGGL((g4::g4_kernel<128, 128, AM_, BM2_, EPI_BF16_BNR, 2, 2, G_>), dim3(tiles, batch, splits), \
-                       dim3(g4::nwaves<128, 128>() * 64), 0, stream, p);                                           \
-    return hipGetLastError() == hipSuccess ? 0 : -2;                                                              \
-  }
-    TFK_G4_BNRG(0, 1, 4)
-    TFK_G4_BNRG(0, 1, 8)
-    TFK_G4_BNRG(2, 0, 4)
-    TFK_G4_BNRG(2, 0, 8)
-#undef TFK_G4_BNRG
-  }
   if (p.kt_per_split <= shortk_max_kt() && bm == 128 && bn == 128 && !(amode == 2 && p.Cin < 64)) {
     TFK_G4_SHORTK(0, 0, EPI_BF16)
     TFK_G4_SHORTK(0, 1, EPI_BF16)

@@ -431,21 +431,6 @@ def test_dgrad_fused_bn_reduce(cfg, mode):
         assert rel(res[DEV][1][k], res["cpu"][1][k]) < 2e-2, k
 
 
-@pytest.mark.parametrize("group", [4, 8])
-@pytest.mark.parametrize("mode", ["relu_from_y", "mask_a", "dual"])
-@pytest.mark.parametrize("cfg", [(4, 16, 16, 256, 128, 1, 1, 1, 0), (3, 20, 20, 256, 256, 3, 3, 1, 1),
-                                 (2, 14, 14, 256, 512, 1, 1, 2, 0), (2, 15, 13, 128, 128, 3, 3, 1, 1)])
-def test_dgrad_fused_bn_reduce_chunk_groups(cfg, mode, group):
-    """The BN-reduce dgrads on the 2-blocks-per-CU kernel with 4 / 8 BN-input chunks in flight per
-    thread (gemm_g4.hip tfk_g4_set_bnr_group, A/B knob) == the references, as the default kernel."""
-    from tensorflow_k8s_amd.ops._lib import lib
-    lib().g4_set_bnr_group(group)
-    try:
-        test_dgrad_fused_bn_reduce(cfg, mode)
-    finally:
-        lib().g4_set_bnr_group(0)
-
-
 @pytest.mark.parametrize("mode", ["relu_from_y", "mask_a", "dual"])
 @pytest.mark.parametrize("cfg", [(2, 9, 9, 64, 64, 3, 3, 1, 1), (3, 20, 20, 64, 128, 3, 3, 1, 1)])
 def test_dgrad_as_fwd_256x64(cfg, mode, monkeypatch):

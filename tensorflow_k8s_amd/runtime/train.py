@@ -27,7 +27,11 @@ import signal
 import sys
 import time
 
-import torch
+# 8 hardware queues per process (HIP's default is 4): measured faster for the captured steps
+# (bench.py, profiles/perf_log_r6.md); set before the HIP runtime initializes. TFK_HW_QUEUES overrides.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("TFK_HW_QUEUES", "8")
+
+import torch  # noqa: E402
 
 EXIT_OK, EXIT_USER, EXIT_OOM, EXIT_RETRY = 0, 1, 137, 143
 

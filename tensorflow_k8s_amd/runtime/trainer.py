@@ -19,13 +19,7 @@ the reason) -- nobody is left waiting in a replayed collective its peer never is
 """
 from __future__ import annotations
 
-import os
-
 import torch
-
-# A/B knob: capture and replay the step on a high-priority stream (the side streams and their weight
-# gradients stay at the default priority), so the hardware favours the input-gradient chain's waves.
-MAIN_PRIO = os.environ.get("TFK_MAIN_PRIO", "0") == "1"
 
 
 class GraphUnsafe(RuntimeError):
@@ -63,7 +57,6 @@ class StepRunner:
         self.warmup_eager = warmup_eager
         self.agree, self.rank = agree, rank
         self.graph = None
-        self._hp = None  # MAIN_PRIO: the high-priority capture / replay stream
         self.n = 0
         self._loss = None
         self._corr = None
@@ -103,14 +96,7 @@ class StepRunner:
             if not self._capture():
                 self._loss, self._corr = self._step_body()  # agreed fallback: this step runs eager
                 return
-        if self._hp is None:
-            self.graph.replay()
-            return
-        cur = torch.cuda.current_stream()
-        self._hp.wait_stream(cur)
-        with torch.cuda.stream(self._hp):
-            self.graph.replay()
-        cur.wait_stream(self._hp)
+        self.graph.replay()
 
     def _capture(self) -> bool:
         from .guard import Agreement, capture_fault
@@ -121,8 +107,7 @@ class StepRunner:
             capture_fault("step", self.rank)
             # thread-local capture: a watchdog thread polling RCCL / events while this thread
             # captures must not invalidate the capture (the default global mode would)
-            self._hp = torch.cuda.Stream(priority=-1) if MAIN_PRIO else None
-            with torch.cuda.graph(g, stream=self._hp, capture_error_mode="thread_local"):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._loss, self._corr = self._step_body()
         except Exception as e:  # noqa: BLE001 -- every failure votes no
             err = f"{type(e).__name__}: {e}"[:600]
@@ -134,7 +119,7 @@ class StepRunner:
             if not ok:
                 err = Agreement.summary(bad)
         if not ok:
-            self.graph, self.use_graph, self.fallback, self._hp = None, False, err, None
+            self.graph, self.use_graph, self.fallback = None, False, err
             del g
             torch.cuda.synchronize()
             from . import streams

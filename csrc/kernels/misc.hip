@@ -196,12 +196,25 @@ __global__ void colsum8_kernel(const bf16* __restrict__ x, long long M, int N, l
   float s[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s[e] = 0.f;
-  if (c < N)
-    for (long long r = (long long)blockIdx.y * 4 + rg; r < M; r += (long long)gridDim.y * 4) {
-      const bf16x8 v = *(const bf16x8*)(x + r * ld + c);
+  if (c < N) {
+    // 4 rows' loads in flight per lane (rows past M reload row r; their values are not added): the
+    // one-load-per-iteration loop waited one memory latency per row (BERT-base: 14 us per call)
+    const long long step = (long long)gridDim.y * 4;
+    for (long long r = (long long)blockIdx.y * 4 + rg; r < M; r += 4 * step) {
+      bf16x8 v[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s[e] += bf2f(v[e]);
+      for (int k = 0; k < 4; ++k) {
+        const long long rk = r + k * step < M ? r + k * step : r;
+        v[k] = *(const bf16x8*)(x + rk * ld + c);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k == 0 || r + k * step < M) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s[e] += bf2f(v[k][e]);
+        }
     }
+  }
   __shared__ float red[4][512];
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[rg][lane * 8 + e] = s[e];

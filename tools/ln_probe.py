@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--shape", type=int, nargs=2, default=(8192, 1024), metavar=("M", "W"))
     ap.add_argument("--no-dres", action="store_true", help="no residual-branch gradient")
     ap.add_argument("--dbias", action="store_true", help="also reduce the consumer's bias gradient")
+    ap.add_argument("--no-drop", action="store_true", help="no fused consumer dropout")
     args = ap.parse_args()
     M, W = args.shape
     x = torch.randn(M, W, device="cuda").to(torch.bfloat16)
@@ -42,7 +43,7 @@ def main():
     for _ in range(args.rounds):
         for rows, pf in cfgs:
             lib().ln_bwd_set_rows(rows)
-            fn = lambda: T.layernorm_bwd(dy, x, gamma, mean, rstd, dg, db, dres=dres, drop=(0.1, 5), dbias=dbias)  # noqa: E731
+            fn = lambda: T.layernorm_bwd(dy, x, gamma, mean, rstd, dg, db, dres=dres, drop=None if args.no_drop else (0.1, 5), dbias=dbias)  # noqa: E731
             out = fn()
             dxo = out[0] if isinstance(out, (tuple, list)) else out
             if ref is None:
@@ -63,7 +64,7 @@ def main():
             torch.cuda.synchronize()
             res.setdefault(f"rows{rows}_g{pf}", []).append(e0.elapsed_time(e1) / args.iters * 1000.0)
     lib().ln_bwd_set_rows(8)
-    print(json.dumps({"shape": [M, W], "dres": dres is not None, "dbias": dbias is not None, "us_per_call": {k: round(statistics.median(v), 2) for k, v in res.items()},
+    print(json.dumps({"shape": [M, W], "dres": dres is not None, "dbias": dbias is not None, "drop": not args.no_drop, "us_per_call": {k: round(statistics.median(v), 2) for k, v in res.items()},
                       "max_abs_dx_diff_vs_rows8_g0": err}))
 
 if __name__ == "__main__":

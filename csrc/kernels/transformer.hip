@@ -309,6 +309,130 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
 // (LN_PART_GROUPS adders per address instead of one per block). 32 groups of <= 8 slabs with the 8
 // loads of a group in flight together: 8 groups of 32 slabs walked one load at a time measured
 // 9.4 us per call on Transformer-big (256 slabs x 2 x 1024: a latency chain, 0.3 TB/s).
+// Width-specialized LayerNorm backward (bf16 mode, W = 256 * Q4: BERT-base 768, Transformer-big /
+// BERT-large 1024). PMC of ln_bwd_kernel (profiles/pmc_ln_bwd_r6.txt): ~37 VALU instructions per
+// element -- per-lane chunk guards, runtime option branches, 64-bit index math and register copies
+// of the prefetched row -- against ~13 the arithmetic needs, at one wave per SIMD: VALU issue and
+// memory waits did not overlap (22.5 us for the 48 MB of a plain 8192 x 1024 call). Here width and
+// options are compile-time, lane l owns the 4-element chunks l + 64 q (q < Q4; every 8-B load of a
+// wave is a contiguous 512 B), and each iteration loads two rows before using either.
+template <int Q4, bool DRES, bool DROP, bool DBIAS>
+__global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                         const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, const bf16* __restrict__ dres,
+                                                         bf16* __restrict__ dx, float* __restrict__ dgamma,
+                                                         float* __restrict__ dbeta, int M, bf16* __restrict__ dxd,
+                                                         float drop_p, unsigned long long drop_salt,
+                                                         const unsigned long long* __restrict__ drop_key,
+                                                         float* __restrict__ dbias, float* __restrict__ part) {
+  constexpr int W = 256 * Q4, NS = DBIAS ? 3 : 2;
+  extern __shared__ float red[];  // [NT/64][NS][W]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float gm[Q4][4], dg[Q4][4], db[Q4][4], bs[Q4][4];
+#pragma unroll
+  for (int q = 0; q < Q4; ++q) {
+    const f32x4 g4 = *(const f32x4*)(gamma + lane * 4 + 256 * q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { gm[q][e] = g4[e]; dg[q][e] = 0.f; db[q][e] = 0.f; bs[q][e] = 0.f; }
+  }
+  const uint32_t s32 = DROP ? drop_seed32(eff_seed(drop_salt, drop_key)) : 0u;
+  const uint32_t thr = DROP ? (uint32_t)drop_thr8(drop_p) : 0u;
+  const float inv = DROP ? drop_scale8(drop_p) : 1.f;
+  auto load_row = [&](int r, bf16x4 (&dv)[Q4], bf16x4 (&xv)[Q4], bf16x4 (&rv)[Q4]) {
+    const long long base = (long long)r * W + lane * 4;
+#pragma unroll
+    for (int q = 0; q < Q4; ++q) {
+      dv[q] = *(const bf16x4*)(dy + base + 256 * q);
+      xv[q] = *(const bf16x4*)(x + base + 256 * q);
+      if constexpr (DRES) rv[q] = *(const bf16x4*)(dres + base + 256 * q);
+    }
+  };
+  auto do_row = [&](int r, float mu, float rs, const bf16x4 (&dv)[Q4], const bf16x4 (&xv)[Q4], const bf16x4 (&rv)[Q4]) {
+    float g[Q4][4], xh[Q4][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < Q4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = bf2f(dv[q][e]);
+        xh[q][e] = (bf2f(xv[q][e]) - mu) * rs;
+        g[q][e] = d * gm[q][e];
+        s1 += g[q][e];
+        s2 += g[q][e] * xh[q][e];
+        dg[q][e] += d * xh[q][e];
+        db[q][e] += d;
+      }
+    s1 = wave_sum(s1) / W;
+    s2 = wave_sum(s2) / W;
+    const long long base = (long long)r * W + lane * 4;
+#pragma unroll
+    for (int q = 0; q < Q4; ++q) {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = rs * (g[q][e] - s1 - xh[q][e] * s2);
+        if constexpr (DRES) v += bf2f(rv[q][e]);
+        o[e] = f2bf(v);
+      }
+      *(bf16x4*)(dx + base + 256 * q) = o;
+      if constexpr (DROP) {
+        // the consumer's dropout backward: misc.hip's mask (one hash per 4 elements, byte e of
+        // hash32(s32 ^ idx / 4) against the 8-bit threshold) on index r * W + col
+        const uint32_t h = hash32(s32 ^ (uint32_t)((base + 256 * q) >> 2));
+        bf16x4 od;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) od[e] = f2bf(((h >> (8 * e)) & 0xffu) >= thr ? bf2f(o[e]) * inv : 0.f);
+        *(bf16x4*)(dxd + base + 256 * q) = od;
+        if constexpr (DBIAS) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bs[q][e] += bf2f(od[e]);
+        }
+      } else if constexpr (DBIAS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bs[q][e] += bf2f(o[e]);
+      }
+    }
+  };
+  const int rstep = gridDim.x * (NT / 64);
+  for (int row = blockIdx.x * (NT / 64) + wid; row < M; row += 2 * rstep) {
+    const bool two = row + rstep < M;
+    const int r1 = two ? row + rstep : row;
+    bf16x4 dA[Q4], xA[Q4], rA[Q4], dB[Q4], xB[Q4], rB[Q4];
+    const float muA = mean[row], rsA = rstd[row], muB = mean[r1], rsB = rstd[r1];
+    load_row(row, dA, xA, rA);
+    load_row(r1, dB, xB, rB);
+    do_row(row, muA, rsA, dA, xA, rA);
+    if (two) do_row(r1, muB, rsB, dB, xB, rB);
+  }
+#pragma unroll
+  for (int q = 0; q < Q4; ++q) {
+    const int c = lane * 4 + 256 * q;
+    *(f32x4*)(red + (wid * NS + 0) * W + c) = f32x4{dg[q][0], dg[q][1], dg[q][2], dg[q][3]};
+    *(f32x4*)(red + (wid * NS + 1) * W + c) = f32x4{db[q][0], db[q][1], db[q][2], db[q][3]};
+    if constexpr (DBIAS) *(f32x4*)(red + (wid * NS + 2) * W + c) = f32x4{bs[q][0], bs[q][1], bs[q][2], bs[q][3]};
+  }
+  __syncthreads();
+  float* prow = part ? part + (long long)blockIdx.x * NS * W : nullptr;
+  for (int col = threadIdx.x; col < W; col += NT) {
+    float a = 0.f, b2 = 0.f, b3 = 0.f;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+      a += red[(w * NS) * W + col];
+      b2 += red[(w * NS + 1) * W + col];
+      if constexpr (DBIAS) b3 += red[(w * NS + 2) * W + col];
+    }
+    if (prow) {
+      prow[col] = a;
+      prow[W + col] = b2;
+      if constexpr (DBIAS) prow[2 * W + col] = b3;
+    } else {
+      atomicAdd(dgamma + col, a);
+      atomicAdd(dbeta + col, b2);
+      if constexpr (DBIAS) atomicAdd(dbias + col, b3);
+    }
+  }
+}
+
 constexpr int LN_PART_GROUPS = 32;
 __global__ void ln_part_reduce_kernel(const float* __restrict__ part, int nblk, int NS, int W, float* __restrict__ dgamma,
                                       float* __restrict__ dbeta, float* __restrict__ dbias) {
@@ -524,6 +648,21 @@ int grid_for(long long work, int per_block, int cap) {
   long long g = (work + per_block - 1) / per_block;
   return (int)(g < 1 ? 1 : (g > cap ? cap : g));
 }
+template <int Q4>
+void ln_bwd_fast_launch(dim3 grid, size_t sh, hipStream_t s, const bf16* dy, const bf16* x, const float* gamma,
+                               const float* mean, const float* rstd, const bf16* dres, bf16* dx, float* dgamma,
+                               float* dbeta, int M, bf16* dxd, float drop_p, unsigned long long drop_seed, float* dbias,
+                               float* part) {
+#define TFK_LNF(R_, D_, B_)                                                                                       \
+  if ((dres != nullptr) == R_ && (dxd != nullptr) == D_ && (dbias != nullptr) == B_) {                            \
+    hipLaunchKernelGGL((ln_bwd_fast_kernel<Q4, R_, D_, B_>), grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, \
+                       dgamma, dbeta, M, dxd, drop_p, drop_seed, tfk_seed_key(), dbias, part);                      \
+    return;                                                                                                      \
+  }
+  TFK_LNF(false, false, false) TFK_LNF(false, false, true) TFK_LNF(false, true, false) TFK_LNF(false, true, true)
+  TFK_LNF(true, false, false) TFK_LNF(true, false, true) TFK_LNF(true, true, false) TFK_LNF(true, true, true)
+#undef TFK_LNF
+}
 }  // namespace
 
 extern "C" {
@@ -557,6 +696,17 @@ int tfk_layernorm_fwd_mx(const bf16* x, const float* gamma, const float* beta, b
 // wave = more blocks per CU in flight, more column-partial slabs for ln_part_reduce_kernel)
 static int g_ln_rows = 8;
 void tfk_ln_bwd_set_rows(int r) { g_ln_rows = r > 0 ? r : 8; }
+// bf16-mode calls at W = 768 / 1024 on ln_bwd_fast_kernel (A/B knob; TFK_LN_FAST=0 disables)
+static int g_ln_fast = -1;
+void tfk_ln_bwd_set_fast(int on) { g_ln_fast = on ? 1 : 0; }
+static bool ln_fast() {
+  if (g_ln_fast < 0) {
+    const char* e = getenv("TFK_LN_FAST");
+    g_ln_fast = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_ln_fast == 1;
+}
+
 int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (NT / 64) * g_ln_rows, 4096); }
 static unsigned ln_bwd_blocks(int M, bool mxo) { return (unsigned)tfk_ln_bwd_blocks(M, mxo ? 1 : 0); }
 // part (optional): f32 workspace [blocks][2 or 3][W] for the column partials (no tail atomics)
@@ -569,7 +719,16 @@ int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const f
   if (mxo && (M % 32 || W % 32 || W > 1024)) return -3;
   dim3 grid(ln_bwd_blocks(M, mxo));
   const size_t sh = (size_t)(NT / 64) * (dbias ? 3 : 2) * W * sizeof(float) + (mxo ? (size_t)32 * (W + 8) * 2 : 0);
-  if (cpl <= 1)
+  const bool aligned = ((((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)(dres ? dres : dy) |
+                          (uintptr_t)(dxd ? dxd : dx)) & 7) == 0) && ((uintptr_t)gamma & 15) == 0;
+  if (!mxo && aligned && (W == 768 || W == 1024) && ln_fast()) {
+    if (W == 768)
+      ln_bwd_fast_launch<3>(grid, sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, dxd, drop_p, drop_seed,
+                            dbias, part);
+    else
+      ln_bwd_fast_launch<4>(grid, sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, dxd, drop_p, drop_seed,
+                            dbias, part);
+  } else if (cpl <= 1)
     hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
                        dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,
                        (unsigned char*)mqt, (unsigned char*)mst, part);

@@ -37,18 +37,18 @@ def main():
     dres = None if args.no_dres else torch.randn(M, W, device="cuda").to(torch.bfloat16)  # residual branch
     dbias = torch.zeros(W, device="cuda") if args.dbias else None
     res, ref, err = {}, None, {}
-    # (rows per wave, unused): issuing 2-8 rows' loads up front and a two-row prefetch ring both
-    # measured slower (profiles/perf_log_r6.md)
-    cfgs = ((8, 0), (4, 0))
+    # (rows per wave, kernel: 0 = generic ln_bwd_kernel, 1 = width-specialized ln_bwd_fast_kernel)
+    cfgs = ((8, 0), (8, 1), (4, 1), (16, 1))
     for _ in range(args.rounds):
         for rows, pf in cfgs:
             lib().ln_bwd_set_rows(rows)
+            lib().ln_bwd_set_fast(pf)
             fn = lambda: T.layernorm_bwd(dy, x, gamma, mean, rstd, dg, db, dres=dres, drop=None if args.no_drop else (0.1, 5), dbias=dbias)  # noqa: E731
             out = fn()
             dxo = out[0] if isinstance(out, (tuple, list)) else out
             if ref is None:
                 ref = dxo.float().clone()
-            err[f"rows{rows}_g{pf}"] = (dxo.float() - ref).abs().max().item()
+            err[f"rows{rows}_fast{pf}"] = (dxo.float() - ref).abs().max().item()
             # the calls replay from one captured graph: host launch overhead (allocation, binding,
             # two launches per call) would otherwise set a ~20-25 us floor of its own
             g = torch.cuda.CUDAGraph()
@@ -62,10 +62,11 @@ def main():
             g.replay()
             e1.record()
             torch.cuda.synchronize()
-            res.setdefault(f"rows{rows}_g{pf}", []).append(e0.elapsed_time(e1) / args.iters * 1000.0)
+            res.setdefault(f"rows{rows}_fast{pf}", []).append(e0.elapsed_time(e1) / args.iters * 1000.0)
     lib().ln_bwd_set_rows(8)
+    lib().ln_bwd_set_fast(1)
     print(json.dumps({"shape": [M, W], "dres": dres is not None, "dbias": dbias is not None, "drop": not args.no_drop, "us_per_call": {k: round(statistics.median(v), 2) for k, v in res.items()},
-                      "max_abs_dx_diff_vs_rows8_g0": err}))
+                      "max_abs_dx_diff_vs_generic": err}))
 
 if __name__ == "__main__":
     main()

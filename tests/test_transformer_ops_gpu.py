@@ -113,7 +113,7 @@ def test_layernorm(W):
         assert rel(out[DEV][k], out["cpu"][k]) < 1e-2, k
 
 
-@pytest.mark.parametrize("W", [1024, 264])
+@pytest.mark.parametrize("W", [1024, 768, 264])
 def test_layernorm_bwd_fused_consumer_dropout(W):
     """LayerNorm backward also emitting dropout(dx) for its consumer: dx unchanged and the second
     output == the standalone dropout of dx, bit for bit (same hash mask, same arithmetic)."""
@@ -129,6 +129,39 @@ def test_layernorm_bwd_fused_consumer_dropout(W):
     dx, (dx2, dxd) = outs
     assert torch.equal(dx, dx2)
     assert torch.equal(dxd, E.dropout(dx, 0.3, 99))
+
+
+@pytest.mark.parametrize("W", [768, 1024])
+@pytest.mark.parametrize("dres_on,drop_on,dbias_on", [(a, b, c) for a in (0, 1) for b in (0, 1) for c in (0, 1)])
+def test_layernorm_bwd_fast_matches_generic(W, dres_on, drop_on, dbias_on):
+    """The width-specialized LayerNorm backward (transformer.hip ln_bwd_fast_kernel) == the generic
+    kernel for every option combination: dx / dropout(dx) / dgamma / dbeta / consumer bias gradient."""
+    from tensorflow_k8s_amd.ops._lib import lib
+    M = 1000
+    x, dy, dres = bf(M, W, seed=51, scale=2.0), bf(M, W, seed=52), bf(M, W, seed=53)
+    g, b = torch.rand(W) + 0.5, torch.randn(W) * 0.1
+    y, mu, rs = T.layernorm_fwd(x.to(DEV), g.to(DEV), b.to(DEV))
+    out = []
+    try:
+        for fast in (0, 1):
+            lib().ln_bwd_set_fast(fast)
+            dg, db = torch.zeros(W, device=DEV), torch.zeros(W, device=DEV)
+            dbias = torch.zeros(W, device=DEV) if dbias_on else None
+            r = T.layernorm_bwd(dy.to(DEV), x.to(DEV), g.to(DEV), mu, rs, dg, db,
+                                dres=dres.to(DEV) if dres_on else None, drop=(0.2, 7) if drop_on else None,
+                                dbias=dbias)
+            dx, dxd = r if drop_on else (r, r)
+            out.append((dx, dxd, dg, db, dbias))
+    finally:
+        lib().ln_bwd_set_fast(1)
+    (dx0, dxd0, dg0, db0, bs0), (dx1, dxd1, dg1, db1, bs1) = out
+    assert rel(dx1, dx0) < 1e-2 and rel(dxd1, dxd0) < 1e-2
+    assert rel(dg1, dg0) < 1e-4 and rel(db1, db0) < 1e-4
+    if dbias_on:
+        assert rel(bs1, bs0) < 1e-3
+    if drop_on:  # the fast kernel's mask is the dropout kernel's, bit for bit
+        from tensorflow_k8s_amd.ops import elementwise as E
+        assert torch.equal(dxd1, E.dropout(dx1, 0.2, 7))
 
 
 def test_embedding():

@@ -118,10 +118,13 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return s;
 }
 
-// tanh from the native exp (v_exp_f32) and a fast divide: 1 - 2/(1 + e^{2u}), saturating to +-1
-// through e^{2u} = inf / 0. Absolute error ~1e-7 (the libm tanhf is ~10x the VALU work, which made
-// BERT's GELU-backward dgrad epilogue VALU-bound: 133 us vs 59 us for the plain dgrad).
-__device__ __forceinline__ float fast_tanh(float u) { return 1.f - __fdividef(2.f, 1.f + __expf(2.f * u)); }
+// tanh from the native exp (v_exp_f32) and reciprocal (v_rcp_f32): 1 - 2/(1 + e^{2u}), saturating to
+// +-1 through e^{2u} = inf / 0. Absolute error ~1e-7 (the libm tanhf is ~10x the VALU work, which made
+// BERT's GELU-backward dgrad epilogue VALU-bound: 133 us vs 59 us for the plain dgrad). __fdividef
+// still lowered to the IEEE division sequence here (v_div_scale / div_fmas / div_fixup per call).
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u));
+}
 
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;

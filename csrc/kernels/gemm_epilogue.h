@@ -203,39 +203,29 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) { csum[j][r] = 0.f; csq[j][r] = 0.f; }
-    // accumulator pass; the activation switch is hoisted out of the element loops (AC = 0: none,
-    // the common case -- convs feeding a BatchNorm, EXT epilogues that activate in the store pass;
-    // per element, the runtime switch cost a chain of scalar compares and branches)
-    auto acc_pass = [&](auto ac) {
-      constexpr bool ACT = decltype(ac)::value;
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int nloc = fcol(j) + nl;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.bias) {
+    for (int j = 0; j < FN; ++j) {
+      const int nloc = fcol(j) + nl;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) bv[r] = (n0 + nloc + r < p.N) ? p.bias[n0 + nloc + r] : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int mloc = frow(i) + ml;
-          bf16x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = acc[i][j][r] * p.alpha + bv[r];
-            if constexpr (ACT) v = act_apply(v, p.act);
-            csum[j][r] += v;
-            csq[j][r] += v * v;
-            o[r] = f2bf(v);
-          }
-          *(bf16x4*)(Cs + cso(mloc, nloc)) = o;
-        }
+        for (int r = 0; r < 4; ++r) bv[r] = (n0 + nloc + r < p.N) ? p.bias[n0 + nloc + r] : 0.f;
       }
-    };
-    if (ext || p.act == 0)
-      acc_pass(std::false_type{});  // EXT: the activation runs in the store pass
-    else
-      acc_pass(std::true_type{});
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int mloc = frow(i) + ml;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] * p.alpha + bv[r];
+          if constexpr (!ext) v = act_apply(v, p.act);  // EXT: in the store pass
+          csum[j][r] += v;
+          csq[j][r] += v * v;
+          o[r] = f2bf(v);
+        }
+        *(bf16x4*)(Cs + cso(mloc, nloc)) = o;
+      }
+    }
     // BN batch statistics (rows >= M were zero-filled -> contribute 0; no bias in conv use):
     // 16-lane row sums by DPP, the WM waves of a column meet in LDS behind the C tile, then ONE
     // coalesced atomic per (column, stat) per block instead of 4-lane atomics per wave.

@@ -17,7 +17,18 @@ def lib():
     global _C
     if _C is None:
         try:
-            from .. import _C as C  # noqa: N811
+            alt = os.environ.get("TFK_C_PATH")
+            if alt:
+                # compile-time A/B: a second build of the extension (tools/build_variant.sh) loaded
+                # under the same module name
+                import importlib.util
+                import sys
+                spec = importlib.util.spec_from_file_location("tensorflow_k8s_amd._C", alt)
+                C = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(C)
+                sys.modules["tensorflow_k8s_amd._C"] = C
+            else:
+                from .. import _C as C  # noqa: N811
         except ImportError as e:  # pragma: no cover - exercised on misconfigured boxes only
             raise RuntimeError(
                 "tfk native extension tensorflow_k8s_amd/_C is not built; run `python tools/build_ext.py` "

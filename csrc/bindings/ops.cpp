@@ -416,7 +416,8 @@ void gemm_mxfp8(torch::Tensor A, torch::Tensor As, torch::Tensor B, torch::Tenso
                 "colsum: bf16 EXT epilogue (aux / dact / dropout), no residual");
   }
   p.colsum = opt_ptr<float>(colsum);
-  int ext = f32 ? 2 : ((p.aux || drop_p > 0.0 || p.dact_src) ? 1 : 0);
+  // an activated bf16 output takes the EXT epilogue (the plain bf16 one is activation-free)
+  int ext = f32 ? 2 : ((p.aux || drop_p > 0.0 || p.dact_src || p.act) ? 1 : 0);
   if (mx_out.has_value()) {
     // MX-fp8 copies of C from the epilogue: [qr [M][N], sr [M][N/32], qc [N][M], sc [N][M/32]]
     const auto& o = *mx_out;

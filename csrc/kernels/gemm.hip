@@ -458,6 +458,9 @@ static int launch_reg(GemmParams p, int bm, int bn, int amode, int bmode, int ep
   TFK_GEMM_TILES_BIG(A_KOUT, B_KOUT, EPI_F32)
   TFK_GEMM_TILES3(A_KOUT, B_KOUT, EPI_BF16) TFK_GEMM_CASE(256, 256, A_KOUT, B_KOUT, EPI_BF16)
   TFK_GEMM_TILES3(A_CONV_FWD, B_KIN, EPI_BF16)
+  // activated bf16 outputs without the EXT extras (inference linears, conv + relu without a BN)
+  TFK_GEMM_TILES3(A_KIN, B_KIN, EPI_BF16_ACT)
+  TFK_GEMM_TILES3(A_CONV_FWD, B_KIN, EPI_BF16_ACT)
   TFK_GEMM_TILES3(A_CONV_DGRAD, B_KIN, EPI_BF16)
   TFK_GEMM_TILES3(A_CONV_DGRAD, B_KOUT, EPI_BF16)
   TFK_GEMM_TILES(A_KOUT, B_CONV_WGRAD, EPI_F32)
@@ -492,6 +495,8 @@ extern "C" int tfk_gemm_launch(GemmParams p, int bm, int bn, int amode, int bmod
   if (p.stats_shards < 1) p.stats_shards = 1;
   if (epi == EPI_BF16 && p.bn_sums) epi = EPI_BF16_BNR;
   if (epi == EPI_BF16 && (p.aux || p.dact_src || p.drop_p > 0.f)) epi = EPI_BF16_EXT;
+  if (p.act != 0 && epi == EPI_BF16_BNR) return -3;  // no activated output feeds a BN-backward reduction
+  if (epi == EPI_BF16 && p.act != 0) epi = EPI_BF16_ACT;  // EPI_BF16's epilogue is activation-free
   // row maps (strided-conv dgrad phases, lattice residual) live in the BN-reduce epilogue, which
   // both engines share
   if ((p.om_hp == 0 && p.rs_sh == 0) || epi == EPI_BF16_BNR) {

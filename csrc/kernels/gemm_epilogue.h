@@ -15,7 +15,11 @@ namespace tfk {
 // fully (a rolled epilogue indexes the accumulators dynamically -> they go to scratch).
 // EXT_MX: EXT + MX-fp8 row and column block copies of the output (GemmParams mx_*), quantized from
 // the LDS C tile after the store pass (the MX-fp8 engine's producer GEMMs: no separate quantize pass).
-enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1, EPI_BF16_BNR = 2, EPI_BF16_EXT = 3, EPI_BF16_EXT_MX = 4 };
+// EPI_BF16 ignores p.act: the launcher (gemm.hip tfk_gemm_launch) sends an activated bf16 output to
+// EPI_BF16_ACT, whose accumulator pass applies the activation per element. Without it, the runtime
+// activation switch compiled to a chain of scalar compares and branches per element in every bf16
+// epilogue -- 0.73 ms of a ResNet-50 step, whose convs feed BatchNorms (act = none).
+enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1, EPI_BF16_BNR = 2, EPI_BF16_EXT = 3, EPI_BF16_EXT_MX = 4, EPI_BF16_ACT = 5 };
 
 // LDS C-tile swizzle. The accumulator pass stores 8-B pieces (ds_write_b64: 4 groups of 16
 // contiguous lanes = 16 rows x one 4-column piece; bank = dword mod 32). With the padded row stride
@@ -218,7 +222,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = acc[i][j][r] * p.alpha + bv[r];
-          if constexpr (!ext) v = act_apply(v, p.act);  // EXT: in the store pass
+          if constexpr (EPI == EPI_BF16_ACT) v = act_apply(v, p.act);  // EXT: in the store pass
           csum[j][r] += v;
           csq[j][r] += v * v;
           o[r] = f2bf(v);

@@ -457,6 +457,8 @@ extern "C" int tfk_g4_launch(const GemmParams& p_in, int bm, int bn, int amode, 
   TFK_G4_TILES(1, 1, EPI_F32)
   TFK_G4_TILES(1, 1, EPI_BF16)
   TFK_G4_TILES(2, 0, EPI_BF16)
+  TFK_G4_TILES(0, 0, EPI_BF16_ACT)  // activated bf16 outputs (EPI_BF16's epilogue is activation-free)
+  TFK_G4_TILES(2, 0, EPI_BF16_ACT)
   // stride-1 conv dgrad run as a forward conv over dY with flipped weights (ops/gemm.py), carrying
   // the fused BN-backward reduction of the layer that produced x
   TFK_G4_TILES(2, 0, EPI_BF16_BNR)

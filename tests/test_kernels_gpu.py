@@ -752,3 +752,28 @@ def test_dgrad_fused_column_sums(M, N, K):
     dx = G.linear_dgrad(dy, w, dact_src=m, dact="relu", drop_p=0.1, drop_seed=9, colsum=cs)
     ref = dx.float().sum(0) + 0.5
     assert float((cs - ref).abs().max()) <= 1e-3 * float(ref.abs().max()) + 1e-4
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu"])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (300, 200, 136)])
+def test_linear_activated_bf16_epilogue(M, N, K, act):
+    """An activated bf16 GEMM output without the EXT extras (no aux / dropout) runs the EPI_BF16_ACT
+    epilogue -- EPI_BF16's own accumulator pass is activation-free (gemm_epilogue.h)."""
+    x, w = bf(M, K, seed=1), bf(N, K, seed=2, scale=0.05)
+    b = torch.randn(N) * 0.1
+    ref = G.linear_fwd(x, w, b, act=act)
+    got = G.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), act=act)
+    assert rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [(2, 8, 8, 64, 128, 1, 1, 1, 0), (2, 9, 9, 64, 64, 3, 3, 1, 1), (2, 12, 12, 8, 16, 5, 5, 1, 2)])
+def test_conv_relu_bf16_epilogue(cfg):
+    """conv + bias + relu (no BatchNorm: LeNet's form) on the activated bf16 epilogue."""
+    N, H, W, C, K, R, S, st_, pd = cfg
+    g = G.ConvGeom(N, H, W, C, K, R, S, st_, st_, pd, pd)
+    x, w = bf(N, H, W, C, seed=3), bf(K, R, S, C, seed=4, scale=0.05)
+    b = torch.randn(K) * 0.1
+    ref = G.conv_fwd(x, w, g, bias=b, act="relu")
+    got = G.conv_fwd(x.to(DEV), w.to(DEV), g, bias=b.to(DEV), act="relu")
+    assert rel(got, ref) < 1e-2
+    assert float(got.float().min()) >= 0.0

@@ -144,6 +144,22 @@ __global__ __launch_bounds__(LNMX_NT) void ln_fwd_mx_kernel(const bf16* __restri
   tfk::mx_rows32_out<LNMX_NT>(&tile[0][0], LNMX_WMAX + 8, W, M, r0, qr, sr, qc, sc);
 }
 
+// Per-element arithmetic of the LayerNorm backward, spelled out with explicit rounding (no
+// compiler contraction choices): ln_bwd_kernel (both modes) and ln_bwd_fast_kernel produce
+// bit-identical outputs.
+__device__ __forceinline__ void ln_bwd_accum(float d, float xv, float mu, float rs, float gmv, float& g, float& xh,
+                                             float& s1, float& s2, float& dgv, float& dbv) {
+  xh = __fmul_rn(__fsub_rn(xv, mu), rs);
+  g = __fmul_rn(d, gmv);
+  s1 = __fadd_rn(s1, g);
+  s2 = __fmaf_rn(g, xh, s2);
+  dgv = __fmaf_rn(d, xh, dgv);
+  dbv = __fadd_rn(dbv, d);
+}
+__device__ __forceinline__ float ln_bwd_out(float g, float xh, float s1, float s2, float rs) {
+  return __fmul_rn(rs, __fmaf_rn(-xh, s2, __fsub_rn(g, s1)));
+}
+
 template <int CPL>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
@@ -213,15 +229,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
       if (c < nch) {
         const bf16x8 dv = cdv[j], xv = cxv[j];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float d = bf2f(dv[e]);
-          xh[j][e] = (bf2f(xv[e]) - mu) * rs;
-          g[j][e] = d * gm[j][e];
-          s1 += g[j][e];
-          s2 += g[j][e] * xh[j][e];
-          dg[j][e] += d * xh[j][e];
-          db[j][e] += d;
-        }
+        for (int e = 0; e < 8; ++e)
+          ln_bwd_accum(bf2f(dv[e]), bf2f(xv[e]), mu, rs, gm[j][e], g[j][e], xh[j][e], s1, s2, dg[j][e], db[j][e]);
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) { g[j][e] = 0.f; xh[j][e] = 0.f; }
@@ -237,8 +246,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float v = rs * (g[j][e] - s1 - xh[j][e] * s2);
-          if (dres) v += bf2f(rv[e]);
+          float v = ln_bwd_out(g[j][e], xh[j][e], s1, s2, rs);
+          if (dres) v = __fadd_rn(v, bf2f(rv[e]));
           o[e] = f2bf(v);
         }
         *(bf16x8*)(dx + (long long)row * W + c * 8) = o;
@@ -360,15 +369,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict_
       const int c = lane + 64 * j;
       if (c < NCH) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float d = bf2f(cdv[j][e]);
-          xh[j][e] = (bf2f(cxv[j][e]) - mu) * rs;
-          g[j][e] = d * gm[j][e];
-          s1 += g[j][e];
-          s2 += g[j][e] * xh[j][e];
-          dg[j][e] += d * xh[j][e];
-          db[j][e] += d;
-        }
+        for (int e = 0; e < 8; ++e)
+          ln_bwd_accum(bf2f(cdv[j][e]), bf2f(cxv[j][e]), mu, rs, gm[j][e], g[j][e], xh[j][e], s1, s2, dg[j][e], db[j][e]);
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) { g[j][e] = 0.f; xh[j][e] = 0.f; }
@@ -383,8 +385,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict_
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float v = rs * (g[j][e] - s1 - xh[j][e] * s2);
-          if constexpr (DRES) v += bf2f(crv[j][e]);
+          float v = ln_bwd_out(g[j][e], xh[j][e], s1, s2, rs);
+          if constexpr (DRES) v = __fadd_rn(v, bf2f(crv[j][e]));
           o[e] = f2bf(v);
         }
         *(bf16x8*)(dx + (long long)row * W + c * 8) = o;

@@ -149,6 +149,7 @@ __global__ __launch_bounds__(LNMX_NT) void ln_fwd_mx_kernel(const bf16* __restri
 // bit-identical outputs.
 __device__ __forceinline__ void ln_bwd_accum(float d, float xv, float mu, float rs, float gmv, float& g, float& xh,
                                              float& s1, float& s2, float& dgv, float& dbv) {
+#pragma clang fp contract(off)
   xh = __fmul_rn(__fsub_rn(xv, mu), rs);
   g = __fmul_rn(d, gmv);
   s1 = __fadd_rn(s1, g);
@@ -156,8 +157,9 @@ __device__ __forceinline__ void ln_bwd_accum(float d, float xv, float mu, float 
   dgv = __fmaf_rn(d, xh, dgv);
   dbv = __fadd_rn(dbv, d);
 }
-__device__ __forceinline__ float ln_bwd_out(float g, float xh, float s1, float s2, float rs) {
-  return __fmul_rn(rs, __fmaf_rn(-xh, s2, __fsub_rn(g, s1)));
+__device__ __forceinline__ float ln_bwd_out(float g, float xh, float s1, float s2, float rs, float res) {
+#pragma clang fp contract(off)
+  return __fadd_rn(__fmul_rn(rs, __fmaf_rn(-xh, s2, __fsub_rn(g, s1))), res);
 }
 
 template <int CPL>
@@ -246,9 +248,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float v = ln_bwd_out(g[j][e], xh[j][e], s1, s2, rs);
-          if (dres) v = __fadd_rn(v, bf2f(rv[e]));
-          o[e] = f2bf(v);
+          o[e] = f2bf(ln_bwd_out(g[j][e], xh[j][e], s1, s2, rs, dres ? bf2f(rv[e]) : 0.f));
         }
         *(bf16x8*)(dx + (long long)row * W + c * 8) = o;
         if (dxd) {
@@ -385,9 +385,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict_
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float v = ln_bwd_out(g[j][e], xh[j][e], s1, s2, rs);
-          if constexpr (DRES) v = __fadd_rn(v, bf2f(crv[j][e]));
-          o[e] = f2bf(v);
+          o[e] = f2bf(ln_bwd_out(g[j][e], xh[j][e], s1, s2, rs, DRES ? bf2f(crv[j][e]) : 0.f));
         }
         *(bf16x8*)(dx + (long long)row * W + c * 8) = o;
         if constexpr (DROP) {

@@ -144,9 +144,8 @@ __global__ __launch_bounds__(LNMX_NT) void ln_fwd_mx_kernel(const bf16* __restri
   tfk::mx_rows32_out<LNMX_NT>(&tile[0][0], LNMX_WMAX + 8, W, M, r0, qr, sr, qc, sc);
 }
 
-// Per-element arithmetic of the LayerNorm backward, spelled out with explicit rounding (no
-// compiler contraction choices): ln_bwd_kernel (both modes) and ln_bwd_fast_kernel produce
-// bit-identical outputs.
+// Per-element arithmetic of the LayerNorm backward, spelled out with explicit rounding and no
+// compiler contraction (shared by ln_bwd_kernel and ln_bwd_fast_kernel).
 __device__ __forceinline__ void ln_bwd_accum(float d, float xv, float mu, float rs, float gmv, float& g, float& xh,
                                              float& s1, float& s2, float& dgv, float& dbv) {
 #pragma clang fp contract(off)
@@ -323,9 +322,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
 // element -- per-lane chunk guards, runtime option branches, 64-bit index math and register copies
 // of the prefetched row -- against ~13 the arithmetic needs, at one wave per SIMD: VALU issue and
 // memory waits did not overlap (22.5 us for the 48 MB of a plain 8192 x 1024 call). Here width and
-// options are compile-time and each iteration loads two rows before using either. The lane -> chunk
-// map (8-element chunks c = lane + 64 j) and every expression are ln_bwd_kernel's, so the outputs are
-// bit-identical to it (and to its MX-output mode, which the fp8 consumers compare against).
+// options are compile-time and each iteration loads two rows before using either (lane -> chunk map
+// and element arithmetic as ln_bwd_kernel; outputs agree to the row reductions' rounding).
 template <int NCH, bool DRES, bool DROP, bool DBIAS>
 __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                          const float* __restrict__ gamma, const float* __restrict__ mean,

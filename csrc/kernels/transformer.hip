@@ -317,14 +317,15 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
 // (LN_PART_GROUPS adders per address instead of one per block). 32 groups of <= 8 slabs with the 8
 // loads of a group in flight together: 8 groups of 32 slabs walked one load at a time measured
 // 9.4 us per call on Transformer-big (256 slabs x 2 x 1024: a latency chain, 0.3 TB/s).
-// Width-specialized LayerNorm backward (bf16 mode, W = 768 / 1024: BERT-base, Transformer-big /
-// BERT-large). PMC of ln_bwd_kernel (profiles/pmc_ln_bwd_r6.txt): ~37 VALU instructions per
+// Width-specialized LayerNorm backward (bf16 mode, W = 256 * Q4: BERT-base 768, Transformer-big /
+// BERT-large 1024). PMC of ln_bwd_kernel (profiles/pmc_ln_bwd_r6.txt): ~37 VALU instructions per
 // element -- per-lane chunk guards, runtime option branches, 64-bit index math and register copies
 // of the prefetched row -- against ~13 the arithmetic needs, at one wave per SIMD: VALU issue and
 // memory waits did not overlap (22.5 us for the 48 MB of a plain 8192 x 1024 call). Here width and
-// options are compile-time and each iteration loads two rows before using either (lane -> chunk map
-// and element arithmetic as ln_bwd_kernel; outputs agree to the row reductions' rounding).
-template <int NCH, bool DRES, bool DROP, bool DBIAS>
+// options are compile-time, lane l owns the 4-element chunks l + 64 q (q < Q4; every 8-B load of a
+// wave is a contiguous 512 B), and each iteration loads two rows before using either. (The generic
+// kernel's 8-element lane map measured 22.1 vs 19.2 us on BERT-base's call form.)
+template <int Q4, bool DRES, bool DROP, bool DBIAS>
 __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                          const float* __restrict__ gamma, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, const bf16* __restrict__ dres,
@@ -333,75 +334,60 @@ __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict_
                                                          float drop_p, unsigned long long drop_salt,
                                                          const unsigned long long* __restrict__ drop_key,
                                                          float* __restrict__ dbias, float* __restrict__ part) {
-  constexpr int W = NCH * 8, CPL = (NCH + 63) / 64, NS = DBIAS ? 3 : 2;
+  constexpr int W = 256 * Q4, NS = DBIAS ? 3 : 2;
   extern __shared__ float red[];  // [NT/64][NS][W]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float gm[CPL][8], dg[CPL][8], db[CPL][8], bs[CPL][8];
+  float gm[Q4][4], dg[Q4][4], db[Q4][4], bs[Q4][4];
 #pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    const int c = lane + 64 * j;
+  for (int q = 0; q < Q4; ++q) {
+    const f32x4 g4 = *(const f32x4*)(gamma + lane * 4 + 256 * q);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      dg[j][e] = 0.f; db[j][e] = 0.f; bs[j][e] = 0.f;
-      gm[j][e] = c < NCH ? gamma[c * 8 + e] : 0.f;
-    }
+    for (int e = 0; e < 4; ++e) { gm[q][e] = g4[e]; dg[q][e] = 0.f; db[q][e] = 0.f; bs[q][e] = 0.f; }
   }
-  const unsigned long long drop_seed = eff_seed(drop_salt, drop_key);
-  auto load_row = [&](int r, bf16x8 (&dv)[CPL], bf16x8 (&xv)[CPL], bf16x8 (&rv)[CPL]) {
+  const uint32_t s32 = DROP ? drop_seed32(eff_seed(drop_salt, drop_key)) : 0u;
+  const uint32_t thr = DROP ? (uint32_t)drop_thr8(drop_p) : 0u;
+  const float inv = DROP ? drop_scale8(drop_p) : 1.f;
+  auto load_row = [&](int r, bf16x4 (&dv)[Q4], bf16x4 (&xv)[Q4], bf16x4 (&rv)[Q4]) {
+    const long long base = (long long)r * W + lane * 4;
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      const int c = lane + 64 * j;
-      if (c < NCH) {
-        dv[j] = *(const bf16x8*)(dy + (long long)r * W + c * 8);
-        xv[j] = *(const bf16x8*)(x + (long long)r * W + c * 8);
-        if constexpr (DRES) rv[j] = *(const bf16x8*)(dres + (long long)r * W + c * 8);
-      }
+    for (int q = 0; q < Q4; ++q) {
+      dv[q] = *(const bf16x4*)(dy + base + 256 * q);
+      xv[q] = *(const bf16x4*)(x + base + 256 * q);
+      if constexpr (DRES) rv[q] = *(const bf16x4*)(dres + base + 256 * q);
     }
   };
-  auto do_row = [&](int row, float mu, float rs, const bf16x8 (&cdv)[CPL], const bf16x8 (&cxv)[CPL],
-                    const bf16x8 (&crv)[CPL]) {
-    float g[CPL][8], xh[CPL][8];
+  auto do_row = [&](int r, float mu, float rs, const bf16x4 (&dv)[Q4], const bf16x4 (&xv)[Q4], const bf16x4 (&rv)[Q4]) {
+    float g[Q4][4], xh[Q4][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      const int c = lane + 64 * j;
-      if (c < NCH) {
+    for (int q = 0; q < Q4; ++q)
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          ln_bwd_accum(bf2f(cdv[j][e]), bf2f(cxv[j][e]), mu, rs, gm[j][e], g[j][e], xh[j][e], s1, s2, dg[j][e], db[j][e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { g[j][e] = 0.f; xh[j][e] = 0.f; }
-      }
-    }
+      for (int e = 0; e < 4; ++e)
+        ln_bwd_accum(bf2f(dv[q][e]), bf2f(xv[q][e]), mu, rs, gm[q][e], g[q][e], xh[q][e], s1, s2, dg[q][e], db[q][e]);
     s1 = wave_sum(s1) / W;
     s2 = wave_sum(s2) / W;
+    const long long base = (long long)r * W + lane * 4;
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      const int c = lane + 64 * j;
-      if (c < NCH) {
-        bf16x8 o;
+    for (int q = 0; q < Q4; ++q) {
+      bf16x4 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          o[e] = f2bf(ln_bwd_out(g[j][e], xh[j][e], s1, s2, rs, DRES ? bf2f(crv[j][e]) : 0.f));
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(ln_bwd_out(g[q][e], xh[q][e], s1, s2, rs, DRES ? bf2f(rv[q][e]) : 0.f));
+      *(bf16x4*)(dx + base + 256 * q) = o;
+      if constexpr (DROP) {
+        // the consumer's dropout backward: misc.hip's mask (one hash per 4 elements, byte e of
+        // hash32(s32 ^ idx / 4) against the 8-bit threshold) on index r * W + col
+        const uint32_t h = hash32(s32 ^ (uint32_t)((base + 256 * q) >> 2));
+        bf16x4 od;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) od[e] = f2bf(((h >> (8 * e)) & 0xffu) >= thr ? bf2f(o[e]) * inv : 0.f);
+        *(bf16x4*)(dxd + base + 256 * q) = od;
+        if constexpr (DBIAS) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bs[q][e] += bf2f(od[e]);
         }
-        *(bf16x8*)(dx + (long long)row * W + c * 8) = o;
-        if constexpr (DROP) {
-          const float inv = drop_scale8(drop_p);
-          const unsigned long long base = (unsigned long long)row * W + c * 8;
-          const unsigned km = drop_keep8(drop_seed32(drop_seed), base, drop_thr8(drop_p));
-          bf16x8 od;
+      } else if constexpr (DBIAS) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) od[e] = f2bf((km >> e) & 1u ? bf2f(o[e]) * inv : 0.f);
-          *(bf16x8*)(dxd + base) = od;
-          if constexpr (DBIAS) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) bs[j][e] += bf2f(od[e]);
-          }
-        } else if constexpr (DBIAS) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) bs[j][e] += bf2f(o[e]);
-        }
+        for (int e = 0; e < 4; ++e) bs[q][e] += bf2f(o[e]);
       }
     }
   };
@@ -409,7 +395,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict_
   for (int row = blockIdx.x * (NT / 64) + wid; row < M; row += 2 * rstep) {
     const bool two = row + rstep < M;
     const int r1 = two ? row + rstep : row;
-    bf16x8 dA[CPL], xA[CPL], rA[CPL], dB[CPL], xB[CPL], rB[CPL];
+    bf16x4 dA[Q4], xA[Q4], rA[Q4], dB[Q4], xB[Q4], rB[Q4];
     const float muA = mean[row], rsA = rstd[row], muB = mean[r1], rsB = rstd[r1];
     load_row(row, dA, xA, rA);
     load_row(r1, dB, xB, rB);
@@ -417,15 +403,11 @@ __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict_
     if (two) do_row(r1, muB, rsB, dB, xB, rB);
   }
 #pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    const int c = lane + 64 * j;
-    if (c < NCH)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        red[(wid * NS + 0) * W + c * 8 + e] = dg[j][e];
-        red[(wid * NS + 1) * W + c * 8 + e] = db[j][e];
-        if constexpr (DBIAS) red[(wid * NS + 2) * W + c * 8 + e] = bs[j][e];
-      }
+  for (int q = 0; q < Q4; ++q) {
+    const int c = lane * 4 + 256 * q;
+    *(f32x4*)(red + (wid * NS + 0) * W + c) = f32x4{dg[q][0], dg[q][1], dg[q][2], dg[q][3]};
+    *(f32x4*)(red + (wid * NS + 1) * W + c) = f32x4{db[q][0], db[q][1], db[q][2], db[q][3]};
+    if constexpr (DBIAS) *(f32x4*)(red + (wid * NS + 2) * W + c) = f32x4{bs[q][0], bs[q][1], bs[q][2], bs[q][3]};
   }
   __syncthreads();
   float* prow = part ? part + (long long)blockIdx.x * NS * W : nullptr;
@@ -664,14 +646,14 @@ int grid_for(long long work, int per_block, int cap) {
   long long g = (work + per_block - 1) / per_block;
   return (int)(g < 1 ? 1 : (g > cap ? cap : g));
 }
-template <int NCH>
+template <int Q4>
 void ln_bwd_fast_launch(dim3 grid, size_t sh, hipStream_t s, const bf16* dy, const bf16* x, const float* gamma,
                                const float* mean, const float* rstd, const bf16* dres, bf16* dx, float* dgamma,
                                float* dbeta, int M, bf16* dxd, float drop_p, unsigned long long drop_seed, float* dbias,
                                float* part) {
 #define TFK_LNF(R_, D_, B_)                                                                                       \
   if ((dres != nullptr) == R_ && (dxd != nullptr) == D_ && (dbias != nullptr) == B_) {                            \
-    hipLaunchKernelGGL((ln_bwd_fast_kernel<NCH, R_, D_, B_>), grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, \
+    hipLaunchKernelGGL((ln_bwd_fast_kernel<Q4, R_, D_, B_>), grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, \
                        dgamma, dbeta, M, dxd, drop_p, drop_seed, tfk_seed_key(), dbias, part);                      \
     return;                                                                                                      \
   }
@@ -736,13 +718,13 @@ int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const f
   dim3 grid(ln_bwd_blocks(M, mxo));
   const size_t sh = (size_t)(NT / 64) * (dbias ? 3 : 2) * W * sizeof(float) + (mxo ? (size_t)32 * (W + 8) * 2 : 0);
   const bool aligned = ((((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)(dres ? dres : dy) |
-                          (uintptr_t)(dxd ? dxd : dx)) & 15) == 0);
+                          (uintptr_t)(dxd ? dxd : dx)) & 7) == 0) && ((uintptr_t)gamma & 15) == 0;
   if (!mxo && aligned && (W == 768 || W == 1024) && ln_fast()) {
     if (W == 768)
-      ln_bwd_fast_launch<96>(grid, sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, dxd, drop_p, drop_seed,
+      ln_bwd_fast_launch<3>(grid, sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, dxd, drop_p, drop_seed,
                             dbias, part);
     else
-      ln_bwd_fast_launch<128>(grid, sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, dxd, drop_p, drop_seed,
+      ln_bwd_fast_launch<4>(grid, sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, dxd, drop_p, drop_seed,
                             dbias, part);
   } else if (cpl <= 1)
     hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,

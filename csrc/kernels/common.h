@@ -151,6 +151,37 @@ __device__ __forceinline__ float act_grad(float z, int act) {
   return 1.f;
 }
 
+// 8-element forms with the (wave-uniform) activation switch taken once per chunk instead of once per
+// element: the per-element switch compiled to a chain of scalar compares and branches per element.
+__device__ __forceinline__ void act_apply8(float (&f)[8], int act) {
+  if (act == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = gelu_tanh(f[e]);
+  } else if (act == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+  } else if (act == 3) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = fast_tanh(f[e]);
+  }
+}
+// f[e] *= act'(z[e])
+__device__ __forceinline__ void act_grad_mul8(float (&f)[8], const bf16x8& z, int act) {
+  if (act == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] *= gelu_tanh_grad(bf2f(z[e]));
+  } else if (act == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] *= bf2f(z[e]) > 0.f ? 1.f : 0.f;
+  } else if (act == 3) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float t = fast_tanh(bf2f(z[e]));
+      f[e] *= 1.f - t * t;
+    }
+  }
+}
+
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 'XCD swizzle must be bijective'):
 // blocks b and b+8 share an XCD under round-robin dispatch, so give each XCD a contiguous range
 // of logical tile ids -> neighbouring tiles (sharing an A panel) hit the same 4 MiB L2.

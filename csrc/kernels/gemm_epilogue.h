@@ -347,16 +347,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
                 for (int e = 0; e < 8; ++e) f[e] = (zb[g] >> e) & 1u ? f[e] : 0.f;
               } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) f[e] *= act_grad(bf2f(zv[g][e]), p.dact);
+                act_grad_mul8(f, zv[g], p.dact);
               }
             }
             if (p.aux) {
               if (p.aux_bits) ((unsigned char*)p.aux)[off[g] >> 3] = relu_bits8(v);
               else *(bf16x8*)((bf16*)p.aux + off[g]) = v;
             }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = act_apply(f[e], p.act);
+            act_apply8(f, p.act);
             if (p.drop_p > 0.f) {
               const unsigned long long lin = (unsigned long long)mlog[g] * p.N + nlog[g];
               const unsigned km = drop_keep8(drop_seed32(eff_seed(p.drop_seed, p.drop_seed_key)), lin, drop_thr8(p.drop_p));
@@ -446,17 +444,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
               for (int e = 0; e < 8; ++e) f[e] = (zb >> e) & 1u ? f[e] : 0.f;
             } else {
-              bf16x8 zv = *(const bf16x8*)((const bf16*)p.dact_src + off);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) f[e] *= act_grad(bf2f(zv[e]), p.dact);
+              const bf16x8 zv = *(const bf16x8*)((const bf16*)p.dact_src + off);
+              act_grad_mul8(f, zv, p.dact);
             }
           }
           if (p.aux) {
             if (p.aux_bits) ((unsigned char*)p.aux)[off >> 3] = relu_bits8(v);
             else *(bf16x8*)((bf16*)p.aux + off) = v;
           }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = act_apply(f[e], p.act);
+          act_apply8(f, p.act);
           if (p.drop_p > 0.f) {
             const unsigned long long lin = (unsigned long long)m * p.N + n;
             const unsigned km = drop_keep8(drop_seed32(eff_seed(p.drop_seed, p.drop_seed_key)), lin, drop_thr8(p.drop_p));

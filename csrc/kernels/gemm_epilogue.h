@@ -173,6 +173,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     // (global_atomic_add_f32, -munsafe-fp-atomics) -- no slab workspace, no reduce pass.
     const bool atomic = p.split_stride < 0;
     float* C = (float*)p.C + bz * p.sC + (atomic ? 0LL : (long long)blockIdx.z * p.split_stride);
+    // interior tile, plain store (the split-K slabs of every weight gradient): no per-element
+    // bounds, atomic or beta checks (each compiled to a compare and an exec-masked branch)
+    if (!atomic && p.beta == 0.f && m0 + BM <= p.M && n0 + BN <= p.N && (p.ldc & 3) == 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          *(f32x4*)(C + (long long)(m0 + frow(i) + ml) * p.ldc + n0 + fcol(j) + nl) = acc[i][j] * p.alpha;
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = m0 + frow(i) + ml;

@@ -19,11 +19,11 @@ import os
 import sys
 import time
 
-# Hardware queues per process, read by the HIP runtime when it initializes (before any device call):
-# 8 measured faster than HIP's default 4 for every captured step (same box, alternating: ResNet-50
-# 21.47 -> 21.35 ms, BERT-base 10.85 -> 10.75, Transformer-big 17.58 -> 17.45; 16 regressed to 25.4:
-# profiles/perf_log_r6.md). TFK_HW_QUEUES overrides.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("TFK_HW_QUEUES", "8")
+# Hardware queues per process (read by the HIP runtime when it initializes): HIP's default 4. 8 was
+# 0.5 % faster without collectives but 6.4 ms/step slower with the RCCL comm stream in the captured
+# step (profiles/perf_log_r6.md); TFK_HW_QUEUES sets it for experiments.
+if os.environ.get("TFK_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["TFK_HW_QUEUES"]
 
 import torch  # noqa: E402
 

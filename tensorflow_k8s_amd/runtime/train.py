@@ -27,9 +27,9 @@ import signal
 import sys
 import time
 
-# 8 hardware queues per process (HIP's default is 4): measured faster for the captured steps
-# (bench.py, profiles/perf_log_r6.md); set before the HIP runtime initializes. TFK_HW_QUEUES overrides.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("TFK_HW_QUEUES", "8")
+# hardware queues per process: HIP's default (4); TFK_HW_QUEUES sets it (bench.py, perf_log_r6.md)
+if os.environ.get("TFK_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["TFK_HW_QUEUES"]
 
 import torch  # noqa: E402
 

@@ -100,8 +100,10 @@ struct Loader {
         ch[i] = pp * p.sh - p.ph;
         cw[i] = qq * p.sw - p.pw;
         // input pixel index of tap (0, 0) (may be negative in the padding: only used when in range;
-        // x < 2^30 elements, checked by tfk_g4_ok, so 32-bit pixel / element math suffices)
-        off[i] = (unsigned)((n * p.H + ch[i]) * p.W + cw[i]);
+        // x < 2^30 elements, checked by tfk_g4_ok, so 32-bit pixel / element math suffices); for
+        // Cin >= 64 premultiplied by Cin (element index), so a K-tile's address needs no multiply
+        const int pix0 = (n * p.H + ch[i]) * p.W + cw[i];
+        off[i] = (unsigned)(SMALLC && p.Cin < BK ? pix0 : pix0 * p.Cin);
       }
     }
   }
@@ -132,18 +134,17 @@ struct Loader {
       __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, NREC, 0x00020000);
       if (!SMALLC || p.Cin >= BK) {
         // K-tile kt covers tap (r, s) = divmod(kt*64 / Cin, S) and channels c0..c0+63 (Cin % 64 == 0);
-        // the tap's pixel shift and channel offset are block-uniform (scalar), per lane: 2 adds,
-        // the bounds test and one 32-bit multiply-add
+        // the tap's element shift and channel offset are block-uniform (scalar), per lane: adds and
+        // the bounds test (off[] holds the premultiplied element index of tap (0, 0))
         const int k0 = kt * BK, rs = k0 / p.Cin, c0 = k0 - rs * p.Cin;
         const int r = rs / p.S, s = rs - r * p.S;
-        const int rdh = r * p.dh, sdw = s * p.dw, tap = rdh * p.W + sdw;
+        const int rdh = r * p.dh, sdw = s * p.dw, tapc = (rdh * p.W + sdw) * p.Cin + c0;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           if (only >= 0 && i != only) continue;
           const int h = ch[i] + rdh, wq = cw[i] + sdw;
           const bool ok = (inner || row_of(i, w, lane) < lim) && (unsigned)h < (unsigned)p.H && (unsigned)wq < (unsigned)p.W;
-          const int pix = (int)off[i] + tap;
-          const unsigned vo = ok && en ? (unsigned)(pix * p.Cin + c0 + k_of(i, w, lane)) * 2u : OOB;
+          const unsigned vo = ok && en ? (off[i] + (unsigned)(tapc + k_of(i, w, lane))) * 2u : OOB;
           lds_dma<16>(rsrc, (LDS_AS void*)(img + (NW * i + w) * 1024), vo);
         }
       } else {

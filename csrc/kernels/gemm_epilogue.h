@@ -299,8 +299,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     // 4 -> 29.52 (208 B/lane of spills). Every
     // load below is from an in-bounds address: absent tensors are not loaded at all (block-uniform
     // branches), and off the residual lattice the (unused) residual load reads C.
+    // EXT groups of 4 (2 until round 6: with the per-element activation switches gone they fit;
+    // BERT-base 9.95 -> 9.89 ms, Transformer-big 16.93 -> 16.85); plain groups of 8 measured level.
     constexpr int GB = BNRG > 0 ? BNRG : 1;
-    constexpr int GCAP = bnr ? GB : (ext ? 2 : 4);
+    constexpr int GCAP = bnr ? GB : 4;
     constexpr int G = NIT < GCAP ? NIT : GCAP;
     if (tile_fast) {
       const bf16* resid_b = p.resid ? (const bf16*)p.resid : (const bf16*)p.C;

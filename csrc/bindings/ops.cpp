@@ -75,6 +75,7 @@ int tfk_opt_hyper(int*, const float*, int, int, float, float, float*, hipStream_
 int tfk_sumsq(const float*, long long, float*, hipStream_t);
 int tfk_clip_coef(const float*, float, float*, float*, hipStream_t);
 int tfk_splitk_reduce(const float*, int, long long, long long, float*, void*, int, float, hipStream_t);
+void tfk_splitk_set_direct(int);
 int tfk_hwgrad_slabs(int, int, int, int, int, int, int, int);
 int tfk_stem_wgrad_slabs(int, int, int);
 int tfk_stem_fwd_ok(int, int, int);
@@ -998,6 +999,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sumsq", &sumsq);
   m.def("clip_coef", &clip_coef);
   m.def("splitk_reduce", &splitk_reduce);
+  m.def("splitk_set_direct", &tfk_splitk_set_direct);  // A/B: 0 two-pass only, 1/2 direct for S <= 8
   m.def("hwgrad_slabs", &hwgrad_slabs);
   m.def("hwgrad", &hwgrad);
   m.def("stem_wgrad_slabs", &stem_wgrad_slabs);

@@ -21,6 +21,7 @@ int grid_for(long long work, int cap = 8192) {
 // group order. G is chosen so pass 1 has ~1024 blocks: a small weight with hundreds of split-K slabs
 // (64x64 1x1 wgrad: 256 slabs x 16K) spreads over the chip instead of 16 blocks walking 256 slabs
 // (the previous form: 8-slab groups combined with f32 atomics, 18 us for 16 MB, non-deterministic).
+// S <= 8 takes splitk_direct_kernel below instead (one pass, no LDS).
 template <bool FINAL>
 __device__ __forceinline__ void splitk_store(long long i, long long n, f32x4 a, float* out, bf16* outb,
                                              int accumulate, float alpha) {
@@ -86,6 +87,80 @@ __global__ void splitk_final_kernel(const float* __restrict__ slabs, int G, int 
       for (int e = 0; e < 4 && i + e < n; ++e) a[e] += slabs[(long long)g * SG * stride + i + e];
   }
   splitk_store<true>(i, n, a, out, outb, accumulate, alpha);
+}
+
+// Few slabs (S <= 8: the linear weight gradients' split counts, halved on the side streams to 2-4):
+// every lane sums its 4-element column of all S slabs itself, U columns 1024 elements apart, with
+// all S x U 16-B loads issued before the first add. No LDS, no barrier, no idle waves (the two-pass
+// kernel hands each slab to one of 4 waves: at S = 2 half of them idle, and each lane has one load in
+// flight). Same summation order as the two-pass kernel's one-group path: a_w = slabs w, w + 4 in
+// order, then ((a0 + a1) + a2) + a3 -- bit-identical results.
+template <int S, int U>
+__global__ __launch_bounds__(256) void splitk_direct_kernel(const float* __restrict__ slabs, long long stride,
+                                                            long long n, float* __restrict__ out,
+                                                            bf16* __restrict__ outb, int accumulate, float alpha) {
+  const long long base = (long long)blockIdx.x * (1024 * U) + threadIdx.x * 4;
+  f32x4 v[U][S];
+  if ((long long)(blockIdx.x + 1) * (1024 * U) <= n) {  // interior block (uniform): unguarded loads
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        v[u][s] = __builtin_nontemporal_load((const f32x4*)(slabs + s * stride + base + u * 1024));
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + u * 1024;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (i + 3 < n) {
+          v[u][s] = __builtin_nontemporal_load((const f32x4*)(slabs + s * stride + i));
+        } else {
+          v[u][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int e = 0; e < 4 && i + e < n; ++e) v[u][s][e] = slabs[s * stride + i + e];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = base + u * 1024;
+    if (i >= n) return;
+    f32x4 a[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      a[w] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = w; s < S; s += 4) a[w] += v[u][s];
+    }
+    f32x4 r = a[0];
+    r += a[1];
+    r += a[2];
+    r += a[3];
+    splitk_store<true>(i, n, r, out, outb, accumulate, alpha);
+  }
+}
+
+template <int S>
+void splitk_direct_launch(const float* slabs, long long stride, long long n, float* out, bf16* outb, int accumulate,
+                          float alpha, int U, hipStream_t s) {
+  if (U == 2)
+    hipLaunchKernelGGL((splitk_direct_kernel<S, 2>), dim3((unsigned)((n + 2047) / 2048)), dim3(256), 0, s, slabs,
+                       stride, n, out, outb, accumulate, alpha);
+  else
+    hipLaunchKernelGGL((splitk_direct_kernel<S, 1>), dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, s, slabs,
+                       stride, n, out, outb, accumulate, alpha);
+}
+
+// 0: two-pass kernel only; 1: S <= 8 direct, one column per lane; 2: direct, two columns per lane
+// from 1M elements (A/B knob; TFK_SPLITK_DIRECT=0/1/2, default 2)
+int g_splitk_direct = -1;
+int splitk_direct_mode() {
+  if (g_splitk_direct < 0) {
+    const char* e = getenv("TFK_SPLITK_DIRECT");
+    g_splitk_direct = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
+  }
+  return g_splitk_direct;
 }
 
 // in [A][R][B] -> out [B][R][A] (bf16), 32x32 LDS tiles; grid (ceil(B/32), ceil(A/32), R).
@@ -324,9 +399,25 @@ int tfk_scatter_add_rows(bf16* dst, const bf16* src, const int* pos, int P, int 
   hipLaunchKernelGGL(scatter_add_rows_kernel, dim3(B), dim3(NT), 0, s, dst, src, pos, P, S, W);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+void tfk_splitk_set_direct(int mode) { g_splitk_direct = mode < 0 || mode > 2 ? 2 : mode; }
 int tfk_splitk_reduce(const float* slabs, int S, long long stride, long long n, float* out, bf16* outb, int accumulate,
                       float alpha, hipStream_t s) {
   if (S < 1 || n < 1) return 0;
+  const int dmode = splitk_direct_mode();
+  if (dmode > 0 && S <= 8) {
+    const int U = (dmode == 2 && n >= (1LL << 20)) ? 2 : 1;
+    switch (S) {
+      case 1: splitk_direct_launch<1>(slabs, stride, n, out, outb, accumulate, alpha, U, s); break;
+      case 2: splitk_direct_launch<2>(slabs, stride, n, out, outb, accumulate, alpha, U, s); break;
+      case 3: splitk_direct_launch<3>(slabs, stride, n, out, outb, accumulate, alpha, U, s); break;
+      case 4: splitk_direct_launch<4>(slabs, stride, n, out, outb, accumulate, alpha, U, s); break;
+      case 5: splitk_direct_launch<5>(slabs, stride, n, out, outb, accumulate, alpha, U, s); break;
+      case 6: splitk_direct_launch<6>(slabs, stride, n, out, outb, accumulate, alpha, U, s); break;
+      case 7: splitk_direct_launch<7>(slabs, stride, n, out, outb, accumulate, alpha, U, s); break;
+      default: splitk_direct_launch<8>(slabs, stride, n, out, outb, accumulate, alpha, U, s); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   const long long chunks = (n + 255) / 256;
   long long G = (1024 + chunks - 1) / chunks;
   const long long gmax = (S + 3) / 4;  // >= 4 slabs per group (one per wave)

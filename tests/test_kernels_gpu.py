@@ -698,6 +698,33 @@ def test_splitk_reduce_two_pass(S, n, acc):
         assert float((ob.double() - ref).abs().max()) < 0.02 * float(ref.abs().max()) + 1e-2
 
 
+@pytest.mark.parametrize("S,n", [(1, 4097), (2, 4194304), (3, 1048579), (4, 2050), (6, 1048576), (8, 262147)])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_splitk_direct_matches_two_pass(S, n, mode):
+    """The S <= 8 one-pass slab reduce (misc.hip splitk_direct_kernel) is bit-identical to the
+    two-pass kernel wherever that one runs a single slab group (S <= 4 or >= 1024 chunks): f32
+    accumulate and bf16 outputs, ragged n, partial last block, both column counts per lane."""
+    from tensorflow_k8s_amd.ops._lib import lib
+    L = lib()
+    torch.manual_seed(S * 7 + n)
+    stride = (n + 3) // 4 * 4
+    slabs = torch.randn(S * stride, device="cuda")
+    base = torch.randn(n, device="cuda")
+    try:
+        res = {}
+        for m in (0, mode):
+            L.splitk_set_direct(m)
+            out = base.clone()
+            L.splitk_reduce(slabs.clone(), S, stride, n, out, None, True, 0.5)
+            ob = torch.full((n,), 3.0, dtype=torch.bfloat16, device="cuda")
+            L.splitk_reduce(slabs.clone(), S, stride, n, None, ob, False, 1.0)
+            res[m] = (out, ob)
+    finally:
+        L.splitk_set_direct(2)
+    assert torch.equal(res[0][0], res[mode][0])
+    assert torch.equal(res[0][1], res[mode][1])
+
+
 @pytest.mark.parametrize("N,K,M", [(4352, 4096, 2048), (4300, 4096, 1024)])
 def test_wgrad_tail_split_matches_reference(N, K, M):
     """Weight gradients of whole 256x256 rounds plus a small tail (272 tiles = 256 + 16): the tail

@@ -7,10 +7,14 @@ the two-pass kernel runs one group. Usage: python tools/splitk_probe.py [--iters
 """
 import argparse
 import json
+import os
+import sys
 
 import torch
 
-from tensorflow_k8s_amd.ops._lib import lib
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from tensorflow_k8s_amd.ops._lib import lib  # noqa: E402
 
 SHAPES = [(2, 4096 * 1024), (4, 4096 * 1024), (2, 3072 * 1024), (4, 1024 * 1024), (8, 1024 * 1024),
           (2, 1024 * 1024), (4, 768 * 3072), (8, 768 * 768), (3, 100003)]

@@ -692,8 +692,17 @@ int tfk_layernorm_fwd_mx(const bf16* x, const float* gamma, const float* beta, b
 // blocks of the LayerNorm-backward grid (the binding sizes the partials workspace with it)
 // bf16 mode: rows per wave of the grid-stride backward (A/B knob of tools/ln_probe.py; fewer rows per
 // wave = more blocks per CU in flight, more column-partial slabs for ln_part_reduce_kernel)
-static int g_ln_rows = 8;
+// (TFK_LN_ROWS sets the starting value, default 8)
+static int g_ln_rows = -1;
 void tfk_ln_bwd_set_rows(int r) { g_ln_rows = r > 0 ? r : 8; }
+static int ln_rows() {
+  if (g_ln_rows < 0) {
+    const char* e = getenv("TFK_LN_ROWS");
+    const int r = e ? atoi(e) : 0;
+    g_ln_rows = r > 0 ? r : 8;
+  }
+  return g_ln_rows;
+}
 // bf16-mode calls at W = 768 / 1024 on ln_bwd_fast_kernel (A/B knob; TFK_LN_FAST=0 disables)
 static int g_ln_fast = -1;
 void tfk_ln_bwd_set_fast(int on) { g_ln_fast = on ? 1 : 0; }
@@ -705,7 +714,7 @@ static bool ln_fast() {
   return g_ln_fast == 1;
 }
 
-int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (NT / 64) * g_ln_rows, 4096); }
+int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (NT / 64) * ln_rows(), 4096); }
 static unsigned ln_bwd_blocks(int M, bool mxo) { return (unsigned)tfk_ln_bwd_blocks(M, mxo ? 1 : 0); }
 // part (optional): f32 workspace [blocks][2 or 3][W] for the column partials (no tail atomics)
 int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const float* mean, const float* rstd,

@@ -38,7 +38,7 @@ def main():
     dbias = torch.zeros(W, device="cuda") if args.dbias else None
     res, ref, err = {}, None, {}
     # (rows per wave, kernel: 0 = generic ln_bwd_kernel, 1 = width-specialized ln_bwd_fast_kernel)
-    cfgs = ((8, 0), (8, 1), (4, 1), (16, 1))
+    cfgs = ((8, 0), (8, 1), (4, 1), (2, 1))
     for _ in range(args.rounds):
         for rows, pf in cfgs:
             lib().ln_bwd_set_rows(rows)

@@ -156,9 +156,11 @@ def test_layernorm_bwd_fast_matches_generic(W, dres_on, drop_on, dbias_on):
     finally:
         lib().ln_bwd_set_fast(1)
     (dx0, dxd0, dg0, db0, bs0), (dx1, dxd1, dg1, db1, bs1), o2 = out
-    # the ping-pong loop visits the same rows in the same order: bit-identical to the plain loop
-    for a, b_ in zip((dx1, dxd1, dg1, db1, bs1), o2):
-        assert (a is None and b_ is None) or torch.equal(a, b_)
+    # the ping-pong loop computes each row as the plain loop does: dx / dropout(dx) bit-identical
+    # (the column sums meet in ln_part_reduce_kernel's atomics: equal up to their order)
+    assert torch.equal(dx1, o2[0]) and torch.equal(dxd1, o2[1])
+    for a, b_ in zip((dg1, db1, bs1), o2[2:]):
+        assert (a is None and b_ is None) or rel(b_, a) < 1e-5
     assert rel(dx1, dx0) < 1e-2 and rel(dxd1, dxd0) < 1e-2
     assert rel(dg1, dg0) < 1e-4 and rel(db1, db0) < 1e-4
     if dbias_on:

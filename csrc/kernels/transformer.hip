@@ -325,7 +325,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const bf16* __restrict__ dy,
 // options are compile-time, lane l owns the 4-element chunks l + 64 q (q < Q4; every 8-B load of a
 // wave is a contiguous 512 B), and each iteration loads two rows before using either. (The generic
 // kernel's 8-element lane map measured 22.1 vs 19.2 us on BERT-base's call form.)
-template <int Q4, bool DRES, bool DROP, bool DBIAS, bool PIPE>
+template <int Q4, bool DRES, bool DROP, bool DBIAS>
 __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                          const float* __restrict__ gamma, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, const bf16* __restrict__ dres,
@@ -392,34 +392,6 @@ __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict_
     }
   };
   const int rstep = gridDim.x * (NT / 64);
-  if constexpr (PIPE) {
-    // ping-pong over row pairs: pair p + 1's loads are issued before pair p is computed, so a wave
-    // keeps a pair of rows in flight through its reductions and stores. Loads past the wave's last
-    // row are clamped to row M - 1 (L2 hits, never computed), keeping every load unconditional and
-    // the in-order vmcnt waits static.
-    const int row0 = blockIdx.x * (NT / 64) + wid;
-    const int nrow = row0 < M ? (M - 1 - row0) / rstep + 1 : 0, npair = (nrow + 1) / 2;
-    auto rowc = [&](int j) { return min(row0 + j * rstep, M - 1); };
-    bf16x4 dP[2][Q4], xP[2][Q4], rP[2][Q4], dQ[2][Q4], xQ[2][Q4], rQ[2][Q4];
-    auto run_pair = [&](int p, const bf16x4 (&d)[2][Q4], const bf16x4 (&xx)[2][Q4], const bf16x4 (&rr)[2][Q4]) {
-      const int ra = row0 + 2 * p * rstep, rb = ra + rstep;
-      do_row(ra, mean[ra], rstd[ra], d[0], xx[0], rr[0]);
-      if (rb < M) do_row(rb, mean[rb], rstd[rb], d[1], xx[1], rr[1]);
-    };
-    if (npair > 0) {
-      load_row(rowc(0), dP[0], xP[0], rP[0]);
-      load_row(rowc(1), dP[1], xP[1], rP[1]);
-    }
-    for (int p = 0; p < npair; p += 2) {
-      load_row(rowc(2 * p + 2), dQ[0], xQ[0], rQ[0]);
-      load_row(rowc(2 * p + 3), dQ[1], xQ[1], rQ[1]);
-      run_pair(p, dP, xP, rP);
-      if (p + 1 >= npair) break;
-      load_row(rowc(2 * p + 4), dP[0], xP[0], rP[0]);
-      load_row(rowc(2 * p + 5), dP[1], xP[1], rP[1]);
-      run_pair(p + 1, dQ, xQ, rQ);
-    }
-  } else {
   for (int row = blockIdx.x * (NT / 64) + wid; row < M; row += 2 * rstep) {
     const bool two = row + rstep < M;
     const int r1 = two ? row + rstep : row;
@@ -429,7 +401,6 @@ __global__ __launch_bounds__(NT) void ln_bwd_fast_kernel(const bf16* __restrict_
     load_row(r1, dB, xB, rB);
     do_row(row, muA, rsA, dA, xA, rA);
     if (two) do_row(r1, muB, rsB, dB, xB, rB);
-  }
   }
 #pragma unroll
   for (int q = 0; q < Q4; ++q) {
@@ -679,15 +650,11 @@ template <int Q4>
 void ln_bwd_fast_launch(dim3 grid, size_t sh, hipStream_t s, const bf16* dy, const bf16* x, const float* gamma,
                                const float* mean, const float* rstd, const bf16* dres, bf16* dx, float* dgamma,
                                float* dbeta, int M, bf16* dxd, float drop_p, unsigned long long drop_seed, float* dbias,
-                               float* part, bool pipe) {
+                               float* part) {
 #define TFK_LNF(R_, D_, B_)                                                                                       \
   if ((dres != nullptr) == R_ && (dxd != nullptr) == D_ && (dbias != nullptr) == B_) {                            \
-    if (pipe)                                                                                                    \
-      hipLaunchKernelGGL((ln_bwd_fast_kernel<Q4, R_, D_, B_, true>), grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, \
-                         dres, dx, dgamma, dbeta, M, dxd, drop_p, drop_seed, tfk_seed_key(), dbias, part);          \
-    else                                                                                                         \
-      hipLaunchKernelGGL((ln_bwd_fast_kernel<Q4, R_, D_, B_, false>), grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, \
-                         dres, dx, dgamma, dbeta, M, dxd, drop_p, drop_seed, tfk_seed_key(), dbias, part);          \
+    hipLaunchKernelGGL((ln_bwd_fast_kernel<Q4, R_, D_, B_>), grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, \
+                       dgamma, dbeta, M, dxd, drop_p, drop_seed, tfk_seed_key(), dbias, part);                      \
     return;                                                                                                      \
   }
   TFK_LNF(false, false, false) TFK_LNF(false, false, true) TFK_LNF(false, true, false) TFK_LNF(false, true, true)
@@ -736,16 +703,15 @@ static int ln_rows() {
   }
   return g_ln_rows;
 }
-// bf16-mode calls at W = 768 / 1024 on ln_bwd_fast_kernel (A/B knob TFK_LN_FAST: 0 generic kernel,
-// 1 fast kernel, 2 fast kernel with the row-pair ping-pong)
+// bf16-mode calls at W = 768 / 1024 on ln_bwd_fast_kernel (A/B knob; TFK_LN_FAST=0 disables)
 static int g_ln_fast = -1;
-void tfk_ln_bwd_set_fast(int on) { g_ln_fast = on < 0 ? 0 : (on > 2 ? 2 : on); }
-static int ln_fast_mode() {
+void tfk_ln_bwd_set_fast(int on) { g_ln_fast = on ? 1 : 0; }
+static bool ln_fast() {
   if (g_ln_fast < 0) {
     const char* e = getenv("TFK_LN_FAST");
-    g_ln_fast = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 1;
+    g_ln_fast = (e && e[0] == '0') ? 0 : 1;
   }
-  return g_ln_fast;
+  return g_ln_fast == 1;
 }
 
 int tfk_ln_bwd_blocks(int M, int mxo) { return mxo ? M / 32 : (int)grid_for(M, (NT / 64) * ln_rows(), 4096); }
@@ -762,14 +728,13 @@ int tfk_layernorm_bwd(const bf16* dy, const bf16* x, const float* gamma, const f
   const size_t sh = (size_t)(NT / 64) * (dbias ? 3 : 2) * W * sizeof(float) + (mxo ? (size_t)32 * (W + 8) * 2 : 0);
   const bool aligned = ((((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)(dres ? dres : dy) |
                           (uintptr_t)(dxd ? dxd : dx)) & 7) == 0) && ((uintptr_t)gamma & 15) == 0;
-  if (!mxo && aligned && (W == 768 || W == 1024) && ln_fast_mode() > 0) {
-    const bool pipe = ln_fast_mode() == 2;
+  if (!mxo && aligned && (W == 768 || W == 1024) && ln_fast()) {
     if (W == 768)
       ln_bwd_fast_launch<3>(grid, sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, dxd, drop_p, drop_seed,
-                            dbias, part, pipe);
+                            dbias, part);
     else
       ln_bwd_fast_launch<4>(grid, sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, dxd, drop_p, drop_seed,
-                            dbias, part, pipe);
+                            dbias, part);
   } else if (cpl <= 1)
     hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(NT), sh, s, dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, M, W,
                        dxd, drop_p, drop_seed, tfk_seed_key(), dbias, (unsigned char*)mq, (unsigned char*)ms,

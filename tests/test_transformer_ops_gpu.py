@@ -134,8 +134,8 @@ def test_layernorm_bwd_fused_consumer_dropout(W):
 @pytest.mark.parametrize("W", [768, 1024])
 @pytest.mark.parametrize("dres_on,drop_on,dbias_on", [(a, b, c) for a in (0, 1) for b in (0, 1) for c in (0, 1)])
 def test_layernorm_bwd_fast_matches_generic(W, dres_on, drop_on, dbias_on):
-    """The width-specialized LayerNorm backward (transformer.hip ln_bwd_fast_kernel, plain and
-    row-pair ping-pong loops) == the generic kernel for every option combination: dx / dropout(dx) (up to the row reductions' rounding),
+    """The width-specialized LayerNorm backward (transformer.hip ln_bwd_fast_kernel) == the generic
+    kernel for every option combination: dx / dropout(dx) (up to the row reductions' rounding),
     dgamma / dbeta / consumer bias gradient."""
     from tensorflow_k8s_amd.ops._lib import lib
     M = 1000
@@ -144,7 +144,7 @@ def test_layernorm_bwd_fast_matches_generic(W, dres_on, drop_on, dbias_on):
     y, mu, rs = T.layernorm_fwd(x.to(DEV), g.to(DEV), b.to(DEV))
     out = []
     try:
-        for fast in (0, 1, 2):  # 2: the row-pair ping-pong loop
+        for fast in (0, 1):
             lib().ln_bwd_set_fast(fast)
             dg, db = torch.zeros(W, device=DEV), torch.zeros(W, device=DEV)
             dbias = torch.zeros(W, device=DEV) if dbias_on else None
@@ -155,12 +155,7 @@ def test_layernorm_bwd_fast_matches_generic(W, dres_on, drop_on, dbias_on):
             out.append((dx, dxd, dg, db, dbias))
     finally:
         lib().ln_bwd_set_fast(1)
-    (dx0, dxd0, dg0, db0, bs0), (dx1, dxd1, dg1, db1, bs1), o2 = out
-    # the ping-pong loop computes each row as the plain loop does: dx / dropout(dx) bit-identical
-    # (the column sums meet in ln_part_reduce_kernel's atomics: equal up to their order)
-    assert torch.equal(dx1, o2[0]) and torch.equal(dxd1, o2[1])
-    for a, b_ in zip((dg1, db1, bs1), o2[2:]):
-        assert (a is None and b_ is None) or rel(b_, a) < 1e-5
+    (dx0, dxd0, dg0, db0, bs0), (dx1, dxd1, dg1, db1, bs1) = out
     assert rel(dx1, dx0) < 1e-2 and rel(dxd1, dxd0) < 1e-2
     assert rel(dg1, dg0) < 1e-4 and rel(db1, db0) < 1e-4
     if dbias_on:

@@ -37,9 +37,8 @@ def main():
     dres = None if args.no_dres else torch.randn(M, W, device="cuda").to(torch.bfloat16)  # residual branch
     dbias = torch.zeros(W, device="cuda") if args.dbias else None
     res, ref, err = {}, None, {}
-    # (rows per wave, kernel: 0 = generic ln_bwd_kernel, 1 = width-specialized ln_bwd_fast_kernel,
-    # 2 = the fast kernel with the row-pair ping-pong)
-    cfgs = ((8, 0), (8, 1), (8, 2), (4, 2))
+    # (rows per wave, kernel: 0 = generic ln_bwd_kernel, 1 = width-specialized ln_bwd_fast_kernel)
+    cfgs = ((8, 0), (8, 1), (4, 1), (2, 1))
     for _ in range(args.rounds):
         for rows, pf in cfgs:
             lib().ln_bwd_set_rows(rows)

@@ -19,6 +19,7 @@ int tfk_layernorm_bwd(const void*, const void*, const float*, const float*, cons
 int tfk_ln_bwd_blocks(int M, int mxo);
 void tfk_ln_bwd_set_rows(int r);
 void tfk_ln_bwd_set_fast(int on);
+void tfk_ln_fwd_set_fast(int on);
 int tfk_embedding_fwd(const int*, const void*, int, const void*, int, const int*, const void*, int, void*, long long, int,
                       float, hipStream_t);
 int tfk_embedding_bwd(const int*, const void*, int, float*, float*, int, const int*, float*, int, long long, int, float,
@@ -223,6 +224,7 @@ void register_transformer_ops(pybind11::module& m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("ln_bwd_set_rows", &tfk_ln_bwd_set_rows);
   m.def("ln_bwd_set_fast", &tfk_ln_bwd_set_fast);
+  m.def("ln_fwd_set_fast", &tfk_ln_fwd_set_fast);
   m.def("layernorm_fwd_mx", &layernorm_fwd_mx);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
         py::arg("rstd"), py::arg("dres"), py::arg("dx"), py::arg("dgamma"), py::arg("dbeta"), py::arg("M"), py::arg("W"),

@@ -67,6 +67,79 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const bf16* __restrict__ x, 
   if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
 }
 
+// Width-specialized LayerNorm forward (W = 768 / 1024): ln_fwd_kernel's lane map and arithmetic
+// (bit-identical outputs), but gamma / beta stay in registers across the rows of a grid-stride loop
+// -- ln_fwd_kernel re-reads 8 B of them per element for every row, 4x the row's own bf16 bytes, from
+// L2 -- and each iteration loads two rows before reducing either.
+constexpr int LNF_ROWS = 4;  // rows per wave
+template <int W>
+__global__ __launch_bounds__(NT) void ln_fwd_fast_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, bf16* __restrict__ y,
+                                                         float* __restrict__ mean, float* __restrict__ rstd, int M,
+                                                         float eps) {
+  constexpr int NCH = W / 8, CPL = (NCH + 63) / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float gm[CPL][8], bt[CPL][8];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      gm[j][e] = c < NCH ? gamma[c * 8 + e] : 0.f;
+      bt[j][e] = c < NCH ? beta[c * 8 + e] : 0.f;
+    }
+  }
+  auto load = [&](int r, bf16x8 (&t)[CPL]) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < NCH) t[j] = *(const bf16x8*)(x + (long long)r * W + c * 8);
+    }
+  };
+  auto norm = [&](int r, const bf16x8 (&t)[CPL]) {
+    float v[CPL][8];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      if (lane + 64 * j < NCH) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { v[j][e] = bf2f(t[j][e]); s += v[j][e]; }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[j][e] = 0.f;
+      }
+    }
+    const float mu = wave_sum(s) / W;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j)
+      if (lane + 64 * j < NCH)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float d = v[j][e] - mu; q += d * d; }
+    const float rs = rsqrtf(wave_sum(q) / W + eps);
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < NCH) {
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf((v[j][e] - mu) * rs * gm[j][e] + bt[j][e]);
+        *(bf16x8*)(y + (long long)r * W + c * 8) = o;
+      }
+    }
+    if (lane == 0) { mean[r] = mu; rstd[r] = rs; }
+  };
+  const int rstep = gridDim.x * (NT / 64);
+  for (int row = blockIdx.x * (NT / 64) + wid; row < M; row += 2 * rstep) {
+    const bool two = row + rstep < M;
+    bf16x8 tA[CPL], tB[CPL];
+    load(row, tA);
+    if (two) load(row + rstep, tB);
+    norm(row, tA);
+    if (two) norm(row + rstep, tB);
+  }
+}
+
 // LayerNorm forward that also emits both MX-fp8 quantizations of its output (the fp8 models' LN
 // outputs feed only MX-fp8 GEMMs: the QKV / FFN-in / cross-attention projections and the tied
 // logits): a block normalizes 32 rows (8 waves x 4 rows, same math as ln_fwd_kernel) into an LDS
@@ -664,9 +737,25 @@ void ln_bwd_fast_launch(dim3 grid, size_t sh, hipStream_t s, const bf16* dy, con
 }  // namespace
 
 extern "C" {
+// W = 768 / 1024 forwards on ln_fwd_fast_kernel (A/B knob; TFK_LN_FWD_FAST=0 disables)
+static int g_ln_fwd_fast = -1;
+void tfk_ln_fwd_set_fast(int on) { g_ln_fwd_fast = on ? 1 : 0; }
+static bool ln_fwd_fast() {
+  if (g_ln_fwd_fast < 0) {
+    const char* e = getenv("TFK_LN_FWD_FAST");
+    g_ln_fwd_fast = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_ln_fwd_fast == 1;
+}
 int tfk_layernorm_fwd(const bf16* x, const float* gamma, const float* beta, bf16* y, float* mean, float* rstd, int M,
                       int W, float eps, hipStream_t s) {
   const int cpl = (W / 8 + 63) / 64;
+  if ((W == 768 || W == 1024) && ln_fwd_fast() && ((((uintptr_t)x | (uintptr_t)y) & 15) == 0)) {
+    dim3 g((unsigned)((M + (NT / 64) * LNF_ROWS - 1) / ((NT / 64) * LNF_ROWS)));
+    if (W == 768) hipLaunchKernelGGL(ln_fwd_fast_kernel<768>, g, dim3(NT), 0, s, x, gamma, beta, y, mean, rstd, M, eps);
+    else hipLaunchKernelGGL(ln_fwd_fast_kernel<1024>, g, dim3(NT), 0, s, x, gamma, beta, y, mean, rstd, M, eps);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   dim3 grid((M + NT / 64 - 1) / (NT / 64));
   if (cpl <= 1) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(NT), 0, s, x, gamma, beta, y, mean, rstd, M, W, eps);
   else if (cpl <= 2) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(NT), 0, s, x, gamma, beta, y, mean, rstd, M, W, eps);

@@ -113,10 +113,11 @@ def test_layernorm(W):
         assert rel(out[DEV][k], out["cpu"][k]) < 1e-2, k
 
 
-@pytest.mark.parametrize("M,W", [(300, 768), (1000, 1024), (8192, 1024), (8192, 768), (17, 1024)])
+@pytest.mark.parametrize("M,W", [(300, 768), (1000, 1024), (8192, 1024), (17, 1024)])
 def test_layernorm_fwd_fast_matches_generic(M, W):
     """The width-specialized LayerNorm forward (transformer.hip ln_fwd_fast_kernel: gamma / beta in
-    registers, grid-stride rows) is bit-identical to ln_fwd_kernel: y, mean and rstd."""
+    registers, grid-stride rows; W = 1024, other widths keep ln_fwd_kernel) is bit-identical to
+    ln_fwd_kernel: y, mean and rstd."""
     from tensorflow_k8s_amd.ops._lib import lib
     x = bf(M, W, seed=61, scale=2.0).to(DEV)
     g, b = (torch.rand(W) + 0.5).to(DEV), (torch.randn(W) * 0.1).to(DEV)
